@@ -1,0 +1,226 @@
+/*
+ * orbfe.h -- C ABI of the MI355X-native ORB front-end (liborbfe.so).
+ *
+ * This is the drop-in boundary for ORB-SLAM2's per-frame feature path. Every entry point below
+ * replaces one reference interface (cited file:line into lreithmayr/ORB_SLAM2_2021):
+ *
+ *   orbfe_extractor_create / _destroy   ORBextractor::ORBextractor          include/ORBextractor.h:56-57,
+ *                                                                            src/ORBextractor.cc:413-473
+ *   orbfe_get_scale_tables              ORBextractor::GetScaleFactors & co.  include/ORBextractor.h:70-98
+ *   orbfe_extract                       ORBextractor::operator()             include/ORBextractor.h:66-68,
+ *                                                                            src/ORBextractor.cc:1041-1103
+ *   orbfe_extract_batch(_device)        N independent operator() calls (Frame.cc:113-116 runs two at once)
+ *   orbfe_get_level                     public ORBextractor::mvImagePyramid  include/ORBextractor.h:100
+ *   orbfe_descriptor_distance(_batch)   ORBmatcher::DescriptorDistance       src/ORBmatcher.cc:1672-1688
+ *   orbfe_search_by_projection_local    ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+ *                                                                            src/ORBmatcher.cc:45-133
+ *   orbfe_search_by_projection_lastframe ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ *                                                                            src/ORBmatcher.cc:1348-1491
+ *   orbfe_search_for_triangulation      ORBmatcher::SearchForTriangulation   src/ORBmatcher.cc:671-839
+ *
+ * Conventions: plain pointers and sizes only; no C++ or torch types. Every function returns an int
+ * status (ORBFE_OK = 0, negative on error) and never throws. Functions without the _device suffix
+ * take HOST pointers and are synchronous. _device functions take DEVICE pointers, enqueue on the
+ * given hipStream_t (passed as void*, NULL = the handle's own stream) and return immediately.
+ * A handle is thread-compatible (one thread at a time), not thread-safe, mirroring one
+ * ORBextractor instance per thread (Frame.cc:113-116).
+ */
+#ifndef ORBFE_H
+#define ORBFE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBFE_OK 0
+#define ORBFE_ERR_ARG -1       /* invalid argument (null pointer, bad size, unsupported geometry) */
+#define ORBFE_ERR_CAPACITY -2  /* caller buffer too small; *n holds the required count */
+#define ORBFE_ERR_HIP -3       /* HIP runtime error (message via orbfe_last_error) */
+#define ORBFE_ERR_STATE -4     /* call order violated (e.g. get_level before any extract) */
+
+#define ORBFE_DESC_BYTES 32
+
+/* cv::KeyPoint field order: pt.x, pt.y, size, angle, response, octave, class_id (28 bytes). */
+typedef struct orbfe_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} orbfe_keypoint;
+
+typedef struct orbfe_extractor orbfe_extractor;
+
+/* Pyramid vertical-rounding mode: OpenCV's x86 SIMD128 form on the columns
+ * its 16/8-lane loops cover (the default build of OpenCV 4.5.x), or the scalar form everywhere. */
+#define ORBFE_RESIZE_SIMD128 0
+#define ORBFE_RESIZE_SCALAR 1
+
+/* ---- extractor ---------------------------------------------------------------------------- */
+
+/* ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST) on HIP device `device`. */
+int orbfe_extractor_create(int nfeatures, float scale_factor, int nlevels, int ini_th_fast,
+                           int min_th_fast, int device, orbfe_extractor** out);
+int orbfe_extractor_destroy(orbfe_extractor* h);
+/* Select the resize rounding mode (default ORBFE_RESIZE_SIMD128). */
+int orbfe_extractor_set_resize_mode(orbfe_extractor* h, int mode);
+
+/* mvScaleFactor, mvInvScaleFactor, mvLevelSigma2, mvInvLevelSigma2 (nlevels floats each) and
+ * mnFeaturesPerLevel (nlevels ints). Any pointer may be NULL. */
+int orbfe_get_scale_tables(const orbfe_extractor* h, float* scale, float* inv_scale,
+                           float* sigma2, float* inv_sigma2, int32_t* features_per_level);
+
+/* Upper bound of keypoints one rows x cols image can produce: the sum over levels of
+ * max(budget + 3, 4 * nIni) (an octree level may overshoot its budget by up to 3 in the refinement
+ * loop, ORBextractor.cc:679-740, and its first pass yields up to 4 children per initial node).
+ * Returns the bound (> 0) or a negative status. */
+int orbfe_max_keypoints(orbfe_extractor* h, int rows, int cols);
+
+/* operator()(image, mask, keypoints, descriptors) on one 8-bit grayscale image (host memory).
+ * Writes *n keypoints (level order, ORBextractor.cc:1074-1102) and n x 32 descriptor bytes.
+ * An empty image (rows == 0 or cols == 0) yields *n = 0 (ORBextractor.cc:1044-1045). */
+int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int rows, int cols, size_t step,
+                  orbfe_keypoint* kps, int cap, uint8_t* desc, int* n);
+
+/* n_images independent operator() calls on same-shaped images (host memory). Image i starts at
+ * imgs[i]; results for image i go to kps + i*cap, desc + i*cap*32, counts[i]. */
+int orbfe_extract_batch(orbfe_extractor* h, int n_images, const uint8_t* const* imgs, int rows,
+                        int cols, size_t step, orbfe_keypoint* kps, uint8_t* desc, int cap,
+                        int32_t* counts);
+
+/* Device-resident batch: d_imgs holds n_images images, image i at d_imgs + i*image_stride, rows
+ * `pitch` bytes apart. Outputs are device buffers laid out as in orbfe_extract_batch. Async on
+ * `stream`. cap must be >= orbfe_max_keypoints(h). */
+int orbfe_extract_batch_device(orbfe_extractor* h, int n_images, const uint8_t* d_imgs,
+                               size_t image_stride, int rows, int cols, size_t pitch,
+                               orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
+                               int32_t* d_counts, void* stream);
+
+/* Lazy D2H of pyramid level `level` of image `image` of the last extract call (mvImagePyramid,
+ * read by Frame::ComputeStereoMatches, Frame.cc:529,620-640). *p stays valid until the next
+ * extract call on this handle. */
+int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p, int* rows,
+                    int* cols, size_t* step);
+
+/* Device pointer of the same level (no copy), for device-side consumers. */
+int orbfe_get_level_device(orbfe_extractor* h, int image, int level, const uint8_t** d_p,
+                           int* rows, int* cols, size_t* step);
+
+/* Per-kernel timing with HIP events recorded on the handle's launch stream.
+ * names/avg_ms/count arrays of length cap; returns number of kernels in *n. */
+int orbfe_set_profiling(orbfe_extractor* h, int enable);
+int orbfe_get_kernel_times(orbfe_extractor* h, char* names, int name_len, double* total_ms,
+                           int32_t* launches, int cap, int* n);
+int orbfe_reset_kernel_times(orbfe_extractor* h);
+
+/* Stream the handle launches on (hipStream_t as void*). */
+void* orbfe_extractor_stream(orbfe_extractor* h);
+
+/* ---- matcher data (packed struct-of-arrays views of Frame / KeyFrame / MapPoint) ---------- */
+
+/* MapPoint occupancy of a keypoint, from Frame::mvpMapPoints / KeyFrame::GetMapPoint:
+ * NONE = NULL pointer; PRESENT = a MapPoint whose Observations() == 0; OBSERVED = Observations()>0. */
+#define ORBFE_MP_NONE 0
+#define ORBFE_MP_PRESENT 1
+#define ORBFE_MP_OBSERVED 2
+
+typedef struct orbfe_frame_view {
+  int32_t n;                      /* Frame::N */
+  const orbfe_keypoint* keys_un;  /* mvKeysUn */
+  const float* u_right;           /* mvuRight (negative = no stereo) */
+  const uint8_t* descriptors;     /* mDescriptors, n x 32 */
+  const uint8_t* mp_state;        /* ORBFE_MP_* per keypoint */
+  int32_t nlevels;
+  const float* scale_factors;     /* mvScaleFactors */
+  const float* level_sigma2;      /* mvLevelSigma2 */
+  float min_x, max_x, min_y, max_y;  /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  float grid_inv_w, grid_inv_h;      /* mfGridElementWidthInv, mfGridElementHeightInv */
+  float fx, fy, cx, cy, bf, b;       /* camera; bf = mbf, b = mb */
+} orbfe_frame_view;
+
+/* DBoW2::FeatureVector as CSR: node ids ascending, indices of node k in
+ * indices[offsets[k] .. offsets[k+1]) in ascending feature order (TemplatedVocabulary.h:1161-1174). */
+typedef struct orbfe_feature_vector {
+  int32_t n_nodes;
+  const uint32_t* node_ids;
+  const int32_t* offsets;  /* n_nodes + 1 */
+  const int32_t* indices;
+} orbfe_feature_vector;
+
+#define ORBFE_MPF_TRACK_IN_VIEW 1u  /* MapPoint::mbTrackInView */
+#define ORBFE_MPF_BAD 2u            /* MapPoint::isBad() */
+#define ORBFE_MPF_OBSERVED 4u       /* MapPoint::Observations() > 0 */
+#define ORBFE_MPF_PRESENT 8u        /* LastFrame.mvpMapPoints[i] != NULL */
+#define ORBFE_MPF_OUTLIER 16u       /* LastFrame.mvbOutlier[i] */
+
+/* Local-map MapPoints as consumed by SearchByProjection(Frame&, vector<MapPoint*>, th). */
+typedef struct orbfe_local_mappoints {
+  int32_t m;
+  const uint8_t* flags;        /* ORBFE_MPF_TRACK_IN_VIEW | _BAD | _OBSERVED */
+  const float* proj_x;         /* mTrackProjX */
+  const float* proj_y;         /* mTrackProjY */
+  const float* proj_xr;        /* mTrackProjXR */
+  const int32_t* level;        /* mnTrackScaleLevel */
+  const float* view_cos;       /* mTrackViewCos */
+  const uint8_t* descriptors;  /* GetDescriptor(), m x 32 */
+} orbfe_local_mappoints;
+
+/* Last frame's MapPoints as consumed by SearchByProjection(Frame&, const Frame&, th, bMono). */
+typedef struct orbfe_lastframe_mappoints {
+  int32_t n;                   /* LastFrame.N */
+  const uint8_t* flags;        /* ORBFE_MPF_PRESENT | _OUTLIER | _OBSERVED */
+  const float* world_pos;      /* GetWorldPos(), n x 3 */
+  const uint8_t* descriptors;  /* GetDescriptor(), n x 32 */
+  const int32_t* octave;       /* LastFrame.mvKeys[i].octave */
+  const float* angle;          /* LastFrame.mvKeysUn[i].angle */
+  float tcw_last[12];          /* LastFrame.mTcw rows 0..2 (3x4, row-major) */
+} orbfe_lastframe_mappoints;
+
+typedef struct orbfe_matcher orbfe_matcher;
+
+/* ORBmatcher(nnratio, checkOri) bound to HIP device `device` (owns scratch + stream). */
+int orbfe_matcher_create(float nnratio, int check_orientation, int device, orbfe_matcher** out);
+int orbfe_matcher_destroy(orbfe_matcher* m);
+
+/* DescriptorDistance over n pairs (host memory): out[i] = popcount(a_i xor b_i). */
+int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b);
+int orbfe_descriptor_distance_batch(orbfe_matcher* m, const uint8_t* a, const uint8_t* b, int n,
+                                    int32_t* out);
+
+/* SearchByProjection(F, vpMapPoints, th): best_idx[i] = keypoint index MapPoint i is assigned to
+ * (F.mvpMapPoints[best_idx[i]] = vpMapPoints[i]; apply in ascending i), -1 if none.
+ * *nmatches = the reference's return value. */
+int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_frame_view* frame,
+                                     const orbfe_local_mappoints* mps, float th,
+                                     int32_t* best_idx, int* nmatches);
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono): best_idx[i] for last-frame keypoint i:
+ * -1 no match; k >= 0 CurrentFrame.mvpMapPoints[k] = LastFrame MapPoint i; k <= -2 the
+ * assignment to keypoint (-2 - k) was made and then undone by the rotation-consistency filter
+ * (ORBmatcher.cc:1469-1488): apply all assignments in ascending i, then NULL every undone
+ * keypoint. tcw_cur = CurrentFrame.mTcw rows 0..2. */
+int orbfe_search_by_projection_lastframe(orbfe_matcher* m, const orbfe_frame_view* current,
+                                         const orbfe_lastframe_mappoints* last,
+                                         const float* tcw_cur, float th, int mono,
+                                         int32_t* best_idx, int* nmatches);
+
+/* SearchForTriangulation(KF1, KF2, F12, pairs, bOnlyStereo): match12[idx1] = idx2 or -1;
+ * the reference's pairs are (i, match12[i]) for ascending i with match12[i] >= 0.
+ * f12: row-major 3x3 (F12.at<float>(r, c) = f12[3r + c]); (ex, ey) the epipole of KF1 in KF2
+ * (ORBmatcher.cc:678-684). */
+int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_frame_view* kf1,
+                                   const orbfe_frame_view* kf2, const orbfe_feature_vector* fv1,
+                                   const orbfe_feature_vector* fv2, const float* f12, float ex,
+                                   float ey, int only_stereo, int32_t* match12, int* nmatches);
+
+/* Last error message of the calling thread (static storage). */
+const char* orbfe_last_error(void);
+
+/* Library build identity, e.g. "orbfe gfx950 <git>" */
+const char* orbfe_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORBFE_H */

@@ -1,0 +1,24 @@
+/*
+ * orbfe_debug.h -- stage-inspection hooks of liborbfe.so used by the per-stage parity tests.
+ * Not part of the ORBextractor/ORBmatcher boundary. Keys are packed x | y<<12 | score<<24.
+ */
+#ifndef ORBFE_DEBUG_H
+#define ORBFE_DEBUG_H
+#include <stdint.h>
+#include "orbfe.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* FAST candidates of (image, level) of the last extract call, in DistributeOctTree input order,
+ * coordinates relative to minBorder (16). */
+int orbfe_debug_get_candidates(orbfe_extractor* h, int image, int level, uint32_t* out, int cap,
+                               int* n);
+/* Octree survivors of (image, level) in output order, level coordinates. */
+int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level, uint32_t* out, int cap,
+                               int* n);
+/* Per level: w, h, ncells, candidate capacity, budget, nIni, key capacity (7 ints per level). */
+int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, int cap);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,42 @@
+/*
+ * orbfe_match_batch.h -- device-resident batch entry points of the matcher (liborbfe.so).
+ *
+ * For pipelines whose keypoints, descriptors and feature vectors already live in HBM (the
+ * benchmark's extract -> SearchForTriangulation step). All pointers inside the structs are DEVICE
+ * pointers; the struct arrays themselves are host memory and are copied on every call.
+ */
+#ifndef ORBFE_MATCH_BATCH_H
+#define ORBFE_MATCH_BATCH_H
+#include <stdint.h>
+#include "orbfe.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One SearchForTriangulation(KF1, KF2, F12, pairs, bOnlyStereo) call (ORBmatcher.cc:671-839). */
+typedef struct orbfe_sft_pair {
+  orbfe_frame_view kf1, kf2;
+  orbfe_feature_vector fv1, fv2;
+  float f12[9];
+  float ex, ey;
+  int32_t* match12;   /* out: kf1.n entries */
+  int32_t* nmatches;  /* out: 1 entry */
+} orbfe_sft_pair;
+
+/* n_pairs independent SearchForTriangulation calls, one workgroup each, async on `stream`
+ * (NULL = the matcher's stream). */
+int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int n_pairs,
+                                                const orbfe_sft_pair* pairs, int only_stereo,
+                                                void* stream);
+
+/* hipStream_t of the matcher (as void*). */
+void* orbfe_matcher_stream(orbfe_matcher* m);
+
+/* Statistics of the last SearchByProjection call: fixpoint rounds run and whether the serial
+ * fallback kernel had to finish the claim order. */
+int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* serial_used);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

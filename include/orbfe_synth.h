@@ -1,0 +1,25 @@
+/*
+ * orbfe_synth.h -- seeded synthetic input frames (host code in liborbfe.so).
+ *
+ * Stands in for the KITTI 00 stereo PNGs the reference benchmarks on (absent offline); see
+ * SURVEY.md section 8(d). Not part of the ORBextractor/ORBmatcher boundary.
+ */
+#ifndef ORBFE_SYNTH_H
+#define ORBFE_SYNTH_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBFE_SYNTH_DEFAULT_RECTS 1200
+
+/* Render stereo frame `index` (seed 0x0B5EED00 ^ index) at rows x cols into left and/or right
+ * (either may be NULL), rows `step` bytes apart. n_rects <= 0 selects the default. */
+int orbfe_synth_frame(uint64_t index, int rows, int cols, int n_rects, uint8_t* left,
+                      uint8_t* right, size_t step);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,74 @@
+/*
+ * orbref.h -- C API of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+ *
+ * The oracle is a plain C++17 restatement of ORB-SLAM2's per-frame feature path
+ * (src/ORBextractor.cc, src/ORBmatcher.cc, src/Frame.cc of lreithmayr/ORB_SLAM2_2021) with the
+ * OpenCV 4.5.x primitives it calls (FAST, resize INTER_LINEAR, GaussianBlur, fastAtan2, cvRound)
+ * re-specified from their published algorithms. It is only ever loaded by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg, always as the checker -- never by
+ * the product path (orb_slam2_2021_amd/).
+ *
+ * Parity status (see DESIGN.md "Oracle"): the ORB-SLAM2 tables (umax, per-level budgets, scale
+ * tables, the 256-pair pattern, Gaussian taps) are pinned by known-answer tests; the reference
+ * itself cannot be built here (it needs OpenCV/Boost/Eigen, none present), so results at the
+ * OpenCV boundary are "parity unpinned".
+ *
+ * Matcher structs are the product's own boundary structs (include/orbfe.h).
+ */
+#ifndef ORBREF_H
+#define ORBREF_H
+#include <stddef.h>
+#include <stdint.h>
+#include "../include/orbfe.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orbref_extractor orbref_extractor;
+
+orbref_extractor* orbref_extractor_create(int nfeatures, float scale_factor, int nlevels,
+                                          int ini_th, int min_th);
+void orbref_extractor_destroy(orbref_extractor* h);
+int orbref_set_resize_mode(orbref_extractor* h, int mode);
+int orbref_get_tables(const orbref_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                      float* inv_sigma2, int32_t* features_per_level, int32_t* umax16);
+int orbref_extract(orbref_extractor* h, const uint8_t* img, int rows, int cols, size_t step,
+                   orbfe_keypoint* kps, int cap, uint8_t* desc, int* n);
+/* Stage outputs of the last extract call (for per-stage parity). */
+int orbref_get_level(const orbref_extractor* h, int level, uint8_t* out, int cap, int* rows,
+                     int* cols);
+/* FAST candidates of `level` in DistributeOctTree input order, packed x | y<<12 | score<<24
+ * (coordinates relative to minBorder = 16). */
+int orbref_get_candidates(const orbref_extractor* h, int level, uint32_t* out, int cap, int* n);
+/* Octree survivors of `level` in output order, same packing, level coordinates. */
+int orbref_get_level_keys(const orbref_extractor* h, int level, uint32_t* out, int cap, int* n);
+
+/* Primitives. */
+int orbref_resize_linear(const uint8_t* src, int sw, int sh, int sstep, uint8_t* dst, int dw,
+                         int dh, int dstep, int mode);
+int orbref_gaussian_blur7(const uint8_t* src, int w, int h, int sstep, uint8_t* dst, int dstep);
+float orbref_fast_atan2(float y, float x);
+int orbref_fast_score_map(const uint8_t* img, int w, int h, int step, uint8_t* m_out);
+int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Matchers (host memory, same semantics and outputs as the orbfe_* functions). */
+int orbref_search_by_projection_local(const orbfe_frame_view* frame,
+                                      const orbfe_local_mappoints* mps, float th, float nnratio,
+                                      int32_t* best_idx, int* nmatches);
+int orbref_search_by_projection_lastframe(const orbfe_frame_view* current,
+                                          const orbfe_lastframe_mappoints* last,
+                                          const float* tcw_cur, float th, int mono,
+                                          int check_ori, int32_t* best_idx, int* nmatches);
+int orbref_search_for_triangulation(const orbfe_frame_view* kf1, const orbfe_frame_view* kf2,
+                                    const orbfe_feature_vector* fv1,
+                                    const orbfe_feature_vector* fv2, const float* f12, float ex,
+                                    float ey, int only_stereo, int check_ori, int32_t* match12,
+                                    int* nmatches);
+/* Frame::AssignFeaturesToGrid as CSR (64 x 48 cells, cell = ix*48 + iy): cell_start[3073]. */
+int orbref_build_grid(const orbfe_frame_view* frame, int32_t* cell_start, int32_t* cell_items);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,175 @@
+"""ctypes binding of liborbfe.so (include/orbfe.h, orbfe_match_batch.h, orbfe_debug.h, orbfe_synth.h).
+
+The shared library is the product: every compute call below runs the HIP kernels in it. There is
+no CPU fallback -- if the library is missing, or no HIP device is present when a compute handle is
+created, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_float, c_int, c_int32,
+                    c_size_t, c_uint8, c_uint32, c_uint64, c_void_p)
+
+import numpy as np
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ORBFE_LIB", os.path.join(_PKG_DIR, "lib", "liborbfe.so"))
+
+ORBFE_OK = 0
+ORBFE_ERR_ARG = -1
+ORBFE_ERR_CAPACITY = -2
+ORBFE_ERR_HIP = -3
+ORBFE_ERR_STATE = -4
+ORBFE_RESIZE_SIMD128 = 0
+ORBFE_RESIZE_SCALAR = 1
+ORBFE_MP_NONE, ORBFE_MP_PRESENT, ORBFE_MP_OBSERVED = 0, 1, 2
+MPF_TRACK_IN_VIEW, MPF_BAD, MPF_OBSERVED, MPF_PRESENT, MPF_OUTLIER = 1, 2, 4, 8, 16
+
+# cv::KeyPoint field order (28 bytes), = orbfe_keypoint
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class OrbfeError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        super().__init__(f"{what} failed with status {status}: {last_error()}")
+        self.status = status
+
+
+class LibraryMissing(ImportError):
+    pass
+
+
+class frame_view(Structure):
+    _fields_ = [("n", c_int32), ("keys_un", c_void_p), ("u_right", c_void_p),
+                ("descriptors", c_void_p), ("mp_state", c_void_p), ("nlevels", c_int32),
+                ("scale_factors", c_void_p), ("level_sigma2", c_void_p),
+                ("min_x", c_float), ("max_x", c_float), ("min_y", c_float), ("max_y", c_float),
+                ("grid_inv_w", c_float), ("grid_inv_h", c_float),
+                ("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float),
+                ("bf", c_float), ("b", c_float)]
+
+
+class feature_vector(Structure):
+    _fields_ = [("n_nodes", c_int32), ("node_ids", c_void_p), ("offsets", c_void_p),
+                ("indices", c_void_p)]
+
+
+class local_mappoints(Structure):
+    _fields_ = [("m", c_int32), ("flags", c_void_p), ("proj_x", c_void_p), ("proj_y", c_void_p),
+                ("proj_xr", c_void_p), ("level", c_void_p), ("view_cos", c_void_p),
+                ("descriptors", c_void_p)]
+
+
+class lastframe_mappoints(Structure):
+    _fields_ = [("n", c_int32), ("flags", c_void_p), ("world_pos", c_void_p),
+                ("descriptors", c_void_p), ("octave", c_void_p), ("angle", c_void_p),
+                ("tcw_last", c_float * 12)]
+
+
+class sft_pair(Structure):
+    _fields_ = [("kf1", frame_view), ("kf2", frame_view), ("fv1", feature_vector),
+                ("fv2", feature_vector), ("f12", c_float * 9), ("ex", c_float), ("ey", c_float),
+                ("match12", c_void_p), ("nmatches", c_void_p)]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "orbfe_last_error": (c_char_p, []),
+    "orbfe_version": (c_char_p, []),
+    "orbfe_extractor_create": (c_int, [c_int, c_float, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "orbfe_extractor_destroy": (c_int, [c_void_p]),
+    "orbfe_extractor_set_resize_mode": (c_int, [c_void_p, c_int]),
+    "orbfe_get_scale_tables": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "orbfe_max_keypoints": (c_int, [c_void_p, c_int, c_int]),
+    "orbfe_extract": (c_int, [c_void_p, c_void_p, c_int, c_int, c_size_t, c_void_p, c_int, c_void_p,
+                              POINTER(c_int)]),
+    "orbfe_extract_batch": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_size_t, c_void_p,
+                                    c_void_p, c_int, c_void_p]),
+    "orbfe_extract_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_int, c_int,
+                                           c_size_t, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "orbfe_get_level": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int),
+                                POINTER(c_int), POINTER(c_size_t)]),
+    "orbfe_get_level_device": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int),
+                                       POINTER(c_int), POINTER(c_size_t)]),
+    "orbfe_set_profiling": (c_int, [c_void_p, c_int]),
+    "orbfe_get_kernel_times": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                       POINTER(c_int)]),
+    "orbfe_reset_kernel_times": (c_int, [c_void_p]),
+    "orbfe_extractor_stream": (c_void_p, [c_void_p]),
+    "orbfe_matcher_create": (c_int, [c_float, c_int, c_int, POINTER(c_void_p)]),
+    "orbfe_matcher_destroy": (c_int, [c_void_p]),
+    "orbfe_matcher_stream": (c_void_p, [c_void_p]),
+    "orbfe_matcher_last_stats": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
+    "orbfe_descriptor_distance": (c_int, [c_void_p, c_void_p]),
+    "orbfe_descriptor_distance_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "orbfe_search_by_projection_local": (c_int, [c_void_p, POINTER(frame_view),
+                                                 POINTER(local_mappoints), c_float, c_void_p,
+                                                 POINTER(c_int)]),
+    "orbfe_search_by_projection_lastframe": (c_int, [c_void_p, POINTER(frame_view),
+                                                     POINTER(lastframe_mappoints), c_void_p,
+                                                     c_float, c_int, c_void_p, POINTER(c_int)]),
+    "orbfe_search_for_triangulation": (c_int, [c_void_p, POINTER(frame_view), POINTER(frame_view),
+                                               POINTER(feature_vector), POINTER(feature_vector),
+                                               c_void_p, c_float, c_float, c_int, c_void_p,
+                                               POINTER(c_int)]),
+    "orbfe_search_for_triangulation_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_int,
+                                                            c_void_p]),
+    "orbfe_debug_get_candidates": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
+    "orbfe_debug_get_level_keys": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
+    "orbfe_debug_geometry": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
+    "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
+}
+
+# symbols declared in include/*.h (checked by tests/test_library.py)
+EXPORTED = sorted(_SIGNATURES)
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load liborbfe.so once (raises LibraryMissing if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
+                f"g.build()'` (or make -C orb_slam2_2021_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    try:
+        s = lib().orbfe_last_error()
+    except Exception:  # pragma: no cover
+        return "<no library>"
+    return s.decode() if s else ""
+
+
+def check(status: int, what: str) -> int:
+    if status < 0:
+        raise OrbfeError(status, what)
+    return status
+
+
+def ptr(a) -> c_void_p:
+    """Address of a numpy array (contiguous) or an int device pointer."""
+    if a is None:
+        return c_void_p(0)
+    if isinstance(a, int):
+        return c_void_p(a)
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return c_void_p(a.ctypes.data)
+    if hasattr(a, "data_ptr"):  # torch tensor (device plumbing)
+        return c_void_p(a.data_ptr())
+    raise TypeError(f"cannot take the address of {type(a)}")

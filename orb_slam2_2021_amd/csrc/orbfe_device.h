@@ -1,0 +1,88 @@
+// orbfe_device.h -- device helpers shared by the extractor and matcher kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// The whole library is compiled with -ffp-contract=off: every float expression below rounds each
+// operation exactly like the reference's scalar x86 code.
+
+#define ORBFE_WAVE 64
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
+__device__ __forceinline__ int wave_id() { return (int)(threadIdx.x >> 6); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  return (1ull << (unsigned)lane_id()) - 1ull;
+}
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return (uint64_t)__ballot(p ? 1 : 0); }
+__device__ __forceinline__ int prefix_in_wave(uint64_t mask) {
+  return __popcll(mask & lanemask_lt());
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// cvRound(float): round half to even (v_rndne_f32)
+__device__ __forceinline__ int cv_round_f(float v) { return (int)__builtin_rintf(v); }
+
+// ORBmatcher::DescriptorDistance (ORBmatcher.cc:1672-1688) = popcount of the 256-bit xor.
+__device__ __forceinline__ int hamming256(const uint4 a0, const uint4 a1, const uint4 b0,
+                                          const uint4 b1) {
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+__device__ __forceinline__ void load_desc(const uint8_t* p, uint4& d0, uint4& d1) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  d0 = q[0];
+  d1 = q[1];
+}
+
+// OpenCV fastAtan2 (atanImpl<float>) in degrees; constants are computed on the host in float
+// exactly as OpenCV's static initialisers do and passed in.
+struct AtanConsts {
+  float p1, p3, p5, p7, eps;
+};
+__device__ __forceinline__ float fast_atan2_dev(float y, float x, const AtanConsts& k) {
+  float ax = fabsf(x), ay = fabsf(y), a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + k.eps);
+    c2 = c * c;
+    a = (((k.p7 * c2 + k.p5) * c2 + k.p3) * c2 + k.p1) * c;
+  } else {
+    c = ax / (ay + k.eps);
+    c2 = c * c;
+    a = 90.f - (((k.p7 * c2 + k.p5) * c2 + k.p3) * c2 + k.p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+#define ORBFE_HIP_CHECK(expr)                                     \
+  do {                                                            \
+    hipError_t _e = (expr);                                       \
+    if (_e != hipSuccess) return orbfe_set_hip_error(_e, #expr); \
+  } while (0)
+
+int orbfe_set_error(int code, const char* msg);
+int orbfe_set_hip_error(hipError_t e, const char* what);

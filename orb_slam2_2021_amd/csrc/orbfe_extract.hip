@@ -1,0 +1,1502 @@
+// orbfe_extract.hip -- ORBextractor::operator() as four CDNA4 kernels (gfx950, wave64).
+//
+// Reference: src/ORBextractor.cc of lreithmayr/ORB_SLAM2_2021 (operator() :1041-1103).
+// Pipeline per batch of same-shaped images, all on one HIP stream:
+//   k_resize   x (nlevels-1)  ComputePyramid :1105-1135 -- one launch per level (level l reads the
+//                             rounded uint8 level l-1, exactly the reference chain), 11-bit fixed
+//                             point bilinear with OpenCV's SIMD128 vertical rounding (Appendix A.3)
+//   k_fast                    the FAST half of ComputeKeyPointsOctTree :792-832 -- one wavefront per
+//                             ~30x30 cell ROI staged in LDS: 9-of-16 arc strength per pixel, strict
+//                             3x3 NMS inside the cell, iniTh -> minTh fallback, row-major compaction
+//                             with wave ballot + popcount
+//   k_octree                  DistributeOctTree :542-766 -- one workgroup per (image, level); the
+//                             list/push_front/erase order of the reference is reproduced with
+//                             parallel passes (block scans + a bitonic sort of the refinement set)
+//   k_describe                IC_Angle :75-102 + GaussianBlur 7x7 :1083-1084 + computeOrbDescriptor
+//                             :105-151 + rescale :1093-1099 -- one wavefront per keypoint on a
+//                             43x43 LDS patch; the 256 tests land as 4 wave ballots (= 32 bytes)
+// Data layout in HBM per image: pyramid levels 1..L-1 packed (64-byte row pitch); FAST candidate
+// slots per cell (u32 x | y<<12 | score<<24, cell-order); octree key ping-pong buffers; per-level
+// survivor keys; outputs orbfe_keypoint[cap] + 32-byte descriptors[cap] + count.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "../../include/orbfe_debug.h"
+#include "orb_pattern31.inc"
+#include "orbfe_device.h"
+
+// ---------------------------------------------------------------------------------------------
+// errors
+static thread_local std::string g_last_error;
+int orbfe_set_error(int code, const char* msg) {
+  g_last_error = msg ? msg : "";
+  return code;
+}
+int orbfe_set_hip_error(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return ORBFE_ERR_HIP;
+}
+extern "C" const char* orbfe_last_error(void) { return g_last_error.c_str(); }
+extern "C" const char* orbfe_version(void) { return "orbfe 0.1 gfx950"; }
+
+// ---------------------------------------------------------------------------------------------
+// geometry tables (host-computed, uploaded once per image shape)
+struct LevelDesc {
+  int w, h, pitch;
+  int pad0;
+  long long pyr_off;     // byte offset of this level inside one image's pyramid block (l >= 1)
+  int cell_begin, ncells;
+  int cand_begin, cand_cap;  // candidate slots of this level inside one image's candidate block
+  int budget;                // mnFeaturesPerLevel[l]
+  int nini;                  // DistributeOctTree initial nodes (:546)
+  float hx;                  // (:548)
+  int rel_w, rel_h;          // maxBorderX - minBorderX, maxBorderY - minBorderY
+  int key_begin, key_cap;    // octree output slots of this level inside one image's key block
+  float scale;               // mvScaleFactor[l]
+  int size;                  // scaledPatchSize (:840)
+  int tab_x, tab_y;          // resize table offsets (l >= 1)
+  int xmax, simd_end;        // resize: first column using the clamped path / end of SIMD columns
+};
+
+struct CellDesc {
+  int16_t level, x0, y0, rw, rh, ox, oy, pad;
+  int32_t slot, cap;
+};
+
+struct ExtractArgs {
+  const LevelDesc* levels;
+  const CellDesc* cells;
+  const int2* xtab;
+  const int2* ytab;
+  int nlevels, ncells, n_images, total_key_slots;
+  const uint8_t* img0;
+  long long img_stride;
+  int img_pitch, pad1;
+  uint8_t* pyr;
+  long long pyr_stride;
+  uint32_t* cand;
+  long long cand_stride;
+  int32_t* cellcnt;
+  uint32_t* keys_a;
+  uint32_t* keys_b;
+  long long keyscr_stride;
+  uint32_t* lvlkeys;
+  long long lvlkey_stride;
+  int32_t* lvlcnt;
+  orbfe_keypoint* out_kps;
+  uint8_t* out_desc;
+  int32_t* out_counts;
+  int out_cap;
+  int ini_th, min_th, tlow;
+  int roi_w_max, roi_h_max;
+  int node_cap, sort_cap;
+  int umax[16];
+  AtanConsts atan;
+  float factor_pi;
+};
+
+__constant__ int8_t c_pattern[1024];
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ const uint8_t* level_ptr(const ExtractArgs& a, const LevelDesc& ld,
+                                                    int img, int l, int& pitch) {
+  if (l == 0) {
+    pitch = a.img_pitch;
+    return a.img0 + (long long)img * a.img_stride;
+  }
+  pitch = ld.pitch;
+  return a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+}
+
+__device__ __forceinline__ int sat16(int v) { return min(max(v, -32768), 32767); }
+
+// ---------------------------------------------------------------------------------------------
+// k_resize: level l from level l-1 (resize INTER_LINEAR, ORBextractor.cc:1118). One thread per
+// output pixel; xofs/alpha and yofs/beta come from host tables built exactly as OpenCV does.
+__global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
+  const LevelDesc ld = a.levels[l];
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  const int img = blockIdx.z;
+  if (x >= ld.w || y >= ld.h) return;
+  const LevelDesc ls = a.levels[l - 1];
+  int spitch;
+  const uint8_t* src = level_ptr(a, ls, img, l - 1, spitch);
+  const int2 xt = a.xtab[ld.tab_x + x];
+  const int2 yt = a.ytab[ld.tab_y + y];
+  const int sx = xt.x;
+  const int a0 = (int)(short)(xt.y & 0xffff), a1 = (int)(short)((unsigned)xt.y >> 16);
+  const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
+  const int sy0 = min(max(yt.x, 0), ls.h - 1), sy1 = min(max(yt.x + 1, 0), ls.h - 1);
+  const uint8_t* r0 = src + (long long)sy0 * spitch;
+  const uint8_t* r1 = src + (long long)sy1 * spitch;
+  int h0, h1;
+  if (x < ld.xmax) {
+    h0 = r0[sx] * a0 + r0[sx + 1] * a1;
+    h1 = r1[sx] * a0 + r1[sx + 1] * a1;
+  } else {
+    h0 = r0[sx] * 2048;
+    h1 = r1[sx] * 2048;
+  }
+  int v;
+  if (x < ld.simd_end) {  // VResizeLinearVec_32s8u (v_mul_hi, saturating adds, rshr_pack_u<2>)
+    const int m0 = (sat16(h0 >> 4) * b0) >> 16, m1 = (sat16(h1 >> 4) * b1) >> 16;
+    v = sat16(sat16(m0 + m1) + 2) >> 2;
+  } else {  // FixedPtCast<int, uchar, 22>
+    v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+  }
+  uint8_t* dst = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+  dst[(long long)y * ld.pitch + x] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ---------------------------------------------------------------------------------------------
+// FAST-9/16 helpers on an LDS tile with row stride `s` (OpenCV fast.cpp FAST_t<16>).
+// Ring offsets (dx, dy) starting at (0, 3): makeOffsets(pixel, step, 16).
+__device__ __forceinline__ int ring_off(int k, int s) {
+  switch (k) {
+    case 0: return 3 * s;
+    case 1: return 1 + 3 * s;
+    case 2: return 2 + 2 * s;
+    case 3: return 3 + s;
+    case 4: return 3;
+    case 5: return 3 - s;
+    case 6: return 2 - 2 * s;
+    case 7: return 1 - 3 * s;
+    case 8: return -3 * s;
+    case 9: return -1 - 3 * s;
+    case 10: return -2 - 2 * s;
+    case 11: return -3 - s;
+    case 12: return -3;
+    case 13: return -3 + s;
+    case 14: return -2 + 2 * s;
+    default: return -1 + 3 * s;
+  }
+}
+
+// Arc strength M = max(v - A, B - v) with A = min over the 16 arcs of 9 of the max ring value and
+// B = max over arcs of the min ring value. The pixel is a FAST corner at threshold t iff
+// M >= t+1, and then cornerScore<16> == M - 1. Returns 0 when the pixel is no corner at tlow
+// (OpenCV's antipodal-pair quick test first).
+__device__ __forceinline__ int arc_strength_lds(const uint8_t* p, int s, int tlow) {
+  const int v = p[0];
+  int x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x[k] = p[ring_off(k, s)];
+  int d = 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int ta = (x[k] < v - tlow ? 1 : 0) | (x[k] > v + tlow ? 2 : 0);
+    const int tb = (x[k + 8] < v - tlow ? 1 : 0) | (x[k + 8] > v + tlow ? 2 : 0);
+    d &= ta | tb;
+  }
+  if (d == 0) return 0;
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = min(x[k], x[(k + 1) & 15]);
+    mx2[k] = max(x[k], x[(k + 1) & 15]);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int B = 0, A = 255;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), x[(k + 8) & 15]);
+    const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), x[(k + 8) & 15]);
+    B = max(B, mn9);
+    A = min(A, mx9);
+  }
+  const int m = max(v - A, B - v);
+  return m < tlow + 1 ? 0 : m;
+}
+
+__device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
+  return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+__device__ __forceinline__ int key_x(uint32_t k) { return (int)(k & 0xfffu); }
+__device__ __forceinline__ int key_y(uint32_t k) { return (int)((k >> 12) & 0xfffu); }
+__device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }
+
+// k_fast: one wavefront per cell (4 cells per 256-thread workgroup). No workgroup barriers: waves
+// are independent and synchronise their own LDS with wave_sync().
+__global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int w = wave_id(), lane = lane_id();
+  const int cell = blockIdx.x * 4 + w;
+  const int img = blockIdx.y;
+  if (cell >= a.ncells) return;
+  const int roi_bytes = (a.roi_w_max * a.roi_h_max + 15) & ~15;
+  const int m_bytes = ((a.roi_w_max - 4) * (a.roi_h_max - 4) + 15) & ~15;
+  uint8_t* roi = smem + w * (roi_bytes + m_bytes);
+  uint8_t* m8 = roi + roi_bytes;
+
+  const CellDesc cd = a.cells[cell];
+  const LevelDesc ld = a.levels[cd.level];
+  int pitch;
+  const uint8_t* lev = level_ptr(a, ld, img, cd.level, pitch);
+  const int rw = cd.rw, rh = cd.rh;
+  const int mw = rw - 4, mh = rh - 4, dw = rw - 6, dh = rh - 6;
+  int32_t* cnt_out = a.cellcnt + (long long)img * a.ncells + cell;
+  if (dw <= 0 || dh <= 0) {
+    if (lane == 0) *cnt_out = 0;
+    return;
+  }
+  for (int i = lane; i < rw * rh; i += 64) {
+    const int r = i / rw, c = i - r * rw;
+    roi[i] = lev[(long long)(cd.y0 + r) * pitch + cd.x0 + c];
+  }
+  for (int i = lane; i < mw * mh; i += 64) m8[i] = 0;
+  wave_sync();
+  for (int q = lane; q < dw * dh; q += 64) {
+    const int rr = q / dw, cc = q - rr * dw;
+    const int m = arc_strength_lds(roi + (rr + 3) * rw + (cc + 3), rw, a.tlow);
+    m8[(rr + 1) * mw + (cc + 1)] = (uint8_t)min(m, 255);
+  }
+  wave_sync();
+  uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
+  int count = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const int t = min(max(pass == 0 ? a.ini_th : a.min_th, 0), 255);
+    for (int q0 = 0; q0 < dw * dh; q0 += 64) {
+      const int q = q0 + lane;
+      bool keep = false;
+      int rr = 0, cc = 0, s = 0;
+      if (q < dw * dh) {
+        rr = q / dw;
+        cc = q - rr * dw;
+        const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
+        const int m = mp[0];
+        if (m >= t + 1) {
+          s = m - 1;
+          keep = true;
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            const int o = k == 0 ? -mw - 1 : k == 1 ? -mw : k == 2 ? -mw + 1 : k == 3 ? -1 :
+                          k == 4 ? 1 : k == 5 ? mw - 1 : k == 6 ? mw : mw + 1;
+            const int mn = mp[o];
+            const int sn = mn >= t + 1 ? mn - 1 : 0;
+            keep = keep && (s > sn);
+          }
+        }
+      }
+      const uint64_t bal = wave_ballot(keep);
+      if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, s);
+      count += __popcll(bal);
+    }
+    if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
+  }
+  if (lane == 0) *cnt_out = count;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_octree: DistributeOctTree (ORBextractor.cc:542-766) for one (image, level).
+//
+// The reference keeps a std::list of nodes; every full pass divides every node with >1 key and
+// push_front()s its non-empty children n1..n4, so after a pass the list is
+//   reverse(children in creation order) ++ (single-key nodes in their old order).
+// A refinement round divides the nodes created in the previous pass/round with >1 key in
+// descending (size, creation order) -- the reference sorts (size, pointer) pairs; SURVEY C.1 --
+// stopping as soon as the list reaches N; its list is
+//   reverse(children of the divided nodes, in processing order) ++ (old list minus divided).
+// Both are computed with block scans; each node's keys stay one contiguous segment, partitioned
+// stably by one wavefront per divided node (ballot + popcount).
+struct ONode {
+  int16_t x0, y0, x1, y1;
+  int32_t begin, count, seq, flags;  // flags: bit0 = key buffer (0: A, 1: B), bit1 = in R set
+};
+
+__device__ int block_scan_excl(int* data, int n, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int per = (n + 255) / 256;
+  const int beg = min(t * per, n), end = min(beg + per, n);
+  int s = 0;
+  for (int i = beg; i < end; i++) s += data[i];
+  int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < w; k++) woff += wsum[k];
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int run = woff + inc - s;
+  for (int i = beg; i < end; i++) {
+    const int v = data[i];
+    data[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
+__device__ __forceinline__ int child_of(uint32_t key, int mx, int my) {
+  return (key_x(key) >= mx ? 1 : 0) | (key_y(key) >= my ? 2 : 0);
+}
+
+// Count the keys of `nd` falling in each of its 4 DivideNode children (wave-level).
+__device__ int4 wave_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
+  const uint32_t* src = (nd.flags & 1) ? kb : ka;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  for (int i0 = 0; i0 < nd.count; i0 += 64) {
+    const int i = i0 + lane_id();
+    const int ch = i < nd.count ? child_of(src[nd.begin + i], mx, my) : -1;
+    c0 += __popcll(wave_ballot(ch == 0));
+    c1 += __popcll(wave_ballot(ch == 1));
+    c2 += __popcll(wave_ballot(ch == 2));
+    c3 += __popcll(wave_ballot(ch == 3));
+  }
+  return make_int4(c0, c1, c2, c3);
+}
+
+// Stable 4-way partition of the node's keys into the other buffer (children contiguous, n1..n4).
+__device__ void wave_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, uint32_t* kb) {
+  const uint32_t* src = (nd.flags & 1) ? kb : ka;
+  uint32_t* dst = (nd.flags & 1) ? ka : kb;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  int o0 = nd.begin, o1 = o0 + cnt.x, o2 = o1 + cnt.y, o3 = o2 + cnt.z;
+  for (int i0 = 0; i0 < nd.count; i0 += 64) {
+    const int i = i0 + lane_id();
+    uint32_t key = 0;
+    int ch = -1;
+    if (i < nd.count) {
+      key = src[nd.begin + i];
+      ch = child_of(key, mx, my);
+    }
+    const uint64_t b0 = wave_ballot(ch == 0), b1 = wave_ballot(ch == 1), b2 = wave_ballot(ch == 2),
+                   b3 = wave_ballot(ch == 3);
+    if (ch == 0) dst[o0 + prefix_in_wave(b0)] = key;
+    if (ch == 1) dst[o1 + prefix_in_wave(b1)] = key;
+    if (ch == 2) dst[o2 + prefix_in_wave(b2)] = key;
+    if (ch == 3) dst[o3 + prefix_in_wave(b3)] = key;
+    o0 += __popcll(b0);
+    o1 += __popcll(b1);
+    o2 += __popcll(b2);
+    o3 += __popcll(b3);
+  }
+}
+
+__device__ __forceinline__ ONode make_child(const ONode& p, int c, int begin, int count, int seq) {
+  const int mx = p.x0 + ((p.x1 - p.x0 + 1) >> 1), my = p.y0 + ((p.y1 - p.y0 + 1) >> 1);
+  ONode n;
+  n.x0 = (int16_t)((c & 1) ? mx : p.x0);
+  n.x1 = (int16_t)((c & 1) ? p.x1 : mx);
+  n.y0 = (int16_t)((c & 2) ? my : p.y0);
+  n.y1 = (int16_t)((c & 2) ? p.y1 : my);
+  n.begin = begin;
+  n.count = count;
+  n.seq = seq;
+  n.flags = ((p.flags & 1) ^ 1) | (count > 1 ? 2 : 0);
+  return n;
+}
+
+__device__ __forceinline__ int nonempty4(int4 c) {
+  return (c.x > 0) + (c.y > 0) + (c.z > 0) + (c.w > 0);
+}
+__device__ __forceinline__ int multi4(int4 c) {
+  return (c.x > 1) + (c.y > 1) + (c.z > 1) + (c.w > 1);
+}
+__device__ __forceinline__ int comp4(int4 c, int k) {
+  return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
+}
+
+__global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int l = blockIdx.x, img = blockIdx.y;
+  const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+  const int NC = a.node_cap, SC = a.sort_cap;
+  ONode* nodes0 = reinterpret_cast<ONode*>(smem);
+  ONode* nodes1 = nodes0 + NC;
+  int4* cc = reinterpret_cast<int4*>(nodes1 + NC);
+  int* sa = reinterpret_cast<int*>(cc + NC);
+  int* sb = sa + NC;
+  int* sx = sb + NC;
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(sx + NC);
+  int* misc = reinterpret_cast<int*>(sk + SC);  // [0..3] scan wave sums, [8..] scalars
+
+  const LevelDesc ld = a.levels[l];
+  const int N = ld.budget;
+  uint32_t* ka = a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin;
+  uint32_t* kb = a.keys_b + (long long)img * a.keyscr_stride + ld.cand_begin;
+  const uint32_t* cand = a.cand + (long long)img * a.cand_stride;
+  const int32_t* ccount = a.cellcnt + (long long)img * a.ncells + ld.cell_begin;
+  uint32_t* out = a.lvlkeys + (long long)img * a.lvlkey_stride + ld.key_begin;
+  int32_t* out_n = a.lvlcnt + (long long)img * a.nlevels + l;
+
+  // 1. gather this level's FAST candidates in cell order (ComputeKeyPointsOctTree :821-829)
+  for (int c = t; c < ld.ncells; c += 256) sa[c] = ccount[c];
+  __syncthreads();
+  const int n = block_scan_excl(sa, ld.ncells, misc);
+  for (int c = w; c < ld.ncells; c += 4) {
+    const int k = ccount[c];
+    const int slot = a.cells[ld.cell_begin + c].slot;
+    for (int i = lane; i < k; i += 64) ka[sa[c] + i] = cand[slot + i];
+  }
+  __syncthreads();
+  if (n == 0) {
+    if (t == 0) *out_n = 0;
+    return;
+  }
+
+  // 2. initial nodes (:555-588): key -> vpIniNodes[(size_t)(x / hX)], then drop empty nodes
+  const int nini = ld.nini;
+  const float hx = ld.hx;
+  if (w == 0) {
+    int run = 0;
+    for (int b = 0; b < nini; b++) {
+      int cnt = 0;
+      for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        bool in = false;
+        uint32_t key = 0;
+        if (i < n) {
+          key = ka[i];
+          in = (int)((float)key_x(key) / hx) == b;
+        }
+        const uint64_t bal = wave_ballot(in);
+        if (in) kb[run + cnt + prefix_in_wave(bal)] = key;
+        cnt += __popcll(bal);
+      }
+      if (lane == 0) sb[b] = cnt;
+      run += cnt;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    int S = 0, run = 0;
+    for (int b = 0; b < nini; b++) {
+      const int cnt = sb[b];
+      if (cnt > 0) {
+        ONode nd;
+        nd.x0 = (int16_t)(int)(hx * (float)b);
+        nd.x1 = (int16_t)(int)(hx * (float)(b + 1));
+        nd.y0 = 0;
+        nd.y1 = (int16_t)ld.rel_h;
+        nd.begin = run;
+        nd.count = cnt;
+        nd.seq = b;
+        nd.flags = 1;  // keys in buffer B
+        nodes0[S++] = nd;
+      }
+      run += cnt;
+    }
+    misc[8] = S;
+  }
+  __syncthreads();
+
+  int S = misc[8];
+  int cur = 0;
+  bool refine = false;
+  for (int iter = 0; iter < 4 * NC + 64; iter++) {
+    ONode* Lc = cur ? nodes1 : nodes0;
+    ONode* Ln = cur ? nodes0 : nodes1;
+    const int prevS = S;
+    if (!refine) {
+      // ---- full pass (:603-668) ----
+      for (int i = w; i < S; i += 4) {
+        const ONode nd = Lc[i];
+        if (nd.count > 1) {
+          const int4 c4 = wave_child_counts(nd, ka, kb);
+          wave_child_partition(nd, c4, ka, kb);
+          if (lane == 0) cc[i] = c4;
+        }
+      }
+      __syncthreads();
+      for (int i = t; i < S; i += 256) {
+        const bool par = Lc[i].count > 1;
+        const int4 c4 = par ? cc[i] : make_int4(0, 0, 0, 0);
+        sa[i] = par ? nonempty4(c4) : 0;
+        sb[i] = par ? 0 : 1;
+        sx[i] = par ? multi4(c4) : 0;
+      }
+      __syncthreads();
+      const int T = block_scan_excl(sa, S, misc);
+      const int NP = block_scan_excl(sb, S, misc);
+      const int nexp = block_scan_excl(sx, S, misc);
+      for (int i = t; i < S; i += 256) {
+        const ONode nd = Lc[i];
+        if (nd.count > 1) {
+          const int4 c4 = cc[i];
+          int e = sa[i], off = nd.begin;
+          for (int k = 0; k < 4; k++) {
+            const int ck = comp4(c4, k);
+            if (ck > 0) {
+              Ln[T - 1 - e] = make_child(nd, k, off, ck, e);
+              e++;
+            }
+            off += ck;
+          }
+        } else {
+          ONode m = nd;
+          m.flags &= 1;
+          Ln[T + sb[i]] = m;
+        }
+      }
+      S = T + NP;
+      cur ^= 1;
+      __syncthreads();
+      if (S >= N || S == prevS) break;
+      if (S + nexp * 3 > N) refine = true;
+    } else {
+      // ---- refinement round (:679-740) ----
+      for (int i = t; i < S; i += 256) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
+      __syncthreads();
+      const int nR = block_scan_excl(sa, S, misc);
+      int P2 = 1;
+      while (P2 < nR) P2 <<= 1;
+      for (int i = t; i < P2; i += 256) sk[i] = 0ull;
+      __syncthreads();
+      for (int i = t; i < S; i += 256) {
+        const ONode nd = Lc[i];
+        if (nd.flags & 2)
+          sk[sa[i]] = ((unsigned long long)nd.count << 40) | ((unsigned long long)nd.seq << 20) |
+                      (unsigned long long)i;
+      }
+      __syncthreads();
+      // bitonic sort, descending: largest (size, creation) first
+      for (int k = 2; k <= P2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = t; i < P2; i += 256) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const unsigned long long x = sk[i], y = sk[ixj];
+              const bool sw = (i & k) == 0 ? (x < y) : (x > y);
+              if (sw) {
+                sk[i] = y;
+                sk[ixj] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // child counts of every candidate, in processing order
+      for (int k = w; k < nR; k += 4) {
+        const int i = (int)(sk[k] & 0xfffffull);
+        const int4 c4 = wave_child_counts(Lc[i], ka, kb);
+        if (lane == 0) cc[k] = c4;
+      }
+      __syncthreads();
+      for (int k = t; k < nR; k += 256) sa[k] = nonempty4(cc[k]) - 1;
+      if (t == 0) misc[9] = nR;
+      __syncthreads();
+      block_scan_excl(sa, nR, misc);
+      for (int k = t; k < nR; k += 256) {
+        const int incl = sa[k] + nonempty4(cc[k]) - 1;
+        if (prevS + incl >= N) atomicMin(&misc[9], k + 1);  // break at the first k reaching N
+      }
+      __syncthreads();
+      const int nproc = misc[9];
+      for (int i = t; i < S; i += 256) sb[i] = -1;
+      __syncthreads();
+      for (int k = t; k < nproc; k += 256) sb[(int)(sk[k] & 0xfffffull)] = k;
+      __syncthreads();
+      // partition the divided nodes' keys
+      for (int k = w; k < nproc; k += 4) {
+        const int i = (int)(sk[k] & 0xfffffull);
+        wave_child_partition(Lc[i], cc[k], ka, kb);
+      }
+      for (int k = t; k < nR; k += 256) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
+      __syncthreads();
+      const int T = block_scan_excl(sx, nR, misc);
+      for (int i = t; i < S; i += 256) sa[i] = sb[i] < 0 ? 1 : 0;
+      __syncthreads();
+      const int NK = block_scan_excl(sa, S, misc);
+      for (int i = t; i < S; i += 256) {
+        const ONode nd = Lc[i];
+        const int k = sb[i];
+        if (k >= 0) {
+          const int4 c4 = cc[k];
+          int e = sx[k], off = nd.begin;
+          for (int c = 0; c < 4; c++) {
+            const int ck = comp4(c4, c);
+            if (ck > 0) {
+              Ln[T - 1 - e] = make_child(nd, c, off, ck, e);
+              e++;
+            }
+            off += ck;
+          }
+        } else {
+          ONode m = nd;
+          m.flags &= 1;
+          Ln[T + sa[i]] = m;
+        }
+      }
+      S = T + NK;
+      cur ^= 1;
+      __syncthreads();
+      if (S >= N || S == prevS) break;
+    }
+  }
+
+  // 3. retain the best key of every node, in list order (:744-763; strict '>' keeps the first)
+  ONode* Lf = cur ? nodes1 : nodes0;
+  for (int i = t; i < S; i += 256) {
+    const ONode nd = Lf[i];
+    const uint32_t* src = (nd.flags & 1) ? kb : ka;
+    uint32_t best = src[nd.begin];
+    for (int k = 1; k < nd.count; k++) {
+      const uint32_t key = src[nd.begin + k];
+      if (key_s(key) > key_s(best)) best = key;
+    }
+    // back to level coordinates: pt += (minBorderX, minBorderY) (:846-847)
+    out[i] = pack_key(key_x(best) + 16, key_y(best) + 16, key_s(best));
+  }
+  if (t == 0) *out_n = S;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_describe: one wavefront per surviving keypoint.
+#define PATCH_R 21  // 18 (max |rotated pattern offset|) + 3 (blur half-width)
+#define PATCH_N (2 * PATCH_R + 1)  // 43
+#define PATCH_S 44
+#define BLUR_N 37
+#define BLUR_S 40
+__device__ __forceinline__ int reflect101(int i, int n) {
+  return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
+}
+
+__global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][PATCH_N * PATCH_S];
+  __shared__ __attribute__((aligned(16))) uint16_t s_h[4][PATCH_N * BLUR_N];
+  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][BLUR_N * BLUR_S];
+  const int w = wave_id(), lane = lane_id();
+  const int img = blockIdx.y;
+  const int slot = blockIdx.x * 4 + w;
+  const int32_t* lc = a.lvlcnt + (long long)img * a.nlevels;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int tot = 0;
+    for (int l = 0; l < a.nlevels; l++) tot += lc[l];
+    a.out_counts[img] = tot;
+  }
+  if (slot >= a.total_key_slots) return;
+  int l = 0;
+  while (l + 1 < a.nlevels && slot >= a.levels[l + 1].key_begin) l++;
+  const LevelDesc ld = a.levels[l];
+  const int idx = slot - ld.key_begin;
+  if (idx >= lc[l]) return;
+  int obase = idx;
+  for (int k = 0; k < l; k++) obase += lc[k];
+  const uint32_t key = a.lvlkeys[(long long)img * a.lvlkey_stride + slot];
+  const int cx = key_x(key), cy = key_y(key), score = key_s(key);
+  int pitch;
+  const uint8_t* lev = level_ptr(a, ld, img, l, pitch);
+  uint8_t* raw = s_raw[w];
+  uint16_t* hb = s_h[w];
+  uint8_t* bl = s_blur[w];
+  for (int i = lane; i < PATCH_N * PATCH_N; i += 64) {
+    const int r = i / PATCH_N, c = i - r * PATCH_N;
+    const int y = reflect101(cy - PATCH_R + r, ld.h), x = reflect101(cx - PATCH_R + c, ld.w);
+    raw[r * PATCH_S + c] = lev[(long long)y * pitch + x];
+  }
+  wave_sync();
+  // IC_Angle (:75-102): integer moments over the umax circle of the unblurred level
+  int m01 = 0, m10 = 0;
+  for (int i = lane; i < 31 * 31; i += 64) {
+    const int v = i / 31 - 15, u = i - (i / 31) * 31 - 15;
+    if (abs(u) <= a.umax[abs(v)]) {
+      const int val = raw[(PATCH_R + v) * PATCH_S + PATCH_R + u];
+      m10 += u * val;
+      m01 += v * val;
+    }
+  }
+  m01 = wave_sum(m01);
+  m10 = wave_sum(m10);
+  const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
+  // GaussianBlur 7x7 sigma 2, fixed point (taps 18,34,49,54,49,34,18 / 256), REFLECT_101 through
+  // the reflected patch load
+  for (int i = lane; i < PATCH_N * BLUR_N; i += 64) {
+    const int r = i / BLUR_N, c = i - r * BLUR_N;
+    const uint8_t* p = raw + r * PATCH_S + c;
+    hb[i] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 54 * p[3]);
+  }
+  wave_sync();
+  for (int i = lane; i < BLUR_N * BLUR_N; i += 64) {
+    const int r = i / BLUR_N, c = i - r * BLUR_N;
+    const uint16_t* p = hb + r * BLUR_N + c;
+    const uint32_t acc = 18u * ((uint32_t)p[0] + p[6 * BLUR_N]) +
+                         34u * ((uint32_t)p[BLUR_N] + p[5 * BLUR_N]) +
+                         49u * ((uint32_t)p[2 * BLUR_N] + p[4 * BLUR_N]) + 54u * p[3 * BLUR_N];
+    bl[r * BLUR_S + c] = (uint8_t)min((acc + 32768u) >> 16, 255u);
+  }
+  wave_sync();
+  // computeOrbDescriptor (:105-151): 256 intensity tests on the rotated pattern
+  const float ang = angle * a.factor_pi;
+  const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+  const uint8_t* center = bl + 18 * BLUR_S + 18;
+  uint64_t words[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int p = q * 64 + lane;
+    const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
+    const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
+    const int t0 = center[cv_round_f(x0 * sb + y0 * ca) * BLUR_S + cv_round_f(x0 * ca - y0 * sb)];
+    const int t1 = center[cv_round_f(x1 * sb + y1 * ca) * BLUR_S + cv_round_f(x1 * ca - y1 * sb)];
+    words[q] = wave_ballot(t0 < t1);
+  }
+  const long long o = (long long)img * a.out_cap + obase;
+  if (lane < 4) {
+    uint64_t* d = reinterpret_cast<uint64_t*>(a.out_desc + o * 32);
+    d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+  }
+  if (lane == 0) {
+    orbfe_keypoint kp;
+    kp.x = (float)cx;
+    kp.y = (float)cy;
+    if (l != 0) {
+      kp.x *= ld.scale;
+      kp.y *= ld.scale;
+    }
+    kp.size = (float)ld.size;
+    kp.angle = angle;
+    kp.response = (float)score;
+    kp.octave = l;
+    kp.class_id = -1;
+    a.out_kps[o] = kp;
+  }
+}
+
+// =============================================================================================
+// host side
+namespace {
+
+inline int h_round(float v) { return (int)std::lrintf(v); }
+inline int h_floor(float v) { int i = (int)v; return i - (i > v); }
+inline short h_sat_short(float v) {
+  int i = h_round(v);
+  return (short)std::min(std::max(i, -32768), 32767);
+}
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct KernelTimer {
+  int kernel;
+  hipEvent_t e0, e1;
+};
+
+}  // namespace
+
+struct orbfe_extractor {
+  int device = 0;
+  int nfeatures, nlevels, ini_th, min_th;
+  double scale_factor;
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+  std::vector<int> nfeat;
+  int umax[16];
+  int resize_mode = ORBFE_RESIZE_SIMD128;
+  hipStream_t stream = nullptr;
+  // geometry
+  int rows = -1, cols = -1, geom_mode = -1;
+  std::vector<LevelDesc> levels;
+  std::vector<CellDesc> cells;
+  std::vector<int2> xtab, ytab;
+  long long pyr_stride = 0, cand_stride = 0, keyscr_stride = 0, lvlkey_stride = 0;
+  int total_key_slots = 0, roi_w_max = 0, roi_h_max = 0, node_cap = 0, sort_cap = 0;
+  LevelDesc* d_levels = nullptr;
+  CellDesc* d_cells = nullptr;
+  int2* d_xtab = nullptr;
+  int2* d_ytab = nullptr;
+  // batch buffers
+  int batch_cap = 0;
+  uint8_t* d_in = nullptr;
+  size_t in_bytes = 0;
+  uint8_t* d_pyr = nullptr;
+  uint32_t* d_cand = nullptr;
+  int32_t* d_cellcnt = nullptr;
+  uint32_t* d_keys_a = nullptr;
+  uint32_t* d_keys_b = nullptr;
+  uint32_t* d_lvlkeys = nullptr;
+  int32_t* d_lvlcnt = nullptr;
+  orbfe_keypoint* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  int32_t* d_counts = nullptr;
+  size_t out_cap_alloc = 0;
+  // last call (for get_level)
+  const uint8_t* last_img0 = nullptr;
+  long long last_img_stride = 0;
+  int last_img_pitch = 0, last_n = 0;
+  std::vector<uint8_t> level_host;
+  // profiling
+  bool profiling = false;
+  std::vector<KernelTimer> pending;
+  std::vector<hipEvent_t> event_pool;
+  double ktime[8] = {0};
+  int klaunch[8] = {0};
+};
+
+static const char* kKernelNames[] = {"k_resize", "k_fast", "k_octree", "k_describe"};
+static const int kNumKernels = 4;
+
+static hipEvent_t pool_event(orbfe_extractor* h) {
+  if (!h->event_pool.empty()) {
+    hipEvent_t e = h->event_pool.back();
+    h->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
+  if (h->rows == rows && h->cols == cols && h->geom_mode == h->resize_mode) return ORBFE_OK;
+  const int L = h->nlevels;
+  std::vector<LevelDesc> lv(L);
+  std::vector<CellDesc> cells;
+  std::vector<int2> xt, yt;
+  long long pyr = 0;
+  int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0;
+  for (int l = 0; l < L; l++) {
+    LevelDesc& d = lv[l];
+    std::memset(&d, 0, sizeof(d));
+    d.w = h_round((float)cols * h->inv_scale[l]);
+    d.h = h_round((float)rows * h->inv_scale[l]);
+    const int minB = 16, maxBX = d.w - 16, maxBY = d.h - 16;  // EDGE_THRESHOLD - 3
+    const int bw = maxBX - minB, bh = maxBY - minB;
+    if (bw < 30 || bh < 30)
+      return orbfe_set_error(ORBFE_ERR_ARG, "image too small for the pyramid: a level has < 62 px");
+    d.nini = (int)std::round((float)bw / bh);
+    if (d.nini < 1 || d.nini > 64)
+      return orbfe_set_error(ORBFE_ERR_ARG, "unsupported aspect ratio (DistributeOctTree nIni)");
+    d.hx = (float)bw / d.nini;
+    d.rel_w = bw;
+    d.rel_h = bh;
+    d.budget = h->nfeat[l];
+    d.scale = h->scale[l];
+    d.size = (int)(31 * h->scale[l]);
+    if (l > 0) {
+      d.pitch = (int)align_up(d.w, 64);
+      d.pyr_off = pyr;
+      pyr += (long long)d.pitch * d.h;
+    }
+    // cells (:776-832)
+    const float width = (float)bw, height = (float)bh;
+    const int nColsC = (int)(width / 30.f), nRowsC = (int)(height / 30.f);
+    const int wCell = (int)std::ceil(width / nColsC), hCell = (int)std::ceil(height / nRowsC);
+    d.cell_begin = (int)cells.size();
+    d.cand_begin = cand;
+    for (int i = 0; i < nRowsC; i++) {
+      const float iniY = (float)(minB + i * hCell);
+      float maxY = iniY + hCell + 6;
+      if (iniY >= maxBY - 3) continue;
+      if (maxY > maxBY) maxY = (float)maxBY;
+      for (int j = 0; j < nColsC; j++) {
+        const float iniX = (float)(minB + j * wCell);
+        float maxX = iniX + wCell + 6;
+        if (iniX >= maxBX - 6) continue;
+        if (maxX > maxBX) maxX = (float)maxBX;
+        CellDesc c;
+        std::memset(&c, 0, sizeof(c));
+        c.level = (int16_t)l;
+        c.x0 = (int16_t)(int)iniX;
+        c.y0 = (int16_t)(int)iniY;
+        c.rw = (int16_t)((int)maxX - (int)iniX);
+        c.rh = (int16_t)((int)maxY - (int)iniY);
+        c.ox = (int16_t)(j * wCell);
+        c.oy = (int16_t)(i * hCell);
+        const int dw = c.rw - 6, dh = c.rh - 6;
+        c.cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
+        c.slot = cand;
+        cand += c.cap;
+        rwmax = std::max(rwmax, (int)c.rw);
+        rhmax = std::max(rhmax, (int)c.rh);
+        cells.push_back(c);
+      }
+    }
+    d.ncells = (int)cells.size() - d.cell_begin;
+    d.cand_cap = cand - d.cand_begin;
+    d.key_begin = keys;
+    d.key_cap = std::max(d.budget + 3, 4 * d.nini);
+    keys += d.key_cap;
+    ncap = std::max(ncap, d.key_cap + 4);
+    // resize tables (OpenCV resize(), INTER_LINEAR, fixed point)
+    if (l > 0) {
+      const LevelDesc& s = lv[l - 1];
+      const double inv_sx = (double)d.w / s.w, inv_sy = (double)d.h / s.h;
+      const double scx = 1. / inv_sx, scy = 1. / inv_sy;
+      d.tab_x = (int)xt.size();
+      d.tab_y = (int)yt.size();
+      int xmax = d.w;
+      for (int dx = 0; dx < d.w; dx++) {
+        float fx = (float)((dx + 0.5) * scx - 0.5);
+        int sx = h_floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx + 1 >= s.w) {
+          xmax = std::min(xmax, dx);
+          if (sx >= s.w - 1) { fx = 0.f; sx = s.w - 1; }
+        }
+        const short a0 = h_sat_short((1.f - fx) * 2048.f), a1 = h_sat_short(fx * 2048.f);
+        xt.push_back(make_int2(sx, (int)(((unsigned)(unsigned short)a1 << 16) | (unsigned short)a0)));
+      }
+      for (int dy = 0; dy < d.h; dy++) {
+        float fy = (float)((dy + 0.5) * scy - 0.5);
+        int sy = h_floor(fy);
+        fy -= sy;
+        const short b0 = h_sat_short((1.f - fy) * 2048.f), b1 = h_sat_short(fy * 2048.f);
+        yt.push_back(make_int2(sy, (int)(((unsigned)(unsigned short)b1 << 16) | (unsigned short)b0)));
+      }
+      d.xmax = xmax;
+      int se = 0;
+      if (h->resize_mode == ORBFE_RESIZE_SIMD128) {
+        se = 16 * (d.w / 16);
+        if (se < d.w - 8) se += 8;
+      }
+      d.simd_end = se;
+    }
+  }
+  // release old geometry buffers and upload new ones
+  hipSetDevice(h->device);
+  hipFree(h->d_levels);
+  hipFree(h->d_cells);
+  hipFree(h->d_xtab);
+  hipFree(h->d_ytab);
+  h->d_levels = nullptr;
+  h->d_cells = nullptr;
+  h->d_xtab = h->d_ytab = nullptr;
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_levels, sizeof(LevelDesc) * L));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_cells, sizeof(CellDesc) * std::max<size_t>(cells.size(), 1)));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_xtab, sizeof(int2) * std::max<size_t>(xt.size(), 1)));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_ytab, sizeof(int2) * std::max<size_t>(yt.size(), 1)));
+  ORBFE_HIP_CHECK(hipMemcpy(h->d_levels, lv.data(), sizeof(LevelDesc) * L, hipMemcpyHostToDevice));
+  if (!cells.empty())
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_cells, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
+  if (!xt.empty())
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice));
+  if (!yt.empty())
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice));
+  h->levels = lv;
+  h->cells = cells;
+  h->xtab = xt;
+  h->ytab = yt;
+  h->pyr_stride = (long long)align_up((size_t)std::max<long long>(pyr, 64), 256);
+  h->cand_stride = (long long)align_up((size_t)std::max(cand, 1), 64);
+  h->keyscr_stride = h->cand_stride;
+  h->lvlkey_stride = (long long)align_up((size_t)keys, 64);
+  h->total_key_slots = keys;
+  h->roi_w_max = rwmax;
+  h->roi_h_max = rhmax;
+  h->node_cap = ncap;
+  int sc = 1;
+  while (sc < ncap) sc <<= 1;
+  h->sort_cap = sc;
+  h->rows = rows;
+  h->cols = cols;
+  h->geom_mode = h->resize_mode;
+  h->batch_cap = 0;  // strides changed: reallocate batch buffers on the next call
+  return ORBFE_OK;
+}
+
+static void free_batch(orbfe_extractor* h) {
+  hipFree(h->d_pyr);
+  hipFree(h->d_cand);
+  hipFree(h->d_cellcnt);
+  hipFree(h->d_keys_a);
+  hipFree(h->d_keys_b);
+  hipFree(h->d_lvlkeys);
+  hipFree(h->d_lvlcnt);
+  h->d_pyr = nullptr;
+  h->d_cand = nullptr;
+  h->d_cellcnt = nullptr;
+  h->d_keys_a = h->d_keys_b = nullptr;
+  h->d_lvlkeys = nullptr;
+  h->d_lvlcnt = nullptr;
+  h->batch_cap = 0;
+}
+
+static int ensure_batch(orbfe_extractor* h, int n) {
+  if (n <= h->batch_cap) return ORBFE_OK;
+  free_batch(h);
+  const int cap = std::max(n, 1);
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_pyr, (size_t)h->pyr_stride * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_cand, (size_t)h->cand_stride * 4 * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_cellcnt, sizeof(int32_t) * h->cells.size() * cap + 4));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_keys_a, (size_t)h->keyscr_stride * 4 * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_keys_b, (size_t)h->keyscr_stride * 4 * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_lvlkeys, (size_t)h->lvlkey_stride * 4 * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_lvlcnt, sizeof(int32_t) * h->nlevels * cap));
+  h->batch_cap = cap;
+  return ORBFE_OK;
+}
+
+static size_t octree_lds(const orbfe_extractor* h) {
+  return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->node_cap +
+         sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16;
+}
+static size_t fast_lds(const orbfe_extractor* h) {
+  const size_t roi = align_up((size_t)h->roi_w_max * h->roi_h_max, 16);
+  const size_t m = align_up((size_t)(h->roi_w_max - 4) * (h->roi_h_max - 4), 16);
+  return 4 * (roi + m);
+}
+
+#define LAUNCH_TIMED(h, kid, stream, ...)                          \
+  do {                                                             \
+    hipEvent_t _e0 = nullptr, _e1 = nullptr;                       \
+    if ((h)->profiling) {                                          \
+      _e0 = pool_event(h);                                         \
+      _e1 = pool_event(h);                                         \
+      hipEventRecord(_e0, stream);                                 \
+    }                                                              \
+    __VA_ARGS__;                                                   \
+    if ((h)->profiling) {                                          \
+      hipEventRecord(_e1, stream);                                 \
+      (h)->pending.push_back(KernelTimer{kid, _e0, _e1});          \
+    }                                                              \
+  } while (0)
+
+static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long long img_stride,
+                          int pitch, orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
+                          int32_t* d_counts, hipStream_t st) {
+  ExtractArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.levels = h->d_levels;
+  a.cells = h->d_cells;
+  a.xtab = h->d_xtab;
+  a.ytab = h->d_ytab;
+  a.nlevels = h->nlevels;
+  a.ncells = (int)h->cells.size();
+  a.n_images = n;
+  a.total_key_slots = h->total_key_slots;
+  a.img0 = d_imgs;
+  a.img_stride = img_stride;
+  a.img_pitch = pitch;
+  a.pyr = h->d_pyr;
+  a.pyr_stride = h->pyr_stride;
+  a.cand = h->d_cand;
+  a.cand_stride = h->cand_stride;
+  a.cellcnt = h->d_cellcnt;
+  a.keys_a = h->d_keys_a;
+  a.keys_b = h->d_keys_b;
+  a.keyscr_stride = h->keyscr_stride;
+  a.lvlkeys = h->d_lvlkeys;
+  a.lvlkey_stride = h->lvlkey_stride;
+  a.lvlcnt = h->d_lvlcnt;
+  a.out_kps = d_kps;
+  a.out_desc = d_desc;
+  a.out_counts = d_counts;
+  a.out_cap = cap;
+  a.ini_th = h->ini_th;
+  a.min_th = h->min_th;
+  a.tlow = std::min(std::min(std::max(h->ini_th, 0), 255), std::min(std::max(h->min_th, 0), 255));
+  a.roi_w_max = h->roi_w_max;
+  a.roi_h_max = h->roi_h_max;
+  a.node_cap = h->node_cap;
+  a.sort_cap = h->sort_cap;
+  for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
+  a.atan.p1 = 0.9997878412794807f * (float)(180 / M_PI);
+  a.atan.p3 = -0.3258083974640975f * (float)(180 / M_PI);
+  a.atan.p5 = 0.1555786518463281f * (float)(180 / M_PI);
+  a.atan.p7 = -0.04432655554792128f * (float)(180 / M_PI);
+  a.atan.eps = (float)DBL_EPSILON;
+  a.factor_pi = (float)(M_PI / 180.f);
+
+  for (int l = 1; l < h->nlevels; l++) {
+    const LevelDesc& d = h->levels[l];
+    dim3 grid((d.w + 63) / 64, (d.h + 3) / 4, n), block(64, 4);
+    LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+  }
+  {
+    dim3 grid((a.ncells + 3) / 4, n);
+    LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast, grid, dim3(256), fast_lds(h), st, a));
+  }
+  {
+    dim3 grid(h->nlevels, n);
+    LAUNCH_TIMED(h, 2, st, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), st, a));
+  }
+  {
+    dim3 grid((h->total_key_slots + 3) / 4, n);
+    LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, a));
+  }
+  ORBFE_HIP_CHECK(hipGetLastError());
+  h->last_img0 = d_imgs;
+  h->last_img_stride = img_stride;
+  h->last_img_pitch = pitch;
+  h->last_n = n;
+  return ORBFE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nlevels,
+                                      int ini_th_fast, int min_th_fast, int device,
+                                      orbfe_extractor** out) {
+  if (!out || nfeatures <= 0 || nlevels <= 0 || nlevels > 32 || !(scale_factor > 1.0f))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extractor_create: bad argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: no HIP device");
+  if (device < 0 || device >= ndev) return orbfe_set_error(ORBFE_ERR_ARG, "bad device index");
+  orbfe_extractor* h = new orbfe_extractor();
+  h->device = device;
+  h->nfeatures = nfeatures;
+  h->nlevels = nlevels;
+  h->ini_th = ini_th_fast;
+  h->min_th = min_th_fast;
+  // ORBextractor::ORBextractor (ORBextractor.cc:413-473); scaleFactor is a double member
+  h->scale_factor = (double)scale_factor;
+  h->scale.assign(nlevels, 1.0f);
+  h->sigma2.assign(nlevels, 1.0f);
+  for (int i = 1; i < nlevels; i++) {
+    h->scale[i] = (float)((double)h->scale[i - 1] * h->scale_factor);
+    h->sigma2[i] = h->scale[i] * h->scale[i];
+  }
+  h->inv_scale.resize(nlevels);
+  h->inv_sigma2.resize(nlevels);
+  for (int i = 0; i < nlevels; i++) {
+    h->inv_scale[i] = 1.0f / h->scale[i];
+    h->inv_sigma2[i] = 1.0f / h->sigma2[i];
+  }
+  h->nfeat.resize(nlevels);
+  const float factor = (float)(1.0 / h->scale_factor);
+  float nd = (float)nfeatures * (1.0f - factor) / (1.0f - (float)std::pow((double)factor, (double)nlevels));
+  int sum = 0;
+  for (int l = 0; l < nlevels - 1; l++) {
+    h->nfeat[l] = h_round(nd);
+    sum += h->nfeat[l];
+    nd *= factor;
+  }
+  h->nfeat[nlevels - 1] = std::max(nfeatures - sum, 0);
+  int v, v0, vmax = h_floor(15 * std::sqrt(2.f) / 2 + 1);
+  const float vminf = 15 * std::sqrt(2.f) / 2;
+  int vmin = (int)vminf;
+  vmin += (vmin < vminf);
+  for (v = 0; v <= vmax; ++v) h->umax[v] = (int)std::lrint(std::sqrt(225.0 - v * v));
+  for (v = 15, v0 = 0; v >= vmin; --v) {
+    while (h->umax[v0] == h->umax[v0 + 1]) ++v0;
+    h->umax[v] = v0;
+    ++v0;
+  }
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: stream creation failed");
+  }
+  static std::once_flag once;
+  static hipError_t pat_err = hipSuccess;
+  std::call_once(once, [] { pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, 1024); });
+  if (pat_err != hipSuccess) {
+    delete h;
+    return orbfe_set_hip_error(pat_err, "upload pattern");
+  }
+  *out = h;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
+  if (!h) return ORBFE_OK;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  free_batch(h);
+  hipFree(h->d_levels);
+  hipFree(h->d_cells);
+  hipFree(h->d_xtab);
+  hipFree(h->d_ytab);
+  hipFree(h->d_in);
+  hipFree(h->d_kps);
+  hipFree(h->d_desc);
+  hipFree(h->d_counts);
+  for (auto& p : h->pending) {
+    hipEventDestroy(p.e0);
+    hipEventDestroy(p.e1);
+  }
+  for (auto e : h->event_pool) hipEventDestroy(e);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_extractor_set_resize_mode(orbfe_extractor* h, int mode) {
+  if (!h || (mode != ORBFE_RESIZE_SIMD128 && mode != ORBFE_RESIZE_SCALAR)) return ORBFE_ERR_ARG;
+  h->resize_mode = mode;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_get_scale_tables(const orbfe_extractor* h, float* scale, float* inv_scale,
+                                      float* sigma2, float* inv_sigma2, int32_t* fpl) {
+  if (!h) return ORBFE_ERR_ARG;
+  for (int l = 0; l < h->nlevels; l++) {
+    if (scale) scale[l] = h->scale[l];
+    if (inv_scale) inv_scale[l] = h->inv_scale[l];
+    if (sigma2) sigma2[l] = h->sigma2[l];
+    if (inv_sigma2) inv_sigma2[l] = h->inv_sigma2[l];
+    if (fpl) fpl[l] = h->nfeat[l];
+  }
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_max_keypoints(orbfe_extractor* h, int rows, int cols) {
+  if (!h) return ORBFE_ERR_ARG;
+  hipSetDevice(h->device);
+  const int st = compute_geometry(h, rows, cols);
+  if (st != ORBFE_OK) return st;
+  return h->total_key_slots;
+}
+
+extern "C" void* orbfe_extractor_stream(orbfe_extractor* h) { return h ? (void*)h->stream : nullptr; }
+
+extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8_t* d_imgs,
+                                          size_t image_stride, int rows, int cols, size_t pitch,
+                                          orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
+                                          int32_t* d_counts, void* stream) {
+  if (!h || n < 0 || !d_imgs || !d_kps || !d_desc || !d_counts || rows <= 0 || cols <= 0 ||
+      pitch < (size_t)cols)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extract_batch_device: bad argument");
+  if (n == 0) return ORBFE_OK;
+  hipSetDevice(h->device);
+  int st = compute_geometry(h, rows, cols);
+  if (st != ORBFE_OK) return st;
+  if (cap < h->total_key_slots) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
+  st = ensure_batch(h, n);
+  if (st != ORBFE_OK) return st;
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  return launch_extract(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
+                        d_counts, s);
+}
+
+static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
+  const size_t need_in = (size_t)n * rows * cols;
+  if (need_in > h->in_bytes) {
+    hipFree(h->d_in);
+    h->d_in = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_in, need_in));
+    h->in_bytes = need_in;
+  }
+  const size_t need_out = (size_t)n * h->total_key_slots;
+  if (need_out > h->out_cap_alloc) {
+    hipFree(h->d_kps);
+    hipFree(h->d_desc);
+    hipFree(h->d_counts);
+    h->d_kps = nullptr;
+    h->d_desc = nullptr;
+    h->d_counts = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_kps, need_out * sizeof(orbfe_keypoint)));
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_desc, need_out * 32));
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_counts, sizeof(int32_t) * n));
+    h->out_cap_alloc = need_out;
+  }
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* const* imgs,
+                                   int rows, int cols, size_t step, orbfe_keypoint* kps,
+                                   uint8_t* desc, int cap, int32_t* counts) {
+  if (!h || n < 0 || !imgs || !counts) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extract_batch: bad argument");
+  if (n == 0) return ORBFE_OK;
+  if (rows == 0 || cols == 0) {  // empty image: operator() returns without output (:1044-1045)
+    for (int i = 0; i < n; i++) counts[i] = 0;
+    return ORBFE_OK;
+  }
+  if (rows < 0 || cols < 0 || step < (size_t)cols) return orbfe_set_error(ORBFE_ERR_ARG, "bad image shape");
+  hipSetDevice(h->device);
+  int st = compute_geometry(h, rows, cols);
+  if (st != ORBFE_OK) return st;
+  st = ensure_batch(h, n);
+  if (st != ORBFE_OK) return st;
+  st = ensure_host_io(h, n, rows, cols);
+  if (st != ORBFE_OK) return st;
+  const int K = h->total_key_slots;
+  for (int i = 0; i < n; i++) {
+    if (!imgs[i]) return orbfe_set_error(ORBFE_ERR_ARG, "null image");
+    ORBFE_HIP_CHECK(hipMemcpy2DAsync(h->d_in + (size_t)i * rows * cols, cols, imgs[i], step, cols,
+                                     rows, hipMemcpyHostToDevice, h->stream));
+  }
+  st = launch_extract(h, n, h->d_in, (long long)rows * cols, cols, h->d_kps, h->d_desc, K,
+                      h->d_counts, h->stream);
+  if (st != ORBFE_OK) return st;
+  std::vector<int32_t> cnt(n);
+  ORBFE_HIP_CHECK(hipMemcpyAsync(cnt.data(), h->d_counts, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  int need = 0;
+  for (int i = 0; i < n; i++) need = std::max(need, (int)cnt[i]);
+  for (int i = 0; i < n; i++) counts[i] = cnt[i];
+  if (need > cap) return orbfe_set_error(ORBFE_ERR_CAPACITY, "keypoint capacity too small");
+  if (need > 0 && (!kps || !desc)) return orbfe_set_error(ORBFE_ERR_ARG, "null output buffer");
+  for (int i = 0; i < n; i++) {
+    if (cnt[i] == 0) continue;
+    ORBFE_HIP_CHECK(hipMemcpyAsync(kps + (size_t)i * cap, h->d_kps + (size_t)i * K,
+                                   sizeof(orbfe_keypoint) * cnt[i], hipMemcpyDeviceToHost, h->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(desc + (size_t)i * cap * 32, h->d_desc + (size_t)i * K * 32,
+                                   (size_t)32 * cnt[i], hipMemcpyDeviceToHost, h->stream));
+  }
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_extract(orbfe_extractor* h, const uint8_t* img, int rows, int cols,
+                             size_t step, orbfe_keypoint* kps, int cap, uint8_t* desc, int* n) {
+  if (!n) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extract: n is NULL");
+  *n = 0;
+  if (rows == 0 || cols == 0) return ORBFE_OK;
+  int32_t cnt = 0;
+  const uint8_t* imgs[1] = {img};
+  const int st = orbfe_extract_batch(h, 1, imgs, rows, cols, step, kps, desc, cap, &cnt);
+  *n = cnt;
+  return st;
+}
+
+extern "C" int orbfe_get_level_device(orbfe_extractor* h, int image, int level,
+                                      const uint8_t** d_p, int* rows, int* cols, size_t* step) {
+  if (!h || !d_p || !rows || !cols || !step) return ORBFE_ERR_ARG;
+  if (!h->last_img0 || image < 0 || image >= h->last_n || level < 0 || level >= h->nlevels)
+    return orbfe_set_error(ORBFE_ERR_STATE, "orbfe_get_level: no such image/level in the last call");
+  const LevelDesc& d = h->levels[level];
+  *rows = d.h;
+  *cols = d.w;
+  if (level == 0) {
+    *d_p = h->last_img0 + (long long)image * h->last_img_stride;
+    *step = (size_t)h->last_img_pitch;
+  } else {
+    *d_p = h->d_pyr + (long long)image * h->pyr_stride + d.pyr_off;
+    *step = (size_t)d.pitch;
+  }
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p,
+                               int* rows, int* cols, size_t* step) {
+  const uint8_t* dp = nullptr;
+  size_t dstep = 0;
+  int st = orbfe_get_level_device(h, image, level, &dp, rows, cols, &dstep);
+  if (st != ORBFE_OK) return st;
+  h->level_host.resize((size_t)(*rows) * (*cols));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  ORBFE_HIP_CHECK(hipMemcpy2D(h->level_host.data(), *cols, dp, dstep, *cols, *rows, hipMemcpyDeviceToHost));
+  *p = h->level_host.data();
+  *step = (size_t)(*cols);
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_set_profiling(orbfe_extractor* h, int enable) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->profiling = enable != 0;
+  return ORBFE_OK;
+}
+
+static int drain_timers(orbfe_extractor* h) {
+  if (h->pending.empty()) return ORBFE_OK;
+  ORBFE_HIP_CHECK(hipEventSynchronize(h->pending.back().e1));
+  for (auto& p : h->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
+      h->ktime[p.kernel] += ms;
+      h->klaunch[p.kernel] += 1;
+    }
+    h->event_pool.push_back(p.e0);
+    h->event_pool.push_back(p.e1);
+  }
+  h->pending.clear();
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_get_kernel_times(orbfe_extractor* h, char* names, int name_len,
+                                      double* total_ms, int32_t* launches, int cap, int* n) {
+  if (!h || !n) return ORBFE_ERR_ARG;
+  const int st = drain_timers(h);
+  if (st != ORBFE_OK) return st;
+  *n = kNumKernels;
+  for (int k = 0; k < kNumKernels && k < cap; k++) {
+    if (names && name_len > 0) {
+      std::strncpy(names + (size_t)k * name_len, kKernelNames[k], name_len - 1);
+      names[(size_t)k * name_len + name_len - 1] = 0;
+    }
+    if (total_ms) total_ms[k] = h->ktime[k];
+    if (launches) launches[k] = h->klaunch[k];
+  }
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_reset_kernel_times(orbfe_extractor* h) {
+  if (!h) return ORBFE_ERR_ARG;
+  const int st = drain_timers(h);
+  for (int k = 0; k < 8; k++) {
+    h->ktime[k] = 0;
+    h->klaunch[k] = 0;
+  }
+  return st;
+}
+
+// ---------------------------------------------------------------------------------------------
+// stage inspection for per-stage parity tests (orbfe_debug.h)
+extern "C" int orbfe_debug_get_candidates(orbfe_extractor* h, int image, int level, uint32_t* out,
+                                          int cap, int* n) {
+  if (!h || !n || image < 0 || image >= h->last_n || level < 0 || level >= h->nlevels)
+    return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  const LevelDesc& d = h->levels[level];
+  std::vector<int32_t> cnt(d.ncells);
+  ORBFE_HIP_CHECK(hipMemcpy(cnt.data(), h->d_cellcnt + (size_t)image * h->cells.size() + d.cell_begin,
+                            sizeof(int32_t) * d.ncells, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> cand(d.cand_cap);
+  if (d.cand_cap)
+    ORBFE_HIP_CHECK(hipMemcpy(cand.data(), h->d_cand + (size_t)image * h->cand_stride + d.cand_begin,
+                              sizeof(uint32_t) * d.cand_cap, hipMemcpyDeviceToHost));
+  int tot = 0;
+  for (int c = 0; c < d.ncells; c++) {
+    const CellDesc& cd = h->cells[d.cell_begin + c];
+    for (int i = 0; i < cnt[c]; i++) {
+      if (out && tot < cap) out[tot] = cand[cd.slot - d.cand_begin + i];
+      tot++;
+    }
+  }
+  *n = tot;
+  return (out && tot > cap) ? ORBFE_ERR_CAPACITY : ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level,
+                                          uint32_t* out, int cap, int* n) {
+  if (!h || !n || image < 0 || image >= h->last_n || level < 0 || level >= h->nlevels)
+    return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  int32_t cnt = 0;
+  ORBFE_HIP_CHECK(hipMemcpy(&cnt, h->d_lvlcnt + (size_t)image * h->nlevels + level, sizeof(int32_t),
+                            hipMemcpyDeviceToHost));
+  *n = cnt;
+  if (!out) return ORBFE_OK;
+  if (cnt > cap) return ORBFE_ERR_CAPACITY;
+  if (cnt > 0)
+    ORBFE_HIP_CHECK(hipMemcpy(out, h->d_lvlkeys + (size_t)image * h->lvlkey_stride + h->levels[level].key_begin,
+                              sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, int cap) {
+  // per level: w, h, ncells, cand_cap, budget, nini, key_cap (7 ints)
+  if (!h || !info) return ORBFE_ERR_ARG;
+  hipSetDevice(h->device);
+  const int st = compute_geometry(h, rows, cols);
+  if (st != ORBFE_OK) return st;
+  if (cap < 7 * h->nlevels) return ORBFE_ERR_CAPACITY;
+  for (int l = 0; l < h->nlevels; l++) {
+    const LevelDesc& d = h->levels[l];
+    int32_t* o = info + 7 * l;
+    o[0] = d.w;
+    o[1] = d.h;
+    o[2] = d.ncells;
+    o[3] = d.cand_cap;
+    o[4] = d.budget;
+    o[5] = d.nini;
+    o[6] = d.key_cap;
+  }
+  return ORBFE_OK;
+}

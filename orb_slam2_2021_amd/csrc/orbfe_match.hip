@@ -1,0 +1,961 @@
+// orbfe_match.hip -- ORBmatcher's Hamming searches as CDNA4 kernels (gfx950, wave64).
+//
+// Reference: src/ORBmatcher.cc of lreithmayr/ORB_SLAM2_2021.
+//   SearchForTriangulation (:671-839): keypoints can only pair inside one vocabulary node and every
+//     feature sits in exactly one node, so nodes are independent. One wavefront owns a node: lanes
+//     hold the KF2 candidates, the KF1 features are walked in order (the reference's claim order,
+//     vbMatched2), and each step is one wave-wide min-reduction that returns the LAST candidate at
+//     the minimal distance (the reference updates on dist <= bestDist). One workgroup per KF pair;
+//     the rotation-consistency histogram (:806-826) runs after a workgroup barrier.
+//   SearchByProjection, local map (:45-133) and last frame (:1348-1491): a keypoint taken by an
+//     earlier MapPoint with Observations() > 0 is skipped by every later MapPoint. Solved as a
+//     parallel fixpoint: round r computes every MapPoint's match against the owners found in round
+//     r-1 (owner(k) = lowest MapPoint index claiming k); the first round whose results equal the
+//     previous round's is the reference's sequential result (proof in DESIGN.md). Rounds run
+//     back-to-back without host syncs; a serial kernel finishes the job if the round budget ran out.
+//   Frame::AssignFeaturesToGrid / GetFeaturesInArea (Frame.cc:279-294, 376-445): the 64x48 grid is
+//     rebuilt on the device as CSR (bitonic sort of cell<<16 | index keys), and candidates are
+//     visited in the reference's order (ix outer, iy inner, ascending index inside a cell).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "../../include/orbfe_match_batch.h"
+#include "orbfe_device.h"
+
+#define TH_HIGH 100
+#define TH_LOW 50
+#define HISTO_LENGTH 30
+#define GRID_COLS 64
+#define GRID_ROWS 48
+#define GRID_CELLS (GRID_COLS * GRID_ROWS)
+#define SBP_MAX_ROUNDS 12
+#define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
+#define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
+
+// ---------------------------------------------------------------------------------------------
+// shared helpers
+__device__ __forceinline__ int rot_bin_dev(float a1, float a2) {
+  // ORBmatcher.cc:781-786 (only bins 0..12 are reachable: round(rot * 1/30); kept as is)
+  const float factor = 1.0f / HISTO_LENGTH;
+  float rot = a1 - a2;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)roundf(rot * factor);
+  if (bin == HISTO_LENGTH) bin = 0;
+  return bin;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:1627-1668) on 30 counts
+__device__ void three_maxima_dev(const int* h, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  ind1 = ind2 = ind3 = -1;
+  for (int i = 0; i < HISTO_LENGTH; i++) {
+    const int s = h[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s; ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+  else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SearchForTriangulation
+__global__ __launch_bounds__(256) void k_sft(const orbfe_sft_pair* pairs, int only_stereo,
+                                             int check_ori) {
+  __shared__ uint32_t s_claim[SFT_MAX_KF2 / 32];
+  __shared__ int s_hist[HISTO_LENGTH];
+  __shared__ int s_misc[8];
+  const orbfe_sft_pair P = pairs[blockIdx.x];
+  const orbfe_frame_view& K1 = P.kf1;
+  const orbfe_frame_view& K2 = P.kf2;
+  const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+  const int nwords = (K2.n + 31) >> 5;
+  for (int i = t; i < K1.n; i += 256) P.match12[i] = -1;
+  for (int i = t; i < nwords; i += 256) s_claim[i] = 0;
+  if (t < HISTO_LENGTH) s_hist[t] = 0;
+  if (t == 0) s_misc[4] = 0;
+  __syncthreads();
+  const float* F = P.f12;
+  for (int a = w; a < P.fv1.n_nodes; a += 4) {
+    const uint32_t id = P.fv1.node_ids[a];
+    // lower_bound in fv2 (the merge-join visits exactly the common node ids, :705-804)
+    int lo = 0, hi = P.fv2.n_nodes;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (P.fv2.node_ids[mid] < id) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= P.fv2.n_nodes || P.fv2.node_ids[lo] != id) continue;
+    const int b = lo;
+    const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
+    const int o2 = P.fv2.offsets[b], n2 = P.fv2.offsets[b + 1] - o2;
+    for (int p1 = o1; p1 < e1; p1++) {
+      const int idx1 = P.fv1.indices[p1];
+      if (K1.mp_state[idx1] != ORBFE_MP_NONE) continue;
+      const bool st1 = K1.u_right[idx1] >= 0;
+      if (only_stereo && !st1) continue;
+      const orbfe_keypoint kp1 = K1.keys_un[idx1];
+      uint4 d10, d11;
+      load_desc(K1.descriptors + (size_t)idx1 * 32, d10, d11);
+      // epipolar line of kp1 in KF2 (CheckDistEpipolarLine :149-151)
+      const float la = kp1.x * F[0] + kp1.y * F[3] + F[6];
+      const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
+      const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
+      const float den = la * la + lb * lb;
+      unsigned long long best = ~0ull;
+      for (int c0 = 0; c0 < n2; c0 += 64) {
+        const int p = c0 + lane;
+        if (p < n2) {
+          const int idx2 = P.fv2.indices[o2 + p];
+          const bool claimed = (s_claim[idx2 >> 5] >> (idx2 & 31)) & 1u;
+          if (!claimed && K2.mp_state[idx2] == ORBFE_MP_NONE) {
+            const bool st2 = K2.u_right[idx2] >= 0;
+            if (!(only_stereo && !st2)) {
+              uint4 d20, d21;
+              load_desc(K2.descriptors + (size_t)idx2 * 32, d20, d21);
+              const int dist = hamming256(d10, d11, d20, d21);
+              if (dist <= TH_LOW) {
+                const orbfe_keypoint kp2 = K2.keys_un[idx2];
+                bool ok = true;
+                if (!st1 && !st2) {
+                  const float dex = P.ex - kp2.x, dey = P.ey - kp2.y;
+                  if (dex * dex + dey * dey < 100 * K2.scale_factors[kp2.octave]) ok = false;
+                }
+                if (ok) {
+                  const float num = la * kp2.x + lb * kp2.y + lc;
+                  if (den == 0) ok = false;
+                  else {
+                    const float dsqr = num * num / den;
+                    ok = (double)dsqr < 3.84 * (double)K2.level_sigma2[kp2.octave];
+                  }
+                }
+                if (ok) {
+                  // min distance; among equal distances the LAST candidate (ties replace, :752)
+                  const unsigned long long key =
+                      ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
+                  best = key < best ? key : best;
+                }
+              }
+            }
+          }
+        }
+      }
+      best = wave_min_u64(best);
+      if (best != ~0ull) {
+        const int p = 0x7fffffff - (int)(best & 0xffffffffull);
+        const int idx2 = P.fv2.indices[o2 + p];
+        if (lane == 0) {
+          P.match12[idx1] = idx2;
+          atomicOr(&s_claim[idx2 >> 5], 1u << (idx2 & 31));  // other waves share the word
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+    }
+  }
+  __syncthreads();
+  if (check_ori) {
+    for (int i = t; i < K1.n; i += 256) {
+      const int m = P.match12[i];
+      if (m >= 0) atomicAdd(&s_hist[rot_bin_dev(K1.keys_un[i].angle, K2.keys_un[m].angle)], 1);
+    }
+    __syncthreads();
+    if (t == 0) three_maxima_dev(s_hist, s_misc[0], s_misc[1], s_misc[2]);
+    __syncthreads();
+    const int i1 = s_misc[0], i2 = s_misc[1], i3 = s_misc[2];
+    for (int i = t; i < K1.n; i += 256) {
+      const int m = P.match12[i];
+      if (m >= 0) {
+        const int bin = rot_bin_dev(K1.keys_un[i].angle, K2.keys_un[m].angle);
+        if (bin != i1 && bin != i2 && bin != i3) P.match12[i] = -1;
+      }
+    }
+    __syncthreads();
+  }
+  int cnt = 0;
+  for (int i = t; i < K1.n; i += 256) cnt += P.match12[i] >= 0;
+  cnt = wave_sum(cnt);
+  if (lane == 0) atomicAdd(&s_misc[4], cnt);
+  __syncthreads();
+  if (t == 0) *P.nmatches = s_misc[4];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Frame grid (AssignFeaturesToGrid) as CSR: start[GRID_CELLS + 1], items[n]
+struct GridArgs {
+  const orbfe_keypoint* keys;
+  int n;
+  float min_x, min_y, inv_w, inv_h;
+  int32_t* start;
+  int32_t* items;
+};
+
+__global__ __launch_bounds__(256) void k_grid(GridArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t skeys[];
+  const int t = threadIdx.x;
+  int P2 = 1;
+  while (P2 < g.n) P2 <<= 1;
+  for (int i = t; i < P2; i += 256) {
+    uint32_t key = 0xffffffffu;
+    if (i < g.n) {
+      const orbfe_keypoint kp = g.keys[i];
+      // PosInGrid (Frame.cc:435-445): round() half away from zero on the float product
+      const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
+      const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
+      if (px >= 0 && px < GRID_COLS && py >= 0 && py < GRID_ROWS)
+        key = ((uint32_t)(px * GRID_ROWS + py) << 16) | (uint32_t)i;
+    }
+    skeys[i] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < P2; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint32_t x = skeys[i], y = skeys[ixj];
+          if ((i & k) == 0 ? (x > y) : (x < y)) {
+            skeys[i] = y;
+            skeys[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = t; i < g.n; i += 256) g.items[i] = (int32_t)(skeys[i] & 0xffffu);
+  for (int c = t; c <= GRID_CELLS; c += 256) {
+    const uint32_t probe = (uint32_t)c << 16;
+    int lo = 0, hi = g.n;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (skeys[mid] < probe) lo = mid + 1;
+      else hi = mid;
+    }
+    g.start[c] = lo;  // start[GRID_CELLS] = number of keys inside the grid
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SearchByProjection (both overloads): queries + fixpoint rounds + finish
+struct SbpQuery {
+  float x, y, r;      // search window centre and half-size (GetFeaturesInArea's x, y, r)
+  float xr, er_lim;   // stereo gate: |xr - uRight| > er_lim rejects
+  int min_level, max_level;
+  int flags;          // bit0 valid query, bit1 claims block (Observations() > 0)
+};
+
+struct SbpArgs {
+  orbfe_frame_view F;        // device pointers
+  const int32_t* grid_start;
+  const int32_t* grid_items;
+  const SbpQuery* q;
+  const uint8_t* qdesc;       // m x 32
+  int m;
+  int mode;                   // 0 local (best + second + ratio), 1 last frame (best only)
+  float nnratio;
+  int32_t* res_prev;
+  int32_t* res_cur;
+  const int32_t* owner_prev;  // INT_MAX = unclaimed in the previous round
+  int32_t* owner_cur;
+  int32_t* state;             // [0] converged flag, [1] rounds run, [2 + r] changed in round r
+  int round;
+};
+
+// One MapPoint's search given a predicate blocked(k). Returns the keypoint index or -1.
+template <class Blocked>
+__device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
+  const SbpQuery q = a.q[i];
+  if (!(q.flags & 1)) return -1;
+  const orbfe_frame_view& F = a.F;
+  const float x = q.x, y = q.y, r = q.r;
+  // GetFeaturesInArea (Frame.cc:376-433)
+  const int nMinCellX = max(0, (int)floorf((x - F.min_x - r) * F.grid_inv_w));
+  if (nMinCellX >= GRID_COLS) return -1;
+  const int nMaxCellX = min(GRID_COLS - 1, (int)ceilf((x - F.min_x + r) * F.grid_inv_w));
+  if (nMaxCellX < 0) return -1;
+  const int nMinCellY = max(0, (int)floorf((y - F.min_y - r) * F.grid_inv_h));
+  if (nMinCellY >= GRID_ROWS) return -1;
+  const int nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((y - F.min_y + r) * F.grid_inv_h));
+  if (nMaxCellY < 0) return -1;
+  const bool checkLevels = (q.min_level > 0) || (q.max_level >= 0);
+  uint4 dq0, dq1;
+  load_desc(a.qdesc + (size_t)i * 32, dq0, dq1);
+  int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+  for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
+    for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+      const int c = ix * GRID_ROWS + iy;
+      const int e = a.grid_start[c + 1];
+      for (int j = a.grid_start[c]; j < e; j++) {
+        const int k = a.grid_items[j];
+        const orbfe_keypoint kp = F.keys_un[k];
+        if (checkLevels) {
+          if (kp.octave < q.min_level) continue;
+          if (q.max_level >= 0 && kp.octave > q.max_level) continue;
+        }
+        const float distx = kp.x - x, disty = kp.y - y;
+        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+        if (blocked(k)) continue;
+        const float ur = F.u_right[k];
+        if (ur > 0) {
+          const float er = fabsf(q.xr - ur);
+          if (er > q.er_lim) continue;
+        }
+        uint4 d0, d1;
+        load_desc(F.descriptors + (size_t)k * 32, d0, d1);
+        const int dist = hamming256(dq0, dq1, d0, d1);
+        if (a.mode == 0) {
+          if (dist < bestDist) {
+            bestDist2 = bestDist;
+            bestDist = dist;
+            bestLevel2 = bestLevel;
+            bestLevel = kp.octave;
+            bestIdx = k;
+          } else if (dist < bestDist2) {
+            bestLevel2 = kp.octave;
+            bestDist2 = dist;
+          }
+        } else if (dist < bestDist) {
+          bestDist = dist;
+          bestIdx = k;
+        }
+      }
+    }
+  }
+  if (bestDist > TH_HIGH) return -1;
+  if (a.mode == 0 && bestLevel == bestLevel2 && (float)bestDist > a.nnratio * (float)bestDist2)
+    return -1;
+  return bestIdx;
+}
+
+__global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
+  if (a.round > 1 && a.state[2 + a.round - 1] == 0) {  // previous round reproduced its input
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.state[0] = 1;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = a.round + 1;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.m) return;
+  const int res = sbp_one(a, i, [&](int k) {
+    return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i;
+  });
+  a.res_cur[i] = res;
+  if (res >= 0 && (a.q[i].flags & 2)) atomicMin(&a.owner_cur[res], i);
+  if (res != a.res_prev[i]) atomicOr(&a.state[2 + a.round], 1);
+}
+
+struct SbpFinishArgs {
+  SbpArgs s;
+  const int32_t* res_final[2];  // result buffers by round parity
+  int32_t* best_out;
+  int32_t* nmatches;
+  int check_ori;
+  const float* q_angle;  // last-frame keypoint angles (mode 1)
+  int32_t* serial_used;
+};
+
+// Sequential fallback (the reference loop verbatim) when the fixpoint did not settle in
+// SBP_MAX_ROUNDS rounds, then counting and (last frame) the rotation-consistency filter.
+__global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* blocked_scratch) {
+  __shared__ int s_hist[HISTO_LENGTH];
+  __shared__ int s_misc[8];
+  const SbpArgs& a = f.s;
+  const int t = threadIdx.x;
+  const int rounds = a.state[1];
+  // settled: a round was skipped, or the last round reproduced the round before it
+  const bool converged = a.state[0] != 0 || (rounds >= 2 && a.state[2 + rounds - 1] == 0);
+  const int32_t* res = f.res_final[(rounds - 1) & 1];
+  if (!converged) {
+    if (t == 0) {
+      *f.serial_used = 1;
+      for (int k = 0; k < a.F.n; k++) blocked_scratch[k] = a.F.mp_state[k] == ORBFE_MP_OBSERVED;
+      for (int i = 0; i < a.m; i++) {
+        const int r = sbp_one(a, i, [&](int k) { return blocked_scratch[k] != 0; });
+        f.best_out[i] = r;
+        if (r >= 0) blocked_scratch[r] = (a.q[i].flags & 2) ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    __threadfence_block();
+  } else {
+    for (int i = t; i < a.m; i += 256) f.best_out[i] = res[i];
+    __syncthreads();
+  }
+  if (t < HISTO_LENGTH) s_hist[t] = 0;
+  if (t == 0) s_misc[4] = 0;
+  __syncthreads();
+  if (f.check_ori) {
+    for (int i = t; i < a.m; i += 256) {
+      const int b = f.best_out[i];
+      if (b >= 0) atomicAdd(&s_hist[rot_bin_dev(f.q_angle[i], a.F.keys_un[b].angle)], 1);
+    }
+    __syncthreads();
+    if (t == 0) three_maxima_dev(s_hist, s_misc[0], s_misc[1], s_misc[2]);
+    __syncthreads();
+  }
+  int cnt = 0;
+  for (int i = t; i < a.m; i += 256) {
+    const int b = f.best_out[i];
+    if (b < 0) continue;
+    if (f.check_ori) {
+      const int bin = rot_bin_dev(f.q_angle[i], a.F.keys_un[b].angle);
+      if (bin != s_misc[0] && bin != s_misc[1] && bin != s_misc[2]) {
+        f.best_out[i] = -2 - b;  // assigned, then undone by the rotation filter
+        continue;
+      }
+    }
+    cnt++;
+  }
+  cnt = wave_sum(cnt);
+  if (lane_id() == 0) atomicAdd(&s_misc[4], cnt);
+  __syncthreads();
+  if (t == 0) *f.nmatches = s_misc[4];
+}
+
+// Queries of SearchByProjection(Frame&, vector<MapPoint*>, th) (ORBmatcher.cc:51-73)
+struct LocalQueryArgs {
+  orbfe_local_mappoints mp;  // device pointers
+  const float* scale_factors;
+  float th;
+  SbpQuery* q;
+};
+__global__ void k_sbp_local_queries(LocalQueryArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.mp.m) return;
+  SbpQuery q = {};
+  const uint8_t fl = a.mp.flags[i];
+  if ((fl & ORBFE_MPF_TRACK_IN_VIEW) && !(fl & ORBFE_MPF_BAD)) {
+    const int lvl = a.mp.level[i];
+    float r = a.mp.view_cos[i] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:135-141)
+    if (a.th != 1.0) r *= a.th;
+    q.x = a.mp.proj_x[i];
+    q.y = a.mp.proj_y[i];
+    q.r = r * a.scale_factors[lvl];
+    q.xr = a.mp.proj_xr[i];
+    q.er_lim = r * a.scale_factors[lvl];
+    q.min_level = lvl - 1;
+    q.max_level = lvl;
+    q.flags = 1 | ((fl & ORBFE_MPF_OBSERVED) ? 2 : 0);
+  }
+  a.q[i] = q;
+}
+
+// Queries of SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1358-1410):
+// projection with cv::Mat float algebra accumulated in double.
+struct LastQueryArgs {
+  orbfe_lastframe_mappoints last;  // device pointers
+  orbfe_frame_view C;              // camera + level tables (device pointers)
+  float rcw[9], tcw[3];
+  int forward, backward;
+  float th;
+  SbpQuery* q;
+};
+__device__ __forceinline__ float gemv_row_dev(const float* r, const float* v, float add) {
+  double s = (double)r[0] * (double)v[0];
+  s += (double)r[1] * (double)v[1];
+  s += (double)r[2] * (double)v[2];
+  s = s + (double)add;
+  return (float)s;
+}
+__global__ void k_sbp_last_queries(LastQueryArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.last.n) return;
+  SbpQuery q = {};
+  const uint8_t fl = a.last.flags[i];
+  if ((fl & ORBFE_MPF_PRESENT) && !(fl & ORBFE_MPF_OUTLIER)) {
+    const float X[3] = {a.last.world_pos[3 * i], a.last.world_pos[3 * i + 1], a.last.world_pos[3 * i + 2]};
+    const float xc = gemv_row_dev(a.rcw, X, a.tcw[0]);
+    const float yc = gemv_row_dev(a.rcw + 3, X, a.tcw[1]);
+    const float zc = gemv_row_dev(a.rcw + 6, X, a.tcw[2]);
+    const float invzc = (float)(1.0 / (double)zc);
+    const float u = a.C.fx * xc * invzc + a.C.cx;
+    const float v = a.C.fy * yc * invzc + a.C.cy;
+    if (!(invzc < 0) && !(u < a.C.min_x || u > a.C.max_x) && !(v < a.C.min_y || v > a.C.max_y)) {
+      const int oct = a.last.octave[i];
+      const float radius = a.th * a.C.scale_factors[oct];
+      q.x = u;
+      q.y = v;
+      q.r = radius;
+      q.xr = u - a.C.bf * invzc;
+      q.er_lim = radius;
+      if (a.forward) { q.min_level = oct; q.max_level = -1; }
+      else if (a.backward) { q.min_level = 0; q.max_level = oct; }
+      else { q.min_level = oct - 1; q.max_level = oct + 1; }
+      q.flags = 1 | ((fl & ORBFE_MPF_OBSERVED) ? 2 : 0);
+    }
+  }
+  a.q[i] = q;
+}
+
+__global__ void k_hamming_batch(const uint8_t* a, const uint8_t* b, int n, int32_t* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint4 a0, a1, b0, b1;
+  load_desc(a + (size_t)i * 32, a0, a1);
+  load_desc(b + (size_t)i * 32, b0, b1);
+  out[i] = hamming256(a0, a1, b0, b1);
+}
+
+// =============================================================================================
+// host side
+struct orbfe_matcher {
+  int device = 0;
+  float nnratio;
+  int check_ori;
+  hipStream_t stream = nullptr;
+  // device arena (grown on demand)
+  uint8_t* arena = nullptr;
+  size_t arena_bytes = 0;
+  orbfe_sft_pair* d_pairs = nullptr;
+  int pairs_cap = 0;
+  int32_t* d_serial = nullptr;
+  int last_rounds = 0, last_serial = 0;
+};
+
+namespace {
+struct Arena {
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    const size_t off = total;
+    total += (bytes + 255) & ~(size_t)255;
+    return off;
+  }
+};
+
+int ensure_arena(orbfe_matcher* m, size_t bytes) {
+  if (bytes <= m->arena_bytes) return ORBFE_OK;
+  hipFree(m->arena);
+  m->arena = nullptr;
+  ORBFE_HIP_CHECK(hipMalloc(&m->arena, bytes));
+  m->arena_bytes = bytes;
+  return ORBFE_OK;
+}
+
+// Layout of one frame view in the arena
+struct FrameOffsets {
+  size_t keys, ur, desc, mp, scale, sigma2;
+};
+FrameOffsets plan_frame(Arena& ar, const orbfe_frame_view* f) {
+  FrameOffsets o;
+  o.keys = ar.add(sizeof(orbfe_keypoint) * std::max(f->n, 1));
+  o.ur = ar.add(sizeof(float) * std::max(f->n, 1));
+  o.desc = ar.add(32 * (size_t)std::max(f->n, 1));
+  o.mp = ar.add(std::max(f->n, 1));
+  o.scale = ar.add(sizeof(float) * std::max(f->nlevels, 1));
+  o.sigma2 = ar.add(sizeof(float) * std::max(f->nlevels, 1));
+  return o;
+}
+int upload_frame(orbfe_matcher* m, const FrameOffsets& o, const orbfe_frame_view* f,
+                 orbfe_frame_view* d) {
+  uint8_t* A = m->arena;
+  *d = *f;
+  d->keys_un = (const orbfe_keypoint*)(A + o.keys);
+  d->u_right = (const float*)(A + o.ur);
+  d->descriptors = A + o.desc;
+  d->mp_state = A + o.mp;
+  d->scale_factors = (const float*)(A + o.scale);
+  d->level_sigma2 = (const float*)(A + o.sigma2);
+  if (f->n > 0) {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.keys, f->keys_un, sizeof(orbfe_keypoint) * f->n, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.ur, f->u_right, sizeof(float) * f->n, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.desc, f->descriptors, 32 * (size_t)f->n, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.mp, f->mp_state, f->n, hipMemcpyHostToDevice, m->stream));
+  }
+  if (f->nlevels > 0) {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.scale, f->scale_factors, sizeof(float) * f->nlevels, hipMemcpyHostToDevice, m->stream));
+    if (f->level_sigma2)
+      ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.sigma2, f->level_sigma2, sizeof(float) * f->nlevels, hipMemcpyHostToDevice, m->stream));
+  }
+  return ORBFE_OK;
+}
+bool frame_ok(const orbfe_frame_view* f) {
+  return f && f->n >= 0 && f->n <= GRID_MAX_KEYS && (f->n == 0 || (f->keys_un && f->u_right && f->descriptors && f->mp_state)) &&
+         f->nlevels > 0 && f->scale_factors;
+}
+bool levels_ok(const orbfe_keypoint* k, int n, int nlevels) {
+  for (int i = 0; i < n; i++)
+    if (k[i].octave < 0 || k[i].octave >= nlevels) return false;
+  return true;
+}
+}  // namespace
+
+extern "C" int orbfe_matcher_create(float nnratio, int check_orientation, int device,
+                                    orbfe_matcher** out) {
+  if (!out) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_matcher_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_matcher_create: no HIP device");
+  if (device < 0 || device >= ndev) return orbfe_set_error(ORBFE_ERR_ARG, "bad device index");
+  orbfe_matcher* m = new orbfe_matcher();
+  m->device = device;
+  m->nnratio = nnratio;
+  m->check_ori = check_orientation ? 1 : 0;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&m->d_serial, sizeof(int32_t) * 4) != hipSuccess) {
+    delete m;
+    return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_matcher_create: HIP setup failed");
+  }
+  *out = m;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_matcher_destroy(orbfe_matcher* m) {
+  if (!m) return ORBFE_OK;
+  hipSetDevice(m->device);
+  if (m->stream) hipStreamSynchronize(m->stream);
+  hipFree(m->arena);
+  hipFree(m->d_pairs);
+  hipFree(m->d_serial);
+  if (m->stream) hipStreamDestroy(m->stream);
+  delete m;
+  return ORBFE_OK;
+}
+
+extern "C" void* orbfe_matcher_stream(orbfe_matcher* m) { return m ? (void*)m->stream : nullptr; }
+
+extern "C" int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  if (!a || !b) return ORBFE_ERR_ARG;
+  int d = 0;
+  for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+  return d;
+}
+
+extern "C" int orbfe_descriptor_distance_batch(orbfe_matcher* m, const uint8_t* a,
+                                               const uint8_t* b, int n, int32_t* out) {
+  if (!m || n < 0 || (n > 0 && (!a || !b || !out))) return ORBFE_ERR_ARG;
+  if (n == 0) return ORBFE_OK;
+  hipSetDevice(m->device);
+  Arena ar;
+  const size_t oa = ar.add(32 * (size_t)n), ob = ar.add(32 * (size_t)n), oo = ar.add(4 * (size_t)n);
+  int st = ensure_arena(m, ar.total);
+  if (st) return st;
+  ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + oa, a, 32 * (size_t)n, hipMemcpyHostToDevice, m->stream));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + ob, b, 32 * (size_t)n, hipMemcpyHostToDevice, m->stream));
+  hipLaunchKernelGGL(k_hamming_batch, dim3((n + 255) / 256), dim3(256), 0, m->stream, m->arena + oa,
+                     m->arena + ob, n, (int32_t*)(m->arena + oo));
+  ORBFE_HIP_CHECK(hipGetLastError());
+  ORBFE_HIP_CHECK(hipMemcpyAsync(out, m->arena + oo, 4 * (size_t)n, hipMemcpyDeviceToHost, m->stream));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  return ORBFE_OK;
+}
+
+// ---- SearchForTriangulation ---------------------------------------------------------------
+extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int n_pairs,
+                                                           const orbfe_sft_pair* pairs,
+                                                           int only_stereo, void* stream) {
+  if (!m || n_pairs < 0 || (n_pairs > 0 && !pairs)) return orbfe_set_error(ORBFE_ERR_ARG, "sft batch: bad argument");
+  if (n_pairs == 0) return ORBFE_OK;
+  hipSetDevice(m->device);
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  if (n_pairs > m->pairs_cap) {
+    hipFree(m->d_pairs);
+    m->d_pairs = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&m->d_pairs, sizeof(orbfe_sft_pair) * n_pairs));
+    m->pairs_cap = n_pairs;
+  }
+  for (int p = 0; p < n_pairs; p++)
+    if (pairs[p].kf2.n > SFT_MAX_KF2) return orbfe_set_error(ORBFE_ERR_ARG, "sft: KF2 too large");
+  ORBFE_HIP_CHECK(hipMemcpyAsync(m->d_pairs, pairs, sizeof(orbfe_sft_pair) * n_pairs, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_sft, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, only_stereo ? 1 : 0, m->check_ori);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_frame_view* kf1,
+                                              const orbfe_frame_view* kf2,
+                                              const orbfe_feature_vector* fv1,
+                                              const orbfe_feature_vector* fv2, const float* f12,
+                                              float ex, float ey, int only_stereo,
+                                              int32_t* match12, int* nmatches) {
+  if (!m || !frame_ok(kf1) || !frame_ok(kf2) || !fv1 || !fv2 || !f12 || !nmatches ||
+      (kf1->n > 0 && !match12) || !kf2->level_sigma2)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_for_triangulation: bad argument");
+  if (!levels_ok(kf2->keys_un, kf2->n, kf2->nlevels))
+    return orbfe_set_error(ORBFE_ERR_ARG, "keypoint octave outside the level tables");
+  hipSetDevice(m->device);
+  Arena ar;
+  const FrameOffsets o1 = plan_frame(ar, kf1), o2 = plan_frame(ar, kf2);
+  auto plan_fv = [&](const orbfe_feature_vector* fv, size_t* ids, size_t* offs, size_t* idx) {
+    *ids = ar.add(4 * (size_t)std::max(fv->n_nodes, 1));
+    *offs = ar.add(4 * (size_t)(fv->n_nodes + 1));
+    *idx = ar.add(4 * (size_t)std::max(fv->n_nodes > 0 ? fv->offsets[fv->n_nodes] : 0, 1));
+  };
+  size_t f1i, f1o, f1x, f2i, f2o, f2x;
+  plan_fv(fv1, &f1i, &f1o, &f1x);
+  plan_fv(fv2, &f2i, &f2o, &f2x);
+  const size_t om = ar.add(4 * (size_t)std::max(kf1->n, 1)), on = ar.add(4);
+  int st = ensure_arena(m, ar.total);
+  if (st) return st;
+  orbfe_sft_pair P;
+  std::memset(&P, 0, sizeof(P));
+  if ((st = upload_frame(m, o1, kf1, &P.kf1))) return st;
+  if ((st = upload_frame(m, o2, kf2, &P.kf2))) return st;
+  auto up_fv = [&](const orbfe_feature_vector* fv, size_t ids, size_t offs, size_t idx,
+                   orbfe_feature_vector* d) -> int {
+    uint8_t* A = m->arena;
+    d->n_nodes = fv->n_nodes;
+    d->node_ids = (const uint32_t*)(A + ids);
+    d->offsets = (const int32_t*)(A + offs);
+    d->indices = (const int32_t*)(A + idx);
+    if (fv->n_nodes > 0) {
+      const int ni = fv->offsets[fv->n_nodes];
+      ORBFE_HIP_CHECK(hipMemcpyAsync(A + ids, fv->node_ids, 4 * (size_t)fv->n_nodes, hipMemcpyHostToDevice, m->stream));
+      ORBFE_HIP_CHECK(hipMemcpyAsync(A + offs, fv->offsets, 4 * (size_t)(fv->n_nodes + 1), hipMemcpyHostToDevice, m->stream));
+      if (ni > 0) ORBFE_HIP_CHECK(hipMemcpyAsync(A + idx, fv->indices, 4 * (size_t)ni, hipMemcpyHostToDevice, m->stream));
+    }
+    return ORBFE_OK;
+  };
+  if ((st = up_fv(fv1, f1i, f1o, f1x, &P.fv1))) return st;
+  if ((st = up_fv(fv2, f2i, f2o, f2x, &P.fv2))) return st;
+  std::memcpy(P.f12, f12, sizeof(float) * 9);
+  P.ex = ex;
+  P.ey = ey;
+  P.match12 = (int32_t*)(m->arena + om);
+  P.nmatches = (int32_t*)(m->arena + on);
+  st = orbfe_search_for_triangulation_batch_device(m, 1, &P, only_stereo, m->stream);
+  if (st) return st;
+  int32_t nm = 0;
+  if (kf1->n > 0)
+    ORBFE_HIP_CHECK(hipMemcpyAsync(match12, P.match12, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, m->stream));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, P.nmatches, 4, hipMemcpyDeviceToHost, m->stream));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  *nmatches = nm;
+  return ORBFE_OK;
+}
+
+// ---- SearchByProjection -----------------------------------------------------------------------
+static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode,
+                   const uint8_t* h_qdesc, const float* h_qangle, int check_ori,
+                   const std::function<int(Arena&)>& plan_q,
+                   const std::function<int(uint8_t*, const orbfe_frame_view&, SbpQuery*)>& make_q,
+                   int32_t* best_idx, int* nmatches) {
+  Arena ar;
+  const FrameOffsets fo = plan_frame(ar, F);
+  const size_t og_start = ar.add(4 * (GRID_CELLS + 1));
+  const size_t og_items = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t oq = ar.add(sizeof(SbpQuery) * std::max(nq, 1));
+  const size_t oqd = ar.add(32 * (size_t)std::max(nq, 1));
+  const size_t oqa = ar.add(4 * (size_t)std::max(nq, 1));
+  const size_t ores0 = ar.add(4 * (size_t)std::max(nq, 1));
+  const size_t ores1 = ar.add(4 * (size_t)std::max(nq, 1));
+  const size_t oown0 = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t oown1 = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t oblk = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t ostate = ar.add(4 * (SBP_MAX_ROUNDS + 4));
+  const size_t obest = ar.add(4 * (size_t)std::max(nq, 1));
+  const size_t onm = ar.add(4);
+  const size_t extra = plan_q(ar);
+  (void)extra;
+  int st = ensure_arena(m, ar.total);
+  if (st) return st;
+  uint8_t* A = m->arena;
+  orbfe_frame_view dF;
+  if ((st = upload_frame(m, fo, F, &dF))) return st;
+  // grid
+  GridArgs g;
+  g.keys = dF.keys_un;
+  g.n = F->n;
+  g.min_x = F->min_x;
+  g.min_y = F->min_y;
+  g.inv_w = F->grid_inv_w;
+  g.inv_h = F->grid_inv_h;
+  g.start = (int32_t*)(A + og_start);
+  g.items = (int32_t*)(A + og_items);
+  int P2 = 1;
+  while (P2 < F->n) P2 <<= 1;
+  hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sizeof(uint32_t) * P2, m->stream, g);
+  SbpQuery* dq = (SbpQuery*)(A + oq);
+  if (nq > 0) {
+    if ((st = make_q(A, dF, dq))) return st;
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + oqd, h_qdesc, 32 * (size_t)nq, hipMemcpyHostToDevice, m->stream));
+    if (h_qangle) ORBFE_HIP_CHECK(hipMemcpyAsync(A + oqa, h_qangle, 4 * (size_t)nq, hipMemcpyHostToDevice, m->stream));
+  }
+  ORBFE_HIP_CHECK(hipMemsetAsync(A + ores0, 0xfe, 4 * (size_t)std::max(nq, 1), m->stream));  // -0x01010102: never a result
+  ORBFE_HIP_CHECK(hipMemsetAsync(A + ores1, 0xfe, 4 * (size_t)std::max(nq, 1), m->stream));
+  ORBFE_HIP_CHECK(hipMemsetAsync(A + oown1, 0x7f, 4 * (size_t)std::max(F->n, 1), m->stream));
+  ORBFE_HIP_CHECK(hipMemsetAsync(A + ostate, 0, 4 * (SBP_MAX_ROUNDS + 4), m->stream));
+  ORBFE_HIP_CHECK(hipMemsetAsync(m->d_serial, 0, 4, m->stream));
+  SbpArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.F = dF;
+  a.grid_start = g.start;
+  a.grid_items = g.items;
+  a.q = dq;
+  a.qdesc = A + oqd;
+  a.m = nq;
+  a.mode = mode;
+  a.nnratio = m->nnratio;
+  a.state = (int32_t*)(A + ostate);
+  int32_t* res[2] = {(int32_t*)(A + ores0), (int32_t*)(A + ores1)};
+  int32_t* own[2] = {(int32_t*)(A + oown0), (int32_t*)(A + oown1)};
+  for (int r = 0; r < SBP_MAX_ROUNDS && nq > 0; r++) {
+    a.round = r;
+    a.res_cur = res[r & 1];
+    a.res_prev = res[(r + 1) & 1];
+    a.owner_cur = own[r & 1];
+    a.owner_prev = own[(r + 1) & 1];
+    ORBFE_HIP_CHECK(hipMemsetAsync(a.owner_cur, 0x7f, 4 * (size_t)std::max(F->n, 1), m->stream));
+    hipLaunchKernelGGL(k_sbp_round, dim3((nq + 255) / 256), dim3(256), 0, m->stream, a);
+  }
+  SbpFinishArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.s = a;
+  f.res_final[0] = res[0];
+  f.res_final[1] = res[1];
+  f.best_out = (int32_t*)(A + obest);
+  f.nmatches = (int32_t*)(A + onm);
+  f.check_ori = check_ori;
+  f.q_angle = (const float*)(A + oqa);
+  f.serial_used = m->d_serial;
+  if (nq > 0) {
+    hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + oblk));
+  }
+  ORBFE_HIP_CHECK(hipGetLastError());
+  int32_t nm = 0, state[2] = {0, 0}, serial = 0;
+  if (nq > 0) {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, f.best_out, 4 * (size_t)nq, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, f.nmatches, 4, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(state, a.state, 8, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
+  }
+  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  m->last_rounds = state[1];
+  m->last_serial = serial;
+  *nmatches = nm;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_frame_view* F,
+                                                const orbfe_local_mappoints* mps, float th,
+                                                int32_t* best_idx, int* nmatches) {
+  if (!m || !frame_ok(F) || !mps || !nmatches || mps->m < 0 ||
+      (mps->m > 0 && (!best_idx || !mps->flags || !mps->proj_x || !mps->proj_y || !mps->proj_xr ||
+                      !mps->level || !mps->view_cos || !mps->descriptors)))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_by_projection_local: bad argument");
+  for (int i = 0; i < mps->m; i++)
+    if ((mps->flags[i] & ORBFE_MPF_TRACK_IN_VIEW) && !(mps->flags[i] & ORBFE_MPF_BAD) &&
+        (mps->level[i] < 0 || mps->level[i] >= F->nlevels))
+      return orbfe_set_error(ORBFE_ERR_ARG, "mnTrackScaleLevel outside the level tables");
+  hipSetDevice(m->device);
+  size_t o_flags = 0, o_px = 0, o_py = 0, o_pxr = 0, o_lvl = 0, o_vc = 0;
+  const int M = mps->m;
+  auto plan = [&](Arena& ar) -> int {
+    o_flags = ar.add(std::max(M, 1));
+    o_px = ar.add(4 * (size_t)std::max(M, 1));
+    o_py = ar.add(4 * (size_t)std::max(M, 1));
+    o_pxr = ar.add(4 * (size_t)std::max(M, 1));
+    o_lvl = ar.add(4 * (size_t)std::max(M, 1));
+    o_vc = ar.add(4 * (size_t)std::max(M, 1));
+    return 0;
+  };
+  auto make = [&](uint8_t* A, const orbfe_frame_view& dF, SbpQuery* dq) -> int {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_flags, mps->flags, M, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_px, mps->proj_x, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_py, mps->proj_y, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_pxr, mps->proj_xr, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_lvl, mps->level, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_vc, mps->view_cos, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    LocalQueryArgs qa;
+    std::memset(&qa, 0, sizeof(qa));
+    qa.mp.m = M;
+    qa.mp.flags = A + o_flags;
+    qa.mp.proj_x = (const float*)(A + o_px);
+    qa.mp.proj_y = (const float*)(A + o_py);
+    qa.mp.proj_xr = (const float*)(A + o_pxr);
+    qa.mp.level = (const int32_t*)(A + o_lvl);
+    qa.mp.view_cos = (const float*)(A + o_vc);
+    qa.scale_factors = dF.scale_factors;
+    qa.th = th;
+    qa.q = dq;
+    hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
+    return ORBFE_OK;
+  };
+  return run_sbp(m, F, M, 0, mps->descriptors, nullptr, 0, plan, make, best_idx, nmatches);
+}
+
+extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
+                                                    const orbfe_frame_view* C,
+                                                    const orbfe_lastframe_mappoints* L,
+                                                    const float* tcw_cur, float th, int mono,
+                                                    int32_t* best_idx, int* nmatches) {
+  if (!m || !frame_ok(C) || !L || !tcw_cur || !nmatches || L->n < 0 ||
+      (L->n > 0 && (!best_idx || !L->flags || !L->world_pos || !L->descriptors || !L->octave || !L->angle)))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_by_projection_lastframe: bad argument");
+  for (int i = 0; i < L->n; i++)
+    if ((L->flags[i] & ORBFE_MPF_PRESENT) && !(L->flags[i] & ORBFE_MPF_OUTLIER) &&
+        (L->octave[i] < 0 || L->octave[i] >= C->nlevels))
+      return orbfe_set_error(ORBFE_ERR_ARG, "last-frame octave outside the level tables");
+  hipSetDevice(m->device);
+  // twc = -Rcw.t() * tcw ; tlc = Rlw * twc + tlw (ORBmatcher.cc:1358-1369), double-accumulated
+  const float* T = tcw_cur;
+  const float Rcw[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+  const float tcw[3] = {T[3], T[7], T[11]};
+  const float* Tl = L->tcw_last;
+  float twc[3];
+  for (int i = 0; i < 3; i++) {
+    double s = (double)Rcw[i] * (double)tcw[0];
+    s += (double)Rcw[3 + i] * (double)tcw[1];
+    s += (double)Rcw[6 + i] * (double)tcw[2];
+    twc[i] = -(float)s;
+  }
+  double s2 = (double)Tl[8] * (double)twc[0];
+  s2 += (double)Tl[9] * (double)twc[1];
+  s2 += (double)Tl[10] * (double)twc[2];
+  s2 = s2 + (double)Tl[11];
+  const float tlc2 = (float)s2;
+  const bool fwd = tlc2 > C->b && !mono;
+  const bool bwd = -tlc2 > C->b && !mono;
+  const int N = L->n;
+  size_t o_flags = 0, o_pos = 0, o_oct = 0;
+  auto plan = [&](Arena& ar) -> int {
+    o_flags = ar.add(std::max(N, 1));
+    o_pos = ar.add(12 * (size_t)std::max(N, 1));
+    o_oct = ar.add(4 * (size_t)std::max(N, 1));
+    return 0;
+  };
+  auto make = [&](uint8_t* A, const orbfe_frame_view& dF, SbpQuery* dq) -> int {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_flags, L->flags, N, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_pos, L->world_pos, 12 * (size_t)N, hipMemcpyHostToDevice, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_oct, L->octave, 4 * (size_t)N, hipMemcpyHostToDevice, m->stream));
+    LastQueryArgs qa;
+    std::memset(&qa, 0, sizeof(qa));
+    qa.last.n = N;
+    qa.last.flags = A + o_flags;
+    qa.last.world_pos = (const float*)(A + o_pos);
+    qa.last.octave = (const int32_t*)(A + o_oct);
+    qa.C = dF;
+    std::memcpy(qa.rcw, Rcw, sizeof(Rcw));
+    std::memcpy(qa.tcw, tcw, sizeof(tcw));
+    qa.forward = fwd;
+    qa.backward = bwd;
+    qa.th = th;
+    qa.q = dq;
+    hipLaunchKernelGGL(k_sbp_last_queries, dim3((N + 255) / 256), dim3(256), 0, m->stream, qa);
+    return ORBFE_OK;
+  };
+  return run_sbp(m, C, N, 1, L->descriptors, L->angle, m->check_ori, plan, make, best_idx, nmatches);
+}
+
+extern "C" int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* serial_used) {
+  if (!m) return ORBFE_ERR_ARG;
+  if (rounds) *rounds = m->last_rounds;
+  if (serial_used) *serial_used = m->last_serial;
+  return ORBFE_OK;
+}

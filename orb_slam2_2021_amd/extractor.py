@@ -1,0 +1,225 @@
+"""ORBextractor on MI355X -- host mirror of include/ORBextractor.h over liborbfe.so.
+
+Same constructor arguments, getters and call semantics as the reference class
+(include/ORBextractor.h:56-100, src/ORBextractor.cc:413-473, 1041-1103): calling the extractor on
+an 8-bit grayscale image returns its keypoints (cv::KeyPoint fields, level order) and the N x 32
+descriptor matrix. All work runs in the HIP kernels of liborbfe.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_size_t, c_void_p
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+
+KeyPoints = np.ndarray  # structured, dtype KEYPOINT_DTYPE
+
+
+class ORBextractor:
+    HARRIS_SCORE = 0  # ORBextractor.h:51-54 (enum kept for API parity)
+    FAST_SCORE = 1
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int,
+                 minThFAST: int, device: int = 0):
+        self._lib = L.lib()
+        h = c_void_p()
+        L.check(self._lib.orbfe_extractor_create(int(nfeatures), float(scaleFactor), int(nlevels),
+                                                 int(iniThFAST), int(minThFAST), int(device),
+                                                 byref(h)), "orbfe_extractor_create")
+        self._h = h
+        self.nfeatures = int(nfeatures)
+        self.scaleFactor = float(scaleFactor)
+        self.nlevels = int(nlevels)
+        self.iniThFAST = int(iniThFAST)
+        self.minThFAST = int(minThFAST)
+        self.device = int(device)
+        n = self.nlevels
+        self._scale = np.zeros(n, np.float32)
+        self._inv = np.zeros(n, np.float32)
+        self._s2 = np.zeros(n, np.float32)
+        self._is2 = np.zeros(n, np.float32)
+        self._fpl = np.zeros(n, np.int32)
+        L.check(self._lib.orbfe_get_scale_tables(self._h, L.ptr(self._scale), L.ptr(self._inv),
+                                                 L.ptr(self._s2), L.ptr(self._is2),
+                                                 L.ptr(self._fpl)), "orbfe_get_scale_tables")
+        self._last_shape: Optional[Tuple[int, int]] = None
+
+    # ---- lifetime -------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.orbfe_extractor_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- getters (ORBextractor.h:70-98) ---------------------------------------------------
+    def GetLevels(self) -> int:
+        return self.nlevels
+
+    def GetScaleFactor(self) -> float:
+        return self.scaleFactor
+
+    def GetScaleFactors(self) -> np.ndarray:
+        return self._scale.copy()
+
+    def GetInverseScaleFactors(self) -> np.ndarray:
+        return self._inv.copy()
+
+    def GetScaleSigmaSquares(self) -> np.ndarray:
+        return self._s2.copy()
+
+    def GetInverseScaleSigmaSquares(self) -> np.ndarray:
+        return self._is2.copy()
+
+    @property
+    def mnFeaturesPerLevel(self) -> np.ndarray:
+        return self._fpl.copy()
+
+    def set_resize_mode(self, mode: int) -> None:
+        L.check(self._lib.orbfe_extractor_set_resize_mode(self._h, int(mode)), "set_resize_mode")
+
+    def max_keypoints(self, rows: int, cols: int) -> int:
+        return L.check(self._lib.orbfe_max_keypoints(self._h, int(rows), int(cols)),
+                       "orbfe_max_keypoints")
+
+    # ---- operator() -----------------------------------------------------------------------
+    def __call__(self, image: np.ndarray, mask=None) -> Tuple[KeyPoints, Optional[np.ndarray]]:
+        """operator()(image, mask, keypoints, descriptors). The mask is ignored, as in the
+        reference (ORBextractor.h:65). Returns (keypoints, descriptors); descriptors is None when
+        no keypoint was found (the reference releases the Mat, ORBextractor.cc:1062-1063)."""
+        img = np.asarray(image)
+        if img.size == 0:
+            return np.zeros(0, L.KEYPOINT_DTYPE), None
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise ValueError("ORBextractor expects a CV_8UC1 image")  # assert at :1048
+        img = np.ascontiguousarray(img)
+        rows, cols = img.shape
+        cap = self.max_keypoints(rows, cols)
+        kps = np.zeros(cap, L.KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = c_int()
+        L.check(self._lib.orbfe_extract(self._h, L.ptr(img), rows, cols, c_size_t(img.strides[0]),
+                                        L.ptr(kps), cap, L.ptr(desc), byref(n)), "orbfe_extract")
+        self._last_shape = (rows, cols)
+        k = n.value
+        return kps[:k].copy(), (desc[:k].copy() if k else None)
+
+    def extract_batch(self, images: Sequence[np.ndarray]) -> List[Tuple[KeyPoints, np.ndarray]]:
+        """Independent operator() calls on same-shaped images in one launch sequence."""
+        imgs = [np.ascontiguousarray(np.asarray(i, np.uint8)) for i in images]
+        if not imgs:
+            return []
+        rows, cols = imgs[0].shape
+        if any(i.shape != (rows, cols) for i in imgs):
+            raise ValueError("extract_batch needs same-shaped images")
+        cap = self.max_keypoints(rows, cols)
+        B = len(imgs)
+        kps = np.zeros(B * cap, L.KEYPOINT_DTYPE)
+        desc = np.zeros((B * cap, 32), np.uint8)
+        counts = np.zeros(B, np.int32)
+        arr = (c_void_p * B)(*[i.ctypes.data for i in imgs])
+        L.check(self._lib.orbfe_extract_batch(self._h, B, ctypes.cast(arr, c_void_p), rows, cols,
+                                              c_size_t(cols), L.ptr(kps), L.ptr(desc), cap,
+                                              L.ptr(counts)), "orbfe_extract_batch")
+        self._last_shape = (rows, cols)
+        out = []
+        for b in range(B):
+            k = int(counts[b])
+            out.append((kps[b * cap:b * cap + k].copy(), desc[b * cap:b * cap + k].copy()))
+        return out
+
+    def extract_batch_device(self, n_images: int, d_imgs: int, image_stride: int, rows: int,
+                             cols: int, pitch: int, d_kps: int, d_desc: int, cap: int,
+                             d_counts: int, stream: Optional[int] = None) -> None:
+        """Device-resident batch (all int arguments are device addresses); async on `stream`."""
+        L.check(self._lib.orbfe_extract_batch_device(
+            self._h, int(n_images), c_void_p(d_imgs), c_size_t(image_stride), int(rows), int(cols),
+            c_size_t(pitch), c_void_p(d_kps), c_void_p(d_desc), int(cap), c_void_p(d_counts),
+            c_void_p(stream or 0)), "orbfe_extract_batch_device")
+        self._last_shape = (rows, cols)
+
+    @property
+    def stream(self) -> int:
+        return self._lib.orbfe_extractor_stream(self._h) or 0
+
+    # ---- mvImagePyramid (ORBextractor.h:100) --------------------------------------------
+    def level(self, level: int, image: int = 0) -> np.ndarray:
+        p = c_void_p()
+        r, c, s = c_int(), c_int(), c_size_t()
+        L.check(self._lib.orbfe_get_level(self._h, image, level, byref(p), byref(r), byref(c),
+                                          byref(s)), "orbfe_get_level")
+        buf = (ctypes.c_uint8 * (r.value * s.value)).from_address(p.value)
+        return np.frombuffer(buf, np.uint8).reshape(r.value, s.value)[:, :c.value].copy()
+
+    @property
+    def mvImagePyramid(self) -> List[np.ndarray]:
+        return [self.level(l) for l in range(self.nlevels)]
+
+    # ---- instrumentation ----------------------------------------------------------------
+    def set_profiling(self, enable: bool) -> None:
+        L.check(self._lib.orbfe_set_profiling(self._h, 1 if enable else 0), "set_profiling")
+
+    def kernel_times(self) -> dict:
+        cap, name_len = 16, 32
+        names = ctypes.create_string_buffer(cap * name_len)
+        total = np.zeros(cap, np.float64)
+        launches = np.zeros(cap, np.int32)
+        n = c_int()
+        L.check(self._lib.orbfe_get_kernel_times(self._h, names, name_len, L.ptr(total),
+                                                 L.ptr(launches), cap, byref(n)), "kernel_times")
+        out = {}
+        for k in range(n.value):
+            nm = names.raw[k * name_len:(k + 1) * name_len].split(b"\0", 1)[0].decode()
+            out[nm] = (float(total[k]), int(launches[k]))
+        return out
+
+    def reset_kernel_times(self) -> None:
+        L.check(self._lib.orbfe_reset_kernel_times(self._h), "reset_kernel_times")
+
+    def debug_candidates(self, level: int, image: int = 0) -> np.ndarray:
+        n = c_int()
+        L.check(self._lib.orbfe_debug_get_candidates(self._h, image, level, None, 0, byref(n)),
+                "debug_candidates")
+        out = np.zeros(max(n.value, 1), np.uint32)
+        L.check(self._lib.orbfe_debug_get_candidates(self._h, image, level, L.ptr(out), len(out),
+                                                     byref(n)), "debug_candidates")
+        return out[:n.value]
+
+    def debug_level_keys(self, level: int, image: int = 0) -> np.ndarray:
+        n = c_int()
+        L.check(self._lib.orbfe_debug_get_level_keys(self._h, image, level, None, 0, byref(n)),
+                "debug_level_keys")
+        out = np.zeros(max(n.value, 1), np.uint32)
+        L.check(self._lib.orbfe_debug_get_level_keys(self._h, image, level, L.ptr(out), len(out),
+                                                     byref(n)), "debug_level_keys")
+        return out[:n.value]
+
+    def geometry(self, rows: int, cols: int) -> np.ndarray:
+        info = np.zeros(7 * self.nlevels, np.int32)
+        L.check(self._lib.orbfe_debug_geometry(self._h, rows, cols, L.ptr(info), len(info)),
+                "geometry")
+        return info.reshape(self.nlevels, 7)
+
+
+def synth_frame(index: int, rows: int = 376, cols: int = 1241, n_rects: int = 0,
+                right: bool = False):
+    """Seeded synthetic KITTI-shaped frame (orbfe_synth.h). Returns left or (left, right)."""
+    lib = L.lib()
+    left = np.zeros((rows, cols), np.uint8)
+    r = np.zeros((rows, cols), np.uint8) if right else None
+    L.check(lib.orbfe_synth_frame(int(index), rows, cols, int(n_rects), L.ptr(left),
+                                  L.ptr(r) if right else None, c_size_t(cols)), "orbfe_synth_frame")
+    return (left, r) if right else left
