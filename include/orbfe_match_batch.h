@@ -36,6 +36,10 @@ void* orbfe_matcher_stream(orbfe_matcher* m);
  * fallback kernel had to finish the claim order. */
 int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* serial_used);
 
+/* Cap the fixpoint rounds of SearchByProjection (1..12, default 12). With too few rounds the
+ * serial kernel finishes the claim order; tests use this to exercise that path. */
+int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,6 +103,7 @@ _SIGNATURES = {
     "orbfe_matcher_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_stream": (c_void_p, [c_void_p]),
     "orbfe_matcher_last_stats": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
+    "orbfe_matcher_set_max_rounds": (c_int, [c_void_p, c_int]),
     "orbfe_descriptor_distance": (c_int, [c_void_p, c_void_p]),
     "orbfe_descriptor_distance_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "orbfe_search_by_projection_local": (c_int, [c_void_p, POINTER(frame_view),

@@ -525,6 +525,7 @@ struct orbfe_matcher {
   int pairs_cap = 0;
   int32_t* d_serial = nullptr;
   int last_rounds = 0, last_serial = 0;
+  int max_rounds = SBP_MAX_ROUNDS;
 };
 
 namespace {
@@ -805,7 +806,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   a.state = (int32_t*)(A + ostate);
   int32_t* res[2] = {(int32_t*)(A + ores0), (int32_t*)(A + ores1)};
   int32_t* own[2] = {(int32_t*)(A + oown0), (int32_t*)(A + oown1)};
-  for (int r = 0; r < SBP_MAX_ROUNDS && nq > 0; r++) {
+  for (int r = 0; r < m->max_rounds && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];
@@ -951,6 +952,12 @@ extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
     return ORBFE_OK;
   };
   return run_sbp(m, C, N, 1, L->descriptors, L->angle, m->check_ori, plan, make, best_idx, nmatches);
+}
+
+extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
+  if (!m || rounds < 1 || rounds > SBP_MAX_ROUNDS) return ORBFE_ERR_ARG;
+  m->max_rounds = rounds;
+  return ORBFE_OK;
 }
 
 extern "C" int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* serial_used) {

@@ -81,6 +81,9 @@ class ORBmatcher:
             return nm.value, best
         raise TypeError("points must be LocalMapPoints or LastFrameMapPoints")
 
+    def set_max_rounds(self, rounds: int) -> None:
+        L.check(self._lib.orbfe_matcher_set_max_rounds(self._h, int(rounds)), "set_max_rounds")
+
     def last_stats(self) -> Tuple[int, int]:
         r, s = c_int(), c_int()
         L.check(self._lib.orbfe_matcher_last_stats(self._h, byref(r), byref(s)), "last_stats")
