@@ -1,0 +1,351 @@
+#!/usr/bin/env python3
+"""Benchmark: ORB extract + match on synthetic 1241x376 KITTI-shaped stereo frames.
+
+One step = one batch of B stereo frames per GPU (BASELINE.json configs[2], "C3"), inputs already
+resident in HBM:
+  1. ORBextractor::operator() on all 2B images        (k_resize x7, k_fast, k_octree, k_describe)
+  2. vocabulary descent -> FeatureVector for each image (k_vocab; KeyFrame::ComputeBoW's half)
+  3. ORBmatcher::SearchForTriangulation(left_i, right_i) for the B pairs        (k_sft)
+  4. with N > 1 GPUs: RCCL gather of every rank's keypoints + descriptors to rank 0 (config C4)
+value = stereo frames processed by all ranks / max-over-ranks wall time of the K timed steps.
+
+Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]; N > 1 via torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec (ORB extract+match) on 1241×376, 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=32, help="stereo frames per GPU per step")
+    p.add_argument("--rows", type=int, default=376)
+    p.add_argument("--cols", type=int, default=1241)
+    p.add_argument("--nfeatures", type=int, default=2000)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-gather", action="store_true")
+    p.add_argument("--no-kernel-events", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame
+    from orb_slam2_2021_amd import _lib as L
+    from orb_slam2_2021_amd import synthetic as S
+    from orb_slam2_2021_amd.frames import epipole
+    from orb_slam2_2021_amd.vocabulary import ORBVocabulary
+
+    B, H, W = args.batch, args.rows, args.cols
+    n_img = 2 * B
+    # ---- inputs: B stereo frames of this rank, resident in HBM (lefts first, then rights) ----
+    host = np.zeros((n_img, H, W), np.uint8)
+    for i in range(B):
+        idx = rank * B + i
+        l, r = synth_frame(idx, H, W, right=True)
+        host[i], host[B + i] = l, r
+    d_img = torch.from_numpy(host).to(dev)
+    ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
+    cap = ext.max_keypoints(H, W)
+    d_kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
+    d_desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
+    d_cnt = torch.zeros(n_img, dtype=torch.int32, device=dev)
+    # ---- matcher inputs: vocabulary, per-keyframe stereo/MapPoint state, geometry ----
+    tree = S.Vocabulary.synthetic()
+    voc = ORBVocabulary.from_tree(tree, device=dev.index)
+    d_ids = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+    d_offs = torch.empty(n_img * (cap + 1), dtype=torch.int32, device=dev)
+    d_idx = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+    d_nodes = torch.zeros(n_img, dtype=torch.int32, device=dev)
+    rng = np.random.default_rng(1234 + rank)
+    ur = np.where(rng.random((n_img, cap)) < 0.5, rng.uniform(10, 1200, (n_img, cap)), -1.0)
+    d_ur = torch.from_numpy(ur.astype(np.float32)).to(dev)
+    mp = np.where(rng.random((n_img, cap)) < 0.3, L.ORBFE_MP_OBSERVED, L.ORBFE_MP_NONE)
+    d_mp = torch.from_numpy(mp.astype(np.uint8)).to(dev)
+    scale = ext.GetScaleFactors()
+    sigma2 = ext.GetScaleSigmaSquares()
+    d_scale = torch.from_numpy(scale).to(dev)
+    d_sigma2 = torch.from_numpy(sigma2).to(dev)
+    cam = S.KITTI_CAM
+    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    F12 = S.compute_f12(t1, t2, S.intrinsics(cam))
+    dummy = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t1)
+    dummy2 = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t2)
+    ex, ey = epipole(dummy, dummy2)
+    d_m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
+    d_nm = torch.zeros(B, dtype=torch.int32, device=dev)
+    matcher = ORBmatcher(0.6, False, device=dev.index)  # LocalMapping.cc:219
+
+    def view(i):
+        v = L.frame_view()
+        v.n = 0  # read on the device from d_cnt[i]
+        v.keys_un = d_kps.data_ptr() + i * cap * 28
+        v.u_right = d_ur.data_ptr() + i * cap * 4
+        v.descriptors = d_desc.data_ptr() + i * cap * 32
+        v.mp_state = d_mp.data_ptr() + i * cap
+        v.nlevels = 8
+        v.scale_factors = d_scale.data_ptr()
+        v.level_sigma2 = d_sigma2.data_ptr()
+        v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(W), 0.0, float(H)
+        v.grid_inv_w = float(dummy.grid_inv_w)
+        v.grid_inv_h = float(dummy.grid_inv_h)
+        v.fx, v.fy, v.cx, v.cy, v.bf = cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["bf"]
+        v.b = float(dummy.mb)
+        return v
+
+    def fvec(i):
+        f = L.feature_vector()
+        f.n_nodes = 0
+        f.node_ids = d_ids.data_ptr() + i * cap * 4
+        f.offsets = d_offs.data_ptr() + i * (cap + 1) * 4
+        f.indices = d_idx.data_ptr() + i * cap * 4
+        return f
+
+    pairs = (L.sft_pair * B)()
+    for i in range(B):
+        p = pairs[i]
+        p.kf1, p.kf2 = view(i), view(B + i)
+        p.fv1, p.fv2 = fvec(i), fvec(B + i)
+        for k, x in enumerate(F12.reshape(9)):
+            p.f12[k] = float(x)
+        p.ex, p.ey = ex, ey
+        p.match12 = d_m12.data_ptr() + i * cap * 4
+        p.nmatches = d_nm.data_ptr() + i * 4
+        p.kf1_n_dev = d_cnt.data_ptr() + i * 4
+        p.kf2_n_dev = d_cnt.data_ptr() + (B + i) * 4
+        p.fv1_nodes_dev = d_nodes.data_ptr() + i * 4
+        p.fv2_nodes_dev = d_nodes.data_ptr() + (B + i) * 4
+    lib = L.lib()
+    gather = world > 1 and not args.no_gather
+    if gather:
+        g_kps = [torch.empty_like(d_kps) for _ in range(world)] if rank == 0 else None
+        g_desc = [torch.empty_like(d_desc) for _ in range(world)] if rank == 0 else None
+        g_cnt = [torch.empty_like(d_cnt) for _ in range(world)] if rank == 0 else None
+
+    ev = {k: [] for k in ("vocab", "sft")}
+
+    def step(timed_events=False):
+        s = torch.cuda.current_stream(dev).cuda_stream
+        ext.extract_batch_device(n_img, d_img.data_ptr(), H * W, H, W, W, d_kps.data_ptr(),
+                                 d_desc.data_ptr(), cap, d_cnt.data_ptr(), stream=s)
+        if timed_events:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        voc.transform_batch_device(n_img, d_desc.data_ptr(), cap * 32, d_cnt.data_ptr(), 0,
+                                   d_ids.data_ptr(), d_offs.data_ptr(), d_idx.data_ptr(),
+                                   d_nodes.data_ptr(), cap, stream=s)
+        if timed_events:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+        L.check(lib.orbfe_search_for_triangulation_batch_device(
+            matcher._h, B, ctypes.cast(pairs, ctypes.c_void_p), 0, ctypes.c_void_p(s)), "sft batch")
+        if timed_events:
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record()
+            ev["vocab"].append((e0, e1))
+            ev["sft"].append((e1, e2))
+        if gather:
+            dist.gather(d_cnt, g_cnt, dst=0)
+            dist.gather(d_kps, g_kps, dst=0)
+            dist.gather(d_desc, g_desc, dst=0)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # all work goes to one non-default stream, so every library call, torch event and RCCL
+    # collective of a step is ordered on it (a NULL stream would select each handle's own stream)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    use_events = not args.no_kernel_events
+    ext.reset_kernel_times()
+    ext.set_profiling(use_events)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed_events=use_events)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    ext.set_profiling(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    kt = ext.kernel_times()
+    for k in ("vocab", "sft"):
+        if ev[k]:
+            kt["k_" + k] = (sum(a.elapsed_time(b) for a, b in ev[k]), len(ev[k]))
+    counts = d_cnt.cpu().numpy()
+    cand = sum(len(ext.debug_candidates(l, image=i)) for i in range(n_img) for l in range(8))
+    nm = d_nm.cpu().numpy()
+    geo = ext.geometry(H, W)
+    roof = roofline(kt, geo, counts, cand, n_img, B, cap)
+    algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "stereo frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded KITTI-shaped stereo frames, orbfe_synth_frame; synthetic vocabulary)",
+        "config": {
+            "workload": f"C3: stereo extract + SearchForTriangulation, {W}x{H}, batch {B} stereo frames/GPU"
+                        + (" + RCCL gather to rank 0 (C4)" if gather else ""),
+            "nfeatures": args.nfeatures, "scale_factor": 1.2, "nlevels": 8, "ini_th_fast": 20,
+            "min_th_fast": 7, "stereo_frames_per_gpu_per_step": B, "images_per_step_per_gpu": n_img,
+            "parallelism": f"frame-sharded x{world}",
+        },
+        "roofline": roof,
+        "pipeline_hbm": {
+            "algorithmic_bytes_per_stereo_frame": int(algo_frame),
+            "achieved_GBps": round(algo_frame * value / 1e9, 3),
+            "frac_of_peak": round(algo_frame * value / 1e9 / HBM_PEAK_GBS, 6),
+        },
+        "kernels_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in kt.items()},
+        "keypoints_per_image": round(float(counts.mean()), 1),
+        "sft_matches_per_pair": round(float(nm.mean()), 1),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def level_pixels(geo):
+    return [int(w) * int(h) for w, h in geo[:, :2]]
+
+
+def roofline(kt, geo, counts, n_cand, n_img, B, cap):
+    """Roofline of the dominant kernel: ALGORITHMIC bytes per launch / average launch duration.
+    Per-kernel algorithmic bytes (per step; DESIGN.md 'Roofline'):
+      k_resize   sum_l>=1 (px_{l-1} + px_l) per image (read the source level once, write the level)
+      k_fast     sum_l px_l per image + 4 B per FAST candidate + 4 B per cell count
+      k_octree   2 x 4 B per candidate (gather + partition) + 4 B per survivor
+      k_describe sum_l px_l per image (each level read once) + 4 B in + 60 B out per keypoint
+      k_vocab    32 B in + 12 B out per descriptor
+      k_sft      per pair 2 N (32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out"""
+    px = level_pixels(geo)
+    ncells = int(geo[:, 2].sum())
+    nkp = int(counts.sum())
+    per_step = {
+        "k_resize": n_img * sum(px[l - 1] + px[l] for l in range(1, len(px))),
+        "k_fast": n_img * (sum(px) + 4 * ncells) + 4 * n_cand,
+        "k_octree": 8 * n_cand + 4 * nkp,
+        "k_describe": n_img * sum(px) + 64 * nkp,
+        "k_vocab": 44 * nkp,
+        "k_sft": 64 * nkp + 4 * nkp // 2,
+    }
+    dom = max(kt, key=lambda k: kt[k][0])
+    total_ms, launches = kt[dom]
+    steps_equiv = launches / (7 if dom == "k_resize" else 1)
+    bytes_per_launch = per_step[dom] / (7 if dom == "k_resize" else 1)
+    avg_s = total_ms / 1e3 / max(launches, 1)
+    achieved = bytes_per_launch / avg_s / 1e9
+    return {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "avg_launch_us": round(avg_s * 1e6, 2), "launches": launches}
+
+
+def pipeline_bytes_per_stereo_frame(geo, counts, B):
+    """per image sum_l px (read once) + sum_l>=1 px (write) + 60 B per keypoint;
+    SearchForTriangulation per pair 2 N (32 + 28 + 4) + N/4 + 8 N."""
+    px = level_pixels(geo)
+    n_per_img = float(counts.mean())
+    extract = sum(px) + sum(px[1:]) + 60 * n_per_img
+    sft = 2 * n_per_img * 64 + 2 * n_per_img / 8 + 4 * 2 * n_per_img
+    return 2 * extract + sft
+
+
+def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey):
+    """The oracle built with the reference's flags (-O3 -march=native, CMakeLists.txt:10-11) timed
+    on one host core: extract left + right, then SearchForTriangulation(left, right), per stereo
+    frame, for about --cpu-seconds (the vocabulary descent is left out of the CPU timing)."""
+    from oracle import orbref
+    from orb_slam2_2021_amd import synthetic as S
+    ref = orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native")
+    tab = ref.tables()
+    rng = np.random.default_rng(5)
+    t_total, frames = 0.0, 0
+    while (t_total < args.cpu_seconds or frames < 2) and frames < B:
+        l, r = host[frames], host[B + frames]
+        t0 = time.perf_counter()
+        k1, d1 = ref(l)
+        k2, d2 = ref(r)
+        t1 = time.perf_counter()
+        F1 = S.make_frame(k1, d1, tab["scale"], tab["sigma2"], H, W, cam, rng)
+        F2 = S.make_frame(k2, d2, tab["scale"], tab["sigma2"], H, W, cam, rng)
+        F1.feat_vec = tree.feature_vector(d1, 0)
+        F2.feat_vec = tree.feature_vector(d2, 0)
+        t2 = time.perf_counter()
+        orbref.search_for_triangulation(F1, F2, F12, ex, ey, False, False)
+        t3 = time.perf_counter()
+        t_total += (t1 - t0) + (t3 - t2)
+        frames += 1
+    import platform
+    cpu = platform.processor() or "x86_64"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(frames / t_total, 3), "unit": "stereo frames/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{frames} stereo frames {W}x{H} (2 x ORBextractor + SearchForTriangulation) on "
+                      f"1 thread of {cpu}; oracle built -O3 -march=native",
+            "seconds": round(t_total, 2)}
+
+
+if __name__ == "__main__":
+    main()

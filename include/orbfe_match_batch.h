@@ -21,6 +21,12 @@ typedef struct orbfe_sft_pair {
   float ex, ey;
   int32_t* match12;   /* out: kf1.n entries */
   int32_t* nmatches;  /* out: 1 entry */
+  /* Optional device-side sizes, for inputs produced on the device in the same stream (NULL =
+   * use kf1.n / kf2.n / fv1.n_nodes / fv2.n_nodes). */
+  const int32_t* kf1_n_dev;
+  const int32_t* kf2_n_dev;
+  const int32_t* fv1_nodes_dev;
+  const int32_t* fv2_nodes_dev;
 } orbfe_sft_pair;
 
 /* n_pairs independent SearchForTriangulation calls, one workgroup each, async on `stream`

@@ -65,6 +65,11 @@ int orbref_search_for_triangulation(const orbfe_frame_view* kf1, const orbfe_fra
                                     const orbfe_feature_vector* fv2, const float* f12, float ex,
                                     float ey, int only_stereo, int check_ori, int32_t* match12,
                                     int* nmatches);
+/* TemplatedVocabulary::transform -> FeatureVector CSR (see orbfe_vocab.h for the tree layout). */
+int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* node_desc,
+                           const int32_t* first_child, const int32_t* n_children,
+                           const float* weights, const uint8_t* desc, int n, int levelsup,
+                           uint32_t* node_ids, int32_t* offsets, int32_t* indices, int* n_out);
 /* Frame::AssignFeaturesToGrid as CSR (64 x 48 cells, cell = ix*48 + iy): cell_start[3073]. */
 int orbref_build_grid(const orbfe_frame_view* frame, int32_t* cell_start, int32_t* cell_items);
 

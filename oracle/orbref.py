@@ -61,6 +61,8 @@ def lib(kind: str = "checker") -> ctypes.CDLL:
                                                       c_void_p, c_float, c_float, c_int, c_int,
                                                       c_void_p, POINTER(c_int)]
         L.orbref_build_grid.argtypes = [c_void_p, c_void_p, c_void_p]
+        L.orbref_vocab_transform.argtypes = [c_int, c_int] + [c_void_p] * 5 + [c_int, c_int] + \
+            [c_void_p] * 3 + [POINTER(c_int)]
         _libs[kind] = L
     return _libs[kind]
 
@@ -212,3 +214,19 @@ def build_grid(F):
     items = np.zeros(max(F.N, 1), np.int32)
     assert lib().orbref_build_grid(byref(fv), _p(start), _p(items)) == 0
     return start, items[:start[-1]]
+
+
+def vocab_transform(voc, desc: np.ndarray, levelsup: int):
+    """(node_ids, offsets, indices) of TemplatedVocabulary::transform's FeatureVector."""
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(desc)
+    ids = np.zeros(max(n, 1), np.uint32)
+    offs = np.zeros(n + 1, np.int32)
+    idx = np.zeros(max(n, 1), np.int32)
+    nn = c_int()
+    st = lib().orbref_vocab_transform(len(voc.descriptors), voc.levels, _p(voc.descriptors),
+                                      _p(voc.first_child), _p(voc.n_children), _p(voc.weights),
+                                      _p(desc), n, levelsup, _p(ids), _p(offs), _p(idx), byref(nn))
+    assert st == 0
+    k = nn.value
+    return ids[:k], offs[:k + 1], idx[:offs[k]]

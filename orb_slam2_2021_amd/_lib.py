@@ -72,7 +72,8 @@ class lastframe_mappoints(Structure):
 class sft_pair(Structure):
     _fields_ = [("kf1", frame_view), ("kf2", frame_view), ("fv1", feature_vector),
                 ("fv2", feature_vector), ("f12", c_float * 9), ("ex", c_float), ("ey", c_float),
-                ("match12", c_void_p), ("nmatches", c_void_p)]
+                ("match12", c_void_p), ("nmatches", c_void_p), ("kf1_n_dev", c_void_p),
+                ("kf2_n_dev", c_void_p), ("fv1_nodes_dev", c_void_p), ("fv2_nodes_dev", c_void_p)]
 
 
 # name -> (restype, argtypes)
@@ -121,6 +122,14 @@ _SIGNATURES = {
     "orbfe_debug_get_candidates": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
     "orbfe_debug_get_level_keys": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
     "orbfe_debug_geometry": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
+    "orbfe_vocab_create": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                   POINTER(c_void_p)]),
+    "orbfe_vocab_destroy": (c_int, [c_void_p]),
+    "orbfe_vocab_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                      c_void_p, POINTER(c_int)]),
+    "orbfe_vocab_transform_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p,
+                                                   c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                   c_int, c_void_p]),
     "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
 }
 

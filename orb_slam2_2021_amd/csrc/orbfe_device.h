@@ -78,6 +78,35 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x, const AtanCons
   return a;
 }
 
+// Exclusive scan of data[0..n) in place by a 256-thread workgroup (4 waves); returns the total.
+// wsum: 4 ints of LDS. Contains __syncthreads(): call from uniform control flow only.
+__device__ inline int block_scan_excl(int* data, int n, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int per = (n + 255) / 256;
+  const int beg = min(t * per, n), end = min(beg + per, n);
+  int s = 0;
+  for (int i = beg; i < end; i++) s += data[i];
+  int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int woff = 0;
+  for (int k = 0; k < w; k++) woff += wsum[k];
+  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int run = woff + inc - s;
+  for (int i = beg; i < end; i++) {
+    const int v = data[i];
+    data[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return total;
+}
+
 #define ORBFE_HIP_CHECK(expr)                                     \
   do {                                                            \
     hipError_t _e = (expr);                                       \

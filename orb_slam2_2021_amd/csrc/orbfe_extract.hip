@@ -323,32 +323,6 @@ struct ONode {
   int32_t begin, count, seq, flags;  // flags: bit0 = key buffer (0: A, 1: B), bit1 = in R set
 };
 
-__device__ int block_scan_excl(int* data, int n, int* wsum) {
-  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int per = (n + 255) / 256;
-  const int beg = min(t * per, n), end = min(beg + per, n);
-  int s = 0;
-  for (int i = beg; i < end; i++) s += data[i];
-  int inc = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  int woff = 0;
-  for (int k = 0; k < w; k++) woff += wsum[k];
-  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  int run = woff + inc - s;
-  for (int i = beg; i < end; i++) {
-    const int v = data[i];
-    data[i] = run;
-    run += v;
-  }
-  __syncthreads();
-  return total;
-}
 
 __device__ __forceinline__ int child_of(uint32_t key, int mx, int my) {
   return (key_x(key) >= mx ? 1 : 0) | (key_y(key) >= my ? 2 : 0);

@@ -79,9 +79,17 @@ __global__ __launch_bounds__(256) void k_sft(const orbfe_sft_pair* pairs, int on
   __shared__ uint32_t s_claim[SFT_MAX_KF2 / 32];
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_misc[8];
-  const orbfe_sft_pair P = pairs[blockIdx.x];
+  orbfe_sft_pair P = pairs[blockIdx.x];
+  if (P.kf1_n_dev) P.kf1.n = *P.kf1_n_dev;
+  if (P.kf2_n_dev) P.kf2.n = *P.kf2_n_dev;
+  if (P.fv1_nodes_dev) P.fv1.n_nodes = *P.fv1_nodes_dev;
+  if (P.fv2_nodes_dev) P.fv2.n_nodes = *P.fv2_nodes_dev;
   const orbfe_frame_view& K1 = P.kf1;
   const orbfe_frame_view& K2 = P.kf2;
+  if (K2.n > SFT_MAX_KF2) {  // device-side size beyond the claim bitmap: report no matches
+    if (threadIdx.x == 0) *P.nmatches = -1;
+    return;
+  }
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
   const int nwords = (K2.n + 31) >> 5;
   for (int i = t; i < K1.n; i += 256) P.match12[i] = -1;
