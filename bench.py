@@ -125,7 +125,7 @@ def main():
 
     def fvec(i):
         f = L.feature_vector()
-        f.n_nodes = 0
+        f.n_nodes = min(cap, tree.k ** tree.levels)  # upper bound; the count is read on the device
         f.node_ids = d_ids.data_ptr() + i * cap * 4
         f.offsets = d_offs.data_ptr() + i * (cap + 1) * 4
         f.indices = d_idx.data_ptr() + i * cap * 4

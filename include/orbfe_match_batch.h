@@ -22,7 +22,8 @@ typedef struct orbfe_sft_pair {
   int32_t* match12;   /* out: kf1.n entries */
   int32_t* nmatches;  /* out: 1 entry */
   /* Optional device-side sizes, for inputs produced on the device in the same stream (NULL =
-   * use kf1.n / kf2.n / fv1.n_nodes / fv2.n_nodes). */
+   * use kf1.n / kf2.n / fv1.n_nodes / fv2.n_nodes). With fv1_nodes_dev set, fv1.n_nodes must
+   * still hold an upper bound of the node count: it sizes the launch grid. */
   const int32_t* kf1_n_dev;
   const int32_t* kf2_n_dev;
   const int32_t* fv1_nodes_dev;

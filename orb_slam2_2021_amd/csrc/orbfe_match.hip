@@ -73,130 +73,189 @@ __device__ void three_maxima_dev(const int* h, int& ind1, int& ind2, int& ind3) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// SearchForTriangulation
-__global__ __launch_bounds__(256) void k_sft(const orbfe_sft_pair* pairs, int only_stereo,
-                                             int check_ori) {
-  __shared__ uint32_t s_claim[SFT_MAX_KF2 / 32];
-  __shared__ int s_hist[HISTO_LENGTH];
-  __shared__ int s_misc[8];
-  orbfe_sft_pair P = pairs[blockIdx.x];
+// SearchForTriangulation: k_sft_init (match12 = -1), k_sft_nodes (one wavefront per common
+// vocabulary node, many workgroups per pair), k_sft_finish (rotation filter + count per pair).
+__device__ __forceinline__ void sft_resolve_sizes(orbfe_sft_pair& P) {
   if (P.kf1_n_dev) P.kf1.n = *P.kf1_n_dev;
   if (P.kf2_n_dev) P.kf2.n = *P.kf2_n_dev;
   if (P.fv1_nodes_dev) P.fv1.n_nodes = *P.fv1_nodes_dev;
   if (P.fv2_nodes_dev) P.fv2.n_nodes = *P.fv2_nodes_dev;
-  const orbfe_frame_view& K1 = P.kf1;
-  const orbfe_frame_view& K2 = P.kf2;
-  if (K2.n > SFT_MAX_KF2) {  // device-side size beyond the claim bitmap: report no matches
-    if (threadIdx.x == 0) *P.nmatches = -1;
-    return;
+}
+
+__global__ __launch_bounds__(256) void k_sft_init(const orbfe_sft_pair* pairs) {
+  orbfe_sft_pair P = pairs[blockIdx.x];
+  sft_resolve_sizes(P);
+  for (int i = threadIdx.x; i < P.kf1.n; i += 256) P.match12[i] = -1;
+}
+
+#define SFT_REG_CHUNKS 4  // node-2 candidates held in registers: 4 x 64 per wavefront
+#define SFT_MAX_NODE (SFT_MAX_KF2)
+
+// Candidate state of one lane for one 64-wide chunk of a node's KF2 features.
+struct SftCand {
+  uint4 d0, d1;
+  float x, y, epi_thr;   // epi_thr = 100 * mvScaleFactors[octave] (:761)
+  double sig_thr;        // 3.84 * mvLevelSigma2[octave] (:162)
+  int idx2;
+  bool usable, stereo;   // usable: in range, no MapPoint, stereo if bOnlyStereo
+};
+
+__device__ __forceinline__ void sft_load_cand(const orbfe_sft_pair& P, int o2, int n2, int p,
+                                              int only_stereo, SftCand& c) {
+  c.usable = false;
+  c.idx2 = -1;
+  if (p >= n2) return;
+  const int idx2 = P.fv2.indices[o2 + p];
+  c.idx2 = idx2;
+  if (P.kf2.mp_state[idx2] != ORBFE_MP_NONE) return;
+  c.stereo = P.kf2.u_right[idx2] >= 0;
+  if (only_stereo && !c.stereo) return;
+  const orbfe_keypoint kp2 = P.kf2.keys_un[idx2];
+  load_desc(P.kf2.descriptors + (size_t)idx2 * 32, c.d0, c.d1);
+  c.x = kp2.x;
+  c.y = kp2.y;
+  c.epi_thr = 100 * P.kf2.scale_factors[kp2.octave];
+  c.sig_thr = 3.84 * (double)P.kf2.level_sigma2[kp2.octave];
+  c.usable = true;
+}
+
+// Key of a passing candidate: smallest distance, then the LAST position (ties replace, :752).
+__device__ __forceinline__ unsigned long long sft_key(const SftCand& c, bool claimed, int p,
+                                                      const uint4& a0, const uint4& a1, bool st1,
+                                                      float ex, float ey, float la, float lb,
+                                                      float lc, float den) {
+  if (!c.usable || claimed) return ~0ull;
+  const int dist = hamming256(a0, a1, c.d0, c.d1);
+  if (dist > TH_LOW) return ~0ull;
+  if (!st1 && !c.stereo) {
+    const float dex = ex - c.x, dey = ey - c.y;
+    if (dex * dex + dey * dey < c.epi_thr) return ~0ull;
   }
-  const int t = threadIdx.x, w = wave_id(), lane = lane_id();
-  const int nwords = (K2.n + 31) >> 5;
-  for (int i = t; i < K1.n; i += 256) P.match12[i] = -1;
-  for (int i = t; i < nwords; i += 256) s_claim[i] = 0;
-  if (t < HISTO_LENGTH) s_hist[t] = 0;
-  if (t == 0) s_misc[4] = 0;
-  __syncthreads();
+  if (den == 0) return ~0ull;  // CheckDistEpipolarLine (:153-162)
+  const float num = la * c.x + lb * c.y + lc;
+  const float dsqr = num * num / den;
+  if (!((double)dsqr < c.sig_thr)) return ~0ull;
+  return ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
+}
+
+__global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
+  __shared__ uint32_t s_claim_far[4][SFT_MAX_NODE / 32];  // claims beyond the register chunks
+  orbfe_sft_pair P = pairs[blockIdx.y];
+  sft_resolve_sizes(P);
+  const int w = wave_id(), lane = lane_id();
+  const int a = blockIdx.x * 4 + w;
+  if (a >= P.fv1.n_nodes || P.kf2.n > SFT_MAX_KF2) return;
+  const uint32_t id = P.fv1.node_ids[a];
+  int lo = 0, hi = P.fv2.n_nodes;  // the merge-join visits exactly the common node ids (:705-804)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (P.fv2.node_ids[mid] < id) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo >= P.fv2.n_nodes || P.fv2.node_ids[lo] != id) return;
+  const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
+  const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
+  uint32_t* far = s_claim_far[w];
+  if (n2 > SFT_REG_CHUNKS * 64)
+    for (int i = lane; i < (n2 + 31) / 32; i += 64) far[i] = 0;
+  SftCand c0, c1, c2, c3;
+  sft_load_cand(P, o2, n2, lane, only_stereo, c0);
+  sft_load_cand(P, o2, n2, 64 + lane, only_stereo, c1);
+  sft_load_cand(P, o2, n2, 128 + lane, only_stereo, c2);
+  sft_load_cand(P, o2, n2, 192 + lane, only_stereo, c3);
+  bool cl0 = false, cl1 = false, cl2 = false, cl3 = false;
   const float* F = P.f12;
-  for (int a = w; a < P.fv1.n_nodes; a += 4) {
-    const uint32_t id = P.fv1.node_ids[a];
-    // lower_bound in fv2 (the merge-join visits exactly the common node ids, :705-804)
-    int lo = 0, hi = P.fv2.n_nodes;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (P.fv2.node_ids[mid] < id) lo = mid + 1;
-      else hi = mid;
+  const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
+              f7 = F[7], f8 = F[8];
+  for (int p1 = o1; p1 < e1; p1++) {
+    const int idx1 = P.fv1.indices[p1];
+    if (P.kf1.mp_state[idx1] != ORBFE_MP_NONE) continue;
+    const bool st1 = P.kf1.u_right[idx1] >= 0;
+    if (only_stereo && !st1) continue;
+    const orbfe_keypoint kp1 = P.kf1.keys_un[idx1];
+    uint4 a0, a1;
+    load_desc(P.kf1.descriptors + (size_t)idx1 * 32, a0, a1);
+    // epipolar line l = x1' F12 (CheckDistEpipolarLine :149-151)
+    const float la = kp1.x * f0 + kp1.y * f3 + f6;
+    const float lb = kp1.x * f1 + kp1.y * f4 + f7;
+    const float lc = kp1.x * f2 + kp1.y * f5 + f8;
+    const float den = la * la + lb * lb;
+    unsigned long long best = sft_key(c0, cl0, lane, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
+    unsigned long long k;
+    if (n2 > 64) {
+      k = sft_key(c1, cl1, 64 + lane, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
+      best = k < best ? k : best;
     }
-    if (lo >= P.fv2.n_nodes || P.fv2.node_ids[lo] != id) continue;
-    const int b = lo;
-    const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
-    const int o2 = P.fv2.offsets[b], n2 = P.fv2.offsets[b + 1] - o2;
-    for (int p1 = o1; p1 < e1; p1++) {
-      const int idx1 = P.fv1.indices[p1];
-      if (K1.mp_state[idx1] != ORBFE_MP_NONE) continue;
-      const bool st1 = K1.u_right[idx1] >= 0;
-      if (only_stereo && !st1) continue;
-      const orbfe_keypoint kp1 = K1.keys_un[idx1];
-      uint4 d10, d11;
-      load_desc(K1.descriptors + (size_t)idx1 * 32, d10, d11);
-      // epipolar line of kp1 in KF2 (CheckDistEpipolarLine :149-151)
-      const float la = kp1.x * F[0] + kp1.y * F[3] + F[6];
-      const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
-      const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
-      const float den = la * la + lb * lb;
-      unsigned long long best = ~0ull;
-      for (int c0 = 0; c0 < n2; c0 += 64) {
-        const int p = c0 + lane;
-        if (p < n2) {
-          const int idx2 = P.fv2.indices[o2 + p];
-          const bool claimed = (s_claim[idx2 >> 5] >> (idx2 & 31)) & 1u;
-          if (!claimed && K2.mp_state[idx2] == ORBFE_MP_NONE) {
-            const bool st2 = K2.u_right[idx2] >= 0;
-            if (!(only_stereo && !st2)) {
-              uint4 d20, d21;
-              load_desc(K2.descriptors + (size_t)idx2 * 32, d20, d21);
-              const int dist = hamming256(d10, d11, d20, d21);
-              if (dist <= TH_LOW) {
-                const orbfe_keypoint kp2 = K2.keys_un[idx2];
-                bool ok = true;
-                if (!st1 && !st2) {
-                  const float dex = P.ex - kp2.x, dey = P.ey - kp2.y;
-                  if (dex * dex + dey * dey < 100 * K2.scale_factors[kp2.octave]) ok = false;
-                }
-                if (ok) {
-                  const float num = la * kp2.x + lb * kp2.y + lc;
-                  if (den == 0) ok = false;
-                  else {
-                    const float dsqr = num * num / den;
-                    ok = (double)dsqr < 3.84 * (double)K2.level_sigma2[kp2.octave];
-                  }
-                }
-                if (ok) {
-                  // min distance; among equal distances the LAST candidate (ties replace, :752)
-                  const unsigned long long key =
-                      ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
-                  best = key < best ? key : best;
-                }
-              }
-            }
-          }
-        }
+    if (n2 > 128) {
+      k = sft_key(c2, cl2, 128 + lane, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
+      best = k < best ? k : best;
+    }
+    if (n2 > 192) {
+      k = sft_key(c3, cl3, 192 + lane, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
+      best = k < best ? k : best;
+    }
+    for (int cbase = SFT_REG_CHUNKS * 64; cbase < n2; cbase += 64) {  // very large nodes
+      SftCand cx;
+      const int p = cbase + lane;
+      sft_load_cand(P, o2, n2, p, only_stereo, cx);
+      const bool clx = p < n2 && ((far[p >> 5] >> (p & 31)) & 1u);
+      k = sft_key(cx, clx, p, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
+      best = k < best ? k : best;
+    }
+    best = wave_min_u64(best);
+    if (best != ~0ull) {
+      const int p = 0x7fffffff - (int)(best & 0xffffffffull);
+      // vbMatched2[bestIdx2] = true (:776): the owning lane marks its candidate claimed
+      cl0 = cl0 || (p == lane);
+      cl1 = cl1 || (p == 64 + lane);
+      cl2 = cl2 || (p == 128 + lane);
+      cl3 = cl3 || (p == 192 + lane);
+      if (lane == 0) {
+        P.match12[idx1] = P.fv2.indices[o2 + p];
+        if (p >= SFT_REG_CHUNKS * 64) far[p >> 5] |= 1u << (p & 31);
       }
-      best = wave_min_u64(best);
-      if (best != ~0ull) {
-        const int p = 0x7fffffff - (int)(best & 0xffffffffull);
-        const int idx2 = P.fv2.indices[o2 + p];
-        if (lane == 0) {
-          P.match12[idx1] = idx2;
-          atomicOr(&s_claim[idx2 >> 5], 1u << (idx2 & 31));  // other waves share the word
-        }
+      if (p >= SFT_REG_CHUNKS * 64) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void k_sft_finish(const orbfe_sft_pair* pairs, int check_ori) {
+  __shared__ int s_hist[HISTO_LENGTH];
+  __shared__ int s_misc[8];
+  orbfe_sft_pair P = pairs[blockIdx.x];
+  sft_resolve_sizes(P);
+  const int t = threadIdx.x, lane = lane_id();
+  if (t < HISTO_LENGTH) s_hist[t] = 0;
+  if (t == 0) s_misc[4] = 0;
   __syncthreads();
-  if (check_ori) {
-    for (int i = t; i < K1.n; i += 256) {
+  if (P.kf2.n > SFT_MAX_KF2) {
+    if (t == 0) *P.nmatches = ORBFE_ERR_CAPACITY;
+    return;
+  }
+  if (check_ori) {  // rotation consistency (:806-826)
+    for (int i = t; i < P.kf1.n; i += 256) {
       const int m = P.match12[i];
-      if (m >= 0) atomicAdd(&s_hist[rot_bin_dev(K1.keys_un[i].angle, K2.keys_un[m].angle)], 1);
+      if (m >= 0) atomicAdd(&s_hist[rot_bin_dev(P.kf1.keys_un[i].angle, P.kf2.keys_un[m].angle)], 1);
     }
     __syncthreads();
     if (t == 0) three_maxima_dev(s_hist, s_misc[0], s_misc[1], s_misc[2]);
     __syncthreads();
     const int i1 = s_misc[0], i2 = s_misc[1], i3 = s_misc[2];
-    for (int i = t; i < K1.n; i += 256) {
+    for (int i = t; i < P.kf1.n; i += 256) {
       const int m = P.match12[i];
       if (m >= 0) {
-        const int bin = rot_bin_dev(K1.keys_un[i].angle, K2.keys_un[m].angle);
+        const int bin = rot_bin_dev(P.kf1.keys_un[i].angle, P.kf2.keys_un[m].angle);
         if (bin != i1 && bin != i2 && bin != i3) P.match12[i] = -1;
       }
     }
     __syncthreads();
   }
   int cnt = 0;
-  for (int i = t; i < K1.n; i += 256) cnt += P.match12[i] >= 0;
+  for (int i = t; i < P.kf1.n; i += 256) cnt += P.match12[i] >= 0;
   cnt = wave_sum(cnt);
   if (lane == 0) atomicAdd(&s_misc[4], cnt);
   __syncthreads();
@@ -682,7 +741,13 @@ extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int
   for (int p = 0; p < n_pairs; p++)
     if (pairs[p].kf2.n > SFT_MAX_KF2) return orbfe_set_error(ORBFE_ERR_ARG, "sft: KF2 too large");
   ORBFE_HIP_CHECK(hipMemcpyAsync(m->d_pairs, pairs, sizeof(orbfe_sft_pair) * n_pairs, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_sft, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, only_stereo ? 1 : 0, m->check_ori);
+  // fv1.n_nodes bounds the node grid (with fv1_nodes_dev set it must be an upper bound)
+  int max_nodes = 1;
+  for (int p = 0; p < n_pairs; p++) max_nodes = std::max(max_nodes, pairs[p].fv1.n_nodes);
+  hipLaunchKernelGGL(k_sft_init, dim3(n_pairs), dim3(256), 0, s, m->d_pairs);
+  hipLaunchKernelGGL(k_sft_nodes, dim3((max_nodes + 3) / 4, n_pairs), dim3(256), 0, s, m->d_pairs,
+                     only_stereo ? 1 : 0);
+  hipLaunchKernelGGL(k_sft_finish, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, m->check_ori);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }
