@@ -263,7 +263,10 @@ def roofline(kt, geo, counts, n_cand, n_img, B, cap):
       k_resize   sum_l>=1 (px_{l-1} + px_l) per image (read the source level once, write the level)
       k_fast     sum_l px_l per image + 4 B per FAST candidate + 4 B per cell count
       k_octree   2 x 4 B per candidate (gather + partition) + 4 B per survivor
-      k_describe sum_l px_l per image (each level read once) + 4 B in + 60 B out per keypoint
+      k_blur     2 x sum_l px_l per image (read each level once, write its blurred copy)
+      k_copy0    2 x px_0 per image
+      k_describe 4 B in + 60 B out per keypoint (+ 749 + 512 gathered bytes per keypoint, not
+                 counted: they overlap between keypoints and come from L2)
       k_vocab    32 B in + 12 B out per descriptor
       k_sft      per pair 2 N (32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out"""
     px = level_pixels(geo)
@@ -273,7 +276,9 @@ def roofline(kt, geo, counts, n_cand, n_img, B, cap):
         "k_resize": n_img * sum(px[l - 1] + px[l] for l in range(1, len(px))),
         "k_fast": n_img * (sum(px) + 4 * ncells) + 4 * n_cand,
         "k_octree": 8 * n_cand + 4 * nkp,
-        "k_describe": n_img * sum(px) + 64 * nkp,
+        "k_describe": 64 * nkp + n_img * 0,  # + the patch pixels it gathers
+        "k_blur": n_img * 2 * sum(px),
+        "k_copy0": n_img * 2 * px[0],
         "k_vocab": 44 * nkp,
         "k_sft": 64 * nkp + 4 * nkp // 2,
     }

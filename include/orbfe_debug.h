@@ -16,6 +16,8 @@ int orbfe_debug_get_candidates(orbfe_extractor* h, int image, int level, uint32_
 /* Octree survivors of (image, level) in output order, level coordinates. */
 int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level, uint32_t* out, int cap,
                                int* n);
+/* GaussianBlur(7x7, 2, REFLECT_101) of (image, level) as computed for the descriptors. */
+int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level, uint8_t* out, int cap);
 /* Per level: w, h, ncells, candidate capacity, budget, nIni, key capacity (7 ints per level). */
 int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, int cap);
 #ifdef __cplusplus

@@ -53,7 +53,7 @@ extern "C" const char* orbfe_version(void) { return "orbfe 0.1 gfx950"; }
 struct LevelDesc {
   int w, h, pitch;
   int pad0;
-  long long pyr_off;     // byte offset of this level inside one image's pyramid block (l >= 1)
+  long long pyr_off;     // byte offset of column 0, row 0 of this level in one image's block
   int cell_begin, ncells;
   int cand_begin, cand_cap;  // candidate slots of this level inside one image's candidate block
   int budget;                // mnFeaturesPerLevel[l]
@@ -65,6 +65,7 @@ struct LevelDesc {
   int size;                  // scaledPatchSize (:840)
   int tab_x, tab_y;          // resize table offsets (l >= 1)
   int xmax, simd_end;        // resize: first column using the clamped path / end of SIMD columns
+  int tile_begin, tiles_x;   // k_blur tiles of this level
 };
 
 struct CellDesc {
@@ -77,11 +78,12 @@ struct ExtractArgs {
   const CellDesc* cells;
   const int2* xtab;
   const int2* ytab;
-  int nlevels, ncells, n_images, total_key_slots;
+  int nlevels, ncells, n_images, total_key_slots, blur_strips;
   const uint8_t* img0;
   long long img_stride;
   int img_pitch, pad1;
   uint8_t* pyr;
+  uint8_t* blur;  // blurred levels, same layout as pyr
   long long pyr_stride;
   uint32_t* cand;
   long long cand_stride;
@@ -114,12 +116,33 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ const uint8_t* level_ptr(const ExtractArgs& a, const LevelDesc& ld,
                                                     int img, int l, int& pitch) {
-  if (l == 0) {
-    pitch = a.img_pitch;
-    return a.img0 + (long long)img * a.img_stride;
-  }
+  (void)l;  // every level, the copied input included, lives in the pyramid block
   pitch = ld.pitch;
   return a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+}
+
+// k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows), so every
+// kernel reads every level with aligned dword loads whatever the caller's pitch.
+__global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
+  const LevelDesc ld = a.levels[0];
+  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  const int img = blockIdx.z;
+  if (x >= ld.w || y >= ld.h) return;
+  const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch + x;
+  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
+  uint32_t v = 0;
+  const int n = min(4, ld.w - x);
+  for (int k = 0; k < n; k++) {
+    const uint8_t b = src[k];
+    v |= (uint32_t)b << (8 * k);
+    const int xx = x + k;
+    if (xx >= 1 && xx <= 3) row[-xx] = b;                        // REFLECT_101 column -xx
+    if (xx >= ld.w - 4 && xx <= ld.w - 2) row[2 * ld.w - 2 - xx] = b;  // column 2w-2-xx
+  }
+  if (n == 4) *reinterpret_cast<uint32_t*>(row + x) = v;
+  else
+    for (int k = 0; k < n; k++) row[x + k] = (uint8_t)(v >> (8 * k));  // keep the padding bytes
 }
 
 __device__ __forceinline__ int sat16(int v) { return min(max(v, -32768), 32767); }
@@ -159,8 +182,11 @@ __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
   } else {  // FixedPtCast<int, uchar, 22>
     v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
   }
-  uint8_t* dst = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-  dst[(long long)y * ld.pitch + x] = (uint8_t)min(max(v, 0), 255);
+  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
+  const uint8_t b = (uint8_t)min(max(v, 0), 255);
+  row[x] = b;
+  if (x >= 1 && x <= 3) row[-x] = b;                         // REFLECT_101 padding for k_blur
+  if (x >= ld.w - 4 && x <= ld.w - 2) row[2 * ld.w - 2 - x] = b;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -237,16 +263,50 @@ __device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }
 
 // k_fast: one wavefront per cell (4 cells per 256-thread workgroup). No workgroup barriers: waves
 // are independent and synchronise their own LDS with wave_sync().
+//   1. the cell ROI (<= roi_w_max x roi_h_max) lands in LDS with aligned dword loads;
+//   2. OpenCV's antipodal quick test at the lower threshold runs on every detection pixel and the
+//      survivors are compacted (ballot + popcount, row-major order kept);
+//   3. the full arc strength runs only on the compacted list, full waves;
+//   4. strict 3x3 NMS at iniThFAST (then minThFAST for an empty cell) visits only list entries.
+__device__ __forceinline__ bool quick_test(const uint8_t* p, int s, int t) {
+  const int v = p[0];
+  int d = 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int x = p[ring_off(k, s)], y = p[ring_off(k + 8, s)];
+    const int ta = (x < v - t ? 1 : 0) | (x > v + t ? 2 : 0);
+    const int tb = (y < v - t ? 1 : 0) | (y > v + t ? 2 : 0);
+    d &= ta | tb;
+  }
+  return d != 0;
+}
+
+struct FastLds {
+  int rs, roi, m8, list;  // row stride and byte offsets inside one wave's region
+  int total;
+};
+__host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max) {
+  FastLds f;
+  f.rs = (rw_max + 4 + 3) & ~3;
+  f.roi = 0;
+  f.m8 = (f.rs * rh_max + 15) & ~15;
+  f.list = f.m8 + (((rw_max - 4) * (rh_max - 4) + 15) & ~15);
+  f.total = f.list + (((rw_max - 6) * (rh_max - 6) * 2 + 15) & ~15);
+  return f;
+}
+
 __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int w = wave_id(), lane = lane_id();
   const int cell = blockIdx.x * 4 + w;
   const int img = blockIdx.y;
   if (cell >= a.ncells) return;
-  const int roi_bytes = (a.roi_w_max * a.roi_h_max + 15) & ~15;
-  const int m_bytes = ((a.roi_w_max - 4) * (a.roi_h_max - 4) + 15) & ~15;
-  uint8_t* roi = smem + w * (roi_bytes + m_bytes);
-  uint8_t* m8 = roi + roi_bytes;
+  const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max);
+  uint8_t* base = smem + w * lay.total;
+  uint8_t* roi = base + lay.roi;
+  uint8_t* m8 = base + lay.m8;
+  uint16_t* list = reinterpret_cast<uint16_t*>(base + lay.list);
+  const int RS = lay.rs;
 
   const CellDesc cd = a.cells[cell];
   const LevelDesc ld = a.levels[cd.level];
@@ -259,33 +319,78 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
     if (lane == 0) *cnt_out = 0;
     return;
   }
-  for (int i = lane; i < rw * rh; i += 64) {
-    const int r = i / rw, c = i - r * rw;
-    roi[i] = lev[(long long)(cd.y0 + r) * pitch + cd.x0 + c];
+  // 1. ROI -> LDS: dword-aligned columns [x0a, x0a + 4 nw) cover [x0, x0 + rw)
+  const int x0a = cd.x0 & ~3, xo = cd.x0 - x0a, nw = (xo + rw + 3) >> 2;
+  for (int i0 = 0; i0 < nw * rh; i0 += 8 * 64) {  // up to 8 dword loads per lane in flight
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = i0 + lane + 64 * k;
+      if (i < nw * rh) {
+        const int r = i / nw, c = i - r * nw;
+        v[k] = *reinterpret_cast<const uint32_t*>(lev + (long long)(cd.y0 + r) * pitch + x0a + 4 * c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int i = i0 + lane + 64 * k;
+      if (i < nw * rh) {
+        const int r = i / nw, c = i - r * nw;
+        *reinterpret_cast<uint32_t*>(roi + r * RS + 4 * c) = v[k];
+      }
+    }
   }
   for (int i = lane; i < mw * mh; i += 64) m8[i] = 0;
   wave_sync();
-  for (int q = lane; q < dw * dh; q += 64) {
-    const int rr = q / dw, cc = q - rr * dw;
-    const int m = arc_strength_lds(roi + (rr + 3) * rw + (cc + 3), rw, a.tlow);
-    m8[(rr + 1) * mw + (cc + 1)] = (uint8_t)min(m, 255);
+  const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
+  // 2. quick test, compacted in row-major order
+  int nlist = 0;
+  for (int q0 = 0; q0 < dw * dh; q0 += 64) {
+    const int q = q0 + lane;
+    bool pass = false;
+    if (q < dw * dh) {
+      const int rr = q / dw, cc = q - rr * dw;
+      pass = quick_test(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
+    }
+    const uint64_t bal = wave_ballot(pass);
+    if (pass) list[nlist + prefix_in_wave(bal)] = (uint16_t)q;
+    nlist += __popcll(bal);
   }
   wave_sync();
+  // 3. arc strength on the list; keep entries that are corners at the lower threshold
+  int ncorner = 0;
+  for (int j0 = 0; j0 < nlist; j0 += 64) {
+    const int j = j0 + lane;
+    int q = 0, m = 0;
+    if (j < nlist) {
+      q = list[j];
+      const int rr = q / dw, cc = q - rr * dw;
+      m = arc_strength_lds(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
+      m8[(rr + 1) * mw + (cc + 1)] = (uint8_t)min(m, 255);
+    }
+    const uint64_t bal = wave_ballot(m > 0);
+    wave_sync();  // every lane has read list[j0 .. j0+63] before it is overwritten
+    if (m > 0) list[ncorner + prefix_in_wave(bal)] = (uint16_t)q;
+    ncorner += __popcll(bal);
+  }
+  wave_sync();
+  // 4. NMS over the corners (out-of-region and non-corner neighbours score 0)
   uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
   int count = 0;
   for (int pass = 0; pass < 2; pass++) {
     const int t = min(max(pass == 0 ? a.ini_th : a.min_th, 0), 255);
-    for (int q0 = 0; q0 < dw * dh; q0 += 64) {
-      const int q = q0 + lane;
+    for (int j0 = 0; j0 < ncorner; j0 += 64) {
+      const int j = j0 + lane;
       bool keep = false;
-      int rr = 0, cc = 0, s = 0;
-      if (q < dw * dh) {
+      int rr = 0, cc = 0, sc = 0;
+      if (j < ncorner) {
+        const int q = list[j];
         rr = q / dw;
         cc = q - rr * dw;
         const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
         const int m = mp[0];
         if (m >= t + 1) {
-          s = m - 1;
+          sc = m - 1;
           keep = true;
 #pragma unroll
           for (int k = 0; k < 8; k++) {
@@ -293,12 +398,12 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
                           k == 4 ? 1 : k == 5 ? mw - 1 : k == 6 ? mw : mw + 1;
             const int mn = mp[o];
             const int sn = mn >= t + 1 ? mn - 1 : 0;
-            keep = keep && (s > sn);
+            keep = keep && (sc > sn);
           }
         }
       }
       const uint64_t bal = wave_ballot(keep);
-      if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, s);
+      if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, sc);
       count += __popcll(bal);
     }
     if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
@@ -641,20 +746,107 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_describe: one wavefront per surviving keypoint.
-#define PATCH_R 21  // 18 (max |rotated pattern offset|) + 3 (blur half-width)
-#define PATCH_N (2 * PATCH_R + 1)  // 43
-#define PATCH_S 44
-#define BLUR_N 37
-#define BLUR_S 40
+// k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (ORBextractor.cc:1083-1084),
+// OpenCV's bit-exact fixed-point form: H = sum k_i p_i (8.8), out = (sum k_j H_j + 2^15) >> 16 with
+// k = [18, 34, 49, 54, 49, 34, 18]. One workgroup per 128 x 16 output tile: the (134 x 22) source
+// tile with reflected borders goes to LDS, the horizontal pass to a u16 LDS tile, the vertical
+// pass to HBM. Tiles of all levels of all images form one launch.
+#define BS_W 256  // columns per wavefront strip (4 per lane)
+#define BS_H 32   // output rows per strip
 __device__ __forceinline__ int reflect101(int i, int n) {
   return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
 
+// Horizontal 7-tap sums of the 4 pixels x..x+3 (bytes 4..7 of P|C|N)
+__device__ __forceinline__ void blur_h4(uint32_t P, uint32_t C, uint32_t N, uint32_t* h) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    // bytes at columns x+j-3 .. x+j+3 = window bytes j+1 .. j+7
+    // v_alignbyte_b32 shifts by (S2 & 3) bytes: j = 3 takes whole dwords
+    const uint32_t lo = j == 3 ? C : __builtin_amdgcn_alignbyte(C, P, j + 1);  // bytes j+1 .. j+4
+    const uint32_t hi = j == 3 ? N : __builtin_amdgcn_alignbyte(N, C, j + 1);  // bytes j+5 .. j+8
+    const uint32_t a0 = lo & 0xff, a1 = (lo >> 8) & 0xff, a2 = (lo >> 16) & 0xff, a3 = lo >> 24;
+    const uint32_t a4 = hi & 0xff, a5 = (hi >> 8) & 0xff, a6 = (hi >> 16) & 0xff;
+    h[j] = 18u * (a0 + a6) + 34u * (a1 + a5) + 49u * (a2 + a4) + 54u * a3;
+  }
+}
+
+// k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (ORBextractor.cc:1083-1084),
+// OpenCV's bit-exact fixed-point form: H = sum k_i p_i (8.8), out = (sum k_j H_j + 2^15) >> 16 with
+// k = [18, 34, 49, 54, 49, 34, 18]. One wavefront per 256 x 32 strip, each lane 4 columns: one
+// aligned dword per input row, neighbours by cross-lane shuffles, the 7-row vertical window in
+// registers, one dword store per output row. Strips of all levels of all images in one launch.
+__global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
+  const int img = blockIdx.y, lane = lane_id();
+  int strip = blockIdx.x * 4 + wave_id(), l = 0;
+  if (strip >= a.blur_strips) return;
+  while (l + 1 < a.nlevels && strip >= a.levels[l + 1].tile_begin) l++;
+  const LevelDesc ld = a.levels[l];
+  strip -= ld.tile_begin;
+  const int sx = strip % ld.tiles_x, sy = strip / ld.tiles_x;
+  const int x = sx * BS_W + 4 * lane, y0 = sy * BS_H;
+  const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+  uint8_t* dst = a.blur + (long long)img * a.pyr_stride + ld.pyr_off;
+  const int w = ld.w, pitch = ld.pitch;
+  // dword C = columns x..x+3; E = the strip-end neighbour (x-4 for lane 0, x+4 for lane 63).
+  // Columns -4..w+7 exist in every row (padding), so no load needs a border branch.
+  const bool cin = x < w + 8, ein = lane == 0 || (lane == 63 && x + 4 < w + 8);
+  const int eoff = lane == 0 ? x - 4 : x + 4;
+  auto row_ptr = [&](int r) { return src + (long long)reflect101(r, ld.h) * pitch; };
+  auto load_c = [&](int r) { return cin ? *reinterpret_cast<const uint32_t*>(row_ptr(r) + x) : 0u; };
+  auto load_e = [&](int r) { return ein ? *reinterpret_cast<const uint32_t*>(row_ptr(r) + eoff) : 0u; };
+  const int yend = min(y0 + BS_H, ld.h);
+  const int nrows = yend - y0 + 6;  // input rows y0-3 .. yend+2
+  // 4-row load lookahead: rows i .. i+3 in flight while row i is consumed
+  uint32_t qc0 = load_c(y0 - 3), qe0 = load_e(y0 - 3);
+  uint32_t qc1 = load_c(y0 - 2), qe1 = load_e(y0 - 2);
+  uint32_t qc2 = load_c(y0 - 1), qe2 = load_e(y0 - 1);
+  uint32_t qc3 = load_c(y0), qe3 = load_e(y0);
+  uint32_t h0[4], h1[4], h2[4], h3[4], h4[4], h5[4], h6[4];
+  for (int i = 0; i < nrows; i++) {
+    const uint32_t C = qc0, E = qe0;
+    qc0 = qc1; qe0 = qe1;
+    qc1 = qc2; qe1 = qe2;
+    qc2 = qc3; qe2 = qe3;
+    if (i + 4 < nrows) {
+      qc3 = load_c(y0 - 3 + i + 4);
+      qe3 = load_e(y0 - 3 + i + 4);
+    }
+    uint32_t P = (uint32_t)__shfl_up((int)C, 1, 64);
+    uint32_t N = (uint32_t)__shfl_down((int)C, 1, 64);
+    if (lane == 0) P = E;
+    if (lane == 63) N = E;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      h0[j] = h1[j];
+      h1[j] = h2[j];
+      h2[j] = h3[j];
+      h3[j] = h4[j];
+      h4[j] = h5[j];
+      h5[j] = h6[j];
+    }
+    blur_h4(P, C, N, h6);
+    if (i >= 6) {
+      const int y = y0 + i - 6;
+      uint32_t o = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t acc = 18u * (h0[j] + h6[j]) + 34u * (h1[j] + h5[j]) +
+                             49u * (h2[j] + h4[j]) + 54u * h3[j];
+        o |= min((acc + 32768u) >> 16, 255u) << (8 * j);
+      }
+      if (x < w) *reinterpret_cast<uint32_t*>(dst + (long long)y * pitch + x) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_describe: one wavefront per surviving keypoint. IC_Angle (:75-102) sums the integer moments of
+// the 749-pixel circle straight from the level (L1/L2 hits); the 256 steered tests (:105-151) read
+// the blurred level; bits land as 4 wave ballots (64 pairs each = 8 descriptor bytes).
+__constant__ int8_t c_circle[2 * 752];  // (v, u) of the IC_Angle circle, 749 used
+
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_raw[4][PATCH_N * PATCH_S];
-  __shared__ __attribute__((aligned(16))) uint16_t s_h[4][PATCH_N * BLUR_N];
-  __shared__ __attribute__((aligned(16))) uint8_t s_blur[4][BLUR_N * BLUR_S];
   const int w = wave_id(), lane = lane_id();
   const int img = blockIdx.y;
   const int slot = blockIdx.x * 4 + w;
@@ -674,59 +866,37 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   for (int k = 0; k < l; k++) obase += lc[k];
   const uint32_t key = a.lvlkeys[(long long)img * a.lvlkey_stride + slot];
   const int cx = key_x(key), cy = key_y(key), score = key_s(key);
-  int pitch;
-  const uint8_t* lev = level_ptr(a, ld, img, l, pitch);
-  uint8_t* raw = s_raw[w];
-  uint16_t* hb = s_h[w];
-  uint8_t* bl = s_blur[w];
-  for (int i = lane; i < PATCH_N * PATCH_N; i += 64) {
-    const int r = i / PATCH_N, c = i - r * PATCH_N;
-    const int y = reflect101(cy - PATCH_R + r, ld.h), x = reflect101(cx - PATCH_R + c, ld.w);
-    raw[r * PATCH_S + c] = lev[(long long)y * pitch + x];
-  }
-  wave_sync();
-  // IC_Angle (:75-102): integer moments over the umax circle of the unblurred level
+  const long long off = (long long)img * a.pyr_stride + ld.pyr_off + (long long)cy * ld.pitch + cx;
+  const uint8_t* center = a.pyr + off;
   int m01 = 0, m10 = 0;
-  for (int i = lane; i < 31 * 31; i += 64) {
-    const int v = i / 31 - 15, u = i - (i / 31) * 31 - 15;
-    if (abs(u) <= a.umax[abs(v)]) {
-      const int val = raw[(PATCH_R + v) * PATCH_S + PATCH_R + u];
-      m10 += u * val;
-      m01 += v * val;
-    }
+  int cv[12], cu[12], val[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {  // 749 circle pixels: 12 independent loads per lane in flight
+    const int i = lane + 64 * k;
+    cv[k] = i < 749 ? c_circle[2 * i] : 0;
+    cu[k] = i < 749 ? c_circle[2 * i + 1] : 0;
+    val[k] = i < 749 ? center[cv[k] * ld.pitch + cu[k]] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    m10 += cu[k] * val[k];
+    m01 += cv[k] * val[k];
   }
   m01 = wave_sum(m01);
   m10 = wave_sum(m10);
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
-  // GaussianBlur 7x7 sigma 2, fixed point (taps 18,34,49,54,49,34,18 / 256), REFLECT_101 through
-  // the reflected patch load
-  for (int i = lane; i < PATCH_N * BLUR_N; i += 64) {
-    const int r = i / BLUR_N, c = i - r * BLUR_N;
-    const uint8_t* p = raw + r * PATCH_S + c;
-    hb[i] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 49 * (p[2] + p[4]) + 54 * p[3]);
-  }
-  wave_sync();
-  for (int i = lane; i < BLUR_N * BLUR_N; i += 64) {
-    const int r = i / BLUR_N, c = i - r * BLUR_N;
-    const uint16_t* p = hb + r * BLUR_N + c;
-    const uint32_t acc = 18u * ((uint32_t)p[0] + p[6 * BLUR_N]) +
-                         34u * ((uint32_t)p[BLUR_N] + p[5 * BLUR_N]) +
-                         49u * ((uint32_t)p[2 * BLUR_N] + p[4 * BLUR_N]) + 54u * p[3 * BLUR_N];
-    bl[r * BLUR_S + c] = (uint8_t)min((acc + 32768u) >> 16, 255u);
-  }
-  wave_sync();
-  // computeOrbDescriptor (:105-151): 256 intensity tests on the rotated pattern
   const float ang = angle * a.factor_pi;
   const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-  const uint8_t* center = bl + 18 * BLUR_S + 18;
+  const uint8_t* bc = a.blur + off;
+  const int pitch = ld.pitch;
   uint64_t words[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int p = q * 64 + lane;
     const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
     const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-    const int t0 = center[cv_round_f(x0 * sb + y0 * ca) * BLUR_S + cv_round_f(x0 * ca - y0 * sb)];
-    const int t1 = center[cv_round_f(x1 * sb + y1 * ca) * BLUR_S + cv_round_f(x1 * ca - y1 * sb)];
+    const int t0 = bc[cv_round_f(x0 * sb + y0 * ca) * pitch + cv_round_f(x0 * ca - y0 * sb)];
+    const int t1 = bc[cv_round_f(x1 * sb + y1 * ca) * pitch + cv_round_f(x1 * ca - y1 * sb)];
     words[q] = wave_ballot(t0 < t1);
   }
   const long long o = (long long)img * a.out_cap + obase;
@@ -785,7 +955,7 @@ struct orbfe_extractor {
   std::vector<CellDesc> cells;
   std::vector<int2> xtab, ytab;
   long long pyr_stride = 0, cand_stride = 0, keyscr_stride = 0, lvlkey_stride = 0;
-  int total_key_slots = 0, roi_w_max = 0, roi_h_max = 0, node_cap = 0, sort_cap = 0;
+  int total_key_slots = 0, roi_w_max = 0, roi_h_max = 0, node_cap = 0, sort_cap = 0, blur_tiles = 0;
   LevelDesc* d_levels = nullptr;
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
@@ -795,6 +965,7 @@ struct orbfe_extractor {
   uint8_t* d_in = nullptr;
   size_t in_bytes = 0;
   uint8_t* d_pyr = nullptr;
+  uint8_t* d_blur = nullptr;
   uint32_t* d_cand = nullptr;
   int32_t* d_cellcnt = nullptr;
   uint32_t* d_keys_a = nullptr;
@@ -818,8 +989,9 @@ struct orbfe_extractor {
   int klaunch[8] = {0};
 };
 
-static const char* kKernelNames[] = {"k_resize", "k_fast", "k_octree", "k_describe"};
-static const int kNumKernels = 4;
+static const char* kKernelNames[] = {"k_resize", "k_fast", "k_octree", "k_describe", "k_copy0",
+                                     "k_blur"};
+static const int kNumKernels = 6;
 
 static hipEvent_t pool_event(orbfe_extractor* h) {
   if (!h->event_pool.empty()) {
@@ -839,7 +1011,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   std::vector<CellDesc> cells;
   std::vector<int2> xt, yt;
   long long pyr = 0;
-  int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0;
+  int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0, tiles = 0;
   for (int l = 0; l < L; l++) {
     LevelDesc& d = lv[l];
     std::memset(&d, 0, sizeof(d));
@@ -858,11 +1030,11 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     d.budget = h->nfeat[l];
     d.scale = h->scale[l];
     d.size = (int)(31 * h->scale[l]);
-    if (l > 0) {
-      d.pitch = (int)align_up(d.w, 64);
-      d.pyr_off = pyr;
-      pyr += (long long)d.pitch * d.h;
-    }
+    // rows carry 4 bytes of left and >= 8 of right padding holding REFLECT_101 columns
+    // (-3..-1 and w..w+2, written by k_copy0 / k_resize) so k_blur reads aligned dwords only
+    d.pitch = (int)align_up(d.w + 4 + 8, 64);
+    d.pyr_off = pyr + 4;  // column 0 of row 0
+    pyr += (long long)d.pitch * d.h;
     // cells (:776-832)
     const float width = (float)bw, height = (float)bh;
     const int nColsC = (int)(width / 30.f), nRowsC = (int)(height / 30.f);
@@ -899,6 +1071,9 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
+    d.tiles_x = (d.w + 255) / 256;  // k_blur strips of 256 x 32
+    d.tile_begin = tiles;
+    tiles += d.tiles_x * ((d.h + 31) / 32);
     d.key_begin = keys;
     d.key_cap = std::max(d.budget + 3, 4 * d.nini);
     keys += d.key_cap;
@@ -968,6 +1143,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->keyscr_stride = h->cand_stride;
   h->lvlkey_stride = (long long)align_up((size_t)keys, 64);
   h->total_key_slots = keys;
+  h->blur_tiles = tiles;
   h->roi_w_max = rwmax;
   h->roi_h_max = rhmax;
   h->node_cap = ncap;
@@ -983,6 +1159,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
 
 static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_pyr);
+  hipFree(h->d_blur);
   hipFree(h->d_cand);
   hipFree(h->d_cellcnt);
   hipFree(h->d_keys_a);
@@ -990,6 +1167,7 @@ static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_lvlkeys);
   hipFree(h->d_lvlcnt);
   h->d_pyr = nullptr;
+  h->d_blur = nullptr;
   h->d_cand = nullptr;
   h->d_cellcnt = nullptr;
   h->d_keys_a = h->d_keys_b = nullptr;
@@ -1003,6 +1181,7 @@ static int ensure_batch(orbfe_extractor* h, int n) {
   free_batch(h);
   const int cap = std::max(n, 1);
   ORBFE_HIP_CHECK(hipMalloc(&h->d_pyr, (size_t)h->pyr_stride * cap));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_blur, (size_t)h->pyr_stride * cap));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_cand, (size_t)h->cand_stride * 4 * cap));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_cellcnt, sizeof(int32_t) * h->cells.size() * cap + 4));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_keys_a, (size_t)h->keyscr_stride * 4 * cap));
@@ -1018,9 +1197,7 @@ static size_t octree_lds(const orbfe_extractor* h) {
          sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16;
 }
 static size_t fast_lds(const orbfe_extractor* h) {
-  const size_t roi = align_up((size_t)h->roi_w_max * h->roi_h_max, 16);
-  const size_t m = align_up((size_t)(h->roi_w_max - 4) * (h->roi_h_max - 4), 16);
-  return 4 * (roi + m);
+  return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max).total;
 }
 
 #define LAUNCH_TIMED(h, kid, stream, ...)                          \
@@ -1051,10 +1228,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.ncells = (int)h->cells.size();
   a.n_images = n;
   a.total_key_slots = h->total_key_slots;
+  a.blur_strips = h->blur_tiles;
   a.img0 = d_imgs;
   a.img_stride = img_stride;
   a.img_pitch = pitch;
   a.pyr = h->d_pyr;
+  a.blur = h->d_blur;
   a.pyr_stride = h->pyr_stride;
   a.cand = h->d_cand;
   a.cand_stride = h->cand_stride;
@@ -1084,6 +1263,11 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
 
+  {
+    const LevelDesc& d = h->levels[0];
+    dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
+    LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
+  }
   for (int l = 1; l < h->nlevels; l++) {
     const LevelDesc& d = h->levels[l];
     dim3 grid((d.w + 63) / 64, (d.h + 3) / 4, n), block(64, 4);
@@ -1096,6 +1280,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   {
     dim3 grid(h->nlevels, n);
     LAUNCH_TIMED(h, 2, st, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), st, a));
+  }
+  {
+    dim3 grid((h->blur_tiles + 3) / 4, n);
+    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, a));
   }
   {
     dim3 grid((h->total_key_slots + 3) / 4, n);
@@ -1168,7 +1356,20 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
   }
   static std::once_flag once;
   static hipError_t pat_err = hipSuccess;
-  std::call_once(once, [] { pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, 1024); });
+  std::call_once(once, [h] {
+    pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, 1024);
+    // IC_Angle circle (ORBextractor.cc:82-98): rows v = -15..15, |u| <= umax[|v|]
+    int8_t circ[2 * 752] = {0};
+    int k = 0;
+    for (int v = -15; v <= 15; v++)
+      for (int u = -h->umax[std::abs(v)]; u <= h->umax[std::abs(v)]; u++) {
+        circ[2 * k] = (int8_t)v;
+        circ[2 * k + 1] = (int8_t)u;
+        k++;
+      }
+    if (pat_err == hipSuccess && k == 749) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_circle), circ, sizeof(circ));
+    else if (pat_err == hipSuccess) pat_err = hipErrorInvalidValue;
+  });
   if (pat_err != hipSuccess) {
     delete h;
     return orbfe_set_hip_error(pat_err, "upload pattern");
@@ -1337,13 +1538,8 @@ extern "C" int orbfe_get_level_device(orbfe_extractor* h, int image, int level,
   const LevelDesc& d = h->levels[level];
   *rows = d.h;
   *cols = d.w;
-  if (level == 0) {
-    *d_p = h->last_img0 + (long long)image * h->last_img_stride;
-    *step = (size_t)h->last_img_pitch;
-  } else {
-    *d_p = h->d_pyr + (long long)image * h->pyr_stride + d.pyr_off;
-    *step = (size_t)d.pitch;
-  }
+  *d_p = h->d_pyr + (long long)image * h->pyr_stride + d.pyr_off;
+  *step = (size_t)d.pitch;
   return ORBFE_OK;
 }
 
@@ -1451,6 +1647,18 @@ extern "C" int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int lev
   if (cnt > 0)
     ORBFE_HIP_CHECK(hipMemcpy(out, h->d_lvlkeys + (size_t)image * h->lvlkey_stride + h->levels[level].key_begin,
                               sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level, uint8_t* out,
+                                       int cap) {
+  if (!h || !out || image < 0 || image >= h->last_n || level < 0 || level >= h->nlevels)
+    return ORBFE_ERR_ARG;
+  const LevelDesc& d = h->levels[level];
+  if (cap < d.w * d.h) return ORBFE_ERR_CAPACITY;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  ORBFE_HIP_CHECK(hipMemcpy2D(out, d.w, h->d_blur + (size_t)image * h->pyr_stride + d.pyr_off, d.pitch,
+                              d.w, d.h, hipMemcpyDeviceToHost));
   return ORBFE_OK;
 }
 

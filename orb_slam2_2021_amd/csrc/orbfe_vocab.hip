@@ -33,6 +33,8 @@ struct orbfe_vocabulary {
   // host-call scratch
   uint8_t* d_scratch = nullptr;
   size_t scratch_bytes = 0;
+  unsigned long long* d_keys = nullptr;  // (node, feature) keys between the two kernels
+  size_t keys_bytes = 0;
 };
 
 struct VocabArgs {
@@ -52,46 +54,54 @@ struct VocabArgs {
   int cap;                // per-image capacity of node_ids / indices; offsets hold cap + 1
 };
 
-__global__ __launch_bounds__(256) void k_vocab(VocabArgs a) {
+// k_vocab_descend: one thread per descriptor of every image (TemplatedVocabulary.h:1231-1272);
+// writes the (node, feature) key, or ~0 for a stopped word / an empty slot.
+__global__ __launch_bounds__(256) void k_vocab_descend(VocabArgs a, unsigned long long* keys) {
+  const int img = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.cap) return;
+  const int n = min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
+  unsigned long long key = ~0ull;
+  if (i < n) {
+    const uint8_t* desc = a.desc + (long long)img * a.desc_stride;
+    uint4 d0, d1;
+    load_desc(desc + (size_t)i * 32, d0, d1);
+    int node = 0, level = 0, nid = 0;
+    while (a.nchild[node] > 0) {
+      ++level;
+      const int f = a.first[node], nc = a.nchild[node];
+      int best = f, best_d;
+      {
+        uint4 c0, c1;
+        load_desc(a.vdesc + (size_t)f * 32, c0, c1);
+        best_d = hamming256(d0, d1, c0, c1);
+      }
+      for (int c = 1; c < nc; c++) {
+        uint4 c0, c1;
+        load_desc(a.vdesc + (size_t)(f + c) * 32, c0, c1);
+        const int dd = hamming256(d0, d1, c0, c1);
+        if (dd < best_d) {  // strict: the first best child wins
+          best_d = dd;
+          best = f + c;
+        }
+      }
+      node = best;
+      if (level == a.nid_level) nid = node;
+    }
+    if (a.weight[node] > 0) key = ((unsigned long long)(unsigned)nid << 32) | (unsigned)i;
+  }
+  keys[(long long)img * a.cap + i] = key;
+}
+
+// k_vocab_csr: one workgroup per image sorts its keys stably (bitonic in LDS) and emits CSR.
+__global__ __launch_bounds__(256) void k_vocab(VocabArgs a, const unsigned long long* keys) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
   __shared__ int s_n;
   const int img = blockIdx.x, t = threadIdx.x;
   const int n = min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
-  const uint8_t* desc = a.desc + (long long)img * a.desc_stride;
   int P2 = 1;
   while (P2 < n) P2 <<= 1;
-  for (int i = t; i < P2; i += 256) {
-    unsigned long long key = ~0ull;
-    if (i < n) {
-      uint4 d0, d1;
-      load_desc(desc + (size_t)i * 32, d0, d1);
-      int node = 0, level = 0, nid = 0;
-      if (a.nid_level <= 0) nid = 0;  // root
-      while (a.nchild[node] > 0) {
-        ++level;
-        const int f = a.first[node], nc = a.nchild[node];
-        int best = f, best_d;
-        {
-          uint4 c0, c1;
-          load_desc(a.vdesc + (size_t)f * 32, c0, c1);
-          best_d = hamming256(d0, d1, c0, c1);
-        }
-        for (int c = 1; c < nc; c++) {
-          uint4 c0, c1;
-          load_desc(a.vdesc + (size_t)(f + c) * 32, c0, c1);
-          const int dd = hamming256(d0, d1, c0, c1);
-          if (dd < best_d) {
-            best_d = dd;
-            best = f + c;
-          }
-        }
-        node = best;
-        if (level == a.nid_level) nid = node;
-      }
-      if (a.weight[node] > 0) key = ((unsigned long long)(unsigned)nid << 32) | (unsigned)i;
-    }
-    skeys[i] = key;
-  }
+  for (int i = t; i < P2; i += 256) skeys[i] = i < n ? keys[(long long)img * a.cap + i] : ~0ull;
   __syncthreads();
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -206,6 +216,7 @@ extern "C" int orbfe_vocab_destroy(orbfe_vocabulary* v) {
   hipFree(v->d_nchild);
   hipFree(v->d_weight);
   hipFree(v->d_scratch);
+  hipFree(v->d_keys);
   if (v->stream) hipStreamDestroy(v->stream);
   delete v;
   return ORBFE_OK;
@@ -234,7 +245,16 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   a.cap = cap;
   int P2 = 1;
   while (P2 < cap) P2 <<= 1;
-  hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(256), sizeof(unsigned long long) * P2, s, a);
+  const size_t need = sizeof(unsigned long long) * (size_t)cap * n_images;
+  if (need > v->keys_bytes) {
+    hipFree(v->d_keys);
+    v->d_keys = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&v->d_keys, need));
+    v->keys_bytes = need;
+  }
+  hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 255) / 256, n_images), dim3(256), 0, s, a, v->d_keys);
+  hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(256), sizeof(unsigned long long) * P2, s, a,
+                     (const unsigned long long*)v->d_keys);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }

@@ -207,6 +207,13 @@ class ORBextractor:
                                                      byref(n)), "debug_level_keys")
         return out[:n.value]
 
+    def debug_blurred(self, level: int, image: int = 0) -> np.ndarray:
+        ref = self.level(level, image)
+        out = np.zeros(ref.shape, np.uint8)
+        L.check(self._lib.orbfe_debug_get_blurred(self._h, image, level, L.ptr(out), out.size),
+                "debug_blurred")
+        return out
+
     def geometry(self, rows: int, cols: int) -> np.ndarray:
         info = np.zeros(7 * self.nlevels, np.int32)
         L.check(self._lib.orbfe_debug_geometry(self._h, rows, cols, L.ptr(info), len(info)),

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from orb_slam2_2021_amd import ORBextractor, synth_frame, ORBFE_RESIZE_SCALAR
+from oracle import orbref
 from oracle.orbref import RefExtractor
 
 pytestmark = pytest.mark.gpu
@@ -26,6 +27,11 @@ def assert_same_extraction(ext, ref, img, image_index=0, got=None):
         assert lg.shape == lr.shape, f"level {l} shape"
         bad = np.argwhere(lg != lr)
         assert len(bad) == 0, f"k_resize: level {l} differs at {len(bad)} px, first {bad[:5].tolist()}"
+    for l in range(ref.nlevels):
+        br = orbref.gaussian_blur7(ref.level(l))
+        bg = ext.debug_blurred(l, image=image_index)
+        bad = np.argwhere(bg != br)
+        assert len(bad) == 0, f"k_blur: level {l} differs at {len(bad)} px, first {bad[:5].tolist()}"
     for l in range(ref.nlevels):
         cr, cg = ref.candidates(l), ext.debug_candidates(l, image=image_index)
         assert len(cg) == len(cr), f"k_fast: level {l} candidate count {len(cg)} vs {len(cr)}"
