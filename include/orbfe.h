@@ -106,9 +106,11 @@ int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p,
 int orbfe_get_level_device(orbfe_extractor* h, int image, int level, const uint8_t** d_p,
                            int* rows, int* cols, size_t* step);
 
-/* Per-kernel timing with HIP events recorded on the handle's launch stream.
- * names/avg_ms/count arrays of length cap; returns number of kernels in *n. */
-int orbfe_set_profiling(orbfe_extractor* h, int enable);
+/* Per-kernel timing with HIP events recorded on the launch stream around the selected kernels.
+ * kernel_mask: 0 = off, -1 = every kernel, else bit k selects kernel k of orbfe_get_kernel_times'
+ * order (k_resize, k_fast, k_octree, k_describe, k_copy0, k_blur). orbfe_get_kernel_times
+ * synchronises and returns, per kernel, the accumulated milliseconds and launch count. */
+int orbfe_set_profiling(orbfe_extractor* h, int kernel_mask);
 int orbfe_get_kernel_times(orbfe_extractor* h, char* names, int name_len, double* total_ms,
                            int32_t* launches, int cap, int* n);
 int orbfe_reset_kernel_times(orbfe_extractor* h);

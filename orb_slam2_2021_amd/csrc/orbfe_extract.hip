@@ -152,41 +152,62 @@ __device__ __forceinline__ int sat16(int v) { return min(max(v, -32768), 32767);
 // output pixel; xofs/alpha and yofs/beta come from host tables built exactly as OpenCV does.
 __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
   const LevelDesc ld = a.levels[l];
-  const int x = blockIdx.x * 64 + threadIdx.x;
+  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;  // 4 output pixels per thread
   const int y = blockIdx.y * 4 + threadIdx.y;
   const int img = blockIdx.z;
   if (x >= ld.w || y >= ld.h) return;
   const LevelDesc ls = a.levels[l - 1];
   int spitch;
   const uint8_t* src = level_ptr(a, ls, img, l - 1, spitch);
-  const int2 xt = a.xtab[ld.tab_x + x];
   const int2 yt = a.ytab[ld.tab_y + y];
-  const int sx = xt.x;
-  const int a0 = (int)(short)(xt.y & 0xffff), a1 = (int)(short)((unsigned)xt.y >> 16);
   const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
   const int sy0 = min(max(yt.x, 0), ls.h - 1), sy1 = min(max(yt.x + 1, 0), ls.h - 1);
   const uint8_t* r0 = src + (long long)sy0 * spitch;
   const uint8_t* r1 = src + (long long)sy1 * spitch;
-  int h0, h1;
-  if (x < ld.xmax) {
-    h0 = r0[sx] * a0 + r0[sx + 1] * a1;
-    h1 = r1[sx] * a0 + r1[sx + 1] * a1;
-  } else {
-    h0 = r0[sx] * 2048;
-    h1 = r1[sx] * 2048;
-  }
-  int v;
-  if (x < ld.simd_end) {  // VResizeLinearVec_32s8u (v_mul_hi, saturating adds, rshr_pack_u<2>)
-    const int m0 = (sat16(h0 >> 4) * b0) >> 16, m1 = (sat16(h1 >> 4) * b1) >> 16;
-    v = sat16(sat16(m0 + m1) + 2) >> 2;
-  } else {  // FixedPtCast<int, uchar, 22>
-    v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+  const int n = min(4, ld.w - x);
+  int2 xt[4];
+  int p00[4], p01[4], p10[4], p11[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xt[k] = a.xtab[ld.tab_x + min(x + k, ld.w - 1)];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // 16 independent source loads in flight
+    const int sx = xt[k].x;
+    p00[k] = r0[sx];
+    p01[k] = r0[sx + 1];  // (for x >= xmax, sx = w-1 and sx+1 is padding: loaded, not used)
+    p10[k] = r1[sx];
+    p11[k] = r1[sx + 1];
   }
   uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
-  const uint8_t b = (uint8_t)min(max(v, 0), 255);
-  row[x] = b;
-  if (x >= 1 && x <= 3) row[-x] = b;                         // REFLECT_101 padding for k_blur
-  if (x >= ld.w - 4 && x <= ld.w - 2) row[2 * ld.w - 2 - x] = b;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xx = x + k;
+    const int a0 = (int)(short)(xt[k].y & 0xffff), a1 = (int)(short)((unsigned)xt[k].y >> 16);
+    int h0, h1;
+    if (xx < ld.xmax) {
+      h0 = p00[k] * a0 + p01[k] * a1;
+      h1 = p10[k] * a0 + p11[k] * a1;
+    } else {
+      h0 = p00[k] * 2048;
+      h1 = p10[k] * 2048;
+    }
+    int v;
+    if (xx < ld.simd_end) {  // VResizeLinearVec_32s8u (v_mul_hi, saturating adds, rshr_pack_u<2>)
+      const int m0 = (sat16(h0 >> 4) * b0) >> 16, m1 = (sat16(h1 >> 4) * b1) >> 16;
+      v = sat16(sat16(m0 + m1) + 2) >> 2;
+    } else {  // FixedPtCast<int, uchar, 22>
+      v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+    }
+    const uint8_t b = (uint8_t)min(max(v, 0), 255);
+    packed |= (uint32_t)b << (8 * k);
+    if (k < n) {
+      if (xx >= 1 && xx <= 3) row[-xx] = b;  // REFLECT_101 padding for k_blur
+      if (xx >= ld.w - 4 && xx <= ld.w - 2) row[2 * ld.w - 2 - xx] = b;
+    }
+  }
+  if (n == 4) *reinterpret_cast<uint32_t*>(row + x) = packed;
+  else
+    for (int k = 0; k < n; k++) row[x + k] = (uint8_t)(packed >> (8 * k));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -656,15 +677,12 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
       // bitonic sort, descending: largest (size, creation) first
       for (int k = 2; k <= P2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = t; i < P2; i += 256) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const unsigned long long x = sk[i], y = sk[ixj];
-              const bool sw = (i & k) == 0 ? (x < y) : (x > y);
-              if (sw) {
-                sk[i] = y;
-                sk[ixj] = x;
-              }
+          for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
+            const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+            const unsigned long long x = sk[i], y = sk[ixj];
+            if ((i & k) == 0 ? (x < y) : (x > y)) {
+              sk[i] = y;
+              sk[ixj] = x;
             }
           }
           __syncthreads();
@@ -982,7 +1000,7 @@ struct orbfe_extractor {
   int last_img_pitch = 0, last_n = 0;
   std::vector<uint8_t> level_host;
   // profiling
-  bool profiling = false;
+  int profile_mask = 0;  // bit k: time kernel k with HIP events
   std::vector<KernelTimer> pending;
   std::vector<hipEvent_t> event_pool;
   double ktime[8] = {0};
@@ -1203,13 +1221,14 @@ static size_t fast_lds(const orbfe_extractor* h) {
 #define LAUNCH_TIMED(h, kid, stream, ...)                          \
   do {                                                             \
     hipEvent_t _e0 = nullptr, _e1 = nullptr;                       \
-    if ((h)->profiling) {                                          \
+    const bool _prof = ((h)->profile_mask >> (kid)) & 1;           \
+    if (_prof) {                                                   \
       _e0 = pool_event(h);                                         \
       _e1 = pool_event(h);                                         \
       hipEventRecord(_e0, stream);                                 \
     }                                                              \
     __VA_ARGS__;                                                   \
-    if ((h)->profiling) {                                          \
+    if (_prof) {                                                   \
       hipEventRecord(_e1, stream);                                 \
       (h)->pending.push_back(KernelTimer{kid, _e0, _e1});          \
     }                                                              \
@@ -1270,7 +1289,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   }
   for (int l = 1; l < h->nlevels; l++) {
     const LevelDesc& d = h->levels[l];
-    dim3 grid((d.w + 63) / 64, (d.h + 3) / 4, n), block(64, 4);
+    dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
     LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
   }
   {
@@ -1557,9 +1576,9 @@ extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const u
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_set_profiling(orbfe_extractor* h, int enable) {
+extern "C" int orbfe_set_profiling(orbfe_extractor* h, int kernel_mask) {
   if (!h) return ORBFE_ERR_ARG;
-  h->profiling = enable != 0;
+  h->profile_mask = kernel_mask;
   return ORBFE_OK;
 }
 

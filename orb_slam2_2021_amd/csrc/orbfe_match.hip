@@ -167,14 +167,42 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
   const float* F = P.f12;
   const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
               f7 = F[7], f8 = F[8];
-  for (int p1 = o1; p1 < e1; p1++) {
-    const int idx1 = P.fv1.indices[p1];
-    if (P.kf1.mp_state[idx1] != ORBFE_MP_NONE) continue;
-    const bool st1 = P.kf1.u_right[idx1] >= 0;
-    if (only_stereo && !st1) continue;
-    const orbfe_keypoint kp1 = P.kf1.keys_un[idx1];
+  // KF1 features of the node, 64 at a time: each lane preloads one (index, usable, position,
+  // descriptor); the sequential walk below broadcasts them with readlane (no global round trip
+  // per step of the claim order)
+  for (int b1 = o1; b1 < e1; b1 += 64) {
+    const int my = b1 + lane;
+    int m_idx = -1;
+    bool m_ok = false, m_st = false;
+    float m_x = 0.f, m_y = 0.f;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+    if (my < e1) {
+      m_idx = P.fv1.indices[my];
+      m_st = P.kf1.u_right[m_idx] >= 0;
+      m_ok = P.kf1.mp_state[m_idx] == ORBFE_MP_NONE && !(only_stereo && !m_st);
+      const orbfe_keypoint k1 = P.kf1.keys_un[m_idx];
+      m_x = k1.x;
+      m_y = k1.y;
+      load_desc(P.kf1.descriptors + (size_t)m_idx * 32, m0, m1);
+    }
+    const uint64_t okmask = wave_ballot(m_ok);
+    const int nb = min(64, e1 - b1);
+  for (int q = 0; q < nb; q++) {
+    if (!((okmask >> q) & 1ull)) continue;  // has a MapPoint, or mono under bOnlyStereo
+    const int idx1 = __builtin_amdgcn_readlane(m_idx, q);
+    const bool st1 = __builtin_amdgcn_readlane((int)m_st, q) != 0;
+    orbfe_keypoint kp1;
+    kp1.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m_x), q));
+    kp1.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m_y), q));
     uint4 a0, a1;
-    load_desc(P.kf1.descriptors + (size_t)idx1 * 32, a0, a1);
+    a0.x = __builtin_amdgcn_readlane(m0.x, q);
+    a0.y = __builtin_amdgcn_readlane(m0.y, q);
+    a0.z = __builtin_amdgcn_readlane(m0.z, q);
+    a0.w = __builtin_amdgcn_readlane(m0.w, q);
+    a1.x = __builtin_amdgcn_readlane(m1.x, q);
+    a1.y = __builtin_amdgcn_readlane(m1.y, q);
+    a1.z = __builtin_amdgcn_readlane(m1.z, q);
+    a1.w = __builtin_amdgcn_readlane(m1.w, q);
     // epipolar line l = x1' F12 (CheckDistEpipolarLine :149-151)
     const float la = kp1.x * f0 + kp1.y * f3 + f6;
     const float lb = kp1.x * f1 + kp1.y * f4 + f7;
@@ -220,6 +248,7 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
     }
+  }
   }
 }
 
@@ -292,14 +321,12 @@ __global__ __launch_bounds__(256) void k_grid(GridArgs g) {
   __syncthreads();
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < P2; i += 256) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint32_t x = skeys[i], y = skeys[ixj];
-          if ((i & k) == 0 ? (x > y) : (x < y)) {
-            skeys[i] = y;
-            skeys[ixj] = x;
-          }
+      for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
+        const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+        const uint32_t x = skeys[i], y = skeys[ixj];
+        if ((i & k) == 0 ? (x > y) : (x < y)) {
+          skeys[i] = y;
+          skeys[ixj] = x;
         }
       }
       __syncthreads();

@@ -103,16 +103,15 @@ __global__ __launch_bounds__(256) void k_vocab(VocabArgs a, const unsigned long 
   while (P2 < n) P2 <<= 1;
   for (int i = t; i < P2; i += 256) skeys[i] = i < n ? keys[(long long)img * a.cap + i] : ~0ull;
   __syncthreads();
+  // bitonic sort, ascending; every thread owns P2/512 compare-exchange pairs per stage
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < P2; i += 256) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long x = skeys[i], y = skeys[ixj];
-          if ((i & k) == 0 ? (x > y) : (x < y)) {
-            skeys[i] = y;
-            skeys[ixj] = x;
-          }
+      for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
+        const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+        const unsigned long long x = skeys[i], y = skeys[ixj];
+        if ((i & k) == 0 ? (x > y) : (x < y)) {
+          skeys[i] = y;
+          skeys[ixj] = x;
         }
       }
       __syncthreads();

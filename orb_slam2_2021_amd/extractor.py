@@ -169,8 +169,19 @@ class ORBextractor:
         return [self.level(l) for l in range(self.nlevels)]
 
     # ---- instrumentation ----------------------------------------------------------------
-    def set_profiling(self, enable: bool) -> None:
-        L.check(self._lib.orbfe_set_profiling(self._h, 1 if enable else 0), "set_profiling")
+    KERNELS = ("k_resize", "k_fast", "k_octree", "k_describe", "k_copy0", "k_blur")
+
+    def set_profiling(self, kernels=True) -> None:
+        """True / False, or an iterable of kernel names to time with HIP events."""
+        if kernels is True:
+            mask = -1
+        elif not kernels:
+            mask = 0
+        else:
+            mask = 0
+            for k in kernels:
+                mask |= 1 << self.KERNELS.index(k)
+        L.check(self._lib.orbfe_set_profiling(self._h, mask), "set_profiling")
 
     def kernel_times(self) -> dict:
         cap, name_len = 16, 32
