@@ -100,7 +100,7 @@ struct ExtractArgs {
   int out_cap;
   int ini_th, min_th, tlow;
   int roi_w_max, roi_h_max;
-  int node_cap, sort_cap;
+  int node_cap, sort_cap, scan_cap, key_lds_cap;
   int umax[16];
   AtanConsts atan;
   float factor_pi;
@@ -521,65 +521,97 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
   return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
 }
 
-__global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+template <bool LDSK>
+__device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, int n, uint32_t* ka,
+                                           uint32_t* kb) {
   const int l = blockIdx.x, img = blockIdx.y;
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
-  const int NC = a.node_cap, SC = a.sort_cap;
+  const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
   ONode* nodes0 = reinterpret_cast<ONode*>(smem);
   ONode* nodes1 = nodes0 + NC;
   int4* cc = reinterpret_cast<int4*>(nodes1 + NC);
   int* sa = reinterpret_cast<int*>(cc + NC);
-  int* sb = sa + NC;
-  int* sx = sb + NC;
-  unsigned long long* sk = reinterpret_cast<unsigned long long*>(sx + NC);
+  int* sb = sa + SA;
+  int* sx = sb + SA;
+  unsigned long long* sk = reinterpret_cast<unsigned long long*>(sx + SA);
   int* misc = reinterpret_cast<int*>(sk + SC);  // [0..3] scan wave sums, [8..] scalars
-
   const LevelDesc ld = a.levels[l];
   const int N = ld.budget;
-  uint32_t* ka = a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin;
-  uint32_t* kb = a.keys_b + (long long)img * a.keyscr_stride + ld.cand_begin;
   const uint32_t* cand = a.cand + (long long)img * a.cand_stride;
-  const int32_t* ccount = a.cellcnt + (long long)img * a.ncells + ld.cell_begin;
   uint32_t* out = a.lvlkeys + (long long)img * a.lvlkey_stride + ld.key_begin;
   int32_t* out_n = a.lvlcnt + (long long)img * a.nlevels + l;
 
-  // 1. gather this level's FAST candidates in cell order (ComputeKeyPointsOctTree :821-829)
-  for (int c = t; c < ld.ncells; c += 256) sa[c] = ccount[c];
-  __syncthreads();
-  const int n = block_scan_excl(sa, ld.ncells, misc);
-  for (int c = w; c < ld.ncells; c += 4) {
-    const int k = ccount[c];
-    const int slot = a.cells[ld.cell_begin + c].slot;
-    for (int i = lane; i < k; i += 64) ka[sa[c] + i] = cand[slot + i];
+  // 1. gather this level's FAST candidates in cell order (ComputeKeyPointsOctTree :821-829):
+  //    sa = exclusive prefix of the cell counts, sx = cell slots (filled by the caller); key i
+  //    belongs to the last cell whose prefix is <= i. Loads batched 4 per thread.
+  const int ncells = ld.ncells;
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = i0 + t + 256 * k;
+      if (i < n) {
+        int lo = 0, hi = ncells;  // upper_bound(sa, i) - 1
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sa[mid] <= i) lo = mid + 1;
+          else hi = mid;
+        }
+        const int c = lo - 1;
+        v[k] = cand[sx[c] + i - sa[c]];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = i0 + t + 256 * k;
+      if (i < n) ka[i] = v[k];
+    }
   }
   __syncthreads();
-  if (n == 0) {
-    if (t == 0) *out_n = 0;
-    return;
-  }
 
-  // 2. initial nodes (:555-588): key -> vpIniNodes[(size_t)(x / hX)], then drop empty nodes
+  // 2. initial nodes (:555-588): key -> vpIniNodes[(size_t)(x / hX)], stable, all 4 waves:
+  //    wave w counts then places the keys of its quarter; bucket offsets in between
   const int nini = ld.nini;
   const float hx = ld.hx;
-  if (w == 0) {
+  int* bcnt = reinterpret_cast<int*>(sk);  // [4][nini] counts, then [4][nini] offsets
+  int* boff = bcnt + 4 * nini;
+  const int R = ((n + 3) / 4 + 63) & ~63;
+  const int wbeg = min(w * R, n), wend = min(wbeg + R, n);
+  for (int bkt = 0; bkt < nini; bkt++) {
+    int cnt = 0;
+    for (int i0 = wbeg; i0 < wend; i0 += 64) {
+      const int i = i0 + lane;
+      const bool in = i < wend && (int)((float)key_x(ka[i]) / hx) == bkt;
+      cnt += __popcll(wave_ballot(in));
+    }
+    if (lane == 0) bcnt[w * nini + bkt] = cnt;
+  }
+  __syncthreads();
+  if (t == 0) {
     int run = 0;
-    for (int b = 0; b < nini; b++) {
-      int cnt = 0;
-      for (int i0 = 0; i0 < n; i0 += 64) {
-        const int i = i0 + lane;
-        bool in = false;
-        uint32_t key = 0;
-        if (i < n) {
-          key = ka[i];
-          in = (int)((float)key_x(key) / hx) == b;
-        }
-        const uint64_t bal = wave_ballot(in);
-        if (in) kb[run + cnt + prefix_in_wave(bal)] = key;
-        cnt += __popcll(bal);
+    for (int bkt = 0; bkt < nini; bkt++) {
+      sb[bkt] = 0;
+      for (int ww = 0; ww < 4; ww++) {
+        boff[ww * nini + bkt] = run;
+        run += bcnt[ww * nini + bkt];
+        sb[bkt] += bcnt[ww * nini + bkt];
       }
-      if (lane == 0) sb[b] = cnt;
-      run += cnt;
+    }
+  }
+  __syncthreads();
+  for (int bkt = 0; bkt < nini; bkt++) {
+    int run = boff[w * nini + bkt];
+    for (int i0 = wbeg; i0 < wend; i0 += 64) {
+      const int i = i0 + lane;
+      uint32_t key = 0;
+      bool in = false;
+      if (i < wend) {
+        key = ka[i];
+        in = (int)((float)key_x(key) / hx) == bkt;
+      }
+      const uint64_t bal = wave_ballot(in);
+      if (in) kb[run + prefix_in_wave(bal)] = key;
+      run += __popcll(bal);
     }
   }
   __syncthreads();
@@ -761,6 +793,35 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
     out[i] = pack_key(key_x(best) + 16, key_y(best) + 16, key_s(best));
   }
   if (t == 0) *out_n = S;
+}
+
+
+__global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int l = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+  const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
+  int* sa = reinterpret_cast<int*>(smem + (sizeof(ONode) * 2 + sizeof(int4)) * NC);
+  int* sx = sa + 2 * SA;
+  int* misc = reinterpret_cast<int*>(reinterpret_cast<unsigned long long*>(sx + SA) + SC);
+  uint32_t* lds_keys = reinterpret_cast<uint32_t*>(misc + 16);
+  const LevelDesc ld = a.levels[l];
+  const int32_t* ccount = a.cellcnt + (long long)img * a.ncells + ld.cell_begin;
+  for (int c = t; c < ld.ncells; c += 256) {
+    sa[c] = ccount[c];
+    sx[c] = a.cells[ld.cell_begin + c].slot;
+  }
+  __syncthreads();
+  const int n = block_scan_excl(sa, ld.ncells, misc);
+  if (n == 0) {
+    if (t == 0) a.lvlcnt[(long long)img * a.nlevels + l] = 0;
+    return;
+  }
+  if (n <= a.key_lds_cap) {  // keys in LDS (two ping-pong halves)
+    octree_run<true>(a, smem, n, lds_keys, lds_keys + a.key_lds_cap);
+  } else {  // very large levels: keys in the global scratch buffers
+    octree_run<false>(a, smem, n, a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin,
+                      a.keys_b + (long long)img * a.keyscr_stride + ld.cand_begin);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -974,6 +1035,7 @@ struct orbfe_extractor {
   std::vector<int2> xtab, ytab;
   long long pyr_stride = 0, cand_stride = 0, keyscr_stride = 0, lvlkey_stride = 0;
   int total_key_slots = 0, roi_w_max = 0, roi_h_max = 0, node_cap = 0, sort_cap = 0, blur_tiles = 0;
+  int scan_cap = 0, key_lds_cap = 0;
   LevelDesc* d_levels = nullptr;
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
@@ -1165,9 +1227,19 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->roi_w_max = rwmax;
   h->roi_h_max = rhmax;
   h->node_cap = ncap;
+  int mc = 0, mini = 0;
+  for (const LevelDesc& d : lv) {
+    mc = std::max(mc, d.ncells);
+    mini = std::max(mini, d.nini);
+  }
   int sc = 1;
-  while (sc < ncap) sc <<= 1;
+  while (sc < std::max(ncap, 4 * mini)) sc <<= 1;  // sk doubles as the [4][nini] bucket tables
   h->sort_cap = sc;
+  h->scan_cap = (std::max(ncap, mc) + 3) & ~3;
+  // octree keys stay in LDS up to this many per level (ping-pong), within a 96 KiB block
+  const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * h->scan_cap +
+                       sizeof(unsigned long long) * sc + sizeof(int) * 16;
+  h->key_lds_cap = fixed < 96 * 1024 ? (int)((96 * 1024 - fixed) / 8) & ~63 : 0;
   h->rows = rows;
   h->cols = cols;
   h->geom_mode = h->resize_mode;
@@ -1211,8 +1283,8 @@ static int ensure_batch(orbfe_extractor* h, int n) {
 }
 
 static size_t octree_lds(const orbfe_extractor* h) {
-  return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->node_cap +
-         sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16;
+  return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->scan_cap +
+         sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16 + sizeof(uint32_t) * 2 * h->key_lds_cap;
 }
 static size_t fast_lds(const orbfe_extractor* h) {
   return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max).total;
@@ -1274,6 +1346,8 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.roi_h_max = h->roi_h_max;
   a.node_cap = h->node_cap;
   a.sort_cap = h->sort_cap;
+  a.scan_cap = h->scan_cap;
+  a.key_lds_cap = h->key_lds_cap;
   for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
   a.atan.p1 = 0.9997878412794807f * (float)(180 / M_PI);
   a.atan.p3 = -0.3258083974640975f * (float)(180 / M_PI);
@@ -1298,6 +1372,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   }
   {
     dim3 grid(h->nlevels, n);
+    if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
+    ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)octree_lds(h)));
     LAUNCH_TIMED(h, 2, st, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), st, a));
   }
   {
