@@ -20,6 +20,9 @@ int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level, uint32_
 int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level, uint8_t* out, int cap);
 /* Per level: w, h, ncells, candidate capacity, budget, nIni, key capacity (7 ints per level). */
 int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, int cap);
+/* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
+ * global-memory path for every level; < 0 restores the automatic size). */
+int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
 #ifdef __cplusplus
 }
 #endif

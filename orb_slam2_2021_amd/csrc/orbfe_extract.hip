@@ -497,6 +497,27 @@ __device__ void wave_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, ui
   }
 }
 
+// Thread-serial forms for small nodes (count <= OCT_SMALL): one lane walks the whole segment.
+#define OCT_SMALL 48
+__device__ __forceinline__ int4 serial_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
+  const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  int c[4] = {0, 0, 0, 0};
+  for (int i = 0; i < nd.count; i++) c[child_of(src[i], mx, my)]++;
+  return make_int4(c[0], c[1], c[2], c[3]);
+}
+
+__device__ __forceinline__ void serial_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, uint32_t* kb) {
+  const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
+  uint32_t* dst = ((nd.flags & 1) ? ka : kb) + nd.begin;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  int o[4] = {0, cnt.x, cnt.x + cnt.y, cnt.x + cnt.y + cnt.z};
+  for (int i = 0; i < nd.count; i++) {
+    const uint32_t key = src[i];
+    dst[o[child_of(key, mx, my)]++] = key;
+  }
+}
+
 __device__ __forceinline__ ONode make_child(const ONode& p, int c, int begin, int count, int seq) {
   const int mx = p.x0 + ((p.x1 - p.x0 + 1) >> 1), my = p.y0 + ((p.y1 - p.y0 + 1) >> 1);
   ONode n;
@@ -646,9 +667,17 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     const int prevS = S;
     if (!refine) {
       // ---- full pass (:603-668) ----
+      for (int i = t; i < S; i += 256) {
+        const ONode nd = Lc[i];
+        if (nd.count > 1 && nd.count <= OCT_SMALL) {
+          const int4 c4 = serial_child_counts(nd, ka, kb);
+          serial_child_partition(nd, c4, ka, kb);
+          cc[i] = c4;
+        }
+      }
       for (int i = w; i < S; i += 4) {
         const ONode nd = Lc[i];
-        if (nd.count > 1) {
+        if (nd.count > OCT_SMALL) {
           const int4 c4 = wave_child_counts(nd, ka, kb);
           wave_child_partition(nd, c4, ka, kb);
           if (lane == 0) cc[i] = c4;
@@ -721,10 +750,16 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         }
       }
       // child counts of every candidate, in processing order
+      for (int k = t; k < nR; k += 256) {
+        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
+        if (nd.count <= OCT_SMALL) cc[k] = serial_child_counts(nd, ka, kb);
+      }
       for (int k = w; k < nR; k += 4) {
-        const int i = (int)(sk[k] & 0xfffffull);
-        const int4 c4 = wave_child_counts(Lc[i], ka, kb);
-        if (lane == 0) cc[k] = c4;
+        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
+        if (nd.count > OCT_SMALL) {
+          const int4 c4 = wave_child_counts(nd, ka, kb);
+          if (lane == 0) cc[k] = c4;
+        }
       }
       __syncthreads();
       for (int k = t; k < nR; k += 256) sa[k] = nonempty4(cc[k]) - 1;
@@ -742,9 +777,13 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       for (int k = t; k < nproc; k += 256) sb[(int)(sk[k] & 0xfffffull)] = k;
       __syncthreads();
       // partition the divided nodes' keys
+      for (int k = t; k < nproc; k += 256) {
+        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
+        if (nd.count <= OCT_SMALL) serial_child_partition(nd, cc[k], ka, kb);
+      }
       for (int k = w; k < nproc; k += 4) {
-        const int i = (int)(sk[k] & 0xfffffull);
-        wave_child_partition(Lc[i], cc[k], ka, kb);
+        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
+        if (nd.count > OCT_SMALL) wave_child_partition(nd, cc[k], ka, kb);
       }
       for (int k = t; k < nR; k += 256) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
       __syncthreads();
@@ -1027,6 +1066,7 @@ struct orbfe_extractor {
   std::vector<int> nfeat;
   int umax[16];
   int resize_mode = ORBFE_RESIZE_SIMD128;
+  int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
   hipStream_t stream = nullptr;
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
@@ -1236,10 +1276,12 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   while (sc < std::max(ncap, 4 * mini)) sc <<= 1;  // sk doubles as the [4][nini] bucket tables
   h->sort_cap = sc;
   h->scan_cap = (std::max(ncap, mc) + 3) & ~3;
-  // octree keys stay in LDS up to this many per level (ping-pong), within a 96 KiB block
+  // octree keys stay in LDS up to this many per level (ping-pong) within an 80 KiB block, so two
+  // blocks share a CU; larger levels use the global scratch path
   const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * h->scan_cap +
                        sizeof(unsigned long long) * sc + sizeof(int) * 16;
-  h->key_lds_cap = fixed < 96 * 1024 ? (int)((96 * 1024 - fixed) / 8) & ~63 : 0;
+  h->key_lds_cap = fixed < 80 * 1024 ? (int)((80 * 1024 - fixed) / 8) & ~63 : 0;
+  if (h->octree_key_cap_override >= 0) h->key_lds_cap = std::min(h->key_lds_cap, h->octree_key_cap_override);
   h->rows = rows;
   h->cols = cols;
   h->geom_mode = h->resize_mode;
@@ -1755,6 +1797,13 @@ extern "C" int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level,
   ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   ORBFE_HIP_CHECK(hipMemcpy2D(out, d.w, h->d_blur + (size_t)image * h->pyr_stride + d.pyr_off, d.pitch,
                               d.w, d.h, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->octree_key_cap_override = cap < 0 ? -1 : (cap & ~63);
+  h->rows = h->cols = -1;  // recompute the geometry on the next call
   return ORBFE_OK;
 }
 

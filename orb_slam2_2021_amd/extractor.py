@@ -225,6 +225,10 @@ class ORBextractor:
                 "debug_blurred")
         return out
 
+    def debug_set_octree_key_cap(self, cap: int) -> None:
+        """Limit the keys DistributeOctTree keeps in LDS (0: global-memory path; <0: auto)."""
+        L.check(self._lib.orbfe_debug_set_octree_key_cap(self._h, int(cap)), "set_octree_key_cap")
+
     def geometry(self, rows: int, cols: int) -> np.ndarray:
         info = np.zeros(7 * self.nlevels, np.int32)
         L.check(self._lib.orbfe_debug_geometry(self._h, rows, cols, L.ptr(info), len(info)),

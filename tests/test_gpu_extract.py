@@ -94,6 +94,17 @@ def test_flat_and_sparse_images(require_gpu):
     assert_same_extraction(ext, ref, noise)
 
 
+@pytest.mark.parametrize("cap", [0, 1024])
+def test_octree_global_key_path(require_gpu, cap):
+    """DistributeOctTree keeps a level's keys in LDS up to a capacity and in global scratch beyond
+    it; force the global path for every level (0) or for the large levels only (1024)."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_octree_key_cap(cap)
+    assert_same_extraction(ext, ref, synth_frame(3, 376, 1241))
+    noise = np.random.default_rng(5).integers(0, 256, (376, 1241), dtype=np.uint8)
+    assert_same_extraction(ext, ref, noise)
+
+
 def test_empty_image(require_gpu):
     k, d = ORBextractor(2000, 1.2, 8, 20, 7)(np.zeros((0, 0), np.uint8))
     assert len(k) == 0 and d is None
