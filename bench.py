@@ -274,6 +274,8 @@ def main():
         "sft_matches_per_pair": round(float(nm.mean()), 1),
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1:
+        out["host_boundary"] = host_boundary_rate(ext, host)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey)
     if rank == 0:
@@ -329,6 +331,22 @@ def pipeline_bytes_per_stereo_frame(geo, counts, B):
     extract = sum(px) + sum(px[1:]) + 60 * n_per_img
     sft = 2 * n_per_img * 64 + 2 * n_per_img / 8 + 4 * 2 * n_per_img
     return 2 * extract + sft
+
+
+def host_boundary_rate(ext, host, reps=5):
+    """PCIe-inclusive extraction rate through the host-buffer entry (orbfe_extract_batch: H2D of
+    the images, the same kernels, D2H of keypoints + descriptors). Reported beside `value`, never as
+    it."""
+    import torch
+    imgs = [host[i] for i in range(len(host))]
+    ext.extract_batch(imgs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ext.extract_batch(imgs)
+    dt = time.perf_counter() - t0
+    return {"value": round(reps * len(imgs) / 2 / dt, 2), "unit": "stereo frames/s",
+            "what": f"orbfe_extract_batch on {len(imgs)} host images (extract only, H2D + D2H included)"}
 
 
 def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey):

@@ -1,7 +1,8 @@
-// orbfe_extract.hip -- ORBextractor::operator() as four CDNA4 kernels (gfx950, wave64).
+// orbfe_extract.hip -- ORBextractor::operator() as six CDNA4 kernels (gfx950, wave64).
 //
 // Reference: src/ORBextractor.cc of lreithmayr/ORB_SLAM2_2021 (operator() :1041-1103).
 // Pipeline per batch of same-shaped images, all on one HIP stream:
+//   k_copy0                   the caller's image -> level 0 of the padded pyramid block
 //   k_resize   x (nlevels-1)  ComputePyramid :1105-1135 -- one launch per level (level l reads the
 //                             rounded uint8 level l-1, exactly the reference chain), 11-bit fixed
 //                             point bilinear with OpenCV's SIMD128 vertical rounding (Appendix A.3)
@@ -12,12 +13,14 @@
 //   k_octree                  DistributeOctTree :542-766 -- one workgroup per (image, level); the
 //                             list/push_front/erase order of the reference is reproduced with
 //                             parallel passes (block scans + a bitonic sort of the refinement set)
-//   k_describe                IC_Angle :75-102 + GaussianBlur 7x7 :1083-1084 + computeOrbDescriptor
-//                             :105-151 + rescale :1093-1099 -- one wavefront per keypoint on a
-//                             43x43 LDS patch; the 256 tests land as 4 wave ballots (= 32 bytes)
-// Data layout in HBM per image: pyramid levels 1..L-1 packed (64-byte row pitch); FAST candidate
-// slots per cell (u32 x | y<<12 | score<<24, cell-order); octree key ping-pong buffers; per-level
-// survivor keys; outputs orbfe_keypoint[cap] + 32-byte descriptors[cap] + count.
+//   k_blur                    GaussianBlur 7x7 :1083-1084 of every level, bit-exact fixed point
+//   k_describe                IC_Angle :75-102 + computeOrbDescriptor :105-151 + rescale
+//                             :1093-1099 -- one wavefront per keypoint; the 256 tests land as 4
+//                             wave ballots (= 32 bytes)
+// Data layout in HBM per image: pyramid levels 0..L-1 packed, rows padded to a 64-byte pitch with
+// REFLECT_101 columns on both sides; the blurred pyramid in the same layout; FAST candidate slots
+// per cell (u32 x | y<<12 | score<<24, cell order); octree key scratch for levels too large for
+// LDS; per-level survivor keys; outputs orbfe_keypoint[cap] + 32-byte descriptors[cap] + count.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -864,11 +867,6 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (ORBextractor.cc:1083-1084),
-// OpenCV's bit-exact fixed-point form: H = sum k_i p_i (8.8), out = (sum k_j H_j + 2^15) >> 16 with
-// k = [18, 34, 49, 54, 49, 34, 18]. One workgroup per 128 x 16 output tile: the (134 x 22) source
-// tile with reflected borders goes to LDS, the horizontal pass to a u16 LDS tile, the vertical
-// pass to HBM. Tiles of all levels of all images form one launch.
 #define BS_W 256  // columns per wavefront strip (4 per lane)
 #define BS_H 32   // output rows per strip
 __device__ __forceinline__ int reflect101(int i, int n) {

@@ -88,3 +88,19 @@ def test_bad_arguments_rejected_without_device():
     assert lib.orbfe_extractor_create(2000, 1.0, 8, 20, 7, 0, byref(h)) == L.ORBFE_ERR_ARG
     assert lib.orbfe_extract(None, None, 10, 10, 10, None, 0, None, None) == L.ORBFE_ERR_ARG
     assert lib.orbfe_descriptor_distance(None, None) == L.ORBFE_ERR_ARG
+
+
+def test_product_never_imports_the_oracle():
+    """The oracle is test infrastructure: the package must not import or load it."""
+    pkg = os.path.join(ROOT, "orb_slam2_2021_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in src and "from oracle" not in src, f
+                assert "orbref" not in src, f
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import orb_slam2_2021_amd, orb_slam2_2021_amd.parallel, orb_slam2_2021_amd.synthetic\n"
+            "print(sorted(m for m in sys.modules if m.startswith('oracle')))" % ROOT)
+    out = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.stdout.strip() == "[]", out.stdout + out.stderr
