@@ -80,6 +80,18 @@ __device__ __forceinline__ float fast_atan2_dev(float y, float x, const AtanCons
 
 // Exclusive scan of data[0..n) in place by a 256-thread workgroup (4 waves); returns the total.
 // wsum: 4 ints of LDS. Contains __syncthreads(): call from uniform control flow only.
+// XCD-aware block remap (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement"; observed
+// round-robin dealing of blocks over the 8 XCDs). Returns the logical (x, y) block of a 2-D grid
+// such that each XCD receives one contiguous range of logical blocks (x fastest): neighbouring
+// cells / keypoints of one image then share an L2. Bijective for any grid size. Speed only.
+__device__ __forceinline__ int2 xcd_block2d() {
+  const int nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * gridDim.x + blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  return make_int2(id % gridDim.x, id / gridDim.x);
+}
+
 __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
   const int per = (n + 255) / 256;

@@ -322,8 +322,9 @@ __host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max) {
 __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int w = wave_id(), lane = lane_id();
-  const int cell = blockIdx.x * 4 + w;
-  const int img = blockIdx.y;
+  const int2 blk = xcd_block2d();
+  const int cell = blk.x * 4 + w;
+  const int img = blk.y;
   if (cell >= a.ncells) return;
   const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max);
   uint8_t* base = smem + w * lay.total;
@@ -893,8 +894,9 @@ __device__ __forceinline__ void blur_h4(uint32_t P, uint32_t C, uint32_t N, uint
 // aligned dword per input row, neighbours by cross-lane shuffles, the 7-row vertical window in
 // registers, one dword store per output row. Strips of all levels of all images in one launch.
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
-  const int img = blockIdx.y, lane = lane_id();
-  int strip = blockIdx.x * 4 + wave_id(), l = 0;
+  const int2 blk = xcd_block2d();
+  const int img = blk.y, lane = lane_id();
+  int strip = blk.x * 4 + wave_id(), l = 0;
   if (strip >= a.blur_strips) return;
   while (l + 1 < a.nlevels && strip >= a.levels[l + 1].tile_begin) l++;
   const LevelDesc ld = a.levels[l];
@@ -964,10 +966,11 @@ __constant__ int8_t c_circle[2 * 752];  // (v, u) of the IC_Angle circle, 749 us
 
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   const int w = wave_id(), lane = lane_id();
-  const int img = blockIdx.y;
-  const int slot = blockIdx.x * 4 + w;
+  const int2 blk = xcd_block2d();
+  const int img = blk.y;
+  const int slot = blk.x * 4 + w;
   const int32_t* lc = a.lvlcnt + (long long)img * a.nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blk.x == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int l = 0; l < a.nlevels; l++) tot += lc[l];
     a.out_counts[img] = tot;
@@ -1094,6 +1097,11 @@ struct orbfe_extractor {
   uint8_t* d_desc = nullptr;
   int32_t* d_counts = nullptr;
   size_t out_cap_alloc = 0;
+  // pinned staging of the host-buffer entry points (one H2D and one D2H burst per call)
+  uint8_t* h_in = nullptr;
+  size_t h_in_bytes = 0;
+  uint8_t* h_out = nullptr;
+  size_t h_out_bytes = 0;
   // last call (for get_level)
   const uint8_t* last_img0 = nullptr;
   long long last_img_stride = 0;
@@ -1527,6 +1535,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_kps);
   hipFree(h->d_desc);
   hipFree(h->d_counts);
+  if (h->h_in) hipHostFree(h->h_in);
+  if (h->h_out) hipHostFree(h->h_out);
   for (auto& p : h->pending) {
     hipEventDestroy(p.e0);
     hipEventDestroy(p.e1);
@@ -1606,6 +1616,19 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMalloc(&h->d_counts, sizeof(int32_t) * n));
     h->out_cap_alloc = need_out;
   }
+  if (need_in > h->h_in_bytes) {
+    if (h->h_in) hipHostFree(h->h_in);
+    h->h_in = nullptr;
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_in, hipHostMallocDefault));
+    h->h_in_bytes = need_in;
+  }
+  const size_t need_hout = need_out * (sizeof(orbfe_keypoint) + 32) + sizeof(int32_t) * n;
+  if (need_hout > h->h_out_bytes) {
+    if (h->h_out) hipHostFree(h->h_out);
+    h->h_out = nullptr;
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_out, need_hout, hipHostMallocDefault));
+    h->h_out_bytes = need_hout;
+  }
   return ORBFE_OK;
 }
 
@@ -1627,30 +1650,39 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
   st = ensure_host_io(h, n, rows, cols);
   if (st != ORBFE_OK) return st;
   const int K = h->total_key_slots;
+  // images -> pinned staging (packed rows) -> one H2D copy
+  const size_t img_bytes = (size_t)rows * cols;
   for (int i = 0; i < n; i++) {
     if (!imgs[i]) return orbfe_set_error(ORBFE_ERR_ARG, "null image");
-    ORBFE_HIP_CHECK(hipMemcpy2DAsync(h->d_in + (size_t)i * rows * cols, cols, imgs[i], step, cols,
-                                     rows, hipMemcpyHostToDevice, h->stream));
+    uint8_t* dst = h->h_in + (size_t)i * img_bytes;
+    if (step == (size_t)cols) {
+      std::memcpy(dst, imgs[i], img_bytes);
+    } else {
+      for (int r = 0; r < rows; r++) std::memcpy(dst + (size_t)r * cols, imgs[i] + (size_t)r * step, cols);
+    }
   }
+  ORBFE_HIP_CHECK(hipMemcpyAsync(h->d_in, h->h_in, (size_t)n * img_bytes, hipMemcpyHostToDevice, h->stream));
   st = launch_extract(h, n, h->d_in, (long long)rows * cols, cols, h->d_kps, h->d_desc, K,
                       h->d_counts, h->stream);
   if (st != ORBFE_OK) return st;
-  std::vector<int32_t> cnt(n);
-  ORBFE_HIP_CHECK(hipMemcpyAsync(cnt.data(), h->d_counts, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  // every image's keypoint and descriptor slots + counts -> pinned staging in one burst
+  orbfe_keypoint* hk = reinterpret_cast<orbfe_keypoint*>(h->h_out);
+  uint8_t* hd = h->h_out + (size_t)n * K * sizeof(orbfe_keypoint);
+  int32_t* hc = reinterpret_cast<int32_t*>(hd + (size_t)n * K * 32);
+  ORBFE_HIP_CHECK(hipMemcpyAsync(hk, h->d_kps, (size_t)n * K * sizeof(orbfe_keypoint), hipMemcpyDeviceToHost, h->stream));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(hd, h->d_desc, (size_t)n * K * 32, hipMemcpyDeviceToHost, h->stream));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(hc, h->d_counts, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
   ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   int need = 0;
-  for (int i = 0; i < n; i++) need = std::max(need, (int)cnt[i]);
-  for (int i = 0; i < n; i++) counts[i] = cnt[i];
+  for (int i = 0; i < n; i++) need = std::max(need, (int)hc[i]);
+  for (int i = 0; i < n; i++) counts[i] = hc[i];
   if (need > cap) return orbfe_set_error(ORBFE_ERR_CAPACITY, "keypoint capacity too small");
   if (need > 0 && (!kps || !desc)) return orbfe_set_error(ORBFE_ERR_ARG, "null output buffer");
   for (int i = 0; i < n; i++) {
-    if (cnt[i] == 0) continue;
-    ORBFE_HIP_CHECK(hipMemcpyAsync(kps + (size_t)i * cap, h->d_kps + (size_t)i * K,
-                                   sizeof(orbfe_keypoint) * cnt[i], hipMemcpyDeviceToHost, h->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(desc + (size_t)i * cap * 32, h->d_desc + (size_t)i * K * 32,
-                                   (size_t)32 * cnt[i], hipMemcpyDeviceToHost, h->stream));
+    if (hc[i] == 0) continue;
+    std::memcpy(kps + (size_t)i * cap, hk + (size_t)i * K, sizeof(orbfe_keypoint) * hc[i]);
+    std::memcpy(desc + (size_t)i * cap * 32, hd + (size_t)i * K * 32, (size_t)32 * hc[i]);
   }
-  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   return ORBFE_OK;
 }
 
