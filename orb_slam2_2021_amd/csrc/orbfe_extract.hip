@@ -239,21 +239,13 @@ __device__ __forceinline__ int ring_off(int k, int s) {
 
 // Arc strength M = max(v - A, B - v) with A = min over the 16 arcs of 9 of the max ring value and
 // B = max over arcs of the min ring value. The pixel is a FAST corner at threshold t iff
-// M >= t+1, and then cornerScore<16> == M - 1. Returns 0 when the pixel is no corner at tlow
-// (OpenCV's antipodal-pair quick test first).
-__device__ __forceinline__ int arc_strength_lds(const uint8_t* p, int s, int tlow) {
+// M >= t+1, and then cornerScore<16> == M - 1. Returns 0 when the pixel is no corner at tlow.
+// Callers run OpenCV's antipodal quick test first (it never rejects a corner).
+__device__ __forceinline__ int arc_strength_nq(const uint8_t* p, int s, int tlow) {
   const int v = p[0];
   int x[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) x[k] = p[ring_off(k, s)];
-  int d = 3;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const int ta = (x[k] < v - tlow ? 1 : 0) | (x[k] > v + tlow ? 2 : 0);
-    const int tb = (x[k + 8] < v - tlow ? 1 : 0) | (x[k + 8] > v + tlow ? 2 : 0);
-    d &= ta | tb;
-  }
-  if (d == 0) return 0;
   int mn2[16], mx2[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
@@ -293,25 +285,36 @@ __device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }
 //   3. the full arc strength runs only on the compacted list, full waves;
 //   4. strict 3x3 NMS at iniThFAST (then minThFAST for an empty cell) visits only list entries.
 __device__ __forceinline__ bool quick_test(const uint8_t* p, int s, int t) {
-  const int v = p[0];
-  int d = 3;
+  // x < v - t  <=>  (x - lo) < 0;  x > v + t  <=>  (hi - x) < 0: the sign bits carry
+  // OpenCV's "d &= tab[x] | tab[y]" bits without compares
+  const int v = p[0], lo = v - t, hi = v + t;
+  int dark = -1, brt = -1;
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const int x = p[ring_off(k, s)], y = p[ring_off(k + 8, s)];
-    const int ta = (x < v - t ? 1 : 0) | (x > v + t ? 2 : 0);
-    const int tb = (y < v - t ? 1 : 0) | (y > v + t ? 2 : 0);
-    d &= ta | tb;
+    dark &= (x - lo) | (y - lo);
+    brt &= (hi - x) | (hi - y);
   }
-  return d != 0;
+  return (dark | brt) < 0;
+}
+
+// two u8 values in the 16-bit halves of a dword, and packed 16-bit add / subtract (v_pk_*_u16)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2(uint32_t lo, uint32_t hi) { return lo | (hi << 16); }
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
 }
 
 struct FastLds {
   int rs, roi, m8, list;  // row stride and byte offsets inside one wave's region
   int total;
 };
-__host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max) {
+__host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max, int rs_fixed) {
   FastLds f;
-  f.rs = (rw_max + 4 + 3) & ~3;
+  f.rs = rs_fixed ? rs_fixed : (rw_max + 4 + 3) & ~3;
   f.roi = 0;
   f.m8 = (f.rs * rh_max + 15) & ~15;
   f.list = f.m8 + (((rw_max - 4) * (rh_max - 4) + 15) & ~15);
@@ -319,6 +322,11 @@ __host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max) {
   return f;
 }
 
+// RSC != 0: the ROI row stride is the compile-time constant RSC (= 64 when every ROI fits in 61
+// columns), so the 16 ring reads of a pixel are one address plus immediate offsets, the ROI load
+// maps lanes with shifts and the row/column split of a detection index is a multiply-shift.
+// RSC == 0: any geometry, runtime stride.
+template <int RSC>
 __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int w = wave_id(), lane = lane_id();
@@ -326,12 +334,12 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   const int cell = blk.x * 4 + w;
   const int img = blk.y;
   if (cell >= a.ncells) return;
-  const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max);
+  const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max, RSC);
   uint8_t* base = smem + w * lay.total;
   uint8_t* roi = base + lay.roi;
   uint8_t* m8 = base + lay.m8;
   uint16_t* list = reinterpret_cast<uint16_t*>(base + lay.list);
-  const int RS = lay.rs;
+  const int RS = RSC ? RSC : lay.rs;
 
   const CellDesc cd = a.cells[cell];
   const LevelDesc ld = a.levels[cd.level];
@@ -346,55 +354,118 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   }
   // 1. ROI -> LDS: dword-aligned columns [x0a, x0a + 4 nw) cover [x0, x0 + rw)
   const int x0a = cd.x0 & ~3, xo = cd.x0 - x0a, nw = (xo + rw + 3) >> 2;
-  for (int i0 = 0; i0 < nw * rh; i0 += 8 * 64) {  // up to 8 dword loads per lane in flight
-    uint32_t v[8];
+  if constexpr (RSC != 0) {
+    constexpr int WPR = RSC / 4;  // dword columns per LDS row
+    constexpr int SH = WPR == 16 ? 4 : WPR == 8 ? 3 : 5;
+    static_assert((1 << SH) == WPR, "RSC must be 32, 64 or 128");
+    for (int i0 = 0; i0 < WPR * rh; i0 += 8 * 64) {
+      uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int i = i0 + lane + 64 * k;
-      if (i < nw * rh) {
-        const int r = i / nw, c = i - r * nw;
-        v[k] = *reinterpret_cast<const uint32_t*>(lev + (long long)(cd.y0 + r) * pitch + x0a + 4 * c);
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + lane + 64 * k, r = i >> SH, c = i & (WPR - 1);
+        if (r < rh && c < nw)
+          v[k] = *reinterpret_cast<const uint32_t*>(lev + (long long)(cd.y0 + r) * pitch + x0a + 4 * c);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + lane + 64 * k, r = i >> SH, c = i & (WPR - 1);
+        if (r < rh && c < nw) *reinterpret_cast<uint32_t*>(roi + r * RSC + 4 * c) = v[k];
       }
     }
+  } else {
+    for (int i0 = 0; i0 < nw * rh; i0 += 8 * 64) {  // up to 8 dword loads per lane in flight
+      uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int i = i0 + lane + 64 * k;
-      if (i < nw * rh) {
-        const int r = i / nw, c = i - r * nw;
-        *reinterpret_cast<uint32_t*>(roi + r * RS + 4 * c) = v[k];
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + lane + 64 * k;
+        if (i < nw * rh) {
+          const int r = i / nw, c = i - r * nw;
+          v[k] = *reinterpret_cast<const uint32_t*>(lev + (long long)(cd.y0 + r) * pitch + x0a + 4 * c);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = i0 + lane + 64 * k;
+        if (i < nw * rh) {
+          const int r = i / nw, c = i - r * nw;
+          *reinterpret_cast<uint32_t*>(roi + r * RS + 4 * c) = v[k];
+        }
       }
     }
   }
+  // row of detection index q: q / dw, as (q * magic) >> 20 on the constant-stride path
+  // (exact while q * dw < 2^20, which the host guarantees by the ROI bounds)
+  const uint32_t magic = ((1u << 20) + dw - 1) / dw;
+  auto row_of = [&](int q) -> int {
+    if constexpr (RSC != 0) return (int)(((uint32_t)q * magic) >> 20);
+    else return q / dw;
+  };
   for (int i = lane; i < mw * mh; i += 64) m8[i] = 0;
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
-  // 2. quick test, compacted in row-major order
+  // 2a. OpenCV's first two antipodal pairs (ring 0/8 = dy +-3, ring 4/12 = dx +-3) at the lower
+  //     threshold, two horizontally adjacent pixels per lane in packed 16-bit halves; survivors
+  //     (about 1 in 8 pixels) are compacted in row-major order
+  const int pw = (dw + 1) >> 1;
+  const uint32_t pmagic = ((1u << 20) + pw - 1) / pw;
+  const uint32_t T2 = (uint32_t)a.tlow * 0x10001u;
   int nlist = 0;
-  for (int q0 = 0; q0 < dw * dh; q0 += 64) {
+  for (int q0 = 0; q0 < pw * dh; q0 += 64) {
     const int q = q0 + lane;
+    bool p0 = false, p1 = false;
+    int px = 0;
+    if (q < pw * dh) {
+      const int rr = RSC != 0 ? (int)(((uint32_t)q * pmagic) >> 20) : q / pw;
+      const int cc = 2 * (q - rr * pw);
+      px = rr * dw + cc;
+      const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
+      const uint32_t c = pack2(p[0], p[1]);
+      const uint32_t lo = pk_sub16(c, T2), hi = pk_add16(c, T2);
+      const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
+      const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
+      const uint32_t dark = (pk_sub16(u, lo) | pk_sub16(d, lo)) & (pk_sub16(r, lo) | pk_sub16(l, lo));
+      const uint32_t brt = (pk_sub16(hi, u) | pk_sub16(hi, d)) & (pk_sub16(hi, r) | pk_sub16(hi, l));
+      const uint32_t res = dark | brt;
+      p0 = (res & 0x8000u) != 0;
+      p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
+    }
+    const uint64_t b0 = wave_ballot(p0), b1 = wave_ballot(p1);
+    const int pos = nlist + prefix_in_wave(b0) + prefix_in_wave(b1);
+    if (p0) list[pos] = (uint16_t)px;
+    if (p1) list[pos + (p0 ? 1 : 0)] = (uint16_t)(px + 1);
+    nlist += __popcll(b0) + __popcll(b1);
+  }
+  wave_sync();
+  // 2b. the full antipodal quick test on the survivors (in place, order kept)
+  int nq = 0;
+  for (int j0 = 0; j0 < nlist; j0 += 64) {
+    const int j = j0 + lane;
+    int q = 0;
     bool pass = false;
-    if (q < dw * dh) {
-      const int rr = q / dw, cc = q - rr * dw;
+    if (j < nlist) {
+      q = list[j];
+      const int rr = row_of(q), cc = q - rr * dw;
       pass = quick_test(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
     }
     const uint64_t bal = wave_ballot(pass);
-    if (pass) list[nlist + prefix_in_wave(bal)] = (uint16_t)q;
-    nlist += __popcll(bal);
+    wave_sync();  // every lane has read list[j0 .. j0+63] before it is overwritten
+    if (pass) list[nq + prefix_in_wave(bal)] = (uint16_t)q;
+    nq += __popcll(bal);
   }
   wave_sync();
   // 3. arc strength on the list; keep entries that are corners at the lower threshold
   int ncorner = 0;
-  for (int j0 = 0; j0 < nlist; j0 += 64) {
+  for (int j0 = 0; j0 < nq; j0 += 64) {
     const int j = j0 + lane;
     int q = 0, m = 0;
-    if (j < nlist) {
+    if (j < nq) {
       q = list[j];
-      const int rr = q / dw, cc = q - rr * dw;
-      m = arc_strength_lds(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
+      const int rr = row_of(q), cc = q - rr * dw;
+      m = arc_strength_nq(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
       m8[(rr + 1) * mw + (cc + 1)] = (uint8_t)min(m, 255);
     }
     const uint64_t bal = wave_ballot(m > 0);
-    wave_sync();  // every lane has read list[j0 .. j0+63] before it is overwritten
+    wave_sync();
     if (m > 0) list[ncorner + prefix_in_wave(bal)] = (uint16_t)q;
     ncorner += __popcll(bal);
   }
@@ -410,7 +481,7 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
       int rr = 0, cc = 0, sc = 0;
       if (j < ncorner) {
         const int q = list[j];
-        rr = q / dw;
+        rr = row_of(q);
         cc = q - rr * dw;
         const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
         const int m = mp[0];
@@ -1334,8 +1405,13 @@ static size_t octree_lds(const orbfe_extractor* h) {
   return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->scan_cap +
          sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16 + sizeof(uint32_t) * 2 * h->key_lds_cap;
 }
+// constant 64-byte ROI rows when every cell ROI fits (xo <= 3 alignment bytes + rw <= 61) and the
+// multiply-shift row split stays exact (dw^2 * dh < 2^20)
+static int fast_rs(const orbfe_extractor* h) {
+  return (h->roi_w_max <= 61 && h->roi_h_max <= 66) ? 64 : 0;
+}
 static size_t fast_lds(const orbfe_extractor* h) {
-  return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max).total;
+  return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max, fast_rs(h)).total;
 }
 
 #define LAUNCH_TIMED(h, kid, stream, ...)                          \
@@ -1416,7 +1492,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   }
   {
     dim3 grid((a.ncells + 3) / 4, n);
-    LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast, grid, dim3(256), fast_lds(h), st, a));
+    if (fast_rs(h) == 64)
+      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<64>, grid, dim3(256), fast_lds(h), st, a));
+    else
+      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), st, a));
   }
   {
     dim3 grid(h->nlevels, n);
