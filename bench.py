@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true")
+    p.add_argument("--level-launches", action="store_true",
+                   help="per-level k_resize launches instead of k_pyramid (comparison)")
     return p.parse_args()
 
 
@@ -76,6 +78,8 @@ def main():
         host[i], host[B + i] = l, r
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
+    if args.level_launches:
+        ext.debug_force_level_launches(True)
     cap = ext.max_keypoints(H, W)
     d_kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
     d_desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
@@ -296,6 +300,7 @@ def roofline(kt, dom, geo, counts, n_cand, n_img):
       k_octree   2 x 4 B per candidate (gather + partition) + 4 B per survivor
       k_blur     2 x sum_l px_l per image (read each level once, write its blurred copy)
       k_copy0    2 x px_0 per image
+      k_pyramid  2 x px_0 + sum_l>=1 px_l per image (read the input, write every level once)
       k_describe 4 B in + 60 B out per keypoint (+ 749 + 512 gathered bytes per keypoint, not
                  counted: they overlap between keypoints and come from L2)
       k_vocab    32 B in + 12 B out per descriptor
@@ -310,6 +315,7 @@ def roofline(kt, dom, geo, counts, n_cand, n_img):
         "k_describe": 64 * nkp + n_img * 0,  # + the patch pixels it gathers
         "k_blur": n_img * 2 * sum(px),
         "k_copy0": n_img * 2 * px[0],
+        "k_pyramid": n_img * (2 * px[0] + sum(px[1:])),
         "k_vocab": 44 * nkp,
         "k_sft": 64 * nkp + 4 * nkp // 2,
     }

@@ -104,6 +104,8 @@ struct ExtractArgs {
   int ini_th, min_th, tlow;
   int roi_w_max, roi_h_max;
   int node_cap, sort_cap, scan_cap, key_lds_cap;
+  const int4* band_rows;  // k_pyramid: per (band, level) {own0, own1, comp0, comp1}
+  int nbands, band_buf;   // bands per image, bytes per LDS row buffer
   int umax[16];
   AtanConsts atan;
   float factor_pi;
@@ -124,64 +126,45 @@ __device__ __forceinline__ const uint8_t* level_ptr(const ExtractArgs& a, const 
   return a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
 }
 
-// k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows), so every
-// kernel reads every level with aligned dword loads whatever the caller's pitch.
-__global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
-  const LevelDesc ld = a.levels[0];
-  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  const int img = blockIdx.z;
-  if (x >= ld.w || y >= ld.h) return;
-  const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch + x;
-  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
-  uint32_t v = 0;
-  const int n = min(4, ld.w - x);
-  for (int k = 0; k < n; k++) {
-    const uint8_t b = src[k];
-    v |= (uint32_t)b << (8 * k);
-    const int xx = x + k;
-    if (xx >= 1 && xx <= 3) row[-xx] = b;                        // REFLECT_101 column -xx
-    if (xx >= ld.w - 4 && xx <= ld.w - 2) row[2 * ld.w - 2 - xx] = b;  // column 2w-2-xx
-  }
-  if (n == 4) *reinterpret_cast<uint32_t*>(row + x) = v;
-  else
-    for (int k = 0; k < n; k++) row[x + k] = (uint8_t)(v >> (8 * k));  // keep the padding bytes
-}
-
 __device__ __forceinline__ int sat16(int v) { return min(max(v, -32768), 32767); }
 
-// ---------------------------------------------------------------------------------------------
-// k_resize: level l from level l-1 (resize INTER_LINEAR, ORBextractor.cc:1118). One thread per
-// output pixel; xofs/alpha and yofs/beta come from host tables built exactly as OpenCV does.
-__global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
-  const LevelDesc ld = a.levels[l];
-  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;  // 4 output pixels per thread
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  const int img = blockIdx.z;
-  if (x >= ld.w || y >= ld.h) return;
-  const LevelDesc ls = a.levels[l - 1];
-  int spitch;
-  const uint8_t* src = level_ptr(a, ls, img, l - 1, spitch);
-  const int2 yt = a.ytab[ld.tab_y + y];
-  const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
-  const int sy0 = min(max(yt.x, 0), ls.h - 1), sy1 = min(max(yt.x + 1, 0), ls.h - 1);
-  const uint8_t* r0 = src + (long long)sy0 * spitch;
-  const uint8_t* r1 = src + (long long)sy1 * spitch;
-  const int n = min(4, ld.w - x);
-  int2 xt[4];
+// Four output pixels x..x+3 of one row of level `ld` (resize INTER_LINEAR, ORBextractor.cc:1118):
+// source rows r0/r1 (level width sw), OpenCV's fixed-point horizontal pass and, for x below
+// simd_end, the SIMD128 vertical rounding (VResizeLinearVec_32s8u), else FixedPtCast<int,uchar,22>.
+struct Taps4 {
   int p00[4], p01[4], p10[4], p11[4];
+};
+
+// the 16 source bytes of 4 output pixels (independent loads, all in flight together)
+__device__ __forceinline__ Taps4 gather4(const uint8_t* r0, const uint8_t* r1, const int2* xt, int sw) {
+  Taps4 t;
 #pragma unroll
-  for (int k = 0; k < 4; k++) xt[k] = a.xtab[ld.tab_x + min(x + k, ld.w - 1)];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {  // 16 independent source loads in flight
-    const int sx = xt[k].x;
-    p00[k] = r0[sx];
-    p01[k] = r0[sx + 1];  // (for x >= xmax, sx = w-1 and sx+1 is padding: loaded, not used)
-    p10[k] = r1[sx];
-    p11[k] = r1[sx + 1];
+  for (int k = 0; k < 4; k++) {
+    const int sx = xt[k].x, sx1 = min(sx + 1, sw - 1);  // (sx1 only used below xmax, where sx+1 < sw)
+    t.p00[k] = r0[sx];
+    t.p01[k] = r0[sx1];
+    t.p10[k] = r1[sx];
+    t.p11[k] = r1[sx1];
   }
-  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
+  return t;
+}
+
+__device__ __forceinline__ uint32_t combine4(const Taps4& t, const int2* xt, int x, const LevelDesc& ld,
+                                             int b0, int b1) {
+  const int *p00 = t.p00, *p01 = t.p01, *p10 = t.p10, *p11 = t.p11;
   uint32_t packed = 0;
+  if (x + 3 < ld.xmax && x + 3 < ld.simd_end) {
+    // interior (the common case): both taps in range and the SIMD128 rounding; the saturations of
+    // VResizeLinearVec_32s8u never bind here (h <= 255 * 2048, betas in [0, 2048])
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int a0 = (int)(short)(xt[k].y & 0xffff), a1 = (int)(short)((unsigned)xt[k].y >> 16);
+      const int h0 = p00[k] * a0 + p01[k] * a1, h1 = p10[k] * a0 + p11[k] * a1;
+      const int m0 = ((h0 >> 4) * b0) >> 16, m1 = ((h1 >> 4) * b1) >> 16;
+      packed |= (uint32_t)((m0 + m1 + 2) >> 2) << (8 * k);
+    }
+    return packed;
+  }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int xx = x + k;
@@ -201,16 +184,162 @@ __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
     } else {  // FixedPtCast<int, uchar, 22>
       v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
     }
-    const uint8_t b = (uint8_t)min(max(v, 0), 255);
-    packed |= (uint32_t)b << (8 * k);
+    packed |= (uint32_t)min(max(v, 0), 255) << (8 * k);
+  }
+  return packed;
+}
+
+template <typename XT>
+__device__ __forceinline__ uint32_t resize4(const uint8_t* r0, const uint8_t* r1, XT xtab, int x,
+                                            const LevelDesc& ld, int sw, int b0, int b1) {
+  int2 xt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xt[k] = xtab[min(x + k, ld.w - 1)];
+  return combine4(gather4(r0, r1, xt, sw), xt, x, ld, b0, b1);
+}
+
+// Store 4 bytes of a pyramid row at column x (n = valid bytes) plus the REFLECT_101 padding
+// columns -3..-1 and w..w+2 that k_blur reads.
+__device__ __forceinline__ void store_row4(uint8_t* row, int x, int w, uint32_t packed) {
+  if (x >= 4 && x + 8 <= w) {  // interior: no padding column is a reflection of these 4
+    *reinterpret_cast<uint32_t*>(row + x) = packed;
+    return;
+  }
+  const int n = min(4, w - x);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xx = x + k;
+    const uint8_t b = (uint8_t)(packed >> (8 * k));
     if (k < n) {
-      if (xx >= 1 && xx <= 3) row[-xx] = b;  // REFLECT_101 padding for k_blur
-      if (xx >= ld.w - 4 && xx <= ld.w - 2) row[2 * ld.w - 2 - xx] = b;
+      if (xx >= 1 && xx <= 3) row[-xx] = b;
+      if (xx >= w - 4 && xx <= w - 2) row[2 * w - 2 - xx] = b;
     }
   }
   if (n == 4) *reinterpret_cast<uint32_t*>(row + x) = packed;
   else
-    for (int k = 0; k < n; k++) row[x + k] = (uint8_t)(packed >> (8 * k));
+    for (int k = 0; k < n; k++) row[x + k] = (uint8_t)(packed >> (8 * k));  // keep the padding bytes
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_resize: level l from level l-1 (ComputePyramid, ORBextractor.cc:1105-1135), one launch per
+// level -- the fallback of k_pyramid for geometries whose row bands do not fit in LDS.
+#define RESIZE_ROWS 8  // output rows per thread (the column taps are loaded once)
+__global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
+  const LevelDesc ld = a.levels[l];
+  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;  // 4 output pixels per thread
+  const int ybeg = (blockIdx.y * 4 + threadIdx.y) * RESIZE_ROWS;
+  const int img = blockIdx.z;
+  if (x >= ld.w || ybeg >= ld.h) return;
+  const int yend = min(ybeg + RESIZE_ROWS, ld.h);
+  const LevelDesc ls = a.levels[l - 1];
+  int spitch;
+  const uint8_t* src = level_ptr(a, ls, img, l - 1, spitch);
+  int2 xt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) xt[k] = a.xtab[ld.tab_x + min(x + k, ld.w - 1)];
+  const int2* ytab = a.ytab + ld.tab_y;
+  uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+  for (int y = ybeg; y < yend; y += 2) {
+    const bool two = y + 1 < yend;
+    const int2 ya = ytab[y], yb = ytab[two ? y + 1 : y];
+    const uint8_t* ra0 = src + (long long)min(max(ya.x, 0), ls.h - 1) * spitch;
+    const uint8_t* ra1 = src + (long long)min(max(ya.x + 1, 0), ls.h - 1) * spitch;
+    const uint8_t* rb0 = src + (long long)min(max(yb.x, 0), ls.h - 1) * spitch;
+    const uint8_t* rb1 = src + (long long)min(max(yb.x + 1, 0), ls.h - 1) * spitch;
+    const Taps4 ta = gather4(ra0, ra1, xt, ls.w);
+    const Taps4 tb = gather4(rb0, rb1, xt, ls.w);
+    const uint32_t pa = combine4(ta, xt, x, ld, (int)(short)(ya.y & 0xffff), (int)(short)((unsigned)ya.y >> 16));
+    store_row4(out + (long long)y * ld.pitch, x, ld.w, pa);
+    if (two) {
+      const uint32_t pb = combine4(tb, xt, x, ld, (int)(short)(yb.y & 0xffff), (int)(short)((unsigned)yb.y >> 16));
+      store_row4(out + (long long)(y + 1) * ld.pitch, x, ld.w, pb);
+    }
+  }
+}
+
+// k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
+// padding columns) -- the fallback path's level 0; k_pyramid does this itself.
+__global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
+  const LevelDesc ld = a.levels[0];
+  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  const int img = blockIdx.z;
+  if (x >= ld.w || y >= ld.h) return;
+  const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch + x;
+  const int n = min(4, ld.w - x);
+  uint32_t v = 0;
+  for (int k = 0; k < n; k++) v |= (uint32_t)src[k] << (8 * k);
+  store_row4(a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch, x, ld.w, v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_pyramid: the whole of ComputePyramid (ORBextractor.cc:1105-1135) plus the level-0 copy in one
+// launch. Workgroup (band, image) owns a horizontal band of rows at every level and computes the
+// rows it needs -- its own rows plus the halo rows the next level's bilinear taps reach, which
+// neighbouring bands also compute (identical bytes) -- level by level from the input image, with
+// the working rows of consecutive levels ping-ponged in LDS. Only own rows go to HBM. Host table
+// band_rows[band][level] = {own0, own1, comp0, comp1}.
+__global__ __launch_bounds__(256) void k_pyramid(ExtractArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int2 blk = xcd_block2d();
+  const int band = blk.x, img = blk.y, t = threadIdx.x;
+  uint8_t* bufs[2] = {smem, smem + a.band_buf};
+  int2* xt_lds = reinterpret_cast<int2*>(smem + 2 * a.band_buf);
+  const int4* br = a.band_rows + band * a.nlevels;
+  const uint8_t* in = a.img0 + (long long)img * a.img_stride;
+  // level 0: own rows of the caller's image -> the padded pyramid block (was k_copy0)
+  {
+    const LevelDesc ld = a.levels[0];
+    const int4 r = br[0];
+    const int G = (ld.w + 3) >> 2;
+    const uint32_t gm = (uint32_t)((0x100000000ull + G - 1) / G);
+    const int items = (r.y - r.x) * G;
+    uint8_t* base = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+    for (int i = t; i < items; i += 256) {
+      const int ry = (int)__umulhi((uint32_t)i, gm), x = 4 * (i - ry * G), y = r.x + ry;
+      const uint8_t* src = in + (long long)y * a.img_pitch + x;
+      const int n = min(4, ld.w - x);
+      uint32_t v = 0;
+      for (int k = 0; k < n; k++) v |= (uint32_t)src[k] << (8 * k);
+      store_row4(base + (long long)y * ld.pitch, x, ld.w, v);
+    }
+  }
+  for (int l = 1; l < a.nlevels; l++) {
+    const LevelDesc ld = a.levels[l], ls = a.levels[l - 1];
+    const int4 r = br[l];
+    for (int i = t; i < ld.w; i += 256) xt_lds[i] = a.xtab[ld.tab_x + i];
+    __syncthreads();
+    // source rows: the input image for level 1, else the previous level's band in LDS
+    const uint8_t* src;
+    long long spitch;
+    int sbase;
+    if (l == 1) {
+      src = in;
+      spitch = a.img_pitch;
+      sbase = 0;
+    } else {
+      src = bufs[(l - 1) & 1];
+      spitch = (ls.w + 3) & ~3;
+      sbase = br[l - 1].z;
+    }
+    uint8_t* dst = bufs[l & 1];
+    const int dpitch = (ld.w + 3) & ~3;
+    const bool keep = l + 1 < a.nlevels;  // the top level is not read again
+    uint8_t* gbase = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+    const int G = (ld.w + 3) >> 2;
+    const uint32_t gm = (uint32_t)((0x100000000ull + G - 1) / G);
+    const int items = (r.w - r.z) * G;
+    for (int i = t; i < items; i += 256) {
+      const int ry = (int)__umulhi((uint32_t)i, gm), x = 4 * (i - ry * G), y = r.z + ry;
+      const int2 yt = a.ytab[ld.tab_y + y];
+      const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
+      const int sy0 = min(max(yt.x, 0), ls.h - 1) - sbase, sy1 = min(max(yt.x + 1, 0), ls.h - 1) - sbase;
+      const uint32_t packed = resize4(src + sy0 * spitch, src + sy1 * spitch, xt_lds, x, ld, ls.w, b0, b1);
+      if (keep) *reinterpret_cast<uint32_t*>(dst + ry * dpitch + x) = packed;
+      if (y >= r.x && y < r.y) store_row4(gbase + (long long)y * ld.pitch, x, ld.w, packed);
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1056,37 +1185,73 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   for (int k = 0; k < l; k++) obase += lc[k];
   const uint32_t key = a.lvlkeys[(long long)img * a.lvlkey_stride + slot];
   const int cx = key_x(key), cy = key_y(key), score = key_s(key);
-  const long long off = (long long)img * a.pyr_stride + ld.pyr_off + (long long)cy * ld.pitch + cx;
-  const uint8_t* center = a.pyr + off;
-  int m01 = 0, m10 = 0;
-  int cv[12], cu[12], val[12];
+  // keypoints lie in [19, w-20] x [19, h-20] (FAST never fires within 3 px of a cell ROI whose
+  // origin is minBorder - 3 = 16), so both windows below stay inside the padded rows
+  const long long lbase = (long long)img * a.pyr_stride + ld.pyr_off;
+  const int pitch = ld.pitch;
+  // 1. blurred window rows cy-18..cy+18, dword columns from xb = (cx-18) & ~3 (10 per row) -> LDS;
+  //    issued first so its loads overlap the moment computation
+  __shared__ uint32_t s_win[4][37 * 10];
+  uint32_t* win = s_win[w];
+  const int xb = (cx - 18) & ~3;
+  const uint8_t* bsrc = a.blur + lbase + (long long)(cy - 18) * pitch + xb;
+  uint32_t bw[6];
 #pragma unroll
-  for (int k = 0; k < 12; k++) {  // 749 circle pixels: 12 independent loads per lane in flight
-    const int i = lane + 64 * k;
-    cv[k] = i < 749 ? c_circle[2 * i] : 0;
-    cu[k] = i < 749 ? c_circle[2 * i + 1] : 0;
-    val[k] = i < 749 ? center[cv[k] * ld.pitch + cu[k]] : 0;
+  for (int k = 0; k < 6; k++) {
+    const int i = lane + 64 * k;  // 370 dwords
+    const int r = i / 10, c = i - 10 * r;
+    bw[k] = i < 370 ? *reinterpret_cast<const uint32_t*>(bsrc + r * pitch + 4 * c) : 0u;
   }
+  // 2. IC_Angle moments (:75-102) over the 749-pixel circle of the unblurred level: each lane takes
+  //    dwords of rows cy-15..cy+15 (9 per row from xa = (cx-15) & ~3), masks the bytes with
+  //    |u| <= umax[|v|], and sums I and col*I with byte dot products
+  const int xa = (cx - 15) & ~3;
+  const uint8_t* usrc = a.pyr + lbase + (long long)(cy - 15) * pitch + xa;
+  uint32_t ud[5];
 #pragma unroll
-  for (int k = 0; k < 12; k++) {
-    m10 += cu[k] * val[k];
-    m01 += cv[k] * val[k];
+  for (int k = 0; k < 5; k++) {
+    const int i = lane + 64 * k;  // 279 dwords
+    const int r = i / 9, c = i - 9 * r;
+    ud[k] = i < 279 ? *reinterpret_cast<const uint32_t*>(usrc + r * pitch + 4 * c) : 0u;
+  }
+  int m01 = 0, m10 = 0;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const int i = lane + 64 * k;
+    const int r = i / 9, c = i - 9 * r, v = r - 15;
+    const int um = i < 279 ? a.umax[v < 0 ? -v : v] : -1000;
+    const int u0 = xa + 4 * c - cx;  // u of the dword's byte 0
+    const int lo = max(-um - u0, 0), hi = min(um - u0, 3);  // bytes [lo, hi] are on the circle
+    uint32_t mask = 0;
+    if (lo <= hi) mask = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (3 - hi)));
+    const uint32_t px = ud[k] & mask;
+    const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
+    const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
+    m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
+    m01 += v * sI;
   }
   m01 = wave_sum(m01);
   m10 = wave_sum(m10);
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
   const float ang = angle * a.factor_pi;
   const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-  const uint8_t* bc = a.blur + off;
-  const int pitch = ld.pitch;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const int i = lane + 64 * k;
+    if (i < 370) win[i] = bw[k];
+  }
+  wave_sync();
+  // 3. the 256 steered tests (:105-151) on the LDS window: pixel (dy, dx) at byte
+  //    (dy + 18) * 40 + (dx + cx - xb)
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(win) + 18 * 40 + (cx - xb);
   uint64_t words[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int p = q * 64 + lane;
     const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
     const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-    const int t0 = bc[cv_round_f(x0 * sb + y0 * ca) * pitch + cv_round_f(x0 * ca - y0 * sb)];
-    const int t1 = bc[cv_round_f(x1 * sb + y1 * ca) * pitch + cv_round_f(x1 * ca - y1 * sb)];
+    const int t0 = wb[cv_round_f(x0 * sb + y0 * ca) * 40 + cv_round_f(x0 * ca - y0 * sb)];
+    const int t1 = wb[cv_round_f(x1 * sb + y1 * ca) * 40 + cv_round_f(x1 * ca - y1 * sb)];
     words[q] = wave_ballot(t0 < t1);
   }
   const long long o = (long long)img * a.out_cap + obase;
@@ -1139,6 +1304,7 @@ struct orbfe_extractor {
   int umax[16];
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
+  int force_level_launches = 0;      // orbfe_debug_force_level_launches
   hipStream_t stream = nullptr;
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
@@ -1152,6 +1318,9 @@ struct orbfe_extractor {
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
   int2* d_ytab = nullptr;
+  int4* d_band_rows = nullptr;
+  int nbands = 0, band_buf = 0;  // k_pyramid plan (nbands 0: per-level launches)
+  size_t pyramid_lds = 0;
   // batch buffers
   int batch_cap = 0;
   uint8_t* d_in = nullptr;
@@ -1187,8 +1356,8 @@ struct orbfe_extractor {
 };
 
 static const char* kKernelNames[] = {"k_resize", "k_fast", "k_octree", "k_describe", "k_copy0",
-                                     "k_blur"};
-static const int kNumKernels = 6;
+                                     "k_blur", "k_pyramid"};
+static const int kNumKernels = 7;
 
 static hipEvent_t pool_event(orbfe_extractor* h) {
   if (!h->event_pool.empty()) {
@@ -1311,8 +1480,58 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
       d.simd_end = se;
     }
   }
+  // k_pyramid row bands: own rows per band at every level, plus the halo rows the next level's
+  // taps reach (computed top-down); the largest working band of levels 1..L-2 sizes the LDS
+  std::vector<int4> bands;
+  int nb_sel = 0, buf_sel = 0;
+  size_t lds_sel = 0;
+  if (L >= 2) {
+    const int cands[] = {16, 24, 32, 48, 64, 12, 8, 4, 2, 1};
+    for (int nb : cands) {
+      if (nb > lv[L - 1].h) continue;
+      std::vector<int4> br((size_t)nb * L);
+      int buf = 0;
+      for (int k = 0; k < nb; k++) {
+        for (int l = 0; l < L; l++) {
+          const int o0 = (int)((long long)k * lv[l].h / nb), o1 = (int)((long long)(k + 1) * lv[l].h / nb);
+          br[(size_t)k * L + l] = make_int4(o0, o1, o0, o1);
+        }
+        for (int l = L - 1; l >= 2; l--) {
+          const int4 c = br[(size_t)k * L + l];
+          const int hs = lv[l - 1].h;
+          const int s0 = std::min(std::max(yt[lv[l].tab_y + c.z].x, 0), hs - 1);
+          const int s1 = std::min(std::max(yt[lv[l].tab_y + c.w - 1].x + 1, 0), hs - 1);
+          int4& p = br[(size_t)k * L + l - 1];
+          p.z = std::min(p.x, s0);
+          p.w = std::max(p.y, s1 + 1);
+        }
+        for (int l = 1; l + 1 < L; l++) {
+          const int4 c = br[(size_t)k * L + l];
+          buf = std::max(buf, (c.w - c.z) * ((lv[l].w + 3) & ~3));
+        }
+      }
+      buf = (buf + 15) & ~15;
+      const size_t lds = 2 * (size_t)buf + sizeof(int2) * lv[1].w;
+      if (lds <= 64 * 1024) {
+        bands = br;
+        nb_sel = nb;
+        buf_sel = buf;
+        lds_sel = lds;
+        break;
+      }
+    }
+  }
   // release old geometry buffers and upload new ones
   hipSetDevice(h->device);
+  hipFree(h->d_band_rows);
+  h->d_band_rows = nullptr;
+  if (!bands.empty()) {
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_band_rows, sizeof(int4) * bands.size()));
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_band_rows, bands.data(), sizeof(int4) * bands.size(), hipMemcpyHostToDevice));
+  }
+  h->nbands = nb_sel;
+  h->band_buf = buf_sel;
+  h->pyramid_lds = lds_sel;
   hipFree(h->d_levels);
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
@@ -1472,6 +1691,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.sort_cap = h->sort_cap;
   a.scan_cap = h->scan_cap;
   a.key_lds_cap = h->key_lds_cap;
+  a.band_rows = h->d_band_rows;
+  a.nbands = h->nbands;
+  a.band_buf = h->band_buf;
   for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
   a.atan.p1 = 0.9997878412794807f * (float)(180 / M_PI);
   a.atan.p3 = -0.3258083974640975f * (float)(180 / M_PI);
@@ -1480,15 +1702,20 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
 
-  {
-    const LevelDesc& d = h->levels[0];
-    dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
-    LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
-  }
-  for (int l = 1; l < h->nlevels; l++) {
-    const LevelDesc& d = h->levels[l];
-    dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
-    LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+  if (h->nbands > 0 && !h->force_level_launches) {
+    dim3 grid(h->nbands, n);
+    LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), h->pyramid_lds, st, a));
+  } else {
+    {
+      const LevelDesc& d = h->levels[0];
+      dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
+      LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
+    }
+    for (int l = 1; l < h->nlevels; l++) {
+      const LevelDesc& d = h->levels[l];
+      dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
+      LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+    }
   }
   {
     dim3 grid((a.ncells + 3) / 4, n);
@@ -1610,6 +1837,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
+  hipFree(h->d_band_rows);
   hipFree(h->d_in);
   hipFree(h->d_kps);
   hipFree(h->d_desc);
@@ -1906,6 +2134,12 @@ extern "C" int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level,
   ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   ORBFE_HIP_CHECK(hipMemcpy2D(out, d.w, h->d_blur + (size_t)image * h->pyr_stride + d.pyr_off, d.pitch,
                               d.w, d.h, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_force_level_launches(orbfe_extractor* h, int on) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->force_level_launches = on ? 1 : 0;
   return ORBFE_OK;
 }
 

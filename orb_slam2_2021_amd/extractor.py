@@ -169,7 +169,7 @@ class ORBextractor:
         return [self.level(l) for l in range(self.nlevels)]
 
     # ---- instrumentation ----------------------------------------------------------------
-    KERNELS = ("k_resize", "k_fast", "k_octree", "k_describe", "k_copy0", "k_blur")
+    KERNELS = ("k_resize", "k_fast", "k_octree", "k_describe", "k_copy0", "k_blur", "k_pyramid")
 
     def set_profiling(self, kernels=True) -> None:
         """True / False, or an iterable of kernel names to time with HIP events."""
@@ -228,6 +228,11 @@ class ORBextractor:
     def debug_set_octree_key_cap(self, cap: int) -> None:
         """Limit the keys DistributeOctTree keeps in LDS (0: global-memory path; <0: auto)."""
         L.check(self._lib.orbfe_debug_set_octree_key_cap(self._h, int(cap)), "set_octree_key_cap")
+
+    def debug_force_level_launches(self, on: bool = True) -> None:
+        """Build the pyramid with one k_resize launch per level instead of k_pyramid."""
+        L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),
+                "force_level_launches")
 
     def geometry(self, rows: int, cols: int) -> np.ndarray:
         info = np.zeros(7 * self.nlevels, np.int32)

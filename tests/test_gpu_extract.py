@@ -72,12 +72,26 @@ def test_other_parameters(require_gpu):
         assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
 
-def test_scalar_resize_mode(require_gpu):
+@pytest.mark.parametrize("level_launches", [False, True])
+def test_scalar_resize_mode(require_gpu, level_launches):
     img = synth_frame(2, 376, 1241)
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_force_level_launches(level_launches)
     ext.set_resize_mode(ORBFE_RESIZE_SCALAR)
     ref.set_resize_mode(ORBFE_RESIZE_SCALAR)
     assert_same_extraction(ext, ref, img)
+
+
+@pytest.mark.parametrize("shape", [(376, 1241), (480, 640), (260, 1500), (900, 700)])
+def test_pyramid_paths_agree(require_gpu, shape):
+    """k_pyramid (banded, one launch) and the per-level k_resize launches give the reference
+    pyramid on wide, tall and KITTI/TUM shapes."""
+    img = synth_frame(9, *shape)
+    ref = RefExtractor(1000, 1.2, 8, 20, 7)
+    for forced in (False, True):
+        ext = ORBextractor(1000, 1.2, 8, 20, 7)
+        ext.debug_force_level_launches(forced)
+        assert_same_extraction(ext, ref, img)
 
 
 def test_flat_and_sparse_images(require_gpu):
