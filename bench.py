@@ -42,8 +42,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true")
-    p.add_argument("--level-launches", action="store_true",
-                   help="per-level k_resize launches instead of k_pyramid (comparison)")
+    p.add_argument("--banded-pyramid", action="store_true",
+                   help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
     return p.parse_args()
 
 
@@ -78,8 +78,8 @@ def main():
         host[i], host[B + i] = l, r
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
-    if args.level_launches:
-        ext.debug_force_level_launches(True)
+    if args.banded_pyramid:
+        ext.debug_force_level_launches(False)
     cap = ext.max_keypoints(H, W)
     d_kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
     d_desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)

@@ -23,8 +23,8 @@ int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, 
 /* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
  * global-memory path for every level; < 0 restores the automatic size). */
 int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
-/* 1: build the pyramid with one k_resize launch per level (the fallback path) instead of the
- * single banded k_pyramid launch; 0: automatic. */
+/* 1 (default): build the pyramid with one k_resize launch per level; 0: one banded k_pyramid
+ * launch when its row bands fit in LDS (currently slower on MI355X; kept for comparison). */
 int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
 #ifdef __cplusplus
 }

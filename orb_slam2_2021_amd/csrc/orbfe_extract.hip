@@ -1304,7 +1304,7 @@ struct orbfe_extractor {
   int umax[16];
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
-  int force_level_launches = 0;      // orbfe_debug_force_level_launches
+  int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level)
   hipStream_t stream = nullptr;
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;

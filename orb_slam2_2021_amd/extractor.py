@@ -230,7 +230,7 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_key_cap(self._h, int(cap)), "set_octree_key_cap")
 
     def debug_force_level_launches(self, on: bool = True) -> None:
-        """Build the pyramid with one k_resize launch per level instead of k_pyramid."""
+        """True (default): one k_resize launch per level; False: the banded k_pyramid launch."""
         L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),
                 "force_level_launches")
 
