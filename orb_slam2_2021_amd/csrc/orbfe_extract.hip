@@ -69,6 +69,7 @@ struct LevelDesc {
   int tab_x, tab_y;          // resize table offsets (l >= 1)
   int xmax, simd_end;        // resize: first column using the clamped path / end of SIMD columns
   int tile_begin, tiles_x;   // k_blur tiles of this level
+  int rgrp_begin, rwin_ok;   // k_resize 4-column group tables; 1 when every group's taps fit 8 bytes
 };
 
 struct CellDesc {
@@ -105,6 +106,8 @@ struct ExtractArgs {
   int roi_w_max, roi_h_max;
   int node_cap, sort_cap, scan_cap, key_lds_cap;
   const int4* band_rows;  // k_pyramid: per (band, level) {own0, own1, comp0, comp1}
+  const uint4* rgrp;      // k_resize: per 4-column group {sel[4]}, {alpha[4]} (2 x uint4)
+  const int* rgx0;        // k_resize: first source column of each group
   int nbands, band_buf;   // bands per image, bytes per LDS row buffer
   int umax[16];
   AtanConsts atan;
@@ -254,6 +257,69 @@ __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
       const uint32_t pb = combine4(tb, xt, x, ld, (int)(short)(yb.y & 0xffff), (int)(short)((unsigned)yb.y >> 16));
       store_row4(out + (long long)(y + 1) * ld.pitch, x, ld.w, pb);
     }
+  }
+}
+
+// k_resize_win: the same level step with the taps of 4 output columns gathered from one 8-byte
+// source window per row: 3 aligned dword loads + 2 v_alignbyte per source row, then per pixel one
+// v_perm (the two taps as u16 halves) and one v_dot2_u32_u16 with the packed alphas. Two output
+// rows per thread (4 source rows, 12 loads in flight). Used when every group's taps span <= 8
+// bytes (LevelDesc::rwin_ok; scale factors up to ~1.6).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2_u16(uint32_t a, uint32_t b) {
+  return (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), 0u, false);
+}
+
+__global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
+  const LevelDesc ld = a.levels[l];
+  const int g = blockIdx.x * 64 + threadIdx.x, x = 4 * g;
+  const int y0 = (blockIdx.y * 4 + threadIdx.y) * 2;
+  const int img = blockIdx.z;
+  if (x >= ld.w || y0 >= ld.h) return;
+  const LevelDesc ls = a.levels[l - 1];
+  const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ls.pyr_off;
+  const int gi = ld.rgrp_begin + g;
+  const int sx0 = a.rgx0[gi];
+  const uint4 sel = a.rgrp[2 * gi], alp = a.rgrp[2 * gi + 1];
+  const bool two = y0 + 1 < ld.h;
+  const int2 ya = a.ytab[ld.tab_y + y0], yb = a.ytab[ld.tab_y + (two ? y0 + 1 : y0)];
+  int rows[4] = {ya.x, ya.x + 1, yb.x, yb.x + 1};
+  uint32_t wv[4][3];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(
+        src + (long long)min(max(rows[r], 0), ls.h - 1) * ls.pitch + (sx0 & ~3));
+#pragma unroll
+    for (int k = 0; k < 3; k++) wv[r][k] = p[k];
+  }
+  const int sh = sx0 & 3;
+  uint32_t W0[4], W1[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
+    W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
+  }
+  const uint32_t sels[4] = {sel.x, sel.y, sel.z, sel.w}, alps[4] = {alp.x, alp.y, alp.z, alp.w};
+  uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+#pragma unroll
+  for (int o = 0; o < 2; o++) {
+    if (o == 1 && !two) break;
+    const int2 yt = o ? yb : ya;
+    const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int h0 = dot2_u16(__builtin_amdgcn_perm(W1[2 * o], W0[2 * o], sels[k]), alps[k]);
+      const int h1 = dot2_u16(__builtin_amdgcn_perm(W1[2 * o + 1], W0[2 * o + 1], sels[k]), alps[k]);
+      int v;
+      if (x + k < ld.simd_end) {  // VResizeLinearVec_32s8u; its saturations never bind here
+        v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+      } else {  // FixedPtCast<int, uchar, 22>
+        v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
+      }
+      packed |= (uint32_t)v << (8 * k);
+    }
+    store_row4(out + (long long)(y0 + o) * ld.pitch, x, ld.w, packed);
   }
 }
 
@@ -1318,6 +1384,8 @@ struct orbfe_extractor {
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
   int2* d_ytab = nullptr;
+  uint4* d_rgrp = nullptr;
+  int* d_rgx0 = nullptr;
   int4* d_band_rows = nullptr;
   int nbands = 0, band_buf = 0;  // k_pyramid plan (nbands 0: per-level launches)
   size_t pyramid_lds = 0;
@@ -1376,6 +1444,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   std::vector<LevelDesc> lv(L);
   std::vector<CellDesc> cells;
   std::vector<int2> xt, yt;
+  std::vector<uint4> rgrp;
+  std::vector<int> rgx0;
   long long pyr = 0;
   int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0, tiles = 0;
   for (int l = 0; l < L; l++) {
@@ -1472,6 +1542,31 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
         yt.push_back(make_int2(sy, (int)(((unsigned)(unsigned short)b1 << 16) | (unsigned short)b0)));
       }
       d.xmax = xmax;
+      // 4-column groups: the taps of output columns 4g..4g+3 as byte selectors into the 8-byte
+      // source window starting at sx(4g); columns at or past xmax take (sx, sx) with alpha
+      // (2048, 0), i.e. S[sx] * ONE as OpenCV does there
+      d.rgrp_begin = (int)rgx0.size();
+      d.rwin_ok = 1;
+      for (int g = 0; 4 * g < d.w; g++) {
+        const int x0 = xt[d.tab_x + 4 * g].x;
+        uint32_t sel[4], alp[4];
+        for (int k = 0; k < 4; k++) {
+          const int col = std::min(4 * g + k, d.w - 1);
+          const int2 e = xt[d.tab_x + col];
+          const int o = e.x - x0;
+          if (col >= xmax) {
+            sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)o << 16) | 0x0c000000u;
+            alp[k] = 2048u;
+          } else {
+            sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
+            alp[k] = (uint32_t)e.y;
+          }
+          if (o < 0 || o + 1 > 7) d.rwin_ok = 0;
+        }
+        rgx0.push_back(x0);
+        rgrp.push_back(make_uint4(sel[0], sel[1], sel[2], sel[3]));
+        rgrp.push_back(make_uint4(alp[0], alp[1], alp[2], alp[3]));
+      }
       int se = 0;
       if (h->resize_mode == ORBFE_RESIZE_SIMD128) {
         se = 16 * (d.w / 16);
@@ -1525,6 +1620,16 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   hipSetDevice(h->device);
   hipFree(h->d_band_rows);
   h->d_band_rows = nullptr;
+  hipFree(h->d_rgrp);
+  hipFree(h->d_rgx0);
+  h->d_rgrp = nullptr;
+  h->d_rgx0 = nullptr;
+  if (!rgx0.empty()) {
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_rgrp, sizeof(uint4) * rgrp.size()));
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_rgx0, sizeof(int) * rgx0.size()));
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_rgrp, rgrp.data(), sizeof(uint4) * rgrp.size(), hipMemcpyHostToDevice));
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_rgx0, rgx0.data(), sizeof(int) * rgx0.size(), hipMemcpyHostToDevice));
+  }
   if (!bands.empty()) {
     ORBFE_HIP_CHECK(hipMalloc(&h->d_band_rows, sizeof(int4) * bands.size()));
     ORBFE_HIP_CHECK(hipMemcpy(h->d_band_rows, bands.data(), sizeof(int4) * bands.size(), hipMemcpyHostToDevice));
@@ -1692,6 +1797,8 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.scan_cap = h->scan_cap;
   a.key_lds_cap = h->key_lds_cap;
   a.band_rows = h->d_band_rows;
+  a.rgrp = h->d_rgrp;
+  a.rgx0 = h->d_rgx0;
   a.nbands = h->nbands;
   a.band_buf = h->band_buf;
   for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
@@ -1713,8 +1820,13 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     }
     for (int l = 1; l < h->nlevels; l++) {
       const LevelDesc& d = h->levels[l];
-      dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
-      LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+      if (d.rwin_ok) {
+        dim3 grid((d.w + 255) / 256, (d.h + 7) / 8, n), block(64, 4);
+        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win, grid, block, 0, st, a, l));
+      } else {
+        dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
+        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+      }
     }
   }
   {
@@ -1838,6 +1950,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_band_rows);
+  hipFree(h->d_rgrp);
+  hipFree(h->d_rgx0);
   hipFree(h->d_in);
   hipFree(h->d_kps);
   hipFree(h->d_desc);

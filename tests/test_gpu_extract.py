@@ -119,6 +119,14 @@ def test_octree_global_key_path(require_gpu, cap):
     assert_same_extraction(ext, ref, noise)
 
 
+@pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
+def test_large_scale_factors(require_gpu, params):
+    """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
+    k_resize path."""
+    img = synth_frame(13, 600, 1241)
+    assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
+
+
 def test_empty_image(require_gpu):
     k, d = ORBextractor(2000, 1.2, 8, 20, 7)(np.zeros((0, 0), np.uint8))
     assert len(k) == 0 and d is None
