@@ -326,16 +326,35 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
 // padding columns) -- the fallback path's level 0; k_pyramid does this itself.
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
+  // 16 columns per thread: 5 aligned dword loads + v_alignbyte (the caller's pitch need not be a
+  // multiple of 4), one 16-byte store; byte loads only for the last columns of a row
   const LevelDesc ld = a.levels[0];
-  const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int x = (blockIdx.x * 64 + threadIdx.x) * 16;
   const int y = blockIdx.y * 4 + threadIdx.y;
   const int img = blockIdx.z;
   if (x >= ld.w || y >= ld.h) return;
   const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch + x;
-  const int n = min(4, ld.w - x);
-  uint32_t v = 0;
-  for (int k = 0; k < n; k++) v |= (uint32_t)src[k] << (8 * k);
-  store_row4(a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch, x, ld.w, v);
+  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
+  uint32_t v[4];
+  if (x + 20 <= ld.w) {  // the 5th dword ends at most 4 bytes past column x + 15: inside the row
+    const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src - sh);
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) w[k] = p[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      v[k] = 0;
+      for (int j = 0; j < 4; j++)
+        if (x + 4 * k + j < ld.w) v[k] |= (uint32_t)src[4 * k + j] << (8 * j);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (x + 4 * k < ld.w) store_row4(row, x + 4 * k, ld.w, v[k]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1230,102 +1249,109 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
 // the blurred level; bits land as 4 wave ballots (64 pairs each = 8 descriptor bytes).
 __constant__ int8_t c_circle[2 * 752];  // (v, u) of the IC_Angle circle, 749 used
 
+__device__ __forceinline__ int group16_sum(int v) {  // sum over the 16-lane group of this lane
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+
+// Four keypoints per wavefront, 16 lanes each, so the per-keypoint scalar work (level lookup,
+// fastAtan2, the double-precision cos/sin of computeOrbDescriptor) is shared by 4 keypoints.
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
-  const int w = wave_id(), lane = lane_id();
+  const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
   const int img = blk.y;
-  const int slot = blk.x * 4 + w;
+  const int slot = (blk.x * 4 + w) * 4 + grp;
   const int32_t* lc = a.lvlcnt + (long long)img * a.nlevels;
   if (blk.x == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int l = 0; l < a.nlevels; l++) tot += lc[l];
     a.out_counts[img] = tot;
   }
-  if (slot >= a.total_key_slots) return;
+  bool valid = slot < a.total_key_slots;
   int l = 0;
   while (l + 1 < a.nlevels && slot >= a.levels[l + 1].key_begin) l++;
   const LevelDesc ld = a.levels[l];
   const int idx = slot - ld.key_begin;
-  if (idx >= lc[l]) return;
+  valid = valid && idx < lc[l];
+  if (__ballot(valid) == 0) return;  // the whole wavefront is past the level ends
   int obase = idx;
   for (int k = 0; k < l; k++) obase += lc[k];
-  const uint32_t key = a.lvlkeys[(long long)img * a.lvlkey_stride + slot];
+  const uint32_t key = valid ? a.lvlkeys[(long long)img * a.lvlkey_stride + slot] : pack_key(19, 19, 0);
+  // (an invalid group reads a harmless in-range window of the same level and writes nothing)
   const int cx = key_x(key), cy = key_y(key), score = key_s(key);
   // keypoints lie in [19, w-20] x [19, h-20] (FAST never fires within 3 px of a cell ROI whose
   // origin is minBorder - 3 = 16), so both windows below stay inside the padded rows
   const long long lbase = (long long)img * a.pyr_stride + ld.pyr_off;
   const int pitch = ld.pitch;
-  // 1. blurred window rows cy-18..cy+18, dword columns from xb = (cx-18) & ~3 (10 per row) -> LDS;
-  //    issued first so its loads overlap the moment computation
-  __shared__ uint32_t s_win[4][37 * 10];
-  uint32_t* win = s_win[w];
+  // 1. blurred window rows cy-18..cy+18, dword columns from xb = (cx-18) & ~3 (10 per row) -> LDS
+  __shared__ uint32_t s_win[16][37 * 10];
+  uint32_t* win = s_win[w * 4 + grp];
   const int xb = (cx - 18) & ~3;
   const uint8_t* bsrc = a.blur + lbase + (long long)(cy - 18) * pitch + xb;
-  uint32_t bw[6];
+  // (370 dwords: two batches of 12 loads per lane, landing in LDS before the moments start)
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int i = lane + 64 * k;  // 370 dwords
-    const int r = i / 10, c = i - 10 * r;
-    bw[k] = i < 370 ? *reinterpret_cast<const uint32_t*>(bsrc + r * pitch + 4 * c) : 0u;
+  for (int b = 0; b < 2; b++) {
+    uint32_t bw[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int i = l16 + 16 * (12 * b + k);
+      const int r = i / 10, c = i - 10 * r;
+      bw[k] = i < 370 ? *reinterpret_cast<const uint32_t*>(bsrc + r * pitch + 4 * c) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      const int i = l16 + 16 * (12 * b + k);
+      if (i < 370) win[i] = bw[k];
+    }
   }
-  // 2. IC_Angle moments (:75-102) over the 749-pixel circle of the unblurred level: each lane takes
-  //    dwords of rows cy-15..cy+15 (9 per row from xa = (cx-15) & ~3), masks the bytes with
-  //    |u| <= umax[|v|], and sums I and col*I with byte dot products
+  // 2. IC_Angle moments (:75-102) over the 749-pixel circle of the unblurred level: dwords of rows
+  //    cy-15..cy+15 (9 per row from xa = (cx-15) & ~3), bytes masked to |u| <= umax[|v|], sums of
+  //    I and col*I by byte dot products
   const int xa = (cx - 15) & ~3;
   const uint8_t* usrc = a.pyr + lbase + (long long)(cy - 15) * pitch + xa;
-  uint32_t ud[5];
-#pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const int i = lane + 64 * k;  // 279 dwords
-    const int r = i / 9, c = i - 9 * r;
-    ud[k] = i < 279 ? *reinterpret_cast<const uint32_t*>(usrc + r * pitch + 4 * c) : 0u;
-  }
   int m01 = 0, m10 = 0;
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const int i = lane + 64 * k;
+  for (int k = 0; k < 18; k++) {
+    const int i = l16 + 16 * k;  // 279 dwords
     const int r = i / 9, c = i - 9 * r, v = r - 15;
+    const uint32_t d = i < 279 ? *reinterpret_cast<const uint32_t*>(usrc + r * pitch + 4 * c) : 0u;
     const int um = i < 279 ? a.umax[v < 0 ? -v : v] : -1000;
     const int u0 = xa + 4 * c - cx;  // u of the dword's byte 0
     const int lo = max(-um - u0, 0), hi = min(um - u0, 3);  // bytes [lo, hi] are on the circle
     uint32_t mask = 0;
     if (lo <= hi) mask = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (3 - hi)));
-    const uint32_t px = ud[k] & mask;
+    const uint32_t px = d & mask;
     const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
     const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
     m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
     m01 += v * sI;
   }
-  m01 = wave_sum(m01);
-  m10 = wave_sum(m10);
+  m01 = group16_sum(m01);
+  m10 = group16_sum(m10);
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
   const float ang = angle * a.factor_pi;
   const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const int i = lane + 64 * k;
-    if (i < 370) win[i] = bw[k];
-  }
   wave_sync();
-  // 3. the 256 steered tests (:105-151) on the LDS window: pixel (dy, dx) at byte
-  //    (dy + 18) * 40 + (dx + cx - xb)
+  // 3. the 256 steered tests (:105-151) on the LDS window, pixel (dy, dx) at byte
+  //    (dy + 18) * 40 + (dx + cx - xb); test p = 16 j + l16 lands in bit l16 of the group's
+  //    16-bit slice of ballot j = descriptor bytes 2j, 2j+1
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(win) + 18 * 40 + (cx - xb);
-  uint64_t words[4];
+  uint32_t dv = 0;  // lane l16 < 8 collects descriptor dword l16 = bytes 4 l16 .. 4 l16 + 3
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int p = q * 64 + lane;
+  for (int j = 0; j < 16; j++) {
+    const int p = 16 * j + l16;
     const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
     const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
     const int t0 = wb[cv_round_f(x0 * sb + y0 * ca) * 40 + cv_round_f(x0 * ca - y0 * sb)];
     const int t1 = wb[cv_round_f(x1 * sb + y1 * ca) * 40 + cv_round_f(x1 * ca - y1 * sb)];
-    words[q] = wave_ballot(t0 < t1);
+    const uint32_t hv = (uint32_t)(wave_ballot(t0 < t1) >> (16 * grp)) & 0xffffu;
+    if (l16 == (j >> 1)) dv |= hv << (16 * (j & 1));
   }
+  if (!valid) return;
   const long long o = (long long)img * a.out_cap + obase;
-  if (lane < 4) {
-    uint64_t* d = reinterpret_cast<uint64_t*>(a.out_desc + o * 32);
-    d[lane] = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
-  }
-  if (lane == 0) {
+  if (l16 < 8) reinterpret_cast<uint32_t*>(a.out_desc + o * 32)[l16] = dv;
+  if (l16 == 0) {
     orbfe_keypoint kp;
     kp.x = (float)cx;
     kp.y = (float)cy;
@@ -1815,7 +1841,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   } else {
     {
       const LevelDesc& d = h->levels[0];
-      dim3 grid((d.w + 255) / 256, (d.h + 3) / 4, n), block(64, 4);
+      dim3 grid((d.w + 1023) / 1024, (d.h + 3) / 4, n), block(64, 4);
       LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
     }
     for (int l = 1; l < h->nlevels; l++) {
@@ -1848,7 +1874,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, a));
   }
   {
-    dim3 grid((h->total_key_slots + 3) / 4, n);
+    dim3 grid((h->total_key_slots + 15) / 16, n);
     LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, a));
   }
   ORBFE_HIP_CHECK(hipGetLastError());
