@@ -484,6 +484,70 @@ __device__ __forceinline__ int arc_strength_nq(const uint8_t* p, int s, int tlow
   return m < tlow + 1 ? 0 : m;
 }
 
+// two u8 values in the 16-bit halves of a dword, and packed 16-bit add / subtract (v_pk_*_u16)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2(uint32_t lo, uint32_t hi) { return lo | (hi << 16); }
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
+}
+
+// Two pixels at once (pa -> low 16 bits, pb -> high 16 bits): OpenCV's full antipodal quick test
+// at tlow, then the arc strength M for the pixels passing it; returns the packed M (0 where the
+// pixel is no corner at tlow), the same values arc_strength_nq gives.
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+typedef short i16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2v, a), __builtin_bit_cast(u16x2v, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2v, a), __builtin_bit_cast(u16x2v, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2v, a), __builtin_bit_cast(i16x2v, b)));
+}
+__device__ __forceinline__ uint32_t arc_strength_pk(const uint8_t* pa, const uint8_t* pb, int s, int tlow) {
+  const uint32_t c = (uint32_t)pa[0] | ((uint32_t)pb[0] << 16);
+  uint32_t x[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x[k] = (uint32_t)pa[ring_off(k, s)] | ((uint32_t)pb[ring_off(k, s)] << 16);
+  const uint32_t T2 = (uint32_t)tlow * 0x10001u;
+  const uint32_t lo = pk_sub16(c, T2), hi = pk_add16(c, T2);
+  uint32_t dark = 0xffffffffu, brt = 0xffffffffu;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    dark &= pk_sub16(x[k], lo) | pk_sub16(x[k + 8], lo);
+    brt &= pk_sub16(hi, x[k]) | pk_sub16(hi, x[k + 8]);
+  }
+  const uint32_t pass = (dark | brt) & 0x80008000u;
+  if (pass == 0) return 0;
+  uint32_t mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = pk_min_u16(x[k], x[(k + 1) & 15]);
+    mx2[k] = pk_max_u16(x[k], x[(k + 1) & 15]);
+  }
+  uint32_t mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = pk_min_u16(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = pk_max_u16(mx2[k], mx2[(k + 2) & 15]);
+  }
+  uint32_t B = 0, A = 0x00ff00ffu;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    B = pk_max_u16(B, pk_min_u16(pk_min_u16(mn4[k], mn4[(k + 4) & 15]), x[(k + 8) & 15]));
+    A = pk_min_u16(A, pk_max_u16(pk_max_u16(mx4[k], mx4[(k + 4) & 15]), x[(k + 8) & 15]));
+  }
+  const uint32_t m = pk_max_i16(pk_sub16(c, A), pk_sub16(B, c));  // max(v - A, B - v), signed
+  const int ma = (int)(short)(m & 0xffffu), mb = (int)(short)(m >> 16);
+  const uint32_t ra = (pass & 0x8000u) && ma >= tlow + 1 ? (uint32_t)ma : 0u;
+  const uint32_t rb = (pass & 0x80000000u) && mb >= tlow + 1 ? (uint32_t)mb : 0u;
+  return ra | (rb << 16);
+}
+
 __device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
   return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
 }
@@ -510,16 +574,6 @@ __device__ __forceinline__ bool quick_test(const uint8_t* p, int s, int t) {
     brt &= (hi - x) | (hi - y);
   }
   return (dark | brt) < 0;
-}
-
-// two u8 values in the 16-bit halves of a dword, and packed 16-bit add / subtract (v_pk_*_u16)
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pack2(uint32_t lo, uint32_t hi) { return lo | (hi << 16); }
-__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
-}
-__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
 }
 
 struct FastLds {
@@ -650,38 +704,32 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
     nlist += __popcll(b0) + __popcll(b1);
   }
   wave_sync();
-  // 2b. the full antipodal quick test on the survivors (in place, order kept)
-  int nq = 0;
-  for (int j0 = 0; j0 < nlist; j0 += 64) {
-    const int j = j0 + lane;
-    int q = 0;
-    bool pass = false;
-    if (j < nlist) {
-      q = list[j];
-      const int rr = row_of(q), cc = q - rr * dw;
-      pass = quick_test(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
-    }
-    const uint64_t bal = wave_ballot(pass);
-    wave_sync();  // every lane has read list[j0 .. j0+63] before it is overwritten
-    if (pass) list[nq + prefix_in_wave(bal)] = (uint16_t)q;
-    nq += __popcll(bal);
-  }
-  wave_sync();
-  // 3. arc strength on the list; keep entries that are corners at the lower threshold
+  // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the full antipodal
+  //     quick test, then the arc strength (OpenCV cornerScore + 1) of the entries that pass; the
+  //     corners at the lower threshold go to m8 and, compacted in order, back into the list
   int ncorner = 0;
-  for (int j0 = 0; j0 < nq; j0 += 64) {
-    const int j = j0 + lane;
-    int q = 0, m = 0;
-    if (j < nq) {
-      q = list[j];
-      const int rr = row_of(q), cc = q - rr * dw;
-      m = arc_strength_nq(R + (rr + 3) * RS + (cc + 3), RS, a.tlow);
-      m8[(rr + 1) * mw + (cc + 1)] = (uint8_t)min(m, 255);
+  for (int j0 = 0; j0 < nlist; j0 += 128) {
+    const int ja = j0 + 2 * lane, jb = ja + 1;
+    int qa = 0, qb = 0;
+    uint32_t m = 0;
+    if (ja < nlist) {
+      qa = list[ja];
+      qb = jb < nlist ? list[jb] : qa;
+      const int ra = row_of(qa), ca = qa - ra * dw, rb = row_of(qb), cb = qb - rb * dw;
+      const uint8_t* pa = R + (ra + 3) * RS + (ca + 3);
+      const uint8_t* pb = R + (rb + 3) * RS + (cb + 3);
+      m = arc_strength_pk(pa, pb, RS, a.tlow);
+      const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
+      if (ma) m8[(ra + 1) * mw + (ca + 1)] = (uint8_t)min(ma, 255);
+      if (mb && jb < nlist) m8[(rb + 1) * mw + (cb + 1)] = (uint8_t)min(mb, 255);
     }
-    const uint64_t bal = wave_ballot(m > 0);
-    wave_sync();
-    if (m > 0) list[ncorner + prefix_in_wave(bal)] = (uint16_t)q;
-    ncorner += __popcll(bal);
+    const bool ka = ja < nlist && (m & 0xffffu) != 0, kb = jb < nlist && (m >> 16) != 0;
+    const uint64_t b0 = wave_ballot(ka), b1 = wave_ballot(kb);
+    wave_sync();  // every lane has read list[j0 .. j0+127] before it is overwritten
+    const int pos = ncorner + prefix_in_wave(b0) + prefix_in_wave(b1);
+    if (ka) list[pos] = (uint16_t)qa;
+    if (kb) list[pos + (ka ? 1 : 0)] = (uint16_t)qb;
+    ncorner += __popcll(b0) + __popcll(b1);
   }
   wave_sync();
   // 4. NMS over the corners (out-of-region and non-corner neighbours score 0)
