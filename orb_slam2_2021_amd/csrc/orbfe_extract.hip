@@ -1446,6 +1446,8 @@ struct orbfe_extractor {
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level)
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
   std::vector<LevelDesc> levels;
@@ -1910,6 +1912,16 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     else
       LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), st, a));
   }
+  // fork: GaussianBlur needs only the pyramid, so it runs on the side stream beside k_octree (a
+  // small, latency-bound grid that leaves most CUs idle); joined before k_describe
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
+  ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+  {
+    hipStream_t sd = h->side;
+    dim3 grid((h->blur_tiles + 3) / 4, n);
+    LAUNCH_TIMED(h, 5, sd, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, sd, a));
+  }
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, h->side));
   {
     dim3 grid(h->nlevels, n);
     if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
@@ -1917,10 +1929,8 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
                                         (int)octree_lds(h)));
     LAUNCH_TIMED(h, 2, st, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), st, a));
   }
-  {
-    dim3 grid((h->blur_tiles + 3) / 4, n);
-    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, st, a));
-  }
+
+  ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
     dim3 grid((h->total_key_slots + 15) / 16, n);
     LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, a));
@@ -1935,6 +1945,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
 
 // ---------------------------------------------------------------------------------------------
 // C ABI
+// The side stream gets the highest priority: the runtime serves each priority from its own
+// hardware queues, so k_blur cannot land behind the caller's stream on a shared queue.
+static hipError_t create_side_stream(hipStream_t* s) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
 extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nlevels,
                                       int ini_th_fast, int min_th_fast, int device,
                                       orbfe_extractor** out) {
@@ -1986,7 +2004,10 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
     ++v0;
   }
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      create_side_stream(&h->side) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) {
     delete h;
     return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: stream creation failed");
   }
@@ -2038,6 +2059,9 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   }
   for (auto e : h->event_pool) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
+  if (h->side) hipStreamDestroy(h->side);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
   delete h;
   return ORBFE_OK;
 }
