@@ -1076,7 +1076,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       for (int k = 2; k <= P2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
           for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
-            const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+            const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
             const unsigned long long x = sk[i], y = sk[ixj];
             if ((i & k) == 0 ? (x < y) : (x > y)) {
               sk[i] = y;

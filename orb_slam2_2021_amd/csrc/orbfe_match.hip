@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void k_grid(GridArgs g) {
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
-        const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
         const uint32_t x = skeys[i], y = skeys[ixj];
         if ((i & k) == 0 ? (x > y) : (x < y)) {
           skeys[i] = y;

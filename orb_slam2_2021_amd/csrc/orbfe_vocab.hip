@@ -93,21 +93,23 @@ __global__ __launch_bounds__(256) void k_vocab_descend(VocabArgs a, unsigned lon
   keys[(long long)img * a.cap + i] = key;
 }
 
-// k_vocab_csr: one workgroup per image sorts its keys stably (bitonic in LDS) and emits CSR.
-__global__ __launch_bounds__(256) void k_vocab(VocabArgs a, const unsigned long long* keys) {
+// k_vocab_csr: one 1024-thread workgroup per image sorts its keys stably (bitonic in LDS) and
+// emits CSR.
+#define VOCAB_THREADS 1024
+__global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsigned long long* keys) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
   __shared__ int s_n;
   const int img = blockIdx.x, t = threadIdx.x;
   const int n = min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
   int P2 = 1;
   while (P2 < n) P2 <<= 1;
-  for (int i = t; i < P2; i += 256) skeys[i] = i < n ? keys[(long long)img * a.cap + i] : ~0ull;
+  for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? keys[(long long)img * a.cap + i] : ~0ull;
   __syncthreads();
-  // bitonic sort, ascending; every thread owns P2/512 compare-exchange pairs per stage
+  // bitonic sort, ascending; every thread owns P2/2048 compare-exchange pairs per stage
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
-        const int i = 2 * j * (pidx / j) + (pidx % j), ixj = i + j;
+      for (int pidx = t; pidx < (P2 >> 1); pidx += VOCAB_THREADS) {
+        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
         const unsigned long long x = skeys[i], y = skeys[ixj];
         if ((i & k) == 0 ? (x > y) : (x < y)) {
           skeys[i] = y;
@@ -119,27 +121,27 @@ __global__ __launch_bounds__(256) void k_vocab(VocabArgs a, const unsigned long 
   }
   // CSR: a node starts where its id differs from the previous key's. Each thread owns a
   // contiguous chunk of the sorted keys; starts are counted, scanned and written in order.
-  __shared__ int s_wsum[4];
+  __shared__ int s_wsum[VOCAB_THREADS / 64];
   uint32_t* ids = a.node_ids + (long long)img * a.cap;
   int32_t* offs = a.offsets + (long long)img * (a.cap + 1);
   int32_t* idx = a.indices + (long long)img * a.cap;
   if (t == 0) s_n = 0;
   __syncthreads();
   int nvalid = 0;
-  for (int i = t; i < n; i += 256) nvalid += skeys[i] != ~0ull;
+  for (int i = t; i < n; i += VOCAB_THREADS) nvalid += skeys[i] != ~0ull;
   nvalid = wave_sum(nvalid);
   if (lane_id() == 0) atomicAdd(&s_n, nvalid);
   __syncthreads();
   const int nv = s_n;  // valid keys sort first
-  for (int i = t; i < nv; i += 256) idx[i] = (int32_t)(skeys[i] & 0xffffffffull);
-  const int per = (nv + 255) / 256;
+  for (int i = t; i < nv; i += VOCAB_THREADS) idx[i] = (int32_t)(skeys[i] & 0xffffffffull);
+  const int per = (nv + VOCAB_THREADS - 1) / VOCAB_THREADS;
   const int beg = min(t * per, nv), end = min(beg + per, nv);
   auto is_start = [&](int i) {
     return i == 0 || (uint32_t)(skeys[i] >> 32) != (uint32_t)(skeys[i - 1] >> 32);
   };
   int cnt = 0;
   for (int i = beg; i < end; i++) cnt += is_start(i);
-  // exclusive scan of cnt over the 256 threads
+  // exclusive scan of cnt over the workgroup
   const int lane = lane_id(), w = wave_id();
   int inc = cnt;
 #pragma unroll
@@ -151,7 +153,8 @@ __global__ __launch_bounds__(256) void k_vocab(VocabArgs a, const unsigned long 
   __syncthreads();
   int pos = inc - cnt;
   for (int k = 0; k < w; k++) pos += s_wsum[k];
-  const int nodes = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  int nodes = 0;
+  for (int k = 0; k < VOCAB_THREADS / 64; k++) nodes += s_wsum[k];
   for (int i = beg; i < end; i++) {
     if (is_start(i)) {
       ids[pos] = (uint32_t)(skeys[i] >> 32);
@@ -252,7 +255,7 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
     v->keys_bytes = need;
   }
   hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 255) / 256, n_images), dim3(256), 0, s, a, v->d_keys);
-  hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(256), sizeof(unsigned long long) * P2, s, a,
+  hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(VOCAB_THREADS), sizeof(unsigned long long) * P2, s, a,
                      (const unsigned long long*)v->d_keys);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
