@@ -92,6 +92,13 @@ __device__ __forceinline__ int2 xcd_block2d() {
   return make_int2(id % gridDim.x, id / gridDim.x);
 }
 
+// LDS visibility among the lanes of one wavefront (no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
   const int per = (n + 255) / 256;

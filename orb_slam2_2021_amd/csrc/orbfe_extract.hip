@@ -116,11 +116,6 @@ struct ExtractArgs {
 
 __constant__ int8_t c_pattern[1024];
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 __device__ __forceinline__ const uint8_t* level_ptr(const ExtractArgs& a, const LevelDesc& ld,
                                                     int img, int l, int& pitch) {

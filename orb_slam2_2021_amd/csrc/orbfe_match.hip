@@ -138,23 +138,168 @@ __device__ __forceinline__ unsigned long long sft_key(const SftCand& c, bool cla
   return ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
 }
 
+// Nodes with at most SFT_FP_MAX features on each side: lanes take KF1 features (two per lane),
+// every lane finds its passing KF2 candidates once (dist <= TH_LOW, the epipole and epipolar
+// checks: the candidate set S_i of the reference loop), then the claim order of :772-777 is
+// solved as a fixpoint -- choice(i) = best of S_i minus the choices of features before i in the
+// node -- iterated from "no claims" until a round reproduces the previous one. That fixpoint is
+// unique and equals the sequential result (feature i's choice is final once those before it are).
+#define SFT_FP_MAX 128
+__device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o1, int n1, int o2, int n2,
+                                                  int only_stereo, uint32_t* cdesc, int* claim) {
+  const int lane = lane_id();
+  // candidates: lane p (and 64 + p) loads KF2 feature p of the node; descriptors go to LDS
+  SftCand c0, c1;
+  sft_load_cand(P, o2, n2, lane, only_stereo, c0);
+  sft_load_cand(P, o2, n2, 64 + lane, only_stereo, c1);
+  if (lane < n2) {
+    *reinterpret_cast<uint4*>(cdesc + 8 * lane) = c0.d0;
+    *reinterpret_cast<uint4*>(cdesc + 8 * lane + 4) = c0.d1;
+  }
+  if (64 + lane < n2) {
+    *reinterpret_cast<uint4*>(cdesc + 8 * (64 + lane)) = c1.d0;
+    *reinterpret_cast<uint4*>(cdesc + 8 * (64 + lane) + 4) = c1.d1;
+  }
+  // KF1 features i = lane and 64 + lane
+  int idx1[2];
+  bool ok1[2], st1[2];
+  float x1[2], y1[2];
+  uint4 a0[2], a1[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int i = 64 * k + lane;
+    idx1[k] = -1;
+    ok1[k] = false;
+    st1[k] = false;
+    x1[k] = y1[k] = 0.f;
+    a0[k] = a1[k] = make_uint4(0, 0, 0, 0);
+    if (i < n1) {
+      idx1[k] = P.fv1.indices[o1 + i];
+      st1[k] = P.kf1.u_right[idx1[k]] >= 0;
+      ok1[k] = P.kf1.mp_state[idx1[k]] == ORBFE_MP_NONE && !(only_stereo && !st1[k]);
+      const orbfe_keypoint kp = P.kf1.keys_un[idx1[k]];
+      x1[k] = kp.x;
+      y1[k] = kp.y;
+      load_desc(P.kf1.descriptors + (size_t)idx1[k] * 32, a0[k], a1[k]);
+    }
+  }
+  wave_sync();
+  const float* F = P.f12;
+  const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
+              f7 = F[7], f8 = F[8];
+  float la[2], lb[2], lc[2], den[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {  // epipolar line l = x1' F12 (CheckDistEpipolarLine :149-151)
+    la[k] = x1[k] * f0 + y1[k] * f3 + f6;
+    lb[k] = x1[k] * f1 + y1[k] * f4 + f7;
+    lc[k] = x1[k] * f2 + y1[k] * f5 + f8;
+    den[k] = la[k] * la[k] + lb[k] * lb[k];
+  }
+  // 1. passing sets (bit p of pm[k][p >> 6]) and the round-0 choice (no claims)
+  uint64_t pm00 = 0, pm01 = 0, pm10 = 0, pm11 = 0;  // pm<k><h>: bit p - 64 h of feature 64 k + lane
+  unsigned long long best0 = ~0ull, best1 = ~0ull;
+  for (int p = 0; p < n2; p++) {
+    const int src = p & 63;
+    const bool hi = p >= 64;
+    SftCand c;  // candidate p broadcast from its lane (scalar registers)
+    c.usable = __builtin_amdgcn_readlane((int)(hi ? c1.usable : c0.usable), src) != 0;
+    if (!c.usable) continue;  // uniform
+    c.stereo = __builtin_amdgcn_readlane((int)(hi ? c1.stereo : c0.stereo), src) != 0;
+    c.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.x : c0.x), src));
+    c.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.y : c0.y), src));
+    c.epi_thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.epi_thr : c0.epi_thr), src));
+    const long long sb = __double_as_longlong(hi ? c1.sig_thr : c0.sig_thr);
+    c.sig_thr = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(sb >> 32), src) << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane((int)(sb & 0xffffffff), src));
+    c.d0 = *reinterpret_cast<const uint4*>(cdesc + 8 * p);
+    c.d1 = *reinterpret_cast<const uint4*>(cdesc + 8 * p + 4);
+    const uint64_t bit = 1ull << (p & 63);
+    if (ok1[0]) {
+      const unsigned long long key = sft_key(c, false, p, a0[0], a1[0], st1[0], P.ex, P.ey, la[0], lb[0], lc[0], den[0]);
+      if (key != ~0ull) {
+        if (hi) pm01 |= bit;
+        else pm00 |= bit;
+        best0 = key < best0 ? key : best0;
+      }
+    }
+    if (ok1[1]) {
+      const unsigned long long key = sft_key(c, false, p, a0[1], a1[1], st1[1], P.ex, P.ey, la[1], lb[1], lc[1], den[1]);
+      if (key != ~0ull) {
+        if (hi) pm11 |= bit;
+        else pm10 |= bit;
+        best1 = key < best1 ? key : best1;
+      }
+    }
+  }
+  int ch[2];
+  ch[0] = best0 == ~0ull ? -1 : 0x7fffffff - (int)(best0 & 0xffffffffull);
+  ch[1] = best1 == ~0ull ? -1 : 0x7fffffff - (int)(best1 & 0xffffffffull);
+  // 2. rounds: claim[p] = first feature choosing p; re-choose among the unclaimed-by-earlier
+  auto rechoose = [&](int i, uint64_t m0, uint64_t m1, const uint4& q0, const uint4& q1) -> int {
+    unsigned long long b = ~0ull;
+    for (int h = 0; h < 2; h++) {
+      uint64_t m = h == 0 ? m0 : m1;
+      while (m) {
+        const int p = 64 * h + __builtin_ctzll(m);
+        m &= m - 1;
+        if (claim[p] < i) continue;  // vbMatched2: taken by an earlier feature of the node
+        const uint4 d0 = *reinterpret_cast<const uint4*>(cdesc + 8 * p);
+        const uint4 d1 = *reinterpret_cast<const uint4*>(cdesc + 8 * p + 4);
+        const unsigned long long key = ((unsigned long long)hamming256(q0, q1, d0, d1) << 32) |
+                                       (unsigned long long)(0x7fffffff - p);
+        b = key < b ? key : b;
+      }
+    }
+    return b == ~0ull ? -1 : 0x7fffffff - (int)(b & 0xffffffffull);
+  };
+  int chA = ch[0], chB = ch[1];
+  const uint4 qa0 = a0[0], qa1 = a1[0], qb0 = a0[1], qb1 = a1[1];
+  for (int round = 0; round <= n1; round++) {
+    for (int p = lane; p < n2; p += 64) claim[p] = 0x7fffffff;
+    wave_sync();
+    if (chA >= 0) atomicMin(&claim[chA], lane);
+    if (chB >= 0) atomicMin(&claim[chB], 64 + lane);
+    wave_sync();
+    const int nA = rechoose(lane, pm00, pm01, qa0, qa1);
+    const int nB = rechoose(64 + lane, pm10, pm11, qb0, qb1);
+    const bool changed = nA != chA || nB != chB;
+    chA = nA;
+    chB = nB;
+    if (wave_ballot(changed) == 0) break;
+    wave_sync();  // claim[] is rewritten by the next round
+  }
+  if (chA >= 0) P.match12[idx1[0]] = P.fv2.indices[o2 + chA];
+  if (chB >= 0) P.match12[idx1[1]] = P.fv2.indices[o2 + chB];
+}
+
 __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
   __shared__ uint32_t s_claim_far[4][SFT_MAX_NODE / 32];  // claims beyond the register chunks
+  __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];        // fixpoint path: node candidates
+  __shared__ int s_fp_claim[4][SFT_FP_MAX];
   orbfe_sft_pair P = pairs[blockIdx.y];
   sft_resolve_sizes(P);
   const int w = wave_id(), lane = lane_id();
   const int a = blockIdx.x * 4 + w;
   if (a >= P.fv1.n_nodes || P.kf2.n > SFT_MAX_KF2) return;
   const uint32_t id = P.fv1.node_ids[a];
-  int lo = 0, hi = P.fv2.n_nodes;  // the merge-join visits exactly the common node ids (:705-804)
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (P.fv2.node_ids[mid] < id) lo = mid + 1;
-    else hi = mid;
-  }
-  if (lo >= P.fv2.n_nodes || P.fv2.node_ids[lo] != id) return;
   const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
+  // the merge-join visits exactly the common node ids (:705-804): find id among KF2's node ids
+  // with 64 independent loads per step (one round trip for the usual <= 64 .. 128 nodes)
+  int lo = -1;
+  for (int b = 0; b < P.fv2.n_nodes && lo < 0; b += 128) {
+    const int i0 = b + lane, i1 = b + 64 + lane;
+    const uint32_t v0 = i0 < P.fv2.n_nodes ? P.fv2.node_ids[i0] : ~0u;
+    const uint32_t v1 = i1 < P.fv2.n_nodes ? P.fv2.node_ids[i1] : ~0u;
+    const uint64_t m0 = wave_ballot(v0 == id), m1 = wave_ballot(v1 == id);
+    if (m0) lo = b + __builtin_ctzll(m0);
+    else if (m1) lo = b + 64 + __builtin_ctzll(m1);
+  }
+  if (lo < 0) return;
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
+  if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
+    sft_node_fixpoint(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
+    return;
+  }
   uint32_t* far = s_claim_far[w];
   if (n2 > SFT_REG_CHUNKS * 64)
     for (int i = lane; i < (n2 + 31) / 32; i += 64) far[i] = 0;
