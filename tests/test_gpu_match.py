@@ -63,6 +63,30 @@ def test_search_for_triangulation(require_gpu, kitti_pair, only_stereo, check_or
         assert nm == 0  # bOnlyStereo with no stereo keypoint: nothing can match
 
 
+@pytest.mark.parametrize("k,levels", [(3, 1), (16, 1), (12, 1), (10, 2)])
+@pytest.mark.parametrize("same_frame", [False, True])
+def test_search_for_triangulation_node_sizes(require_gpu, kitti_pair, k, levels, same_frame):
+    """Vocabulary shapes that put ~700, ~125, ~170 and ~20 features in a node: the large-node
+    sequential path, the 128-feature boundary of the fixpoint path, and the fixpoint rounds under
+    heavy claim conflicts (KF2 = KF1 with shuffled features, so every feature has a twin)."""
+    k1, d1, k2, d2, scale, sigma2 = kitti_pair
+    if same_frame:
+        perm = np.random.default_rng(3).permutation(len(k1))
+        k2, d2 = k1[perm], d1[perm]
+    rng = np.random.default_rng(11)
+    voc = S.Vocabulary.synthetic(k=k, levels=levels)
+    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    F1 = S.make_frame(k1, d1, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.4, tcw=t1)
+    F2 = S.make_frame(k2, d2, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.4, tcw=t2)
+    F1.feat_vec, F2.feat_vec = voc.feature_vector(d1, 0), voc.feature_vector(d2, 0)
+    F12 = S.compute_f12(t1, t2, S.intrinsics(S.KITTI_CAM))
+    ex, ey = -1.0e7, 185.0
+    nm, _, m12 = ORBmatcher(0.6, True).SearchForTriangulation(F1, F2, F12, False, epipole_xy=(ex, ey))
+    nr, r12 = orbref.search_for_triangulation(F1, F2, F12, ex, ey, False, True)
+    assert nm == nr and np.array_equal(m12, r12)
+    assert nm > 0
+
+
 def test_search_for_triangulation_epipole_from_poses(require_gpu, kitti_pair):
     k1, d1, k2, d2, scale, sigma2 = kitti_pair
     rng = np.random.default_rng(8)
