@@ -663,12 +663,13 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
     if constexpr (RSC != 0) return (int)(((uint32_t)q * magic) >> 20);
     else return q / dw;
   };
-  for (int i = lane; i < mw * mh; i += 64) m8[i] = 0;
+  for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
   // 2a. OpenCV's first two antipodal pairs (ring 0/8 = dy +-3, ring 4/12 = dx +-3) at the lower
-  //     threshold, two horizontally adjacent pixels per lane in packed 16-bit halves; survivors
-  //     (about 1 in 8 pixels) are compacted in row-major order
+  //     threshold, two horizontally adjacent pixels per lane in packed 16-bit halves:
+  //     dark <=> max(min(u,d), min(l,r)) < v - t, bright <=> min(max(u,d), max(l,r)) > v + t.
+  //     Survivors (about 1 in 8 pixels) are compacted in row-major order.
   const int pw = (dw + 1) >> 1;
   const uint32_t pmagic = ((1u << 20) + pw - 1) / pw;
   const uint32_t T2 = (uint32_t)a.tlow * 0x10001u;
@@ -683,12 +684,11 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
       px = rr * dw + cc;
       const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
       const uint32_t c = pack2(p[0], p[1]);
-      const uint32_t lo = pk_sub16(c, T2), hi = pk_add16(c, T2);
       const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
       const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
-      const uint32_t dark = (pk_sub16(u, lo) | pk_sub16(d, lo)) & (pk_sub16(r, lo) | pk_sub16(l, lo));
-      const uint32_t brt = (pk_sub16(hi, u) | pk_sub16(hi, d)) & (pk_sub16(hi, r) | pk_sub16(hi, l));
-      const uint32_t res = dark | brt;
+      const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
+      const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
+      const uint32_t res = pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
       p0 = (res & 0x8000u) != 0;
       p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
     }
