@@ -1196,31 +1196,43 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-#define BS_W 256  // columns per wavefront strip (4 per lane)
+#define BS_W 248  // output columns per wavefront strip: lanes 1..62, 4 each (lanes 0 and 63 halo)
 #define BS_H 32   // output rows per strip
 __device__ __forceinline__ int reflect101(int i, int n) {
   return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
 
-// Horizontal 7-tap sums of the 4 pixels x..x+3 (bytes 4..7 of P|C|N)
-__device__ __forceinline__ void blur_h4(uint32_t P, uint32_t C, uint32_t N, uint32_t* h) {
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    // bytes at columns x+j-3 .. x+j+3 = window bytes j+1 .. j+7
-    // v_alignbyte_b32 shifts by (S2 & 3) bytes: j = 3 takes whole dwords
-    const uint32_t lo = j == 3 ? C : __builtin_amdgcn_alignbyte(C, P, j + 1);  // bytes j+1 .. j+4
-    const uint32_t hi = j == 3 ? N : __builtin_amdgcn_alignbyte(N, C, j + 1);  // bytes j+5 .. j+8
-    const uint32_t a0 = lo & 0xff, a1 = (lo >> 8) & 0xff, a2 = (lo >> 16) & 0xff, a3 = lo >> 24;
-    const uint32_t a4 = hi & 0xff, a5 = (hi >> 8) & 0xff, a6 = (hi >> 16) & 0xff;
-    h[j] = 18u * (a0 + a6) + 34u * (a1 + a5) + 49u * (a2 + a4) + 54u * a3;
-  }
+// whole-wavefront lane shifts (DPP wave_shr:1 / wave_shl:1, gfx9): lane i <- lane i-1 / i+1
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2v, a) * __builtin_bit_cast(u16x2v, b) +
+                                          __builtin_bit_cast(u16x2v, c));
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2v, a) + __builtin_bit_cast(u16x2v, b));
+}
+// 7-tap [18 34 49 54 49 34 18] over 7 packed rows (each half one column; sums <= 65280 fit u16)
+__device__ __forceinline__ uint32_t vtap7(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t r4,
+                                          uint32_t r5, uint32_t r6) {
+  uint32_t v = pk_mad_u16(r3, 0x00360036u, 0u);
+  v = pk_mad_u16(pk_add_u16(r2, r4), 0x00310031u, v);
+  v = pk_mad_u16(pk_add_u16(r1, r5), 0x00220022u, v);
+  return pk_mad_u16(pk_add_u16(r0, r6), 0x00120012u, v);
 }
 
 // k_blur: GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level (ORBextractor.cc:1083-1084),
-// OpenCV's bit-exact fixed-point form: H = sum k_i p_i (8.8), out = (sum k_j H_j + 2^15) >> 16 with
-// k = [18, 34, 49, 54, 49, 34, 18]. One wavefront per 256 x 32 strip, each lane 4 columns: one
-// aligned dword per input row, neighbours by cross-lane shuffles, the 7-row vertical window in
-// registers, one dword store per output row. Strips of all levels of all images in one launch.
+// OpenCV's bit-exact fixed-point form out = (sum_j k_j sum_i k_i p_ij + 2^15) >> 16 with
+// k = [18, 34, 49, 54, 49, 34, 18]; the sums are exact integers, so the vertical pass may run
+// first. One wavefront per 248 x 32 strip, each lane one dword (4 columns) per input row: the
+// 7-row window is kept as packed 16-bit (even, odd) column pairs, the vertical taps are v_pk_mad_u16
+// (V <= 65280), the neighbours' V come by DPP lane shifts (lanes 0 and 63 are halo), and the
+// horizontal taps are 4 v_dot2_u32_u16 per pixel on consecutive column pairs built with v_perm.
+// Strips of all levels of all images in one launch.
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   const int2 blk = xcd_block2d();
   const int img = blk.y, lane = lane_id();
@@ -1230,59 +1242,56 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   const LevelDesc ld = a.levels[l];
   strip -= ld.tile_begin;
   const int sx = strip % ld.tiles_x, sy = strip / ld.tiles_x;
-  const int x = sx * BS_W + 4 * lane, y0 = sy * BS_H;
+  const int x = sx * BS_W - 4 + 4 * lane, y0 = sy * BS_H;  // this lane's 4 columns
   const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
   uint8_t* dst = a.blur + (long long)img * a.pyr_stride + ld.pyr_off;
   const int w = ld.w, pitch = ld.pitch;
-  // dword C = columns x..x+3; E = the strip-end neighbour (x-4 for lane 0, x+4 for lane 63).
-  // Columns -4..w+7 exist in every row (padding), so no load needs a border branch.
-  const bool cin = x < w + 8, ein = lane == 0 || (lane == 63 && x + 4 < w + 8);
-  const int eoff = lane == 0 ? x - 4 : x + 4;
-  auto row_ptr = [&](int r) { return src + (long long)reflect101(r, ld.h) * pitch; };
-  auto load_c = [&](int r) { return cin ? *reinterpret_cast<const uint32_t*>(row_ptr(r) + x) : 0u; };
-  auto load_e = [&](int r) { return ein ? *reinterpret_cast<const uint32_t*>(row_ptr(r) + eoff) : 0u; };
+  // columns -4 .. w+7 exist in every row (padding; -3..-1 and w..w+2 hold the reflections)
+  const bool cin = x < w + 8;
+  const bool out = lane >= 1 && lane <= 62 && x < w;
+  auto load_row = [&](int r) {
+    return cin ? *reinterpret_cast<const uint32_t*>(src + (long long)reflect101(r, ld.h) * pitch + x) : 0u;
+  };
+  auto ev = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c020c00u); };  // columns 0, 2
+  auto od = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c01u); };  // columns 1, 3
   const int yend = min(y0 + BS_H, ld.h);
   const int nrows = yend - y0 + 6;  // input rows y0-3 .. yend+2
-  // 4-row load lookahead: rows i .. i+3 in flight while row i is consumed
-  uint32_t qc0 = load_c(y0 - 3), qe0 = load_e(y0 - 3);
-  uint32_t qc1 = load_c(y0 - 2), qe1 = load_e(y0 - 2);
-  uint32_t qc2 = load_c(y0 - 1), qe2 = load_e(y0 - 1);
-  uint32_t qc3 = load_c(y0), qe3 = load_e(y0);
-  uint32_t h0[4], h1[4], h2[4], h3[4], h4[4], h5[4], h6[4];
+  uint32_t q0 = load_row(y0 - 3), q1 = load_row(y0 - 2), q2 = load_row(y0 - 1), q3 = load_row(y0);
+  uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;  // window, even columns
+  uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;  // window, odd columns
   for (int i = 0; i < nrows; i++) {
-    const uint32_t C = qc0, E = qe0;
-    qc0 = qc1; qe0 = qe1;
-    qc1 = qc2; qe1 = qe2;
-    qc2 = qc3; qe2 = qe3;
-    if (i + 4 < nrows) {
-      qc3 = load_c(y0 - 3 + i + 4);
-      qe3 = load_e(y0 - 3 + i + 4);
-    }
-    uint32_t P = (uint32_t)__shfl_up((int)C, 1, 64);
-    uint32_t N = (uint32_t)__shfl_down((int)C, 1, 64);
-    if (lane == 0) P = E;
-    if (lane == 63) N = E;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      h0[j] = h1[j];
-      h1[j] = h2[j];
-      h2[j] = h3[j];
-      h3[j] = h4[j];
-      h4[j] = h5[j];
-      h5[j] = h6[j];
-    }
-    blur_h4(P, C, N, h6);
-    if (i >= 6) {
-      const int y = y0 + i - 6;
-      uint32_t o = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t acc = 18u * (h0[j] + h6[j]) + 34u * (h1[j] + h5[j]) +
-                             49u * (h2[j] + h4[j]) + 54u * h3[j];
-        o |= min((acc + 32768u) >> 16, 255u) << (8 * j);
-      }
-      if (x < w) *reinterpret_cast<uint32_t*>(dst + (long long)y * pitch + x) = o;
-    }
+    const uint32_t C = q0;
+    q0 = q1;
+    q1 = q2;
+    q2 = q3;
+    if (i + 4 < nrows) q3 = load_row(y0 - 3 + i + 4);  // 4-row load lookahead
+    e0 = e1; e1 = e2; e2 = e3; e3 = e4; e4 = e5; e5 = e6; e6 = ev(C);
+    o0 = o1; o1 = o2; o2 = o3; o3 = o4; o4 = o5; o5 = o6; o6 = od(C);
+    if (i < 6) continue;
+    // vertical: V of columns x, x+2 (VE) and x+1, x+3 (VO)
+    const uint32_t VE = vtap7(e0, e1, e2, e3, e4, e5, e6), VO = vtap7(o0, o1, o2, o3, o4, o5, o6);
+    const uint32_t LE = from_left(VE), LO = from_left(VO), RE = from_right(VE), RO = from_right(VO);
+    // consecutive column pairs P(k) = (V(x+k), V(x+k+1)), k = -3..6
+    const uint32_t Pm3 = __builtin_amdgcn_perm(LE, LO, 0x07060100u);  // (V-3, V-2)
+    const uint32_t Pm2 = __builtin_amdgcn_perm(LO, LE, 0x07060302u);  // (V-2, V-1)
+    const uint32_t Pm1 = __builtin_amdgcn_perm(VE, LO, 0x05040302u);  // (V-1, V0)
+    const uint32_t P0 = __builtin_amdgcn_perm(VO, VE, 0x05040100u);   // (V0, V1)
+    const uint32_t P1 = __builtin_amdgcn_perm(VE, VO, 0x07060100u);   // (V1, V2)
+    const uint32_t P2 = __builtin_amdgcn_perm(VO, VE, 0x07060302u);   // (V2, V3)
+    const uint32_t P3 = __builtin_amdgcn_perm(RE, VO, 0x05040302u);   // (V3, V4)
+    const uint32_t P4 = __builtin_amdgcn_perm(RO, RE, 0x05040100u);   // (V4, V5)
+    const uint32_t P5 = __builtin_amdgcn_perm(RE, RO, 0x07060100u);   // (V5, V6)
+    const uint32_t P6 = __builtin_amdgcn_perm(RO, RE, 0x07060302u);   // (V6, V7)
+    auto hz = [](uint32_t pa, uint32_t pb, uint32_t pc, uint32_t pd) {
+      int s = dot2_u16(pa, 0x00220012u);   // 18 V(j-3) + 34 V(j-2)
+      s += dot2_u16(pb, 0x00360031u);      // 49 V(j-1) + 54 V(j)
+      s += dot2_u16(pc, 0x00220031u);      // 49 V(j+1) + 34 V(j+2)
+      s += dot2_u16(pd, 0x00000012u);      // 18 V(j+3)
+      return (uint32_t)(s + 32768) >> 16;
+    };
+    const uint32_t r = hz(Pm3, Pm1, P1, P3) | (hz(Pm2, P0, P2, P4) << 8) | (hz(Pm1, P1, P3, P5) << 16) |
+                       (hz(P0, P2, P4, P6) << 24);
+    if (out) *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + i - 6) * pitch + x) = r;
   }
 }
 
@@ -1578,7 +1587,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
-    d.tiles_x = (d.w + 255) / 256;  // k_blur strips of 256 x 32
+    d.tiles_x = (d.w + 247) / 248;  // k_blur strips of 248 x 32
     d.tile_begin = tiles;
     tiles += d.tiles_x * ((d.h + 31) / 32);
     d.key_begin = keys;
