@@ -585,9 +585,10 @@ __host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max, int r
   return f;
 }
 
-// RSC != 0: the ROI row stride is the compile-time constant RSC (= 64 when every ROI fits in 61
-// columns), so the 16 ring reads of a pixel are one address plus immediate offsets, the ROI load
-// maps lanes with shifts and the row/column split of a detection index is a multiply-shift.
+// RSC != 0: the ROI row stride is the compile-time constant RSC (68 bytes = 17 banks apart, so
+// the rows a wavefront touches spread over the 32 LDS banks) when every ROI fits in 61 columns:
+// the 16 ring reads of a pixel are one address plus immediate offsets, the ROI load maps lanes
+// with shifts and the row/column split of a detection index is a multiply-shift.
 // RSC == 0: any geometry, runtime stride.
 template <int RSC>
 __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
@@ -618,9 +619,8 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
   // 1. ROI -> LDS: dword-aligned columns [x0a, x0a + 4 nw) cover [x0, x0 + rw)
   const int x0a = cd.x0 & ~3, xo = cd.x0 - x0a, nw = (xo + rw + 3) >> 2;
   if constexpr (RSC != 0) {
-    constexpr int WPR = RSC / 4;  // dword columns per LDS row
-    constexpr int SH = WPR == 16 ? 4 : WPR == 8 ? 3 : 5;
-    static_assert((1 << SH) == WPR, "RSC must be 32, 64 or 128");
+    constexpr int WPR = 16;  // dword columns loaded per ROI row (ROI <= 61 columns + 3 alignment)
+    constexpr int SH = 4;
     for (int i0 = 0; i0 < WPR * rh; i0 += 8 * 64) {
       uint32_t v[8];
 #pragma unroll
@@ -1809,10 +1809,10 @@ static size_t octree_lds(const orbfe_extractor* h) {
   return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->scan_cap +
          sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16 + sizeof(uint32_t) * 2 * h->key_lds_cap;
 }
-// constant 64-byte ROI rows when every cell ROI fits (xo <= 3 alignment bytes + rw <= 61) and the
+// constant 68-byte ROI rows when every cell ROI fits (xo <= 3 alignment bytes + rw <= 61) and the
 // multiply-shift row split stays exact (dw^2 * dh < 2^20)
 static int fast_rs(const orbfe_extractor* h) {
-  return (h->roi_w_max <= 61 && h->roi_h_max <= 66) ? 64 : 0;
+  return (h->roi_w_max <= 61 && h->roi_h_max <= 66) ? 68 : 0;
 }
 static size_t fast_lds(const orbfe_extractor* h) {
   return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max, fast_rs(h)).total;
@@ -1911,8 +1911,8 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   }
   {
     dim3 grid((a.ncells + 3) / 4, n);
-    if (fast_rs(h) == 64)
-      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<64>, grid, dim3(256), fast_lds(h), st, a));
+    if (fast_rs(h) == 68)
+      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<68>, grid, dim3(256), fast_lds(h), st, a));
     else
       LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), st, a));
   }
