@@ -244,7 +244,8 @@ def main():
     cand = sum(len(ext.debug_candidates(l, image=i)) for i in range(n_img) for l in range(8))
     nm = d_nm.cpu().numpy()
     geo = ext.geometry(H, W)
-    roof = roofline(timed if dominant in timed else probe, dominant, geo, counts, cand, n_img)
+    roof = roofline(timed if dominant in timed else probe, dominant, geo, counts, cand, n_img,
+                    args.steps if dominant in timed else probe_steps)
     roof["measured_in"] = "timed region" if dominant in timed else "probe pass (--no-kernel-events)"
     algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
     out = {
@@ -292,8 +293,10 @@ def level_pixels(geo):
     return [int(w) * int(h) for w, h in geo[:, :2]]
 
 
-def roofline(kt, dom, geo, counts, n_cand, n_img):
-    """Roofline of the dominant kernel: ALGORITHMIC bytes per launch / average launch duration.
+def roofline(kt, dom, geo, counts, n_cand, n_img, steps):
+    """Roofline of the dominant kernel: ALGORITHMIC bytes per step / its HIP-event time per step
+    (a kernel may run as several launches per step, e.g. k_resize once per level and k_fast as
+    level 0 beside the resize chain + levels 1..7; per launch = per step / launches_per_step).
     Per-kernel algorithmic bytes (per step; DESIGN.md 'Roofline'):
       k_resize   sum_l>=1 (px_{l-1} + px_l) per image (read the source level once, write the level)
       k_fast     sum_l px_l per image + 4 B per FAST candidate + 4 B per cell count
@@ -320,13 +323,16 @@ def roofline(kt, dom, geo, counts, n_cand, n_img):
         "k_sft": 64 * nkp + 4 * nkp // 2,
     }
     total_ms, launches = kt[dom]
-    bytes_per_launch = per_step[dom] / (7 if dom == "k_resize" else 1)
-    avg_s = total_ms / 1e3 / max(launches, 1)
-    achieved = bytes_per_launch / avg_s / 1e9
+    per_launch_steps = max(launches // max(steps, 1), 1)  # launches per step
+    step_s = total_ms / 1e3 / max(steps, 1)
+    achieved = per_step[dom] / step_s / 1e9
     return {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-            "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            "avg_launch_us": round(avg_s * 1e6, 2), "launches": launches}
+            "algorithmic_bytes_per_step": int(per_step[dom]),
+            "algorithmic_bytes_per_launch": int(per_step[dom] / per_launch_steps),
+            "kernel_us_per_step": round(step_s * 1e6, 2),
+            "avg_launch_us": round(step_s * 1e6 / per_launch_steps, 2),
+            "launches_per_step": per_launch_steps}
 
 
 def pipeline_bytes_per_stereo_frame(geo, counts, B):

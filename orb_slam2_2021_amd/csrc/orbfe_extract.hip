@@ -591,13 +591,13 @@ __host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max, int r
 // with shifts and the row/column split of a detection index is a multiply-shift.
 // RSC == 0: any geometry, runtime stride.
 template <int RSC>
-__global__ __launch_bounds__(256) void k_fast(ExtractArgs a) {
+__global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell1) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int w = wave_id(), lane = lane_id();
   const int2 blk = xcd_block2d();
-  const int cell = blk.x * 4 + w;
+  const int cell = cell0 + blk.x * 4 + w;  // cells [cell0, cell1) of this launch
   const int img = blk.y;
-  if (cell >= a.ncells) return;
+  if (cell >= cell1) return;
   const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max, RSC);
   uint8_t* base = smem + w * lay.total;
   uint8_t* roi = base + lay.roi;
@@ -1451,7 +1451,7 @@ struct orbfe_extractor {
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
   std::vector<LevelDesc> levels;
@@ -1889,15 +1889,32 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
 
+  auto launch_fast = [&](hipStream_t s, int c0, int c1) -> int {
+    if (c1 <= c0) return ORBFE_OK;
+    dim3 grid((c1 - c0 + 3) / 4, n);
+    if (fast_rs(h) == 68)
+      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<68>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
+    else
+      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
+    return ORBFE_OK;
+  };
+  const int lv1_cells = h->nlevels > 1 ? h->levels[1].cell_begin : a.ncells;
   if (h->nbands > 0 && !h->force_level_launches) {
     dim3 grid(h->nbands, n);
     LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), h->pyramid_lds, st, a));
+    launch_fast(st, 0, a.ncells);
   } else {
     {
       const LevelDesc& d = h->levels[0];
       dim3 grid((d.w + 1023) / 1024, (d.h + 3) / 4, n), block(64, 4);
       LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
     }
+    // level 0's FAST cells run on the side stream while the main stream builds levels 1..L-1
+    // (a chain of small, dependent resize launches that leaves most CUs idle)
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_l0, 0));
+    launch_fast(h->side, 0, lv1_cells);
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
     for (int l = 1; l < h->nlevels; l++) {
       const LevelDesc& d = h->levels[l];
       if (d.rwin_ok) {
@@ -1908,13 +1925,8 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
         LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
       }
     }
-  }
-  {
-    dim3 grid((a.ncells + 3) / 4, n);
-    if (fast_rs(h) == 68)
-      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<68>, grid, dim3(256), fast_lds(h), st, a));
-    else
-      LAUNCH_TIMED(h, 1, st, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), st, a));
+    launch_fast(st, lv1_cells, a.ncells);
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   }
   // fork: GaussianBlur needs only the pyramid, so it runs on the side stream beside k_octree (a
   // small, latency-bound grid that leaves most CUs idle); joined before k_describe
@@ -2011,7 +2023,9 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
       hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       create_side_stream(&h->side) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_l0, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_f0, hipEventDisableTiming) != hipSuccess) {
     delete h;
     return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: stream creation failed");
   }
@@ -2066,6 +2080,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->side) hipStreamDestroy(h->side);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
+  if (h->ev_l0) hipEventDestroy(h->ev_l0);
+  if (h->ev_f0) hipEventDestroy(h->ev_f0);
   delete h;
   return ORBFE_OK;
 }
