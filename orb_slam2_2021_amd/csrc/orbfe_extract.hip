@@ -518,23 +518,28 @@ __device__ __forceinline__ uint32_t arc_strength_pk(const uint8_t* pa, const uin
   }
   const uint32_t pass = (dark | brt) & 0x80008000u;
   if (pass == 0) return 0;
-  uint32_t mn2[16], mx2[16];
+  // A = min over the 16 arcs of 9 of the arc max, then B = max over arcs of the arc min (one
+  // network at a time keeps 32 values live instead of 64)
+  uint32_t A = 0x00ff00ffu, B = 0;
+  {
+    uint32_t m4[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = pk_min_u16(x[k], x[(k + 1) & 15]);
-    mx2[k] = pk_max_u16(x[k], x[(k + 1) & 15]);
+    for (int k = 0; k < 16; k++) m4[k] = pk_max_u16(x[k], x[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m4[k] = pk_max_u16(m4[k], pk_max_u16(x[(k + 2) & 15], x[(k + 3) & 15]));
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      A = pk_min_u16(A, pk_max_u16(pk_max_u16(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]));
   }
-  uint32_t mn4[16], mx4[16];
+  {
+    uint32_t m4[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = pk_min_u16(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = pk_max_u16(mx2[k], mx2[(k + 2) & 15]);
-  }
-  uint32_t B = 0, A = 0x00ff00ffu;
+    for (int k = 0; k < 16; k++) m4[k] = pk_min_u16(x[k], x[(k + 1) & 15]);
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
-    B = pk_max_u16(B, pk_min_u16(pk_min_u16(mn4[k], mn4[(k + 4) & 15]), x[(k + 8) & 15]));
-    A = pk_min_u16(A, pk_max_u16(pk_max_u16(mx4[k], mx4[(k + 4) & 15]), x[(k + 8) & 15]));
+    for (int k = 0; k < 16; k++) m4[k] = pk_min_u16(m4[k], pk_min_u16(x[(k + 2) & 15], x[(k + 3) & 15]));
+#pragma unroll
+    for (int k = 0; k < 16; k++)
+      B = pk_max_u16(B, pk_min_u16(pk_min_u16(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]));
   }
   const uint32_t m = pk_max_i16(pk_sub16(c, A), pk_sub16(B, c));  // max(v - A, B - v), signed
   const int ma = (int)(short)(m & 0xffffu), mb = (int)(short)(m >> 16);
