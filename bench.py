@@ -247,6 +247,7 @@ def main():
     roof = roofline(timed if dominant in timed else probe, dominant, geo, counts, cand, n_img,
                     args.steps if dominant in timed else probe_steps)
     roof["measured_in"] = "timed region" if dominant in timed else "probe pass (--no-kernel-events)"
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B)
     algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
     out = {
         "metric": METRIC,
@@ -333,6 +334,25 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, steps):
             "kernel_us_per_step": round(step_s * 1e6, 2),
             "avg_launch_us": round(step_s * 1e6 / per_launch_steps, 2),
             "launches_per_step": per_launch_steps}
+
+
+def pmc_traffic(kernel, W, H, B):
+    """HBM bytes per step of `kernel` from the committed rocprofv3 PMC summary of this workload
+    (profiles/pmc_traffic.json, written by profiles/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of `bench.py --no-cpu`; FETCH_SIZE doubled per MI355X_MICROARCH.md), or None
+    when no summary for this kernel and workload is committed."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if doc.get("workload") != {"cols": W, "rows": H, "batch": B}:
+        return None, None
+    k = doc.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return int(k["traffic_bytes_per_step"]), doc.get("source")
 
 
 def pipeline_bytes_per_stereo_frame(geo, counts, B):

@@ -4,11 +4,20 @@ launch per kernel, with the gfx950 corrections of MI355X_MICROARCH.md ("HBM"): F
 counts half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE (KiB) is taken as is.
 
 usage: pmc_summary.py FETCH_CSV WRITE_CSV [OUT_JSON]
+Per step = mean per launch x launches per step (k_resize_win: one per pyramid level; k_fast: level
+0 beside the resize chain + levels 1..7; every other kernel once).
 """
 import csv
 import json
 import sys
 from collections import defaultdict
+
+
+def kname(raw):
+    name = raw.split("(")[0]
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("<")[0]
 
 
 def per_kernel(path, counter):
@@ -17,7 +26,7 @@ def per_kernel(path, counter):
         for row in csv.DictReader(f):
             if row["Counter_Name"] != counter:
                 continue
-            name = row["Kernel_Name"].split("(")[0]
+            name = kname(row["Kernel_Name"])
             acc[name][0] += float(row["Counter_Value"])
             acc[name][1] += 1
     return {k: (v[0] / v[1], v[1]) for k, v in acc.items()}
@@ -26,15 +35,22 @@ def per_kernel(path, counter):
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    out = {}
+    lps = {"k_resize_win": 7, "k_resize": 7, "k_fast": 2}
+    kernels = {}
     for k in sorted(set(fetch) & set(write)):
-        if k.startswith("__amd"):
+        if k.startswith("__amd") or k.startswith("at::") or "native" in k:
             continue
         fb = 2.0 * fetch[k][0] * 1024.0
         wb = write[k][0] * 1024.0
-        out[k] = {"fetch_bytes_corrected": round(fb), "write_bytes": round(wb),
-                  "traffic_bytes_per_launch": round(fb + wb), "launches": fetch[k][1]}
-    text = json.dumps(out, indent=1)
+        per_step = lps.get(k, 1)
+        kernels[k] = {"fetch_bytes_corrected_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                      "traffic_bytes_per_launch": round(fb + wb), "launches_per_step": per_step,
+                      "traffic_bytes_per_step": round((fb + wb) * per_step)}
+    doc = {"workload": {"cols": 1241, "rows": 376, "batch": 32},
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
+                     "bench.py --no-cpu; FETCH_SIZE x 2 (gfx950 correction), KiB -> bytes",
+           "kernels": kernels}
+    text = json.dumps(doc, indent=1)
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:
             f.write(text + "\n")
