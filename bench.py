@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true")
+    p.add_argument("--no-legs", action="store_true", help="skip the secondary C5 measurement")
     p.add_argument("--banded-pyramid", action="store_true",
                    help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
     return p.parse_args()
@@ -282,6 +283,8 @@ def main():
     }
     if rank == 0 and world == 1:
         out["host_boundary"] = host_boundary_rate(ext, host)
+        if not args.no_legs:
+            out["legs"] = {"c5_search_by_projection": sbp_leg(args)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey)
     if rank == 0:
@@ -363,6 +366,37 @@ def pipeline_bytes_per_stereo_frame(geo, counts, B):
     extract = sum(px) + sum(px[1:]) + 60 * n_per_img
     sft = 2 * n_per_img * 64 + 2 * n_per_img / 8 + 4 * 2 * n_per_img
     return 2 * extract + sft
+
+
+def sbp_leg(args, m_points=50000, reps=20):
+    """Secondary measurement (BASELINE config C5 shape): ORBmatcher::SearchByProjection(Frame,
+    50k local MapPoints, th=3) on a 640x480 frame, through the host-buffer C ABI (frame and
+    MapPoint SoA uploaded every call, so PCIe is included), beside the CPU oracle on the same
+    input. Reported, not `value`."""
+    from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame
+    from orb_slam2_2021_amd import synthetic as S
+    ext = ORBextractor(args.nfeatures, 1.2, 8, 12, 7)  # arducam.yaml:126-127
+    k, d = ext(synth_frame(7, 480, 640))
+    rng = np.random.default_rng(0x50C0DE)
+    F = S.make_frame(k, d, ext.GetScaleFactors(), ext.GetScaleSigmaSquares(), 480, 640,
+                     S.ARDUCAM_CAM, rng, mp_frac=0.0)
+    mps = S.make_local_mappoints(F, m_points, rng)
+    m = ORBmatcher(0.8, True)  # Tracking.cc:1207
+    nm, _ = m.SearchByProjection(F, mps, 3.0)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        m.SearchByProjection(F, mps, 3.0)
+    gpu_s = (time.perf_counter() - t0) / reps
+    out = {"frames_per_s": round(1.0 / gpu_s, 1), "ms_per_frame": round(1e3 * gpu_s, 3),
+           "map_points": m_points, "keypoints": int(len(k)), "matches": int(nm),
+           "what": "host C ABI per call (H2D of frame + MapPoints, kernels, D2H), 1 GPU"}
+    if not args.no_cpu:
+        from oracle import orbref
+        t0 = time.perf_counter()
+        nr, _ = orbref.search_by_projection_local(F, mps, 3.0, 0.8)
+        out["cpu_oracle_ms_per_frame"] = round(1e3 * (time.perf_counter() - t0), 3)
+        out["cpu_matches_equal"] = bool(nr == nm)
+    return out
 
 
 def host_boundary_rate(ext, host, reps=5):

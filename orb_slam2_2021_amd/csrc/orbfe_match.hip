@@ -762,6 +762,7 @@ struct orbfe_matcher {
   size_t arena_bytes = 0;
   orbfe_sft_pair* d_pairs = nullptr;
   int pairs_cap = 0;
+  std::vector<orbfe_sft_pair> pairs_uploaded;  // host copy of d_pairs (skip identical uploads)
   int32_t* d_serial = nullptr;
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
@@ -907,12 +908,19 @@ extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int
   if (n_pairs > m->pairs_cap) {
     hipFree(m->d_pairs);
     m->d_pairs = nullptr;
+    m->pairs_uploaded.clear();
     ORBFE_HIP_CHECK(hipMalloc(&m->d_pairs, sizeof(orbfe_sft_pair) * n_pairs));
     m->pairs_cap = n_pairs;
   }
   for (int p = 0; p < n_pairs; p++)
     if (pairs[p].kf2.n > SFT_MAX_KF2) return orbfe_set_error(ORBFE_ERR_ARG, "sft: KF2 too large");
-  ORBFE_HIP_CHECK(hipMemcpyAsync(m->d_pairs, pairs, sizeof(orbfe_sft_pair) * n_pairs, hipMemcpyHostToDevice, s));
+  // the pair descriptors are usually identical from call to call (device-resident batches):
+  // upload only when they changed
+  if ((int)m->pairs_uploaded.size() != n_pairs ||
+      std::memcmp(m->pairs_uploaded.data(), pairs, sizeof(orbfe_sft_pair) * n_pairs) != 0) {
+    ORBFE_HIP_CHECK(hipMemcpyAsync(m->d_pairs, pairs, sizeof(orbfe_sft_pair) * n_pairs, hipMemcpyHostToDevice, s));
+    m->pairs_uploaded.assign(pairs, pairs + n_pairs);
+  }
   // fv1.n_nodes bounds the node grid (with fv1_nodes_dev set it must be an upper bound)
   int max_nodes = 1;
   for (int p = 0; p < n_pairs; p++) max_nodes = std::max(max_nodes, pairs[p].fv1.n_nodes);
