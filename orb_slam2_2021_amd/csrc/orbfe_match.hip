@@ -512,14 +512,66 @@ struct SbpArgs {
   int32_t* res_cur;
   const int32_t* owner_prev;  // INT_MAX = unclaimed in the previous round
   int32_t* owner_cur;
+  int32_t* owner_next;        // cleared by this round for the next one
   int32_t* state;             // [0] converged flag, [1] rounds run, [2 + r] changed in round r
   int round;
+  // per-query candidate cache filled in round 0 (keypoints passing the window, level and stereo
+  // gates, in GetFeaturesInArea order, with their distances); later rounds only re-apply the
+  // claims. cand_n[i] < 0: more than SBP_CAND candidates, the query re-searches every round.
+  int16_t* cand_k;
+  uint8_t* cand_d;
+  uint8_t* cand_l;
+  int32_t* cand_n;
 };
+#define SBP_CAND 48
 
 // One MapPoint's search given a predicate blocked(k). Returns the keypoint index or -1.
+// Best / second-best bookkeeping of the reference loop (:106-118 local; :1417-1450 last frame).
+struct SbpBest {
+  int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+  __device__ __forceinline__ void add(int mode, int dist, int level, int k) {
+    if (mode == 0) {
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = level;
+        bestIdx = k;
+      } else if (dist < bestDist2) {
+        bestLevel2 = level;
+        bestDist2 = dist;
+      }
+    } else if (dist < bestDist) {
+      bestDist = dist;
+      bestIdx = k;
+    }
+  }
+  __device__ __forceinline__ int result(int mode, float nnratio) const {
+    if (bestDist > TH_HIGH) return -1;
+    if (mode == 0 && bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return -1;
+    return bestIdx;
+  }
+};
+
+// Round > 0 with a cached candidate list: only the claims changed.
 template <class Blocked>
+__device__ int sbp_cached(const SbpArgs& a, int i, int n, Blocked blocked) {
+  SbpBest b;
+  const int16_t* ck = a.cand_k + (size_t)i * SBP_CAND;
+  const uint8_t* cd = a.cand_d + (size_t)i * SBP_CAND;
+  const uint8_t* cl = a.cand_l + (size_t)i * SBP_CAND;
+  for (int c = 0; c < n; c++) {
+    const int k = ck[c];
+    if (blocked(k)) continue;
+    b.add(a.mode, cd[c], cl[c], k);
+  }
+  return b.result(a.mode, a.nnratio);
+}
+
+template <class Blocked, bool RECORD = false>
 __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
   const SbpQuery q = a.q[i];
+  if (RECORD) a.cand_n[i] = 0;
   if (!(q.flags & 1)) return -1;
   const orbfe_frame_view& F = a.F;
   const float x = q.x, y = q.y, r = q.r;
@@ -535,7 +587,8 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
   const bool checkLevels = (q.min_level > 0) || (q.max_level >= 0);
   uint4 dq0, dq1;
   load_desc(a.qdesc + (size_t)i * 32, dq0, dq1);
-  int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+  SbpBest b;
+  int nc = 0;
   for (int ix = nMinCellX; ix <= nMaxCellX; ix++) {
     for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
       const int c = ix * GRID_ROWS + iy;
@@ -549,7 +602,7 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
         }
         const float distx = kp.x - x, disty = kp.y - y;
         if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
-        if (blocked(k)) continue;
+        if (!RECORD && blocked(k)) continue;
         const float ur = F.u_right[k];
         if (ur > 0) {
           const float er = fabsf(q.xr - ur);
@@ -558,28 +611,43 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
         uint4 d0, d1;
         load_desc(F.descriptors + (size_t)k * 32, d0, d1);
         const int dist = hamming256(dq0, dq1, d0, d1);
-        if (a.mode == 0) {
-          if (dist < bestDist) {
-            bestDist2 = bestDist;
-            bestDist = dist;
-            bestLevel2 = bestLevel;
-            bestLevel = kp.octave;
-            bestIdx = k;
-          } else if (dist < bestDist2) {
-            bestLevel2 = kp.octave;
-            bestDist2 = dist;
+        if (RECORD) {
+          if (nc < SBP_CAND) {
+            a.cand_k[(size_t)i * SBP_CAND + nc] = (int16_t)k;
+            a.cand_d[(size_t)i * SBP_CAND + nc] = (uint8_t)dist;
+            a.cand_l[(size_t)i * SBP_CAND + nc] = (uint8_t)kp.octave;
           }
-        } else if (dist < bestDist) {
-          bestDist = dist;
-          bestIdx = k;
+          nc++;
+          if (blocked(k)) continue;
         }
+        b.add(a.mode, dist, kp.octave, k);
       }
     }
   }
-  if (bestDist > TH_HIGH) return -1;
-  if (a.mode == 0 && bestLevel == bestLevel2 && (float)bestDist > a.nnratio * (float)bestDist2)
-    return -1;
-  return bestIdx;
+  if (RECORD) a.cand_n[i] = nc <= SBP_CAND ? nc : -1;
+  return b.result(a.mode, a.nnratio);
+}
+
+struct SbpInit {
+  int32_t *res0, *res1, *own0, *own2, *state, *nmatches, *serial;
+  int nq, nf;
+};
+// One launch for the per-call initialisation (results "never", owners unclaimed, counters 0).
+__global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < in.nq) {
+    in.res0[i] = (int32_t)0xfefefefe;  // never a result
+    in.res1[i] = (int32_t)0xfefefefe;
+  }
+  if (i < in.nf) {
+    in.own0[i] = 0x7fffffff;
+    in.own2[i] = 0x7fffffff;
+  }
+  if (i < SBP_MAX_ROUNDS + 4) in.state[i] = 0;
+  if (i == 0) {
+    *in.nmatches = 0;
+    *in.serial = 0;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
@@ -589,10 +657,18 @@ __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = a.round + 1;
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < a.F.n) a.owner_next[i] = 0x7fffffff;
   if (i >= a.m) return;
-  const int res = sbp_one(a, i, [&](int k) {
-    return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i;
-  });
+  auto blocked = [&](int k) { return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i; };
+  int res;
+  if (!a.cand_n) {
+    res = sbp_one(a, i, blocked);
+  } else if (a.round == 0) {
+    res = sbp_one<decltype(blocked), true>(a, i, blocked);
+  } else {
+    const int n = a.cand_n[i];
+    res = n >= 0 ? sbp_cached(a, i, n, blocked) : sbp_one(a, i, blocked);
+  }
   a.res_cur[i] = res;
   if (res >= 0 && (a.q[i].flags & 2)) atomicMin(&a.owner_cur[res], i);
   if (res != a.res_prev[i]) atomicOr(&a.state[2 + a.round], 1);
@@ -610,14 +686,36 @@ struct SbpFinishArgs {
 
 // Sequential fallback (the reference loop verbatim) when the fixpoint did not settle in
 // SBP_MAX_ROUNDS rounds, then counting and (last frame) the rotation-consistency filter.
+__device__ __forceinline__ bool sbp_converged(const SbpArgs& a) {
+  // settled: a round was skipped, or the last round reproduced the round before it
+  const int rounds = a.state[1];
+  return a.state[0] != 0 || (rounds >= 2 && a.state[2 + rounds - 1] == 0);
+}
+
+// Converged without a rotation filter (the local search): results and count, grid-wide.
+__global__ __launch_bounds__(256) void k_sbp_collect(SbpFinishArgs f) {
+  const SbpArgs& a = f.s;
+  if (f.check_ori || !sbp_converged(a)) return;  // k_sbp_finish handles those
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int32_t* res = f.res_final[(a.state[1] - 1) & 1];
+  int c = 0;
+  if (i < a.m) {
+    const int r = res[i];
+    f.best_out[i] = r;
+    c = r >= 0;
+  }
+  c = wave_sum(c);
+  if (lane_id() == 0 && c) atomicAdd(f.nmatches, c);
+}
+
 __global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* blocked_scratch) {
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_misc[8];
   const SbpArgs& a = f.s;
   const int t = threadIdx.x;
   const int rounds = a.state[1];
-  // settled: a round was skipped, or the last round reproduced the round before it
-  const bool converged = a.state[0] != 0 || (rounds >= 2 && a.state[2 + rounds - 1] == 0);
+  const bool converged = sbp_converged(a);
+  if (converged && !f.check_ori) return;  // done by k_sbp_collect
   const int32_t* res = f.res_final[(rounds - 1) & 1];
   if (!converged) {
     if (t == 0) {
@@ -764,6 +862,11 @@ struct orbfe_matcher {
   int pairs_cap = 0;
   std::vector<orbfe_sft_pair> pairs_uploaded;  // host copy of d_pairs (skip identical uploads)
   int32_t* d_serial = nullptr;
+  // pinned mirror of the arena: host inputs are staged at their arena offsets and uploaded in one
+  // H2D copy per call instead of one pageable copy per array
+  uint8_t* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  size_t stage_lo = SIZE_MAX, stage_hi = 0;
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
 };
@@ -779,11 +882,39 @@ struct Arena {
 };
 
 int ensure_arena(orbfe_matcher* m, size_t bytes) {
-  if (bytes <= m->arena_bytes) return ORBFE_OK;
-  hipFree(m->arena);
-  m->arena = nullptr;
-  ORBFE_HIP_CHECK(hipMalloc(&m->arena, bytes));
-  m->arena_bytes = bytes;
+  m->stage_lo = SIZE_MAX;
+  m->stage_hi = 0;
+  if (bytes > m->arena_bytes) {
+    hipFree(m->arena);
+    m->arena = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&m->arena, bytes));
+    m->arena_bytes = bytes;
+  }
+  if (bytes > m->pinned_bytes) {
+    if (m->pinned) hipHostFree(m->pinned);
+    m->pinned = nullptr;
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&m->pinned, bytes, hipHostMallocDefault));
+    m->pinned_bytes = bytes;
+  }
+  return ORBFE_OK;
+}
+
+// Stage n host bytes for arena address dst (uploaded by flush_h2d).
+void stage_h2d(orbfe_matcher* m, const void* dst, const void* src, size_t n) {
+  if (n == 0) return;
+  const size_t off = (size_t)((const uint8_t*)dst - m->arena);
+  std::memcpy(m->pinned + off, src, n);
+  m->stage_lo = std::min(m->stage_lo, off);
+  m->stage_hi = std::max(m->stage_hi, off + n);
+}
+
+// One H2D copy of the staged span (arena regions in between are written by kernels afterwards).
+int flush_h2d(orbfe_matcher* m) {
+  if (m->stage_hi > m->stage_lo)
+    ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + m->stage_lo, m->pinned + m->stage_lo, m->stage_hi - m->stage_lo,
+                                   hipMemcpyHostToDevice, m->stream));
+  m->stage_lo = SIZE_MAX;
+  m->stage_hi = 0;
   return ORBFE_OK;
 }
 
@@ -812,15 +943,14 @@ int upload_frame(orbfe_matcher* m, const FrameOffsets& o, const orbfe_frame_view
   d->scale_factors = (const float*)(A + o.scale);
   d->level_sigma2 = (const float*)(A + o.sigma2);
   if (f->n > 0) {
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.keys, f->keys_un, sizeof(orbfe_keypoint) * f->n, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.ur, f->u_right, sizeof(float) * f->n, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.desc, f->descriptors, 32 * (size_t)f->n, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.mp, f->mp_state, f->n, hipMemcpyHostToDevice, m->stream));
+    stage_h2d(m, A + o.keys, f->keys_un, sizeof(orbfe_keypoint) * f->n);
+    stage_h2d(m, A + o.ur, f->u_right, sizeof(float) * f->n);
+    stage_h2d(m, A + o.desc, f->descriptors, 32 * (size_t)f->n);
+    stage_h2d(m, A + o.mp, f->mp_state, f->n);
   }
   if (f->nlevels > 0) {
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.scale, f->scale_factors, sizeof(float) * f->nlevels, hipMemcpyHostToDevice, m->stream));
-    if (f->level_sigma2)
-      ORBFE_HIP_CHECK(hipMemcpyAsync(A + o.sigma2, f->level_sigma2, sizeof(float) * f->nlevels, hipMemcpyHostToDevice, m->stream));
+    stage_h2d(m, A + o.scale, f->scale_factors, sizeof(float) * f->nlevels);
+    if (f->level_sigma2) stage_h2d(m, A + o.sigma2, f->level_sigma2, sizeof(float) * f->nlevels);
   }
   return ORBFE_OK;
 }
@@ -970,9 +1100,9 @@ extern "C" int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_fram
     d->indices = (const int32_t*)(A + idx);
     if (fv->n_nodes > 0) {
       const int ni = fv->offsets[fv->n_nodes];
-      ORBFE_HIP_CHECK(hipMemcpyAsync(A + ids, fv->node_ids, 4 * (size_t)fv->n_nodes, hipMemcpyHostToDevice, m->stream));
-      ORBFE_HIP_CHECK(hipMemcpyAsync(A + offs, fv->offsets, 4 * (size_t)(fv->n_nodes + 1), hipMemcpyHostToDevice, m->stream));
-      if (ni > 0) ORBFE_HIP_CHECK(hipMemcpyAsync(A + idx, fv->indices, 4 * (size_t)ni, hipMemcpyHostToDevice, m->stream));
+      stage_h2d(m, A + ids, fv->node_ids, 4 * (size_t)fv->n_nodes);
+      stage_h2d(m, A + offs, fv->offsets, 4 * (size_t)(fv->n_nodes + 1));
+      if (ni > 0) stage_h2d(m, A + idx, fv->indices, 4 * (size_t)ni);
     }
     return ORBFE_OK;
   };
@@ -983,6 +1113,7 @@ extern "C" int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_fram
   P.ey = ey;
   P.match12 = (int32_t*)(m->arena + om);
   P.nmatches = (int32_t*)(m->arena + on);
+  if ((st = flush_h2d(m))) return st;
   st = orbfe_search_for_triangulation_batch_device(m, 1, &P, only_stereo, m->stream);
   if (st) return st;
   int32_t nm = 0;
@@ -1001,27 +1132,42 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
                    const std::function<int(uint8_t*, const orbfe_frame_view&, SbpQuery*)>& make_q,
                    int32_t* best_idx, int* nmatches) {
   Arena ar;
+  // host-staged inputs first (frame, query inputs, query descriptors/angles): one contiguous
+  // span for the single H2D copy; device-only scratch after
   const FrameOffsets fo = plan_frame(ar, F);
+  const size_t extra = plan_q(ar);
+  (void)extra;
+  const size_t oqd = ar.add(32 * (size_t)std::max(nq, 1));
+  const size_t oqa = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t og_start = ar.add(4 * (GRID_CELLS + 1));
   const size_t og_items = ar.add(4 * (size_t)std::max(F->n, 1));
   const size_t oq = ar.add(sizeof(SbpQuery) * std::max(nq, 1));
-  const size_t oqd = ar.add(32 * (size_t)std::max(nq, 1));
-  const size_t oqa = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t ores0 = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t ores1 = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t oown0 = ar.add(4 * (size_t)std::max(F->n, 1));
   const size_t oown1 = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t oown2 = ar.add(4 * (size_t)std::max(F->n, 1));
   const size_t oblk = ar.add(4 * (size_t)std::max(F->n, 1));
   const size_t ostate = ar.add(4 * (SBP_MAX_ROUNDS + 4));
   const size_t obest = ar.add(4 * (size_t)std::max(nq, 1));
+  const bool cache = F->n <= 32767;  // candidate keypoint indices are int16
+  const size_t ocand_k = ar.add(cache ? 2 * (size_t)SBP_CAND * std::max(nq, 1) : 0);
+  const size_t ocand_d = ar.add(cache ? (size_t)SBP_CAND * std::max(nq, 1) : 0);
+  const size_t ocand_l = ar.add(cache ? (size_t)SBP_CAND * std::max(nq, 1) : 0);
+  const size_t ocand_n = ar.add(cache ? 4 * (size_t)std::max(nq, 1) : 0);
   const size_t onm = ar.add(4);
-  const size_t extra = plan_q(ar);
-  (void)extra;
   int st = ensure_arena(m, ar.total);
   if (st) return st;
   uint8_t* A = m->arena;
   orbfe_frame_view dF;
   if ((st = upload_frame(m, fo, F, &dF))) return st;
+  SbpQuery* dq = (SbpQuery*)(A + oq);
+  if (nq > 0) {
+    stage_h2d(m, A + oqd, h_qdesc, 32 * (size_t)nq);
+    if (h_qangle) stage_h2d(m, A + oqa, h_qangle, 4 * (size_t)nq);
+    if ((st = make_q(A, dF, dq))) return st;  // stages the query inputs, flushes, builds queries
+  }
+  if ((st = flush_h2d(m))) return st;
   // grid
   GridArgs g;
   g.keys = dF.keys_un;
@@ -1035,17 +1181,19 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   int P2 = 1;
   while (P2 < F->n) P2 <<= 1;
   hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sizeof(uint32_t) * P2, m->stream, g);
-  SbpQuery* dq = (SbpQuery*)(A + oq);
-  if (nq > 0) {
-    if ((st = make_q(A, dF, dq))) return st;
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + oqd, h_qdesc, 32 * (size_t)nq, hipMemcpyHostToDevice, m->stream));
-    if (h_qangle) ORBFE_HIP_CHECK(hipMemcpyAsync(A + oqa, h_qangle, 4 * (size_t)nq, hipMemcpyHostToDevice, m->stream));
+  {
+    SbpInit in;
+    in.res0 = (int32_t*)(A + ores0);
+    in.res1 = (int32_t*)(A + ores1);
+    in.own0 = (int32_t*)(A + oown0);
+    in.own2 = (int32_t*)(A + oown2);
+    in.state = (int32_t*)(A + ostate);
+    in.nmatches = (int32_t*)(A + onm);
+    in.serial = m->d_serial;
+    in.nq = std::max(nq, 1);
+    in.nf = std::max(F->n, 1);
+    hipLaunchKernelGGL(k_sbp_init, dim3((std::max(in.nq, in.nf) + 255) / 256), dim3(256), 0, m->stream, in);
   }
-  ORBFE_HIP_CHECK(hipMemsetAsync(A + ores0, 0xfe, 4 * (size_t)std::max(nq, 1), m->stream));  // -0x01010102: never a result
-  ORBFE_HIP_CHECK(hipMemsetAsync(A + ores1, 0xfe, 4 * (size_t)std::max(nq, 1), m->stream));
-  ORBFE_HIP_CHECK(hipMemsetAsync(A + oown1, 0x7f, 4 * (size_t)std::max(F->n, 1), m->stream));
-  ORBFE_HIP_CHECK(hipMemsetAsync(A + ostate, 0, 4 * (SBP_MAX_ROUNDS + 4), m->stream));
-  ORBFE_HIP_CHECK(hipMemsetAsync(m->d_serial, 0, 4, m->stream));
   SbpArgs a;
   std::memset(&a, 0, sizeof(a));
   a.F = dF;
@@ -1057,16 +1205,24 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   a.mode = mode;
   a.nnratio = m->nnratio;
   a.state = (int32_t*)(A + ostate);
+  if (cache) {
+    a.cand_k = (int16_t*)(A + ocand_k);
+    a.cand_d = A + ocand_d;
+    a.cand_l = A + ocand_l;
+    a.cand_n = (int32_t*)(A + ocand_n);
+  }
   int32_t* res[2] = {(int32_t*)(A + ores0), (int32_t*)(A + ores1)};
-  int32_t* own[2] = {(int32_t*)(A + oown0), (int32_t*)(A + oown1)};
+  // owner buffers rotate over three: round r claims into own[r % 3], reads own[(r + 2) % 3] and
+  // clears own[(r + 1) % 3] for round r + 1 (nobody reads it during round r)
+  int32_t* own[3] = {(int32_t*)(A + oown0), (int32_t*)(A + oown1), (int32_t*)(A + oown2)};
   for (int r = 0; r < m->max_rounds && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];
-    a.owner_cur = own[r & 1];
-    a.owner_prev = own[(r + 1) & 1];
-    ORBFE_HIP_CHECK(hipMemsetAsync(a.owner_cur, 0x7f, 4 * (size_t)std::max(F->n, 1), m->stream));
-    hipLaunchKernelGGL(k_sbp_round, dim3((nq + 255) / 256), dim3(256), 0, m->stream, a);
+    a.owner_cur = own[r % 3];
+    a.owner_prev = own[(r + 2) % 3];
+    a.owner_next = own[(r + 1) % 3];
+    hipLaunchKernelGGL(k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
   }
   SbpFinishArgs f;
   std::memset(&f, 0, sizeof(f));
@@ -1079,6 +1235,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   f.q_angle = (const float*)(A + oqa);
   f.serial_used = m->d_serial;
   if (nq > 0) {
+    hipLaunchKernelGGL(k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
     hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + oblk));
   }
   ORBFE_HIP_CHECK(hipGetLastError());
@@ -1120,12 +1277,14 @@ extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_fr
     return 0;
   };
   auto make = [&](uint8_t* A, const orbfe_frame_view& dF, SbpQuery* dq) -> int {
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_flags, mps->flags, M, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_px, mps->proj_x, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_py, mps->proj_y, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_pxr, mps->proj_xr, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_lvl, mps->level, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_vc, mps->view_cos, 4 * (size_t)M, hipMemcpyHostToDevice, m->stream));
+    stage_h2d(m, A + o_flags, mps->flags, M);
+    stage_h2d(m, A + o_px, mps->proj_x, 4 * (size_t)M);
+    stage_h2d(m, A + o_py, mps->proj_y, 4 * (size_t)M);
+    stage_h2d(m, A + o_pxr, mps->proj_xr, 4 * (size_t)M);
+    stage_h2d(m, A + o_lvl, mps->level, 4 * (size_t)M);
+    stage_h2d(m, A + o_vc, mps->view_cos, 4 * (size_t)M);
+    int st = flush_h2d(m);
+    if (st) return st;
     LocalQueryArgs qa;
     std::memset(&qa, 0, sizeof(qa));
     qa.mp.m = M;
@@ -1185,9 +1344,11 @@ extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
     return 0;
   };
   auto make = [&](uint8_t* A, const orbfe_frame_view& dF, SbpQuery* dq) -> int {
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_flags, L->flags, N, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_pos, L->world_pos, 12 * (size_t)N, hipMemcpyHostToDevice, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(A + o_oct, L->octave, 4 * (size_t)N, hipMemcpyHostToDevice, m->stream));
+    stage_h2d(m, A + o_flags, L->flags, N);
+    stage_h2d(m, A + o_pos, L->world_pos, 12 * (size_t)N);
+    stage_h2d(m, A + o_oct, L->octave, 4 * (size_t)N);
+    int st = flush_h2d(m);
+    if (st) return st;
     LastQueryArgs qa;
     std::memset(&qa, 0, sizeof(qa));
     qa.last.n = N;
