@@ -624,20 +624,32 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
   // 1. ROI -> LDS: dword-aligned columns [x0a, x0a + 4 nw) cover [x0, x0 + rw)
   const int x0a = cd.x0 & ~3, xo = cd.x0 - x0a, nw = (xo + rw + 3) >> 2;
   if constexpr (RSC != 0) {
-    constexpr int WPR = 16;  // dword columns loaded per ROI row (ROI <= 61 columns + 3 alignment)
-    constexpr int SH = 4;
-    for (int i0 = 0; i0 < WPR * rh; i0 += 8 * 64) {
-      uint32_t v[8];
+    // 16-byte loads, 4 lanes per ROI row (<= 61 columns + 3 alignment bytes = 16 dwords); the last
+    // quad of a row may read up to 12 bytes past the ROI (row padding / next row / the +256 slack)
+    const int nq4 = (nw + 3) >> 2;
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = i0 + lane + 64 * k, r = i >> SH, c = i & (WPR - 1);
-        if (r < rh && c < nw)
-          v[k] = *reinterpret_cast<const uint32_t*>(lev + (long long)(cd.y0 + r) * pitch + x0a + 4 * c);
+    for (int k = 0; k < 3; k++) {  // rh <= 48 rows: 192 quads
+      const int i = lane + 64 * k, r = i >> 2, q = i & 3;
+      if (r < rh && q < nq4) {
+        uint4 v;
+        __builtin_memcpy(&v, lev + (long long)(cd.y0 + r) * pitch + x0a + 16 * q, 16);
+        uint32_t* d = reinterpret_cast<uint32_t*>(roi + r * RSC + 16 * q);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
       }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const int i = i0 + lane + 64 * k, r = i >> SH, c = i & (WPR - 1);
-        if (r < rh && c < nw) *reinterpret_cast<uint32_t*>(roi + r * RSC + 4 * c) = v[k];
+    }
+    for (int i = lane + 192; i < 4 * rh; i += 64) {  // taller ROIs (rh > 48)
+      const int r = i >> 2, q = i & 3;
+      if (q < nq4) {
+        uint4 v;
+        __builtin_memcpy(&v, lev + (long long)(cd.y0 + r) * pitch + x0a + 16 * q, 16);
+        uint32_t* d = reinterpret_cast<uint32_t*>(roi + r * RSC + 16 * q);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
       }
     }
   } else {
@@ -1798,8 +1810,9 @@ static int ensure_batch(orbfe_extractor* h, int n) {
   if (n <= h->batch_cap) return ORBFE_OK;
   free_batch(h);
   const int cap = std::max(n, 1);
-  ORBFE_HIP_CHECK(hipMalloc(&h->d_pyr, (size_t)h->pyr_stride * cap));
-  ORBFE_HIP_CHECK(hipMalloc(&h->d_blur, (size_t)h->pyr_stride * cap));
+  // (+256: k_fast's 16-byte ROI loads may run up to 15 bytes past the last row of the block)
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_pyr, (size_t)h->pyr_stride * cap + 256));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_blur, (size_t)h->pyr_stride * cap + 256));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_cand, (size_t)h->cand_stride * 4 * cap));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_cellcnt, sizeof(int32_t) * h->cells.size() * cap + 4));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_keys_a, (size_t)h->keyscr_stride * 4 * cap));
