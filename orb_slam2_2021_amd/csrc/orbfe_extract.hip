@@ -1316,7 +1316,13 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
 // k_describe: one wavefront per surviving keypoint. IC_Angle (:75-102) sums the integer moments of
 // the 749-pixel circle straight from the level (L1/L2 hits); the 256 steered tests (:105-151) read
 // the blurred level; bits land as 4 wave ballots (64 pairs each = 8 descriptor bytes).
-__constant__ int8_t c_circle[2 * 752];  // (v, u) of the IC_Angle circle, 749 used
+// k_describe tables: the 256 test pairs as floats (x0, y0, x1, y1), and for each alignment
+// s = (cx - 15) & 3 the byte masks of the 31 x 9 dwords of the IC_Angle window that keep the
+// circle |u| <= umax[|v|] (ORBextractor.cc:82-98)
+__constant__ float4 c_patf[256];
+__constant__ uint32_t c_momask[4][31][9];
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int group16_sum(int v) {  // sum over the 16-lane group of this lane
 #pragma unroll
@@ -1380,17 +1386,13 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   const int xa = (cx - 15) & ~3;
   const uint8_t* usrc = a.pyr + lbase + (long long)(cy - 15) * pitch + xa;
   int m01 = 0, m10 = 0;
+  const uint32_t* mtab = &c_momask[(cx - 15) & 3][0][0];
 #pragma unroll
   for (int k = 0; k < 18; k++) {
     const int i = l16 + 16 * k;  // 279 dwords
     const int r = i / 9, c = i - 9 * r, v = r - 15;
     const uint32_t d = i < 279 ? *reinterpret_cast<const uint32_t*>(usrc + r * pitch + 4 * c) : 0u;
-    const int um = i < 279 ? a.umax[v < 0 ? -v : v] : -1000;
-    const int u0 = xa + 4 * c - cx;  // u of the dword's byte 0
-    const int lo = max(-um - u0, 0), hi = min(um - u0, 3);  // bytes [lo, hi] are on the circle
-    uint32_t mask = 0;
-    if (lo <= hi) mask = (0xffffffffu << (8 * lo)) & (0xffffffffu >> (8 * (3 - hi)));
-    const uint32_t px = d & mask;
+    const uint32_t px = i < 279 ? d & mtab[i] : 0u;  // bytes on the circle (|u| <= umax[|v|])
     const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
     const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
     m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
@@ -1410,10 +1412,17 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const int p = 16 * j + l16;
-    const float x0 = (float)c_pattern[4 * p], y0 = (float)c_pattern[4 * p + 1];
-    const float x1 = (float)c_pattern[4 * p + 2], y1 = (float)c_pattern[4 * p + 3];
-    const int t0 = wb[cv_round_f(x0 * sb + y0 * ca) * 40 + cv_round_f(x0 * ca - y0 * sb)];
-    const int t1 = wb[cv_round_f(x1 * sb + y1 * ca) * 40 + cv_round_f(x1 * ca - y1 * sb)];
+    // row = cvRound(x sin + y cos), col = cvRound(x cos - y sin) (:115-117): the products and the
+    // sum in packed fp32 (separately rounded, as the reference), cvRound's half-even by adding
+    // 1.5 * 2^23 and reading the integer out of the mantissa
+    const float4 P = c_patf[p];
+    const f32x2 sc = {sb, ca}, cs = {ca, -sb}, magic = {12582912.0f, 12582912.0f};
+    const f32x2 q0 = (f32x2){P.x, P.x} * sc + (f32x2){P.y, P.y} * cs + magic;
+    const f32x2 q1 = (f32x2){P.z, P.z} * sc + (f32x2){P.w, P.w} * cs + magic;
+    const int i0 = __float_as_int(q0.x) * 40 + __float_as_int(q0.y) - 0x4B400000 * 41;
+    const int i1 = __float_as_int(q1.x) * 40 + __float_as_int(q1.y) - 0x4B400000 * 41;
+    const int t0 = wb[i0];
+    const int t1 = wb[i1];
     const uint32_t hv = (uint32_t)(wave_ballot(t0 < t1) >> (16 * grp)) & 0xffffu;
     if (l16 == (j >> 1)) dv |= hv << (16 * (j & 1));
   }
@@ -2051,16 +2060,25 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
   static hipError_t pat_err = hipSuccess;
   std::call_once(once, [h] {
     pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, 1024);
-    // IC_Angle circle (ORBextractor.cc:82-98): rows v = -15..15, |u| <= umax[|v|]
-    int8_t circ[2 * 752] = {0};
-    int k = 0;
-    for (int v = -15; v <= 15; v++)
-      for (int u = -h->umax[std::abs(v)]; u <= h->umax[std::abs(v)]; u++) {
-        circ[2 * k] = (int8_t)v;
-        circ[2 * k + 1] = (int8_t)u;
-        k++;
-      }
-    if (pat_err == hipSuccess && k == 749) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_circle), circ, sizeof(circ));
+    float patf[1024];
+    for (int i = 0; i < 1024; i++) patf[i] = (float)kOrbPattern31[i];
+    if (pat_err == hipSuccess) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_patf), patf, sizeof(patf));
+    // IC_Angle circle masks: window dword c of row v covers u = -15 - s + 4c .. +3
+    uint32_t masks[4][31][9];
+    int npx = 0;
+    for (int sh = 0; sh < 4; sh++)
+      for (int r = 0; r < 31; r++)
+        for (int c = 0; c < 9; c++) {
+          const int um = h->umax[std::abs(r - 15)];
+          uint32_t m = 0;
+          for (int b = 0; b < 4; b++) {
+            const int u = -15 - sh + 4 * c + b;
+            if (u >= -um && u <= um) m |= 0xffu << (8 * b);
+          }
+          masks[sh][r][c] = m;
+          if (sh == 0) npx += __builtin_popcount(m) / 8;
+        }
+    if (pat_err == hipSuccess && npx == 749) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_momask), masks, sizeof(masks));
     else if (pat_err == hipSuccess) pat_err = hipErrorInvalidValue;
   });
   if (pat_err != hipSuccess) {
