@@ -43,9 +43,9 @@ def parse():
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true")
     p.add_argument("--no-legs", action="store_true", help="skip the secondary C5 measurement")
-    p.add_argument("--graph", type=int, default=0,
-                   help="1: replay the step as a captured HIP graph in the timed region (measured: no "
-                        "gain over stream launches; the roofline then comes from the probe pass)")
+    p.add_argument("--pipeline", type=int, default=2,
+                   help="output sets in flight: 2 overlaps a step's matching with the next step's "
+                        "extraction (1: strictly one step at a time)")
     p.add_argument("--banded-pyramid", action="store_true",
                    help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
     return p.parse_args()
@@ -85,16 +85,9 @@ def main():
     if args.banded_pyramid:
         ext.debug_force_level_launches(False)
     cap = ext.max_keypoints(H, W)
-    d_kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
-    d_desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
-    d_cnt = torch.zeros(n_img, dtype=torch.int32, device=dev)
     # ---- matcher inputs: vocabulary, per-keyframe stereo/MapPoint state, geometry ----
     tree = S.Vocabulary.synthetic()
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
-    d_ids = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
-    d_offs = torch.empty(n_img * (cap + 1), dtype=torch.int32, device=dev)
-    d_idx = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
-    d_nodes = torch.zeros(n_img, dtype=torch.int32, device=dev)
     rng = np.random.default_rng(1234 + rank)
     ur = np.where(rng.random((n_img, cap)) < 0.5, rng.uniform(10, 1200, (n_img, cap)), -1.0)
     d_ur = torch.from_numpy(ur.astype(np.float32)).to(dev)
@@ -110,80 +103,108 @@ def main():
     dummy = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t1)
     dummy2 = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t2)
     ex, ey = epipole(dummy, dummy2)
-    d_m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
-    d_nm = torch.zeros(B, dtype=torch.int32, device=dev)
-    matcher = ORBmatcher(0.6, False, device=dev.index)  # LocalMapping.cc:219
 
-    def view(i):
-        v = L.frame_view()
-        v.n = 0  # read on the device from d_cnt[i]
-        v.keys_un = d_kps.data_ptr() + i * cap * 28
-        v.u_right = d_ur.data_ptr() + i * cap * 4
-        v.descriptors = d_desc.data_ptr() + i * cap * 32
-        v.mp_state = d_mp.data_ptr() + i * cap
-        v.nlevels = 8
-        v.scale_factors = d_scale.data_ptr()
-        v.level_sigma2 = d_sigma2.data_ptr()
-        v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(W), 0.0, float(H)
-        v.grid_inv_w = float(dummy.grid_inv_w)
-        v.grid_inv_h = float(dummy.grid_inv_h)
-        v.fx, v.fy, v.cx, v.cy, v.bf = cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["bf"]
-        v.b = float(dummy.mb)
-        return v
+    # ---- output sets: the step's extraction writes set (step % depth) while the matching of the
+    # previous step still reads the other one (a two-deep pipeline across steps; every step does
+    # all of its work, the streams only overlap one step's matching with the next's extraction)
+    depth = max(1, args.pipeline)
 
-    def fvec(i):
-        f = L.feature_vector()
-        f.n_nodes = min(cap, tree.k ** tree.levels)  # upper bound; the count is read on the device
-        f.node_ids = d_ids.data_ptr() + i * cap * 4
-        f.offsets = d_offs.data_ptr() + i * (cap + 1) * 4
-        f.indices = d_idx.data_ptr() + i * cap * 4
-        return f
+    class OutSet:
+        def __init__(self):
+            self.kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
+            self.desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
+            self.cnt = torch.zeros(n_img, dtype=torch.int32, device=dev)
+            self.ids = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+            self.offs = torch.empty(n_img * (cap + 1), dtype=torch.int32, device=dev)
+            self.idx = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+            self.nodes = torch.zeros(n_img, dtype=torch.int32, device=dev)
+            self.m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
+            self.nm = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.matcher = ORBmatcher(0.6, False, device=dev.index)  # LocalMapping.cc:219
+            self.pairs = (L.sft_pair * B)()
+            for i in range(B):
+                p = self.pairs[i]
+                p.kf1, p.kf2 = self.view(i), self.view(B + i)
+                p.fv1, p.fv2 = self.fvec(i), self.fvec(B + i)
+                for k, x in enumerate(F12.reshape(9)):
+                    p.f12[k] = float(x)
+                p.ex, p.ey = ex, ey
+                p.match12 = self.m12.data_ptr() + i * cap * 4
+                p.nmatches = self.nm.data_ptr() + i * 4
+                p.kf1_n_dev = self.cnt.data_ptr() + i * 4
+                p.kf2_n_dev = self.cnt.data_ptr() + (B + i) * 4
+                p.fv1_nodes_dev = self.nodes.data_ptr() + i * 4
+                p.fv2_nodes_dev = self.nodes.data_ptr() + (B + i) * 4
+            self.extracted = torch.cuda.Event()
+            self.matched = torch.cuda.Event()
 
-    pairs = (L.sft_pair * B)()
-    for i in range(B):
-        p = pairs[i]
-        p.kf1, p.kf2 = view(i), view(B + i)
-        p.fv1, p.fv2 = fvec(i), fvec(B + i)
-        for k, x in enumerate(F12.reshape(9)):
-            p.f12[k] = float(x)
-        p.ex, p.ey = ex, ey
-        p.match12 = d_m12.data_ptr() + i * cap * 4
-        p.nmatches = d_nm.data_ptr() + i * 4
-        p.kf1_n_dev = d_cnt.data_ptr() + i * 4
-        p.kf2_n_dev = d_cnt.data_ptr() + (B + i) * 4
-        p.fv1_nodes_dev = d_nodes.data_ptr() + i * 4
-        p.fv2_nodes_dev = d_nodes.data_ptr() + (B + i) * 4
+        def view(self, i):
+            v = L.frame_view()
+            v.n = 0  # read on the device from cnt[i]
+            v.keys_un = self.kps.data_ptr() + i * cap * 28
+            v.u_right = d_ur.data_ptr() + i * cap * 4
+            v.descriptors = self.desc.data_ptr() + i * cap * 32
+            v.mp_state = d_mp.data_ptr() + i * cap
+            v.nlevels = 8
+            v.scale_factors = d_scale.data_ptr()
+            v.level_sigma2 = d_sigma2.data_ptr()
+            v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(W), 0.0, float(H)
+            v.grid_inv_w = float(dummy.grid_inv_w)
+            v.grid_inv_h = float(dummy.grid_inv_h)
+            v.fx, v.fy, v.cx, v.cy, v.bf = cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["bf"]
+            v.b = float(dummy.mb)
+            return v
+
+        def fvec(self, i):
+            f = L.feature_vector()
+            f.n_nodes = min(cap, tree.k ** tree.levels)  # upper bound; the count is read on the device
+            f.node_ids = self.ids.data_ptr() + i * cap * 4
+            f.offsets = self.offs.data_ptr() + i * (cap + 1) * 4
+            f.indices = self.idx.data_ptr() + i * cap * 4
+            return f
+
+    sets = [OutSet() for _ in range(depth)]
     lib = L.lib()
     gather = world > 1 and not args.no_gather
 
     ev = {k: [] for k in ("k_vocab", "k_sft")}
     ev_sel = set()  # which of the two non-extractor kernels get events in this pass
+    stream = torch.cuda.Stream(dev)   # extraction
+    mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
+    counter = [0]
 
     def step():
-        s = torch.cuda.current_stream(dev).cuda_stream
-        ext.extract_batch_device(n_img, d_img.data_ptr(), H * W, H, W, W, d_kps.data_ptr(),
-                                 d_desc.data_ptr(), cap, d_cnt.data_ptr(), stream=s)
+        o = sets[counter[0] % depth]
+        counter[0] += 1
+        stream.wait_event(o.matched)  # the matching that last read this set is done
+        ext.extract_batch_device(n_img, d_img.data_ptr(), H * W, H, W, W, o.kps.data_ptr(),
+                                 o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=stream.cuda_stream)
+        o.extracted.record(stream)
+        mstream.wait_event(o.extracted)
+        ms = mstream.cuda_stream
         if "k_vocab" in ev_sel:
             e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        voc.transform_batch_device(n_img, d_desc.data_ptr(), cap * 32, d_cnt.data_ptr(), 0,
-                                   d_ids.data_ptr(), d_offs.data_ptr(), d_idx.data_ptr(),
-                                   d_nodes.data_ptr(), cap, stream=s)
+            e0.record(mstream)
+        voc.transform_batch_device(n_img, o.desc.data_ptr(), cap * 32, o.cnt.data_ptr(), 0,
+                                   o.ids.data_ptr(), o.offs.data_ptr(), o.idx.data_ptr(),
+                                   o.nodes.data_ptr(), cap, stream=ms)
         if "k_vocab" in ev_sel:
             e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
+            e1.record(mstream)
             ev["k_vocab"].append((e0, e1))
         if "k_sft" in ev_sel:
             e2 = torch.cuda.Event(enable_timing=True)
-            e2.record()
+            e2.record(mstream)
         L.check(lib.orbfe_search_for_triangulation_batch_device(
-            matcher._h, B, ctypes.cast(pairs, ctypes.c_void_p), 0, ctypes.c_void_p(s)), "sft batch")
+            o.matcher._h, B, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(ms)), "sft batch")
         if "k_sft" in ev_sel:
             e3 = torch.cuda.Event(enable_timing=True)
-            e3.record()
+            e3.record(mstream)
             ev["k_sft"].append((e2, e3))
         if gather:  # C4: every rank's keypoints + descriptors to rank 0 over RCCL
-            gather_to_root(d_cnt, d_kps, d_desc, dst=0)
+            with torch.cuda.stream(mstream):
+                gather_to_root(o.cnt, o.kps, o.desc, dst=0)
+        o.matched.record(mstream)
 
     def kernel_times():
         kt = ext.kernel_times()
@@ -196,9 +217,9 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # all work goes to one non-default stream, so every library call, torch event and RCCL
-    # collective of a step is ordered on it (a NULL stream would select each handle's own stream)
-    stream = torch.cuda.Stream(dev)
+    # all work goes to two non-default streams (extraction / matching) ordered by events, so every
+    # library call, torch event and RCCL collective of a step is ordered (a NULL stream would
+    # select each handle's own stream)
     torch.cuda.set_stream(stream)
     for _ in range(args.warmup):
         step()
@@ -218,24 +239,9 @@ def main():
     ev["k_vocab"].clear()
     ev["k_sft"].clear()
     dominant = max(probe, key=lambda k: probe[k][0])
-    # timed region. With --graph 1 the step (all kernels of both streams, fork/join included) is
-    # captured once into a HIP graph and replayed; the kernels and buffers are the same as the
-    # launched step's. The dominant kernel's time then comes from the probe pass's events.
-    graph = None
-    if args.graph and not gather:
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=stream):
-                step()
-            torch.cuda.synchronize()
-            graph.replay()
-            torch.cuda.synchronize()
-        except Exception as e:  # capture unsupported here: launch normally
-            print(f"graph capture failed ({e}); launching", file=sys.stderr)
-            graph = None
-            torch.cuda.set_stream(stream)
+    # timed region: events only around the dominant kernel's launches
     ext.reset_kernel_times()
-    if not args.no_kernel_events and graph is None:
+    if not args.no_kernel_events:
         if dominant in ext.KERNELS:
             ext.set_profiling([dominant])
         else:
@@ -244,10 +250,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        if graph is not None:
-            graph.replay()
-        else:
-            step()
+        step()
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -262,15 +265,13 @@ def main():
 
     frames = world * B * args.steps
     value = frames / elapsed
-    counts = d_cnt.cpu().numpy()
+    counts = sets[0].cnt.cpu().numpy()
     cand = sum(len(ext.debug_candidates(l, image=i)) for i in range(n_img) for l in range(8))
-    nm = d_nm.cpu().numpy()
+    nm = sets[0].nm.cpu().numpy()
     geo = ext.geometry(H, W)
     roof = roofline(timed if dominant in timed else probe, dominant, geo, counts, cand, n_img,
                     args.steps if dominant in timed else probe_steps)
-    roof["measured_in"] = ("timed region" if dominant in timed else
-                           "probe pass (the timed region replays a graph)" if graph is not None
-                           else "probe pass (--no-kernel-events)")
+    roof["measured_in"] = "timed region" if dominant in timed else "probe pass (--no-kernel-events)"
     roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B)
     algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
     out = {
@@ -292,7 +293,8 @@ def main():
             "nfeatures": args.nfeatures, "scale_factor": 1.2, "nlevels": 8, "ini_th_fast": 20,
             "min_th_fast": 7, "stereo_frames_per_gpu_per_step": B, "images_per_step_per_gpu": n_img,
             "parallelism": f"frame-sharded x{world}",
-            "launch": "hip graph replay" if graph is not None else "stream launches",
+            "pipeline": f"{depth} output sets: step i's matching overlaps step i+1's extraction"
+                        if depth > 1 else "one step at a time",
         },
         "roofline": roof,
         "pipeline_hbm": {
