@@ -1272,19 +1272,20 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   auto ev = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c020c00u); };  // columns 0, 2
   auto od = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c01u); };  // columns 1, 3
   const int yend = min(y0 + BS_H, ld.h);
-  const int nrows = yend - y0 + 6;  // input rows y0-3 .. yend+2
-  uint32_t q0 = load_row(y0 - 3), q1 = load_row(y0 - 2), q2 = load_row(y0 - 1), q3 = load_row(y0);
+  const int nrows = yend - y0 + 6;  // input rows y0-3 .. yend+2 (<= BS_H + 6)
+  // every input row of the strip is loaded up front (fully unrolled: all loads in flight at once,
+  // the window below is renamed, not moved)
+  uint32_t rowv[BS_H + 6];
+#pragma unroll
+  for (int i = 0; i < BS_H + 6; i++) rowv[i] = i < nrows ? load_row(y0 - 3 + i) : 0u;
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;  // window, even columns
   uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;  // window, odd columns
-  for (int i = 0; i < nrows; i++) {
-    const uint32_t C = q0;
-    q0 = q1;
-    q1 = q2;
-    q2 = q3;
-    if (i + 4 < nrows) q3 = load_row(y0 - 3 + i + 4);  // 4-row load lookahead
+#pragma unroll
+  for (int i = 0; i < BS_H + 6; i++) {
+    const uint32_t C = rowv[i];
     e0 = e1; e1 = e2; e2 = e3; e3 = e4; e4 = e5; e5 = e6; e6 = ev(C);
     o0 = o1; o1 = o2; o2 = o3; o3 = o4; o4 = o5; o5 = o6; o6 = od(C);
-    if (i < 6) continue;
+    if (i < 6 || i >= nrows) continue;
     // vertical: V of columns x, x+2 (VE) and x+1, x+3 (VO)
     const uint32_t VE = vtap7(e0, e1, e2, e3, e4, e5, e6), VO = vtap7(o0, o1, o2, o3, o4, o5, o6);
     const uint32_t LE = from_left(VE), LO = from_left(VO), RE = from_right(VE), RO = from_right(VO);
