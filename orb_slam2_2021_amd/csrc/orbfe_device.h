@@ -126,6 +126,55 @@ __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
   return total;
 }
 
+// Three exclusive scans at once (one pair of barriers instead of three); wsum holds 12 ints.
+__device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int per = (n + 255) / 256;
+  const int beg = min(t * per, n), end = min(beg + per, n);
+  int sa = 0, sb = 0, sc = 0;
+  for (int i = beg; i < end; i++) {
+    sa += a[i];
+    sb += b[i];
+    sc += c[i];
+  }
+  int ia = sa, ib = sb, ic = sc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int ya = __shfl_up(ia, o, 64), yb = __shfl_up(ib, o, 64), yc = __shfl_up(ic, o, 64);
+    if (lane >= o) {
+      ia += ya;
+      ib += yb;
+      ic += yc;
+    }
+  }
+  if (lane == 63) {
+    wsum[w] = ia;
+    wsum[4 + w] = ib;
+    wsum[8 + w] = ic;
+  }
+  __syncthreads();
+  int oa = 0, ob = 0, oc = 0;
+  for (int k = 0; k < w; k++) {
+    oa += wsum[k];
+    ob += wsum[4 + k];
+    oc += wsum[8 + k];
+  }
+  const int3 tot = make_int3(wsum[0] + wsum[1] + wsum[2] + wsum[3], wsum[4] + wsum[5] + wsum[6] + wsum[7],
+                             wsum[8] + wsum[9] + wsum[10] + wsum[11]);
+  int ra = oa + ia - sa, rb = ob + ib - sb, rc = oc + ic - sc;
+  for (int i = beg; i < end; i++) {
+    const int va = a[i], vb = b[i], vc = c[i];
+    a[i] = ra;
+    b[i] = rb;
+    c[i] = rc;
+    ra += va;
+    rb += vb;
+    rc += vc;
+  }
+  __syncthreads();
+  return tot;
+}
+
 #define ORBFE_HIP_CHECK(expr)                                     \
   do {                                                            \
     hipError_t _e = (expr);                                       \

@@ -1041,9 +1041,9 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         sx[i] = par ? multi4(c4) : 0;
       }
       __syncthreads();
-      const int T = block_scan_excl(sa, S, misc);
-      const int NP = block_scan_excl(sb, S, misc);
-      const int nexp = block_scan_excl(sx, S, misc);
+      // (sk is free during full passes: its first 12 ints hold the scan's wave sums)
+      const int3 tot3 = block_scan_excl3(sa, sb, sx, S, reinterpret_cast<int*>(sk));
+      const int T = tot3.x, NP = tot3.y, nexp = tot3.z;
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
         if (nd.count > 1) {
@@ -1075,8 +1075,10 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       const int nR = block_scan_excl(sa, S, misc);
       int P2 = 1;
       while (P2 < nR) P2 <<= 1;
-      for (int i = t; i < P2; i += 256) sk[i] = 0ull;
-      __syncthreads();
+      if (nR > 1024) {
+        for (int i = t; i < P2; i += 256) sk[i] = 0ull;
+        __syncthreads();
+      }
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
         if (nd.flags & 2)
@@ -1084,18 +1086,45 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
                       (unsigned long long)i;
       }
       __syncthreads();
-      // bitonic sort, descending: largest (size, creation) first
-      for (int k = 2; k <= P2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
-            const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
-            const unsigned long long x = sk[i], y = sk[ixj];
-            if ((i & k) == 0 ? (x < y) : (x > y)) {
-              sk[i] = y;
-              sk[ixj] = x;
+      if (nR <= 1024) {
+        // rank sort, descending (largest (size, creation) first; the keys are distinct): every
+        // key counts the larger ones with broadcast LDS reads -- two barriers instead of a
+        // bitonic network's log^2
+        unsigned long long kk[4];
+        int rk[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int k = t + 256 * r;
+          kk[r] = k < nR ? sk[k] : 0ull;
+          rk[r] = 0;
+        }
+        const int per = (nR + 255) >> 8;
+        for (int j = 0; j < nR; j++) {
+          const unsigned long long y = sk[j];
+          rk[0] += y > kk[0];
+          if (per > 1) rk[1] += y > kk[1];
+          if (per > 2) rk[2] += y > kk[2];
+          if (per > 3) rk[3] += y > kk[3];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          if (t + 256 * r < nR) sk[rk[r]] = kk[r];
+        __syncthreads();
+      } else {
+        // bitonic sort, descending: largest (size, creation) first
+        for (int k = 2; k <= P2; k <<= 1) {
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
+              const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
+              const unsigned long long x = sk[i], y = sk[ixj];
+              if ((i & k) == 0 ? (x < y) : (x > y)) {
+                sk[i] = y;
+                sk[ixj] = x;
+              }
             }
+            __syncthreads();
           }
-          __syncthreads();
         }
       }
       // child counts of every candidate, in processing order

@@ -1,0 +1,48 @@
+"""bench.py's reporting helpers on CPU: the roofline object carries the contract's keys with
+consistent arithmetic, the committed PMC summary is found for the benchmark workload, and the
+CLI defaults are N=1 with a short run."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+# level geometry of 1241x376 / 8 levels / 1.2 (w, h, ncells per level; other columns unused here)
+GEO = np.array([[1241, 376, 429], [1034, 313, 297], [862, 261, 196], [718, 218, 138],
+                [598, 181, 95], [499, 151, 64], [416, 126, 42], [346, 105, 30]])
+GEO = np.hstack([GEO, np.zeros((8, 4), np.int64)])
+
+
+def test_roofline_object():
+    counts = np.full(64, 2007, np.int32)
+    kt = {"k_fast": (50 * 0.25, 100)}  # 50 steps, 2 launches per step, 0.25 ms per step
+    r = bench.roofline(kt, "k_fast", GEO, counts, 13_000 * 64, 64, 50)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["launches_per_step"] == 2
+    per_step = r["algorithmic_bytes_per_step"]
+    assert abs(r["achieved"] - per_step / 0.25e-3 / 1e9) < 0.05
+    assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-5
+    px = sum(int(w) * int(h) for w, h in GEO[:, :2])
+    assert per_step == 64 * (px + 4 * int(GEO[:, 2].sum())) + 4 * 13_000 * 64
+
+
+def test_committed_pmc_traffic_matches_workload():
+    t, src = bench.pmc_traffic("k_fast", 1241, 376, 32)
+    assert t is not None and t > 0 and "FETCH_SIZE" in src
+    assert bench.pmc_traffic("k_fast", 640, 480, 32) == (None, None)  # other workload: not reported
+
+
+def test_cli_defaults():
+    saved = sys.argv
+    sys.argv = ["bench.py"]
+    try:
+        a = bench.parse()
+    finally:
+        sys.argv = saved
+    assert a.gpus == 1 and 0 < a.steps <= 100 and 0 <= a.warmup <= 20 and a.batch == 32
+    assert a.pipeline == 2
