@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <list>
@@ -1064,5 +1065,125 @@ extern "C" int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* no
   }
   offsets[nodes] = (int32_t)fv.size();
   *n_out = nodes;
+  return ORBFE_OK;
+}
+
+// =============================================================================================
+// Frame::ComputeStereoMatches (src/Frame.cc:522-700), restated. Keypoints are the extractor's
+// output (level-0 coordinates, octave = level); the pyramids are the left / right extractors'
+// mvImagePyramid (ORBextractor.h:100), one row-major view per level.
+extern "C" int orbref_compute_stereo_matches(const orbfe_keypoint* kl, const uint8_t* dl, int nl,
+                                             const orbfe_keypoint* kr, const uint8_t* dr, int nr,
+                                             const orbref_level_view* pyr_l,
+                                             const orbref_level_view* pyr_r, int nlevels,
+                                             const float* scale, const float* inv_scale, float mb,
+                                             float mbf, float* u_right, float* depth) {
+  if ((nl > 0 && (!kl || !dl || !u_right || !depth)) || (nr > 0 && (!kr || !dr)) || !pyr_l ||
+      !pyr_r || !scale || !inv_scale || nlevels <= 0)
+    return ORBFE_ERR_ARG;
+  for (int i = 0; i < nl; i++) u_right[i] = depth[i] = -1.0f;  // :524-525
+  const int thOrbDist = (TH_HIGH + TH_LOW) / 2;                 // :527
+  const int nRows = pyr_l[0].rows;                               // :529
+  // right keypoints into the rows they may match (:532-548)
+  std::vector<std::vector<int>> rows(nRows);
+  for (int iR = 0; iR < nr; iR++) {
+    const float kpY = kr[iR].y;
+    const float r = 2.0f * scale[kr[iR].octave];
+    const int maxr = (int)std::ceil(kpY + r);
+    const int minr = (int)std::floor(kpY - r);
+    for (int yi = minr; yi <= maxr; yi++)
+      if (yi >= 0 && yi < nRows) rows[yi].push_back(iR);  // (the reference indexes unchecked)
+  }
+  const float minZ = mb, minD = 0, maxD = mbf / minZ;  // :551-553
+  std::vector<std::pair<int, int>> dist_idx;
+  for (int iL = 0; iL < nl; iL++) {
+    const orbfe_keypoint& kpL = kl[iL];
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    if (!(vL >= 0.0f) || vL >= (float)nRows) continue;  // (out of the table: UB in the reference)
+    const std::vector<int>& cand = rows[(size_t)vL];  // :567 (float row -> index, truncation)
+    if (cand.empty()) continue;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) continue;
+    int bestDist = TH_HIGH;
+    int bestIdxR = 0;
+    for (int iR : cand) {  // :586-606
+      const orbfe_keypoint& kpR = kr[iR];
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = hamming32(dl + (size_t)iL * 32, dr + (size_t)iR * 32);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdxR = iR;
+        }
+      }
+    }
+    if (bestDist >= thOrbDist) continue;  // :609
+    // sub-pixel match by correlation (:611-672): 11x11 SAD of centred windows over 11 shifts.
+    // The window values are integers, so the reference's float L1 norm is an exact integer.
+    const float uR0 = kr[bestIdxR].x;
+    const float sf = inv_scale[kpL.octave];
+    const float scaleduL = std::round(kpL.x * sf);
+    const float scaledvL = std::round(kpL.y * sf);
+    const float scaleduR0 = std::round(uR0 * sf);
+    const int w = 5, L = 5;
+    const orbref_level_view& PL = pyr_l[kpL.octave];
+    const orbref_level_view& PR = pyr_r[kpL.octave];
+    const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
+    const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
+    if (iniu < 0 || endu >= PR.cols) continue;  // :633-635
+    // windows the reference's rowRange/colRange would reject with a cv::Exception; extractor
+    // keypoints lie >= 16 px inside their level, so these never fire on operator() output
+    if (yL - w < 0 || yL + w >= PL.rows || yL + w >= PR.rows || xL - w < 0 || xL + w >= PL.cols ||
+        xR0 - L - w < 0)
+      continue;
+    const int cL = PL.data[(size_t)yL * PL.stride + xL];
+    int best_sad = INT_MAX, bestincR = 0;
+    float vDists[2 * L + 1];
+    for (int incR = -L; incR <= L; incR++) {
+      const int xc = xR0 + incR;
+      const int cR = PR.data[(size_t)yL * PR.stride + xc];
+      int sad = 0;
+      for (int dy = -w; dy <= w; dy++)
+        for (int dx = -w; dx <= w; dx++) {
+          const int a = (int)PL.data[(size_t)(yL + dy) * PL.stride + xL + dx] - cL;
+          const int b = (int)PR.data[(size_t)(yL + dy) * PR.stride + xc + dx] - cR;
+          sad += std::abs(a - b);
+        }
+      if ((float)sad < (float)best_sad) {  // float dist < int bestDist (:645)
+        best_sad = sad;
+        bestincR = incR;
+      }
+      vDists[L + incR] = (float)sad;
+    }
+    if (bestincR == -L || bestincR == L) continue;  // :654-655
+    const float dist1 = vDists[L + bestincR - 1], dist2 = vDists[L + bestincR],
+                dist3 = vDists[L + bestincR + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) continue;  // :663-664
+    float bestuR = scale[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+    float disparity = (uL - bestuR);
+    if (disparity >= minD && disparity < maxD) {  // :671-684
+      if (disparity <= 0) {
+        disparity = 0.01;
+        bestuR = uL - 0.01;
+      }
+      depth[iL] = mbf / disparity;
+      u_right[iL] = bestuR;
+      dist_idx.push_back(std::make_pair(best_sad, iL));
+    }
+  }
+  // outlier rejection against the median SAD (:686-699; the reference indexes an empty vector
+  // when nothing matched -- here nothing is rejected then)
+  if (dist_idx.empty()) return ORBFE_OK;
+  std::sort(dist_idx.begin(), dist_idx.end());
+  const float median = (float)dist_idx[dist_idx.size() / 2].first;
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = (int)dist_idx.size() - 1; i >= 0; i--) {
+    if ((float)dist_idx[i].first < thDist) break;
+    u_right[dist_idx[i].second] = -1;
+    depth[dist_idx[i].second] = -1;
+  }
   return ORBFE_OK;
 }

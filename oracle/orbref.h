@@ -70,6 +70,18 @@ int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* node_desc,
                            const int32_t* first_child, const int32_t* n_children,
                            const float* weights, const uint8_t* desc, int n, int levelsup,
                            uint32_t* node_ids, int32_t* offsets, int32_t* indices, int* n_out);
+/* One pyramid level (ORBextractor::mvImagePyramid[l]): rows x cols bytes, row stride. */
+typedef struct orbref_level_view {
+  const uint8_t* data;
+  int rows, cols, stride;
+} orbref_level_view;
+/* Frame::ComputeStereoMatches (src/Frame.cc:522-700): u_right / depth per left keypoint (-1 when
+ * unmatched). */
+int orbref_compute_stereo_matches(const orbfe_keypoint* kl, const uint8_t* dl, int nl,
+                                  const orbfe_keypoint* kr, const uint8_t* dr, int nr,
+                                  const orbref_level_view* pyr_l, const orbref_level_view* pyr_r,
+                                  int nlevels, const float* scale, const float* inv_scale, float mb,
+                                  float mbf, float* u_right, float* depth);
 /* Frame::AssignFeaturesToGrid as CSR (64 x 48 cells, cell = ix*48 + iy): cell_start[3073]. */
 int orbref_build_grid(const orbfe_frame_view* frame, int32_t* cell_start, int32_t* cell_items);
 

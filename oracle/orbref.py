@@ -60,6 +60,9 @@ def lib(kind: str = "checker") -> ctypes.CDLL:
         L.orbref_search_for_triangulation.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p,
                                                       c_void_p, c_float, c_float, c_int, c_int,
                                                       c_void_p, POINTER(c_int)]
+        L.orbref_compute_stereo_matches.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                                    c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                                    c_void_p, c_float, c_float, c_void_p, c_void_p]
         L.orbref_build_grid.argtypes = [c_void_p, c_void_p, c_void_p]
         L.orbref_vocab_transform.argtypes = [c_int, c_int] + [c_void_p] * 5 + [c_int, c_int] + \
             [c_void_p] * 3 + [POINTER(c_int)]
@@ -230,3 +233,31 @@ def vocab_transform(voc, desc: np.ndarray, levelsup: int):
     assert st == 0
     k = nn.value
     return ids[:k], offs[:k + 1], idx[:offs[k]]
+
+
+class _LevelView(ctypes.Structure):
+    _fields_ = [("data", c_void_p), ("rows", c_int), ("cols", c_int), ("stride", c_int)]
+
+
+def compute_stereo_matches(kl, dl, kr, dr, pyr_l, pyr_r, scale, inv_scale, mb: float, mbf: float):
+    """Frame::ComputeStereoMatches (src/Frame.cc:522-700). kl/kr: KEYPOINT_DTYPE arrays, dl/dr: n x 32
+    uint8, pyr_l/pyr_r: lists of 2-D uint8 level images. Returns (u_right, depth) float32 arrays."""
+    L = lib()
+    kl = np.ascontiguousarray(kl, dtype=KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kr, dtype=KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, dtype=np.uint8)
+    dr = np.ascontiguousarray(dr, dtype=np.uint8)
+    lv = [np.ascontiguousarray(a, dtype=np.uint8) for a in pyr_l]
+    rv = [np.ascontiguousarray(a, dtype=np.uint8) for a in pyr_r]
+    nlev = len(lv)
+    VL = (_LevelView * nlev)(*[_LevelView(a.ctypes.data, a.shape[0], a.shape[1], a.shape[1]) for a in lv])
+    VR = (_LevelView * nlev)(*[_LevelView(a.ctypes.data, a.shape[0], a.shape[1], a.shape[1]) for a in rv])
+    sc = np.ascontiguousarray(scale, dtype=np.float32)
+    isc = np.ascontiguousarray(inv_scale, dtype=np.float32)
+    ur = np.empty(len(kl), np.float32)
+    dep = np.empty(len(kl), np.float32)
+    st = L.orbref_compute_stereo_matches(_p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr), VL, VR, nlev,
+                                         _p(sc), _p(isc), mb, mbf, _p(ur), _p(dep))
+    if st != 0:
+        raise RuntimeError(f"orbref_compute_stereo_matches failed ({st})")
+    return ur, dep

@@ -1,4 +1,5 @@
-"""ctypes binding of liborbfe.so (include/orbfe.h, orbfe_match_batch.h, orbfe_debug.h, orbfe_synth.h).
+"""ctypes binding of liborbfe.so (include/orbfe.h, orbfe_match_batch.h, orbfe_debug.h, orbfe_synth.h,
+orbfe_vocab.h, orbfe_stereo.h).
 
 The shared library is the product: every compute call below runs the HIP kernels in it. There is
 no CPU fallback -- if the library is missing, or no HIP device is present when a compute handle is
@@ -133,6 +134,15 @@ _SIGNATURES = {
     "orbfe_vocab_transform_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p,
                                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                                    c_int, c_void_p]),
+    "orbfe_compute_stereo_matches_batch_device": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p,
+                                                          c_void_p, c_void_p, c_int, c_float,
+                                                          c_float, c_void_p, c_void_p, c_void_p]),
+    "orbfe_compute_stereo_matches": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_int, c_float, c_float, c_void_p,
+                                             c_void_p]),
+    "orbfe_stereo_frame": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_size_t, c_float,
+                                   c_float, c_void_p, c_void_p, POINTER(c_int), c_void_p, c_void_p,
+                                   POINTER(c_int), c_int, c_void_p, c_void_p]),
     "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
 }
 

@@ -36,6 +36,7 @@
 #include "../../include/orbfe_debug.h"
 #include "orb_pattern31.inc"
 #include "orbfe_device.h"
+#include "orbfe_internal.h"
 
 // ---------------------------------------------------------------------------------------------
 // errors
@@ -1556,6 +1557,8 @@ struct orbfe_extractor {
   std::vector<KernelTimer> pending;
   std::vector<hipEvent_t> event_pool;
   double ktime[8] = {0};
+  // Frame::ComputeStereoMatches scratch (orbfe_stereo.hip)
+  OrbfeStereoScratch* stereo = nullptr;
   int klaunch[8] = {0};
 };
 
@@ -2123,6 +2126,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (!h) return ORBFE_OK;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  orbfe_internal_stereo_free(h->stereo);
   free_batch(h);
   hipFree(h->d_levels);
   hipFree(h->d_cells);
@@ -2315,6 +2319,35 @@ extern "C" int orbfe_get_level_device(orbfe_extractor* h, int image, int level,
   *step = (size_t)d.pitch;
   return ORBFE_OK;
 }
+
+int orbfe_internal_pyramid(orbfe_extractor* h, OrbfePyramid* out) {
+  if (!h || !out) return ORBFE_ERR_ARG;
+  if (!h->last_img0 || h->last_n <= 0)
+    return orbfe_set_error(ORBFE_ERR_STATE, "no extract call on this handle yet");
+  if (h->nlevels > ORBFE_MAX_LEVELS) return orbfe_set_error(ORBFE_ERR_ARG, "too many levels");
+  out->base = h->d_pyr;
+  out->image_stride = h->pyr_stride;
+  out->n_images = h->last_n;
+  out->nlevels = h->nlevels;
+  for (int l = 0; l < h->nlevels; l++) {
+    const LevelDesc& d = h->levels[l];
+    out->w[l] = d.w;
+    out->h[l] = d.h;
+    out->pitch[l] = d.pitch;
+    out->off[l] = d.pyr_off;
+    out->scale[l] = h->scale[l];
+    out->inv_scale[l] = h->inv_scale[l];
+  }
+  out->total_key_slots = h->total_key_slots;
+  out->io_kps = h->d_kps;
+  out->io_desc = h->d_desc;
+  out->io_counts = h->d_counts;
+  out->stream = h->stream;
+  out->device = h->device;
+  return ORBFE_OK;
+}
+
+OrbfeStereoScratch** orbfe_internal_stereo_slot(orbfe_extractor* h) { return &h->stereo; }
 
 extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p,
                                int* rows, int* cols, size_t* step) {

@@ -1,0 +1,514 @@
+// orbfe_stereo.hip -- Frame::ComputeStereoMatches (src/Frame.cc:522-700) for gfx950.
+//
+// Three launches per batch of rectified pairs, all reading the pyramids and keypoints the
+// extractor left resident in HBM:
+//   k_stereo_rows    one block per pair: counting sort of the right keypoints by floor(y) into
+//                    row buckets (CSR) with each keypoint's packed row span (Frame.cc:532-548).
+//   k_stereo_match   16 lanes per left keypoint: the Hamming search over the row band
+//                    (:557-607), then the 11x11 SAD sweep over 11 shifts -- lane = window row --
+//                    and the parabola fit / disparity test (:609-684).
+//   k_stereo_median  one block per pair: radix-select of the median SAD and the 2.1x-median
+//                    rejection (:686-699).
+// The reference's row table lists, for row v, the right keypoints whose [floor(y-r), ceil(y+r)]
+// span covers v, in iR order, and keeps the first minimum. Here the candidates of row v are the
+// bucket range of rows v-rb..v+rb filtered by that exact span test, and ties are broken by the
+// smallest iR -- the same winner.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbfe.h"
+#include "../../include/orbfe_stereo.h"
+#include "orbfe_device.h"
+#include "orbfe_internal.h"
+
+namespace {
+
+constexpr int ST_W = 5;   // half window (Frame.cc:617)
+constexpr int ST_L = 5;   // half shift range (:627)
+constexpr int ST_TH_ORB = (100 + 50) / 2;  // thOrbDist = (TH_HIGH + TH_LOW) / 2 (:527)
+constexpr int ST_ROWS_MAX = 16000;         // LDS row histogram bound
+
+struct StereoGeom {
+  const uint8_t* pyr;
+  long long image_stride;
+  int left0, right0, cap, nlevels, rows0, rb;
+  float mbf, maxD;
+  int w[ORBFE_MAX_LEVELS], pitch[ORBFE_MAX_LEVELS];
+  int h[ORBFE_MAX_LEVELS];
+  long long off[ORBFE_MAX_LEVELS];
+  float scale[ORBFE_MAX_LEVELS], inv_scale[ORBFE_MAX_LEVELS];
+};
+
+// ---- k_stereo_rows ----------------------------------------------------------------------------
+// Bucket entry: {x bits, (minr & 0xffff) | maxr << 16, octave, iR}; minr/maxr as Frame.cc:543-544.
+__global__ __launch_bounds__(256) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
+                                                     const int32_t* __restrict__ counts,
+                                                     int32_t* __restrict__ row_start,
+                                                     uint4* __restrict__ buckets) {
+  extern __shared__ int s_hist[];  // rows0 + 1 counters, then 16 ints of scan scratch
+  int* wsum = s_hist + g.rows0 + 1;
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int img = g.right0 + p;
+  const int nR = min(counts[img], g.cap);
+  const orbfe_keypoint* K = kps + (long long)img * g.cap;
+  for (int r = t; r <= g.rows0; r += 256) s_hist[r] = 0;
+  __syncthreads();
+  for (int i = t; i < nR; i += 256) {
+    const int b = min(max((int)floorf(K[i].y), 0), g.rows0 - 1);
+    atomicAdd(&s_hist[b], 1);
+  }
+  __syncthreads();
+  block_scan_excl(s_hist, g.rows0 + 1, wsum);
+  int32_t* rs = row_start + (long long)p * (g.rows0 + 1);
+  for (int r = t; r <= g.rows0; r += 256) rs[r] = s_hist[r];
+  __syncthreads();
+  uint4* B = buckets + (long long)p * g.cap;
+  for (int i = t; i < nR; i += 256) {
+    const orbfe_keypoint kp = K[i];
+    const int b = min(max((int)floorf(kp.y), 0), g.rows0 - 1);
+    const int slot = atomicAdd(&s_hist[b], 1);
+    const float r = 2.0f * g.scale[kp.octave];
+    const int maxr = (int)ceilf(kp.y + r);
+    const int minr = (int)floorf(kp.y - r);
+    B[slot] = make_uint4(__float_as_uint(kp.x), ((unsigned)minr & 0xffffu) | ((unsigned)maxr << 16),
+                         (unsigned)kp.octave, (unsigned)i);
+  }
+}
+
+// ---- k_stereo_match ---------------------------------------------------------------------------
+__device__ __forceinline__ int group16_sum(int v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+__device__ __forceinline__ unsigned long long group16_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    const unsigned long long w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int byte_at(const uint32_t* a, int k) { return (a[k >> 2] >> (8 * (k & 3))) & 255; }
+
+__global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
+                                                      const uint8_t* __restrict__ desc,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int32_t* __restrict__ row_start,
+                                                      const uint4* __restrict__ buckets,
+                                                      float* __restrict__ u_right, float* __restrict__ depth,
+                                                      int32_t* __restrict__ sad_out) {
+  const int2 blk = xcd_block2d();
+  const int p = blk.y;
+  const int j = threadIdx.x & 15;
+  const int i = blk.x * 16 + (threadIdx.x >> 4);
+  const int imgL = g.left0 + p, imgR = g.right0 + p;
+  const int nL = min(counts[imgL], g.cap);
+  if (i >= nL) return;  // whole 16-lane group leaves together; no barriers below
+  const orbfe_keypoint kpL = kps[(long long)imgL * g.cap + i];
+  const long long o = (long long)p * g.cap + i;
+  float ur_out = -1.0f, dep_out = -1.0f;
+  int sad_best = -1;
+  const float vL = kpL.y, uL = kpL.x;
+  const int levelL = kpL.octave;
+  const float minU = uL - g.maxD, maxU = uL - 0.0f;  // minD = 0 (:552-575)
+  if (vL >= 0.0f && vL < (float)g.rows0 && !(maxU < 0)) {
+    const int v = (int)vL;
+    const int lo = max(0, v - g.rb), hi = min(g.rows0 - 1, v + g.rb);
+    const int32_t* rs = row_start + (long long)p * (g.rows0 + 1);
+    const int beg = rs[lo], end = rs[hi + 1];
+    uint4 dl0, dl1;
+    load_desc(desc + ((long long)imgL * g.cap + i) * 32, dl0, dl1);
+    const uint4* B = buckets + (long long)p * g.cap;
+    const uint8_t* DR = desc + (long long)imgR * g.cap * 32;
+    unsigned long long best = ~0ull;
+    for (int k = beg + j; k < end; k += 16) {
+      const uint4 e = B[k];
+      const int minr = (int)(int16_t)(e.y & 0xffffu), maxr = (int)e.y >> 16;
+      const int oct = (int)e.z;
+      const float uR = __uint_as_float(e.x);
+      if (v >= minr && v <= maxr && oct >= levelL - 1 && oct <= levelL + 1 && uR >= minU && uR <= maxU) {
+        uint4 d0, d1;
+        load_desc(DR + (long long)e.w * 32, d0, d1);
+        const int dist = hamming256(dl0, dl1, d0, d1);
+        if (dist < 100) {  // bestDist starts at TH_HIGH (:578)
+          const unsigned long long key = ((unsigned long long)dist << 32) | e.w;
+          best = key < best ? key : best;
+        }
+      }
+    }
+    best = group16_min_u64(best);
+    const int bestDist = best == ~0ull ? 100 : (int)(best >> 32);
+    if (bestDist < ST_TH_ORB) {
+      const int iR = (int)(best & 0xffffffffu);
+      const float uR0 = kps[(long long)imgR * g.cap + iR].x;
+      const float sf = g.inv_scale[levelL];
+      const float scaleduL = roundf(kpL.x * sf);
+      const float scaledvL = roundf(kpL.y * sf);
+      const float scaleduR0 = roundf(uR0 * sf);
+      const float iniu = scaleduR0 + ST_L - ST_W;
+      const float endu = scaleduR0 + ST_L + ST_W + 1;
+      const int yL = (int)scaledvL, xL = (int)scaleduL, xR0 = (int)scaleduR0;
+      const int cols = g.w[levelL], rows = g.h[levelL];
+      // :633-635, plus the windows OpenCV's rowRange/colRange would reject (never on extractor
+      // output; the oracle skips them the same way)
+      const bool ok = !(iniu < 0 || endu >= cols) && yL - ST_W >= 0 && yL + ST_W < rows &&
+                      xL - ST_W >= 0 && xL + ST_W < cols && xR0 - ST_L - ST_W >= 0;
+      if (ok) {
+        const int row = yL + min(j, 2 * ST_W) - ST_W;
+        const uint8_t* pl = g.pyr + (long long)imgL * g.image_stride + g.off[levelL] +
+                            (long long)row * g.pitch[levelL] + (xL - ST_W);
+        const uint8_t* pr = g.pyr + (long long)imgR * g.image_stride + g.off[levelL] +
+                            (long long)row * g.pitch[levelL] + (xR0 - ST_L - ST_W);
+        // dword loads from the aligned-down address; v_alignbyte to the window start
+        const uint32_t* ql = reinterpret_cast<const uint32_t*>((uintptr_t)pl & ~(uintptr_t)3);
+        const uint32_t* qr = reinterpret_cast<const uint32_t*>((uintptr_t)pr & ~(uintptr_t)3);
+        const int sl = (int)((uintptr_t)pl & 3), sr = (int)((uintptr_t)pr & 3);
+        uint32_t wl[4], wr[7], al[3], ar[6];
+#pragma unroll
+        for (int k = 0; k < 4; k++) wl[k] = ql[k];
+#pragma unroll
+        for (int k = 0; k < 7; k++) wr[k] = qr[k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) al[k] = __builtin_amdgcn_alignbyte(wl[k + 1], wl[k], sl);
+#pragma unroll
+        for (int k = 0; k < 6; k++) ar[k] = __builtin_amdgcn_alignbyte(wr[k + 1], wr[k], sr);
+        // window centres (row yL = lane 5 of the group): IL(w,w) and IR(w,w) of each shift
+        const int src = (threadIdx.x & 63 & ~15) + ST_W;
+        const int cL = __shfl(byte_at(al, ST_W), src, 64);
+        int sums[2 * ST_L + 1];
+#pragma unroll
+        for (int s = 0; s < 2 * ST_L + 1; s++) {
+          const int cR = __shfl(byte_at(ar, s + ST_W), src, 64);
+          int acc = 0;
+#pragma unroll
+          for (int dx = 0; dx < 2 * ST_W + 1; dx++)
+            acc += abs((byte_at(al, dx) - cL) - (byte_at(ar, s + dx) - cR));
+          sums[s] = group16_sum(j <= 2 * ST_W ? acc : 0);
+        }
+        // cv::norm(NORM_L1) of integer-valued windows is exact; strict < keeps the first minimum
+        int best_sad = 0x7fffffff, bestinc = 0;
+#pragma unroll
+        for (int s = 0; s < 2 * ST_L + 1; s++)
+          if ((float)sums[s] < (float)best_sad) {
+            best_sad = sums[s];
+            bestinc = s - ST_L;
+          }
+        if (bestinc != -ST_L && bestinc != ST_L) {
+          float d1 = 0, d2 = 0, d3 = 0;
+#pragma unroll
+          for (int s = 1; s < 2 * ST_L; s++)
+            if (s == bestinc + ST_L) {
+              d1 = (float)sums[s - 1];
+              d2 = (float)sums[s];
+              d3 = (float)sums[s + 1];
+            }
+          const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));  // :661
+          if (!(deltaR < -1 || deltaR > 1)) {
+            float bestuR = g.scale[levelL] * ((float)scaleduR0 + (float)bestinc + deltaR);
+            float disparity = uL - bestuR;
+            if (disparity >= 0.0f && disparity < g.maxD) {
+              if (disparity <= 0) {
+                disparity = (float)0.01;
+                bestuR = (float)((double)uL - 0.01);
+              }
+              dep_out = g.mbf / disparity;
+              ur_out = bestuR;
+              sad_best = best_sad;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (j == 0) {
+    u_right[o] = ur_out;
+    depth[o] = dep_out;
+    sad_out[o] = sad_best;
+  }
+}
+
+// ---- k_stereo_median ---------------------------------------------------------------------------
+// median = the (M/2)-th smallest SAD of the M matches (:686-688); SADs are < 2^16 (121 * 510), so
+// two 8-bit radix-select passes find it. Every match with SAD >= 1.5*1.4*median is dropped.
+__global__ __launch_bounds__(256) void k_stereo_median(int left0, int cap, const int32_t* __restrict__ counts,
+                                                       const int32_t* __restrict__ sad_in,
+                                                       float* __restrict__ u_right, float* __restrict__ depth) {
+  __shared__ int hist[256];
+  __shared__ int s_sel[3];
+  const int p = blockIdx.x, t = threadIdx.x;
+  const int nL = min(counts[left0 + p], cap);
+  const int32_t* S = sad_in + (long long)p * cap;
+  if (t < 3) s_sel[t] = 0;
+  hist[t] = 0;
+  __syncthreads();
+  int m = 0;
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0) {
+      m++;
+      atomicAdd(&hist[(s >> 8) & 255], 1);
+    }
+  }
+  m = wave_sum(m);
+  if (lane_id() == 0) atomicAdd(&s_sel[0], m);
+  __syncthreads();
+  const int M = s_sel[0];
+  if (M == 0) return;  // the reference indexes an empty vector here; nothing is rejected
+  if (t == 0) {
+    int k = M / 2, b = 0;
+    while (k >= hist[b]) k -= hist[b++];
+    s_sel[1] = b;
+    s_sel[2] = k;
+  }
+  __syncthreads();
+  const int hb = s_sel[1];
+  hist[t] = 0;
+  __syncthreads();
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0 && ((s >> 8) & 255) == hb && (s >> 16) == 0) atomicAdd(&hist[s & 255], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int k = s_sel[2], b = 0;
+    while (k >= hist[b]) k -= hist[b++];
+    s_sel[1] = (hb << 8) | b;
+  }
+  __syncthreads();
+  const float median = (float)s_sel[1];
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0 && !((float)s < thDist)) {
+      u_right[(long long)p * cap + i] = -1.0f;
+      depth[(long long)p * cap + i] = -1.0f;
+    }
+  }
+}
+
+}  // namespace
+
+// ---- scratch owned by the extractor handle ------------------------------------------------------
+struct OrbfeStereoScratch {
+  int32_t* d_row_start = nullptr;
+  size_t row_start_n = 0;
+  uint4* d_buckets = nullptr;
+  int32_t* d_sad = nullptr;
+  size_t slots_n = 0;
+  // host-buffer entry points
+  orbfe_keypoint* d_kps = nullptr;
+  uint8_t* d_desc = nullptr;
+  int32_t* d_counts = nullptr;
+  float* d_out = nullptr;
+  size_t io_n = 0;
+  uint8_t* h_stage = nullptr;
+  size_t h_stage_n = 0;
+};
+
+void orbfe_internal_stereo_free(OrbfeStereoScratch* s) {
+  if (!s) return;
+  hipFree(s->d_row_start);
+  hipFree(s->d_buckets);
+  hipFree(s->d_sad);
+  hipFree(s->d_kps);
+  hipFree(s->d_desc);
+  hipFree(s->d_counts);
+  hipFree(s->d_out);
+  if (s->h_stage) hipHostFree(s->h_stage);
+  delete s;
+}
+
+static OrbfeStereoScratch* scratch_of(orbfe_extractor* h) {
+  OrbfeStereoScratch** slot = orbfe_internal_stereo_slot(h);
+  if (!*slot) *slot = new OrbfeStereoScratch();
+  return *slot;
+}
+
+extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int n_pairs, int left0,
+                                                         int right0, const orbfe_keypoint* d_kps,
+                                                         const uint8_t* d_desc, const int32_t* d_counts,
+                                                         int cap, float mbf, float mb, float* d_u_right,
+                                                         float* d_depth, void* stream) {
+  if (!h || n_pairs < 0 || cap <= 0 || !d_kps || !d_desc || !d_counts || !d_u_right || !d_depth)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_compute_stereo_matches_batch_device: bad argument");
+  if (n_pairs == 0) return ORBFE_OK;
+  OrbfePyramid P;
+  int st = orbfe_internal_pyramid(h, &P);
+  if (st != ORBFE_OK) return st;
+  if (left0 < 0 || right0 < 0 || left0 + n_pairs > P.n_images || right0 + n_pairs > P.n_images)
+    return orbfe_set_error(ORBFE_ERR_ARG, "stereo pair images outside the last extract call");
+  if (cap < P.total_key_slots) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
+  if (P.h[0] > ST_ROWS_MAX) return orbfe_set_error(ORBFE_ERR_ARG, "image taller than the stereo row table");
+  hipSetDevice(P.device);
+  OrbfeStereoScratch* S = scratch_of(h);
+  const size_t rs_n = (size_t)n_pairs * (P.h[0] + 1), sl_n = (size_t)n_pairs * cap;
+  if (rs_n > S->row_start_n) {
+    hipFree(S->d_row_start);
+    S->d_row_start = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_row_start, rs_n * sizeof(int32_t)));
+    S->row_start_n = rs_n;
+  }
+  if (sl_n > S->slots_n) {
+    hipFree(S->d_buckets);
+    hipFree(S->d_sad);
+    S->d_buckets = nullptr;
+    S->d_sad = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_buckets, sl_n * sizeof(uint4)));
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_sad, sl_n * sizeof(int32_t)));
+    S->slots_n = sl_n;
+  }
+  StereoGeom g;
+  std::memset(&g, 0, sizeof(g));
+  g.pyr = P.base;
+  g.image_stride = P.image_stride;
+  g.left0 = left0;
+  g.right0 = right0;
+  g.cap = cap;
+  g.nlevels = P.nlevels;
+  g.rows0 = P.h[0];
+  g.mbf = mbf;
+  const float minZ = mb;
+  g.maxD = mbf / minZ;  // :553
+  float rmax = 0.0f;
+  for (int l = 0; l < P.nlevels; l++) {
+    g.w[l] = P.w[l];
+    g.h[l] = P.h[l];
+    g.pitch[l] = P.pitch[l];
+    g.off[l] = P.off[l];
+    g.scale[l] = P.scale[l];
+    g.inv_scale[l] = P.inv_scale[l];
+    rmax = std::max(rmax, 2.0f * P.scale[l]);
+  }
+  g.rb = (int)std::ceil(rmax) + 3;  // bucket rows that can hold a keypoint whose span covers v
+  hipStream_t s = stream ? (hipStream_t)stream : P.stream;
+  const size_t lds = sizeof(int) * (g.rows0 + 1 + 16);
+  hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(256), lds, s, g, d_kps, d_counts,
+                     S->d_row_start, S->d_buckets);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
+                     d_counts, S->d_row_start, S->d_buckets, d_u_right, d_depth, S->d_sad);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(256), 0, s, left0, cap, d_counts, S->d_sad,
+                     d_u_right, d_depth);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  return ORBFE_OK;
+}
+
+static int ensure_io(OrbfeStereoScratch* S, size_t slots) {
+  if (slots > S->io_n) {
+    hipFree(S->d_kps);
+    hipFree(S->d_desc);
+    hipFree(S->d_counts);
+    hipFree(S->d_out);
+    if (S->h_stage) hipHostFree(S->h_stage);
+    S->d_kps = nullptr;
+    S->d_desc = nullptr;
+    S->d_counts = nullptr;
+    S->d_out = nullptr;
+    S->h_stage = nullptr;
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_kps, 2 * slots * sizeof(orbfe_keypoint)));
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_desc, 2 * slots * 32));
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_counts, 2 * sizeof(int32_t)));
+    ORBFE_HIP_CHECK(hipMalloc(&S->d_out, 2 * slots * sizeof(float)));
+    ORBFE_HIP_CHECK(hipHostMalloc(&S->h_stage, 2 * slots * (sizeof(orbfe_keypoint) + 32 + sizeof(float)) + 64));
+    S->io_n = slots;
+  }
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_compute_stereo_matches(orbfe_extractor* h, const orbfe_keypoint* kps_l,
+                                            const uint8_t* desc_l, int n_l, const orbfe_keypoint* kps_r,
+                                            const uint8_t* desc_r, int n_r, float mbf, float mb,
+                                            float* u_right, float* depth) {
+  if (!h || n_l < 0 || n_r < 0 || (n_l > 0 && (!kps_l || !desc_l || !u_right || !depth)) ||
+      (n_r > 0 && (!kps_r || !desc_r)))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_compute_stereo_matches: bad argument");
+  if (n_l == 0) return ORBFE_OK;
+  OrbfePyramid P;
+  int st = orbfe_internal_pyramid(h, &P);
+  if (st != ORBFE_OK) return st;
+  if (P.n_images < 2) return orbfe_set_error(ORBFE_ERR_STATE, "the last extract call held no stereo pair");
+  hipSetDevice(P.device);
+  const int cap = std::max(P.total_key_slots, std::max(n_l, n_r));
+  OrbfeStereoScratch* S = scratch_of(h);
+  st = ensure_io(S, (size_t)cap);
+  if (st != ORBFE_OK) return st;
+  // stage both keypoint / descriptor sets (image 0 = left, image 1 = right) in one H2D burst each
+  orbfe_keypoint* hk = reinterpret_cast<orbfe_keypoint*>(S->h_stage);
+  uint8_t* hd = S->h_stage + 2 * (size_t)cap * sizeof(orbfe_keypoint);
+  std::memcpy(hk, kps_l, sizeof(orbfe_keypoint) * n_l);
+  if (n_r) std::memcpy(hk + cap, kps_r, sizeof(orbfe_keypoint) * n_r);
+  std::memcpy(hd, desc_l, (size_t)n_l * 32);
+  if (n_r) std::memcpy(hd + (size_t)cap * 32, desc_r, (size_t)n_r * 32);
+  int32_t* hc = reinterpret_cast<int32_t*>(hd + 2 * (size_t)cap * 32);
+  hc[0] = n_l;
+  hc[1] = n_r;
+  hipStream_t s = P.stream;
+  ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_kps, hk, 2 * (size_t)cap * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_desc, hd, 2 * (size_t)cap * 32, hipMemcpyHostToDevice, s));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_counts, hc, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(s));  // hc is reused for the results below
+  st = orbfe_compute_stereo_matches_batch_device(h, 1, 0, 1, S->d_kps, S->d_desc, S->d_counts, cap, mbf, mb,
+                                                 S->d_out, S->d_out + cap, s);
+  if (st != ORBFE_OK) return st;
+  float* ho = reinterpret_cast<float*>(hk);
+  ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * n_l, hipMemcpyDeviceToHost, s));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(ho + n_l, S->d_out + cap, sizeof(float) * n_l, hipMemcpyDeviceToHost, s));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(s));
+  std::memcpy(u_right, ho, sizeof(float) * n_l);
+  std::memcpy(depth, ho + n_l, sizeof(float) * n_l);
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const uint8_t* right, int rows,
+                                  int cols, size_t step, float mbf, float mb, orbfe_keypoint* kps_l,
+                                  uint8_t* desc_l, int* n_l, orbfe_keypoint* kps_r, uint8_t* desc_r, int* n_r,
+                                  int cap, float* u_right, float* depth) {
+  if (!h || !left || !right || !n_l || !n_r)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stereo_frame: bad argument");
+  *n_l = *n_r = 0;
+  if (rows == 0 || cols == 0) return ORBFE_OK;  // N = 0: the constructor returns early (:120-121)
+  const int K = orbfe_max_keypoints(h, rows, cols);
+  if (K < 0) return K;
+  if (cap < K) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
+  if (!kps_l || !desc_l || !kps_r || !desc_r || !u_right || !depth)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stereo_frame: null output buffer");
+  // ExtractORB(0) and ExtractORB(1) as one batch (:113-116); the results stay on the device
+  const uint8_t* imgs[2] = {left, right};
+  std::vector<orbfe_keypoint> k2(2 * (size_t)K);
+  std::vector<uint8_t> d2(2 * (size_t)K * 32);
+  int32_t counts[2] = {0, 0};
+  int st = orbfe_extract_batch(h, 2, imgs, rows, cols, step, k2.data(), d2.data(), K, counts);
+  if (st != ORBFE_OK) return st;
+  *n_l = counts[0];
+  *n_r = counts[1];
+  std::memcpy(kps_l, k2.data(), sizeof(orbfe_keypoint) * counts[0]);
+  std::memcpy(desc_l, d2.data(), (size_t)counts[0] * 32);
+  std::memcpy(kps_r, k2.data() + K, sizeof(orbfe_keypoint) * counts[1]);
+  std::memcpy(desc_r, d2.data() + (size_t)K * 32, (size_t)counts[1] * 32);
+  if (counts[0] == 0) return ORBFE_OK;
+  OrbfePyramid P;
+  st = orbfe_internal_pyramid(h, &P);
+  if (st != ORBFE_OK) return st;
+  OrbfeStereoScratch* S = scratch_of(h);
+  st = ensure_io(S, (size_t)K);
+  if (st != ORBFE_OK) return st;
+  st = orbfe_compute_stereo_matches_batch_device(h, 1, 0, 1, P.io_kps, P.io_desc, P.io_counts, K, mbf, mb,
+                                                 S->d_out, S->d_out + K, P.stream);
+  if (st != ORBFE_OK) return st;
+  float* ho = reinterpret_cast<float*>(S->h_stage);
+  ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * counts[0], hipMemcpyDeviceToHost, P.stream));
+  ORBFE_HIP_CHECK(hipMemcpyAsync(ho + counts[0], S->d_out + K, sizeof(float) * counts[0], hipMemcpyDeviceToHost,
+                                 P.stream));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(P.stream));
+  std::memcpy(u_right, ho, sizeof(float) * counts[0]);
+  std::memcpy(depth, ho + counts[0], sizeof(float) * counts[0]);
+  return ORBFE_OK;
+}

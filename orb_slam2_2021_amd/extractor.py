@@ -151,6 +151,66 @@ class ORBextractor:
             c_void_p(stream or 0)), "orbfe_extract_batch_device")
         self._last_shape = (rows, cols)
 
+    # ---- Frame::ComputeStereoMatches (src/Frame.cc:522-700) -------------------------------
+    def compute_stereo_matches(self, kps_l: KeyPoints, desc_l: np.ndarray, kps_r: KeyPoints,
+                               desc_r: np.ndarray, mbf: float, mb: float
+                               ) -> Tuple[np.ndarray, np.ndarray]:
+        """(mvuRight, mvDepth) of the left keypoints against the right ones, on the pyramids of
+        images 0 (left) and 1 (right) of the last extract call (e.g. extract_batch([l, r])).
+        mb: the reference uses the Frame's mb before assigning it (Frame.cc:125 vs :149); pass
+        mbf / fx, or 0 for an unbounded disparity range."""
+        kl = np.ascontiguousarray(kps_l, L.KEYPOINT_DTYPE)
+        kr = np.ascontiguousarray(kps_r, L.KEYPOINT_DTYPE)
+        dl = np.ascontiguousarray(desc_l if desc_l is not None else np.zeros((0, 32)), np.uint8)
+        dr = np.ascontiguousarray(desc_r if desc_r is not None else np.zeros((0, 32)), np.uint8)
+        n = len(kl)
+        ur = np.full(n, -1.0, np.float32)
+        dep = np.full(n, -1.0, np.float32)
+        L.check(self._lib.orbfe_compute_stereo_matches(
+            self._h, L.ptr(kl), L.ptr(dl), n, L.ptr(kr), L.ptr(dr), len(kr), float(mbf), float(mb),
+            L.ptr(ur), L.ptr(dep)), "orbfe_compute_stereo_matches")
+        return ur, dep
+
+    def stereo_frame(self, left: np.ndarray, right: np.ndarray, mbf: float, mb: float):
+        """The stereo Frame constructor's hot path (Frame.cc:113-125): ExtractORB(0, left),
+        ExtractORB(1, right), ComputeStereoMatches. Returns (kps_l, desc_l, kps_r, desc_r,
+        u_right, depth)."""
+        l = np.ascontiguousarray(np.asarray(left, np.uint8))
+        r = np.ascontiguousarray(np.asarray(right, np.uint8))
+        if l.shape != r.shape or l.ndim != 2:
+            raise ValueError("stereo_frame needs two same-shaped CV_8UC1 images")
+        rows, cols = l.shape
+        if l.size == 0:
+            e = np.zeros(0, L.KEYPOINT_DTYPE)
+            return e, None, e.copy(), None, np.zeros(0, np.float32), np.zeros(0, np.float32)
+        cap = self.max_keypoints(rows, cols)
+        kl = np.zeros(cap, L.KEYPOINT_DTYPE)
+        kr = np.zeros(cap, L.KEYPOINT_DTYPE)
+        dl = np.zeros((cap, 32), np.uint8)
+        dr = np.zeros((cap, 32), np.uint8)
+        ur = np.zeros(cap, np.float32)
+        dep = np.zeros(cap, np.float32)
+        nl, nr = c_int(), c_int()
+        L.check(self._lib.orbfe_stereo_frame(self._h, L.ptr(l), L.ptr(r), rows, cols, c_size_t(cols),
+                                             float(mbf), float(mb), L.ptr(kl), L.ptr(dl), byref(nl),
+                                             L.ptr(kr), L.ptr(dr), byref(nr), cap, L.ptr(ur),
+                                             L.ptr(dep)), "orbfe_stereo_frame")
+        self._last_shape = (rows, cols)
+        a, b = nl.value, nr.value
+        return (kl[:a].copy(), dl[:a].copy() if a else None, kr[:b].copy(),
+                dr[:b].copy() if b else None, ur[:a].copy(), dep[:a].copy())
+
+    def compute_stereo_matches_batch_device(self, n_pairs: int, left0: int, right0: int, d_kps: int,
+                                            d_desc: int, d_counts: int, cap: int, mbf: float,
+                                            mb: float, d_u_right: int, d_depth: int,
+                                            stream: Optional[int] = None) -> None:
+        """Device-resident ComputeStereoMatches over pairs (left0 + p, right0 + p) of the last
+        extract_batch_device call; outputs at p*cap + i. Async on `stream`."""
+        L.check(self._lib.orbfe_compute_stereo_matches_batch_device(
+            self._h, int(n_pairs), int(left0), int(right0), c_void_p(d_kps), c_void_p(d_desc),
+            c_void_p(d_counts), int(cap), float(mbf), float(mb), c_void_p(d_u_right),
+            c_void_p(d_depth), c_void_p(stream or 0)), "orbfe_compute_stereo_matches_batch_device")
+
     @property
     def stream(self) -> int:
         return self._lib.orbfe_extractor_stream(self._h) or 0
