@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--pipeline", type=int, default=2,
                    help="output sets in flight: 2 overlaps a step's matching with the next step's "
                         "extraction (1: strictly one step at a time)")
+    p.add_argument("--stereo", action="store_true",
+                   help="run Frame::ComputeStereoMatches on every pair after extraction (the stereo "
+                        "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
     p.add_argument("--banded-pyramid", action="store_true",
                    help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
     return p.parse_args()
@@ -120,6 +123,8 @@ def main():
             self.nodes = torch.zeros(n_img, dtype=torch.int32, device=dev)
             self.m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
             self.nm = torch.zeros(B, dtype=torch.int32, device=dev)
+            self.ur = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
+            self.dep = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
             self.matcher = ORBmatcher(0.6, False, device=dev.index)  # LocalMapping.cc:219
             self.pairs = (L.sft_pair * B)()
             for i in range(B):
@@ -142,7 +147,9 @@ def main():
             v = L.frame_view()
             v.n = 0  # read on the device from cnt[i]
             v.keys_un = self.kps.data_ptr() + i * cap * 28
-            v.u_right = d_ur.data_ptr() + i * cap * 4
+            # left keyframes take mvuRight from ComputeStereoMatches when it runs (--stereo)
+            v.u_right = (self.ur.data_ptr() + i * cap * 4 if args.stereo and i < B
+                         else d_ur.data_ptr() + i * cap * 4)
             v.descriptors = self.desc.data_ptr() + i * cap * 32
             v.mp_state = d_mp.data_ptr() + i * cap
             v.nlevels = 8
@@ -167,7 +174,7 @@ def main():
     lib = L.lib()
     gather = world > 1 and not args.no_gather
 
-    ev = {k: [] for k in ("k_vocab", "k_sft")}
+    ev = {k: [] for k in ("k_vocab", "k_sft", "k_stereo")}
     ev_sel = set()  # which of the two non-extractor kernels get events in this pass
     stream = torch.cuda.Stream(dev)   # extraction
     mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
@@ -179,6 +186,18 @@ def main():
         stream.wait_event(o.matched)  # the matching that last read this set is done
         ext.extract_batch_device(n_img, d_img.data_ptr(), H * W, H, W, W, o.kps.data_ptr(),
                                  o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=stream.cuda_stream)
+        if args.stereo:  # Frame.cc:125, on the extraction stream while the pyramids are current
+            if "k_stereo" in ev_sel:
+                s0 = torch.cuda.Event(enable_timing=True)
+                s0.record(stream)
+            ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
+                                                    o.cnt.data_ptr(), cap, cam["bf"], float(dummy.mb),
+                                                    o.ur.data_ptr(), o.dep.data_ptr(),
+                                                    stream=stream.cuda_stream)
+            if "k_stereo" in ev_sel:
+                s1 = torch.cuda.Event(enable_timing=True)
+                s1.record(stream)
+                ev["k_stereo"].append((s0, s1))
         o.extracted.record(stream)
         mstream.wait_event(o.extracted)
         ms = mstream.cuda_stream
@@ -208,7 +227,7 @@ def main():
 
     def kernel_times():
         kt = ext.kernel_times()
-        for k in ("k_vocab", "k_sft"):
+        for k in ("k_vocab", "k_sft", "k_stereo"):
             if ev[k]:
                 kt[k] = (sum(a.elapsed_time(b) for a, b in ev[k]), len(ev[k]))
         return {k: v for k, v in kt.items() if v[1] > 0}
@@ -229,7 +248,7 @@ def main():
     probe_steps = max(3, min(args.steps, 10))
     ext.reset_kernel_times()
     ext.set_profiling(True)
-    ev_sel.update(("k_vocab", "k_sft"))
+    ev_sel.update(("k_vocab", "k_sft", "k_stereo"))
     for _ in range(probe_steps):
         step()
     torch.cuda.synchronize()
@@ -238,6 +257,7 @@ def main():
     ev_sel.clear()
     ev["k_vocab"].clear()
     ev["k_sft"].clear()
+    ev["k_stereo"].clear()
     dominant = max(probe, key=lambda k: probe[k][0])
     # timed region: events only around the dominant kernel's launches
     ext.reset_kernel_times()
@@ -288,7 +308,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded KITTI-shaped stereo frames, orbfe_synth_frame; synthetic vocabulary)",
         "config": {
-            "workload": f"C3: stereo extract + SearchForTriangulation, {W}x{H}, batch {B} stereo frames/GPU"
+            "workload": f"C3: stereo extract + "
+                        + ("ComputeStereoMatches + " if args.stereo else "")
+                        + f"SearchForTriangulation, {W}x{H}, batch {B} stereo frames/GPU"
                         + (" + RCCL gather to rank 0 (C4)" if gather else ""),
             "nfeatures": args.nfeatures, "scale_factor": 1.2, "nlevels": 8, "ini_th_fast": 20,
             "min_th_fast": 7, "stereo_frames_per_gpu_per_step": B, "images_per_step_per_gpu": n_img,
@@ -305,6 +327,8 @@ def main():
         "kernels_ms_per_step": {k: round(v[0] / probe_steps, 4) for k, v in probe.items()},
         "keypoints_per_image": round(float(counts.mean()), 1),
         "sft_matches_per_pair": round(float(nm.mean()), 1),
+        "stereo_matches_per_pair": (round(float((sets[0].ur >= 0).sum().item()) / B, 1)
+                                    if args.stereo else None),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
@@ -312,7 +336,8 @@ def main():
         if not args.no_legs:
             out["legs"] = {"c5_search_by_projection": sbp_leg(args)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey)
+        out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey,
+                                           float(dummy.mb))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -337,7 +362,9 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, steps):
       k_describe 4 B in + 60 B out per keypoint (+ 749 + 512 gathered bytes per keypoint, not
                  counted: they overlap between keypoints and come from L2)
       k_vocab    32 B in + 12 B out per descriptor
-      k_sft      per pair 2 N (32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out"""
+      k_sft      per pair 2 N (32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out
+      k_stereo   per pair 2 N (28 + 32) B + 2 x 16 B per right keypoint (buckets) + 12 B per left
+                 keypoint (the 11x11 windows and candidate descriptors come from L2)"""
     px = level_pixels(geo)
     ncells = int(geo[:, 2].sum())
     nkp = int(counts.sum())
@@ -351,6 +378,9 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, steps):
         "k_pyramid": n_img * (2 * px[0] + sum(px[1:])),
         "k_vocab": 44 * nkp,
         "k_sft": 64 * nkp + 4 * nkp // 2,
+        # ComputeStereoMatches (3 launches): both sides' keypoints + descriptors, right-keypoint
+        # buckets written and read (16 B), u_right / depth / SAD out (12 B per left keypoint)
+        "k_stereo": 60 * nkp + 32 * nkp // 2 + 12 * nkp // 2,
     }
     total_ms, launches = kt[dom]
     per_launch_steps = max(launches // max(steps, 1), 1)  # launches per step
@@ -441,13 +471,15 @@ def host_boundary_rate(ext, host, reps=5):
             "what": f"orbfe_extract_batch on {len(imgs)} host images (extract only, H2D + D2H included)"}
 
 
-def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey):
+def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey, mb):
     """The oracle built with the reference's flags (-O3 -march=native, CMakeLists.txt:10-11) timed
-    on one host core: extract left + right, then SearchForTriangulation(left, right), per stereo
-    frame, for about --cpu-seconds (the vocabulary descent is left out of the CPU timing)."""
+    on one host core: extract left + right (+ ComputeStereoMatches with --stereo), then
+    SearchForTriangulation(left, right), per stereo frame, for about --cpu-seconds (the vocabulary
+    descent is left out of the CPU timing)."""
     from oracle import orbref
     from orb_slam2_2021_amd import synthetic as S
     ref = orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native")
+    ref_r = orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native")
     tab = ref.tables()
     rng = np.random.default_rng(5)
     t_total, frames = 0.0, 0
@@ -455,8 +487,15 @@ def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey):
         l, r = host[frames % B], host[B + frames % B]
         t0 = time.perf_counter()
         k1, d1 = ref(l)
-        k2, d2 = ref(r)
+        k2, d2 = ref_r(r)
         t1 = time.perf_counter()
+        if args.stereo:  # ComputeStereoMatches on the two extractors' pyramids (copies untimed)
+            lv = [ref.level(i) for i in range(8)]
+            rv = [ref_r.level(i) for i in range(8)]
+            ts = time.perf_counter()
+            orbref.compute_stereo_matches(k1, d1, k2, d2, lv, rv, tab["scale"], tab["inv_scale"],
+                                          mb, cam["bf"], kind="native")
+            t1 += time.perf_counter() - ts
         F1 = S.make_frame(k1, d1, tab["scale"], tab["sigma2"], H, W, cam, rng)
         F2 = S.make_frame(k2, d2, tab["scale"], tab["sigma2"], H, W, cam, rng)
         F1.feat_vec = tree.feature_vector(d1, 0)
@@ -478,7 +517,8 @@ def cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey):
         pass
     return {"value": round(frames / t_total, 3), "unit": "stereo frames/s", "cores": 1,
             "kind": "port",
-            "sample": f"{frames} stereo frames (cycling the step's {B}) {W}x{H} (2 x ORBextractor + SearchForTriangulation) on "
+            "sample": f"{frames} stereo frames (cycling the step's {B}) {W}x{H} (2 x ORBextractor + "
+                      + ("ComputeStereoMatches + " if args.stereo else "") + "SearchForTriangulation) on "
                       f"1 thread of {cpu}; oracle built -O3 -march=native",
             "seconds": round(t_total, 2)}
 

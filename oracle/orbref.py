@@ -239,10 +239,11 @@ class _LevelView(ctypes.Structure):
     _fields_ = [("data", c_void_p), ("rows", c_int), ("cols", c_int), ("stride", c_int)]
 
 
-def compute_stereo_matches(kl, dl, kr, dr, pyr_l, pyr_r, scale, inv_scale, mb: float, mbf: float):
+def compute_stereo_matches(kl, dl, kr, dr, pyr_l, pyr_r, scale, inv_scale, mb: float, mbf: float,
+                           kind: str = "checker"):
     """Frame::ComputeStereoMatches (src/Frame.cc:522-700). kl/kr: KEYPOINT_DTYPE arrays, dl/dr: n x 32
     uint8, pyr_l/pyr_r: lists of 2-D uint8 level images. Returns (u_right, depth) float32 arrays."""
-    L = lib()
+    L = lib(kind)
     kl = np.ascontiguousarray(kl, dtype=KEYPOINT_DTYPE)
     kr = np.ascontiguousarray(kr, dtype=KEYPOINT_DTYPE)
     dl = np.ascontiguousarray(dl, dtype=np.uint8)

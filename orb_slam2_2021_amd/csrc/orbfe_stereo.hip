@@ -10,8 +10,9 @@
 //   k_stereo_median  one block per pair: radix-select of the median SAD and the 2.1x-median
 //                    rejection (:686-699).
 // The reference's row table lists, for row v, the right keypoints whose [floor(y-r), ceil(y+r)]
-// span covers v, in iR order, and keeps the first minimum. Here the candidates of row v are the
-// bucket range of rows v-rb..v+rb filtered by that exact span test, and ties are broken by the
+// span covers v, in iR order, and keeps the first minimum. Here right keypoints are bucketed by
+// (octave, floor(y)); the candidates of a level-L keypoint on row v are the bucket rows of octaves
+// L-1..L+1 within each octave's band, filtered by that exact span test, and ties are broken by the
 // smallest iR -- the same winner.
 #include <hip/hip_runtime.h>
 
@@ -30,47 +31,51 @@ namespace {
 constexpr int ST_W = 5;   // half window (Frame.cc:617)
 constexpr int ST_L = 5;   // half shift range (:627)
 constexpr int ST_TH_ORB = (100 + 50) / 2;  // thOrbDist = (TH_HIGH + TH_LOW) / 2 (:527)
-constexpr int ST_ROWS_MAX = 16000;         // LDS row histogram bound
+constexpr int ST_TAB_MAX = 16384;          // LDS bucket table bound (ints)
 
 struct StereoGeom {
   const uint8_t* pyr;
   long long image_stride;
-  int left0, right0, cap, nlevels, rows0, rb;
+  int left0, right0, cap, nlevels, rows0;
+  int nbk;  // octave buckets: nlevels (bucket per octave and row) or 1 (per row only)
   float mbf, maxD;
   int w[ORBFE_MAX_LEVELS], pitch[ORBFE_MAX_LEVELS];
   int h[ORBFE_MAX_LEVELS];
+  int rbo[ORBFE_MAX_LEVELS];  // row band of each octave bucket (see launch code)
   long long off[ORBFE_MAX_LEVELS];
   float scale[ORBFE_MAX_LEVELS], inv_scale[ORBFE_MAX_LEVELS];
 };
 
 // ---- k_stereo_rows ----------------------------------------------------------------------------
-// Bucket entry: {x bits, (minr & 0xffff) | maxr << 16, octave, iR}; minr/maxr as Frame.cc:543-544.
+// Counting sort of pair p's right keypoints into buckets (octave, floor(y)); bucket entry
+// {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544.
 __global__ __launch_bounds__(256) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
                                                      const int32_t* __restrict__ counts,
                                                      int32_t* __restrict__ row_start,
                                                      uint4* __restrict__ buckets) {
-  extern __shared__ int s_hist[];  // rows0 + 1 counters, then 16 ints of scan scratch
-  int* wsum = s_hist + g.rows0 + 1;
+  extern __shared__ int s_hist[];  // nbk*(rows0+1) counters, then 16 ints of scan scratch
+  const int ntab = g.nbk * (g.rows0 + 1);
+  int* wsum = s_hist + ntab;
   const int p = blockIdx.x, t = threadIdx.x;
   const int img = g.right0 + p;
   const int nR = min(counts[img], g.cap);
   const orbfe_keypoint* K = kps + (long long)img * g.cap;
-  for (int r = t; r <= g.rows0; r += 256) s_hist[r] = 0;
+  for (int r = t; r < ntab; r += 256) s_hist[r] = 0;
   __syncthreads();
-  for (int i = t; i < nR; i += 256) {
-    const int b = min(max((int)floorf(K[i].y), 0), g.rows0 - 1);
-    atomicAdd(&s_hist[b], 1);
-  }
+  auto bucket = [&](const orbfe_keypoint& kp) {
+    const int row = min(max((int)floorf(kp.y), 0), g.rows0 - 1);
+    return (g.nbk > 1 ? kp.octave * (g.rows0 + 1) : 0) + row;
+  };
+  for (int i = t; i < nR; i += 256) atomicAdd(&s_hist[bucket(K[i])], 1);
   __syncthreads();
-  block_scan_excl(s_hist, g.rows0 + 1, wsum);
-  int32_t* rs = row_start + (long long)p * (g.rows0 + 1);
-  for (int r = t; r <= g.rows0; r += 256) rs[r] = s_hist[r];
+  block_scan_excl(s_hist, ntab, wsum);
+  int32_t* rs = row_start + (long long)p * ntab;
+  for (int r = t; r < ntab; r += 256) rs[r] = s_hist[r];
   __syncthreads();
   uint4* B = buckets + (long long)p * g.cap;
   for (int i = t; i < nR; i += 256) {
     const orbfe_keypoint kp = K[i];
-    const int b = min(max((int)floorf(kp.y), 0), g.rows0 - 1);
-    const int slot = atomicAdd(&s_hist[b], 1);
+    const int slot = atomicAdd(&s_hist[bucket(kp)], 1);
     const float r = 2.0f * g.scale[kp.octave];
     const int maxr = (int)ceilf(kp.y + r);
     const int minr = (int)floorf(kp.y - r);
@@ -80,12 +85,16 @@ __global__ __launch_bounds__(256) void k_stereo_rows(StereoGeom g, const orbfe_k
 }
 
 // ---- k_stereo_match ---------------------------------------------------------------------------
-__device__ __forceinline__ int group16_sum(int v) {
-  v += __shfl_xor(v, 8, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 1, 64);
+// DPP within the 16-lane row that holds one keypoint
+__device__ __forceinline__ unsigned row_sum16(unsigned v) {
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);  // row_ror:2
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);  // row_ror:1
   return v;
+}
+__device__ __forceinline__ unsigned row_bcast5(unsigned v) {  // lane 5 of the row to all 16
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x155, 0xf, 0xf, false);  // row_newbcast:5
 }
 __device__ __forceinline__ unsigned long long group16_min_u64(unsigned long long v) {
 #pragma unroll
@@ -95,7 +104,15 @@ __device__ __forceinline__ unsigned long long group16_min_u64(unsigned long long
   }
   return v;
 }
-__device__ __forceinline__ int byte_at(const uint32_t* a, int k) { return (a[k >> 2] >> (8 * (k & 3))) & 255; }
+__device__ __forceinline__ unsigned byte_at(const uint32_t* a, int k) { return (a[k >> 2] >> (8 * (k & 3))) & 255u; }
+// u16 pair (byte k, byte k+1) of a little-endian byte string held in dwords
+__device__ __forceinline__ unsigned pair_at(const uint32_t* a, int k) {
+  const int w = k >> 2, b = k & 3;
+  if (b == 0) return __builtin_amdgcn_perm(0u, a[w], 0x0c010c00u);
+  if (b == 1) return __builtin_amdgcn_perm(0u, a[w], 0x0c020c01u);
+  if (b == 2) return __builtin_amdgcn_perm(0u, a[w], 0x0c030c02u);
+  return __builtin_amdgcn_perm(a[w + 1], a[w], 0x0c040c03u);
+}
 
 __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
                                                       const uint8_t* __restrict__ desc,
@@ -120,16 +137,34 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
   const float minU = uL - g.maxD, maxU = uL - 0.0f;  // minD = 0 (:552-575)
   if (vL >= 0.0f && vL < (float)g.rows0 && !(maxU < 0)) {
     const int v = (int)vL;
-    const int lo = max(0, v - g.rb), hi = min(g.rows0 - 1, v + g.rb);
-    const int32_t* rs = row_start + (long long)p * (g.rows0 + 1);
-    const int beg = rs[lo], end = rs[hi + 1];
+    // candidate ranges: the bucket rows of octaves levelL-1..levelL+1 that can hold a right
+    // keypoint whose row span covers v (one range of all octaves when nbk == 1)
+    const int ntab = g.nbk * (g.rows0 + 1);
+    const int32_t* rs = row_start + (long long)p * ntab;
+    int b0 = 0, n0 = 0, b1 = 0, n1 = 0, b2 = 0, n2 = 0;
+    auto range = [&](int ob, int& b, int& n) {
+      const int rb = g.rbo[ob];
+      const int lo = max(0, v - rb), hi = min(g.rows0 - 1, v + rb);
+      const int base = ob * (g.rows0 + 1);
+      b = rs[base + lo];
+      n = rs[base + hi + 1] - b;
+    };
+    if (g.nbk > 1) {
+      if (levelL - 1 >= 0) range(levelL - 1, b0, n0);
+      range(levelL, b1, n1);
+      if (levelL + 1 < g.nlevels) range(levelL + 1, b2, n2);
+    } else {
+      range(0, b1, n1);
+    }
     uint4 dl0, dl1;
     load_desc(desc + ((long long)imgL * g.cap + i) * 32, dl0, dl1);
     const uint4* B = buckets + (long long)p * g.cap;
     const uint8_t* DR = desc + (long long)imgR * g.cap * 32;
     unsigned long long best = ~0ull;
-    for (int k = beg + j; k < end; k += 16) {
-      const uint4 e = B[k];
+    const int total = n0 + n1 + n2;
+    for (int k = j; k < total; k += 16) {
+      const int idx = k < n0 ? b0 + k : (k < n0 + n1 ? b1 + (k - n0) : b2 + (k - n0 - n1));
+      const uint4 e = B[idx];
       const int minr = (int)(int16_t)(e.y & 0xffffu), maxr = (int)e.y >> 16;
       const int oct = (int)e.z;
       const float uR = __uint_as_float(e.x);
@@ -137,7 +172,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
         uint4 d0, d1;
         load_desc(DR + (long long)e.w * 32, d0, d1);
         const int dist = hamming256(dl0, dl1, d0, d1);
-        if (dist < 100) {  // bestDist starts at TH_HIGH (:578)
+        if (dist < 100) {  // bestDist starts at TH_HIGH (:578); ties: smallest iR (first in :586)
           const unsigned long long key = ((unsigned long long)dist << 32) | e.w;
           best = key < best ? key : best;
         }
@@ -161,43 +196,63 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
       const bool ok = !(iniu < 0 || endu >= cols) && yL - ST_W >= 0 && yL + ST_W < rows &&
                       xL - ST_W >= 0 && xL + ST_W < cols && xR0 - ST_L - ST_W >= 0;
       if (ok) {
+        // lane j = window row j (lanes 11..15 re-read row 10 and contribute nothing)
         const int row = yL + min(j, 2 * ST_W) - ST_W;
         const uint8_t* pl = g.pyr + (long long)imgL * g.image_stride + g.off[levelL] +
                             (long long)row * g.pitch[levelL] + (xL - ST_W);
         const uint8_t* pr = g.pyr + (long long)imgR * g.image_stride + g.off[levelL] +
                             (long long)row * g.pitch[levelL] + (xR0 - ST_L - ST_W);
-        // dword loads from the aligned-down address; v_alignbyte to the window start
         const uint32_t* ql = reinterpret_cast<const uint32_t*>((uintptr_t)pl & ~(uintptr_t)3);
         const uint32_t* qr = reinterpret_cast<const uint32_t*>((uintptr_t)pr & ~(uintptr_t)3);
         const int sl = (int)((uintptr_t)pl & 3), sr = (int)((uintptr_t)pr & 3);
-        uint32_t wl[4], wr[7], al[3], ar[6];
+        uint32_t wl[4], wr[7], al[4], ar[7];
 #pragma unroll
         for (int k = 0; k < 4; k++) wl[k] = ql[k];
 #pragma unroll
         for (int k = 0; k < 7; k++) wr[k] = qr[k];
 #pragma unroll
         for (int k = 0; k < 3; k++) al[k] = __builtin_amdgcn_alignbyte(wl[k + 1], wl[k], sl);
+        al[3] = 0;
 #pragma unroll
         for (int k = 0; k < 6; k++) ar[k] = __builtin_amdgcn_alignbyte(wr[k + 1], wr[k], sr);
-        // window centres (row yL = lane 5 of the group): IL(w,w) and IR(w,w) of each shift
-        const int src = (threadIdx.x & 63 & ~15) + ST_W;
-        const int cL = __shfl(byte_at(al, ST_W), src, 64);
-        int sums[2 * ST_L + 1];
+        ar[6] = 0;
+        // |(IL - IL(w,w)) - (IR - IR(w,w))| = |(IL + IR(w,w)) - (IR + IL(w,w))|, all terms in
+        // [0, 510]: packed u16 pairs through v_sad_u16 (2 columns per instruction)
+        const unsigned cL = row_bcast5(byte_at(al, ST_W));
+        const unsigned cL2 = cL | (cL << 16);
+        unsigned Lp[6];
+#pragma unroll
+        for (int k = 0; k < 5; k++) Lp[k] = pair_at(al, 2 * k);
+        Lp[5] = byte_at(al, 10);  // column 10 alone (hi half 0)
+        unsigned Bp[21];           // Bp[c] = (IR[c] + cL, IR[c+1] + cL), c = 0..20
+#pragma unroll
+        for (int c = 0; c < 21; c++) Bp[c] = pair_at(ar, c) + cL2;
+        unsigned acc[2 * ST_L + 1];
 #pragma unroll
         for (int s = 0; s < 2 * ST_L + 1; s++) {
-          const int cR = __shfl(byte_at(ar, s + ST_W), src, 64);
-          int acc = 0;
+          const unsigned cR = row_bcast5(byte_at(ar, s + ST_W));
+          const unsigned cR2 = cR | (cR << 16);
+          unsigned a = 0;
 #pragma unroll
-          for (int dx = 0; dx < 2 * ST_W + 1; dx++)
-            acc += abs((byte_at(al, dx) - cL) - (byte_at(ar, s + dx) - cR));
-          sums[s] = group16_sum(j <= 2 * ST_W ? acc : 0);
+          for (int k = 0; k < 5; k++) a = __builtin_amdgcn_sad_u16(Lp[k] + cR2, Bp[s + 2 * k], a);
+          a = __builtin_amdgcn_sad_u16(Lp[5] + cR, Bp[s + 10] & 0xffffu, a);
+          acc[s] = j <= 2 * ST_W ? a : 0u;
         }
+        // per-shift totals (< 2^16: 121 * 510) two to a dword, summed over the 16 lanes
+        unsigned tot[2 * ST_L + 1];
+#pragma unroll
+        for (int t2 = 0; t2 < ST_L; t2++) {
+          const unsigned q = row_sum16(acc[2 * t2] | (acc[2 * t2 + 1] << 16));
+          tot[2 * t2] = q & 0xffffu;
+          tot[2 * t2 + 1] = q >> 16;
+        }
+        tot[2 * ST_L] = row_sum16(acc[2 * ST_L]);
         // cv::norm(NORM_L1) of integer-valued windows is exact; strict < keeps the first minimum
         int best_sad = 0x7fffffff, bestinc = 0;
 #pragma unroll
         for (int s = 0; s < 2 * ST_L + 1; s++)
-          if ((float)sums[s] < (float)best_sad) {
-            best_sad = sums[s];
+          if ((float)tot[s] < (float)best_sad) {
+            best_sad = (int)tot[s];
             bestinc = s - ST_L;
           }
         if (bestinc != -ST_L && bestinc != ST_L) {
@@ -205,9 +260,9 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
 #pragma unroll
           for (int s = 1; s < 2 * ST_L; s++)
             if (s == bestinc + ST_L) {
-              d1 = (float)sums[s - 1];
-              d2 = (float)sums[s];
-              d3 = (float)sums[s + 1];
+              d1 = (float)tot[s - 1];
+              d2 = (float)tot[s];
+              d3 = (float)tot[s + 1];
             }
           const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));  // :661
           if (!(deltaR < -1 || deltaR > 1)) {
@@ -237,15 +292,37 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
 // ---- k_stereo_median ---------------------------------------------------------------------------
 // median = the (M/2)-th smallest SAD of the M matches (:686-688); SADs are < 2^16 (121 * 510), so
 // two 8-bit radix-select passes find it. Every match with SAD >= 1.5*1.4*median is dropped.
+__device__ __forceinline__ void select_bin(const int* hist, int k, int* s_out, int* wsum) {
+  // the bin b with prefix(b) <= k < prefix(b+1): block-wide inclusive scan of 256 bins
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int hv = hist[t];
+  int inc = hv;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  for (int q = 0; q < w; q++) inc += wsum[q];
+  const int exc = inc - hv;
+  if (exc <= k && k < inc) {
+    s_out[0] = t;
+    s_out[1] = k - exc;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_stereo_median(int left0, int cap, const int32_t* __restrict__ counts,
                                                        const int32_t* __restrict__ sad_in,
                                                        float* __restrict__ u_right, float* __restrict__ depth) {
   __shared__ int hist[256];
+  __shared__ int wsum[4];
   __shared__ int s_sel[3];
   const int p = blockIdx.x, t = threadIdx.x;
   const int nL = min(counts[left0 + p], cap);
   const int32_t* S = sad_in + (long long)p * cap;
-  if (t < 3) s_sel[t] = 0;
+  if (t == 0) s_sel[2] = 0;
   hist[t] = 0;
   __syncthreads();
   int m = 0;
@@ -257,32 +334,21 @@ __global__ __launch_bounds__(256) void k_stereo_median(int left0, int cap, const
     }
   }
   m = wave_sum(m);
-  if (lane_id() == 0) atomicAdd(&s_sel[0], m);
+  if (lane_id() == 0) atomicAdd(&s_sel[2], m);
   __syncthreads();
-  const int M = s_sel[0];
+  const int M = s_sel[2];
   if (M == 0) return;  // the reference indexes an empty vector here; nothing is rejected
-  if (t == 0) {
-    int k = M / 2, b = 0;
-    while (k >= hist[b]) k -= hist[b++];
-    s_sel[1] = b;
-    s_sel[2] = k;
-  }
-  __syncthreads();
-  const int hb = s_sel[1];
+  select_bin(hist, M / 2, s_sel, wsum);
+  const int hb = s_sel[0], k2 = s_sel[1];
   hist[t] = 0;
   __syncthreads();
   for (int i = t; i < nL; i += 256) {
     const int s = S[i];
-    if (s >= 0 && ((s >> 8) & 255) == hb && (s >> 16) == 0) atomicAdd(&hist[s & 255], 1);
+    if (s >= 0 && (s >> 8) == hb) atomicAdd(&hist[s & 255], 1);
   }
   __syncthreads();
-  if (t == 0) {
-    int k = s_sel[2], b = 0;
-    while (k >= hist[b]) k -= hist[b++];
-    s_sel[1] = (hb << 8) | b;
-  }
-  __syncthreads();
-  const float median = (float)s_sel[1];
+  select_bin(hist, k2, s_sel, wsum);
+  const float median = (float)((hb << 8) | s_sel[0]);
   const float thDist = 1.5f * 1.4f * median;
   for (int i = t; i < nL; i += 256) {
     const int s = S[i];
@@ -345,10 +411,9 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
   if (left0 < 0 || right0 < 0 || left0 + n_pairs > P.n_images || right0 + n_pairs > P.n_images)
     return orbfe_set_error(ORBFE_ERR_ARG, "stereo pair images outside the last extract call");
   if (cap < P.total_key_slots) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
-  if (P.h[0] > ST_ROWS_MAX) return orbfe_set_error(ORBFE_ERR_ARG, "image taller than the stereo row table");
   hipSetDevice(P.device);
   OrbfeStereoScratch* S = scratch_of(h);
-  const size_t rs_n = (size_t)n_pairs * (P.h[0] + 1), sl_n = (size_t)n_pairs * cap;
+  const size_t rs_n = (size_t)n_pairs * P.nlevels * (P.h[0] + 1), sl_n = (size_t)n_pairs * cap;
   if (rs_n > S->row_start_n) {
     hipFree(S->d_row_start);
     S->d_row_start = nullptr;
@@ -376,7 +441,6 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
   g.mbf = mbf;
   const float minZ = mb;
   g.maxD = mbf / minZ;  // :553
-  float rmax = 0.0f;
   for (int l = 0; l < P.nlevels; l++) {
     g.w[l] = P.w[l];
     g.h[l] = P.h[l];
@@ -384,11 +448,21 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
     g.off[l] = P.off[l];
     g.scale[l] = P.scale[l];
     g.inv_scale[l] = P.inv_scale[l];
-    rmax = std::max(rmax, 2.0f * P.scale[l]);
   }
-  g.rb = (int)std::ceil(rmax) + 3;  // bucket rows that can hold a keypoint whose span covers v
+  // Row band of a bucket: a right keypoint at row floor(y) = b of octave o covers v only if
+  // floor(y - r) <= v <= ceil(y + r), r = 2 scale[o] (:541-544), i.e. |b - v| <= ceil(r) + 1;
+  // one more row absorbs the float rounding of y -+ r.
+  g.nbk = P.nlevels * (g.rows0 + 1) <= ST_TAB_MAX ? P.nlevels : 1;
+  if (g.nbk == 1 && g.rows0 + 1 > ST_TAB_MAX)
+    return orbfe_set_error(ORBFE_ERR_ARG, "image taller than the stereo row table");
+  int rb_all = 0;
+  for (int l = 0; l < P.nlevels; l++) {
+    g.rbo[l] = (int)std::ceil(2.0f * P.scale[l]) + 2;
+    rb_all = std::max(rb_all, g.rbo[l]);
+  }
+  if (g.nbk == 1) g.rbo[0] = rb_all;
   hipStream_t s = stream ? (hipStream_t)stream : P.stream;
-  const size_t lds = sizeof(int) * (g.rows0 + 1 + 16);
+  const size_t lds = sizeof(int) * (g.nbk * (g.rows0 + 1) + 16);
   hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(256), lds, s, g, d_kps, d_counts,
                      S->d_row_start, S->d_buckets);
   ORBFE_HIP_CHECK(hipGetLastError());
