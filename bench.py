@@ -334,7 +334,9 @@ def main():
     if rank == 0 and world == 1:
         out["host_boundary"] = host_boundary_rate(ext, host)
         if not args.no_legs:
-            out["legs"] = {"c5_search_by_projection": sbp_leg(args)}
+            out["legs"] = {"c5_search_by_projection": sbp_leg(args),
+                           "compute_stereo_matches": stereo_leg(args, ext, d_img, host, B, H, W, cap,
+                                                                cam["bf"], float(dummy.mb))}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(host, B, H, W, args, tree, cam, F12, ex, ey,
                                            float(dummy.mb))
@@ -453,6 +455,82 @@ def sbp_leg(args, m_points=50000, reps=20):
         out["cpu_oracle_ms_per_frame"] = round(1e3 * (time.perf_counter() - t0), 3)
         out["cpu_matches_equal"] = bool(nr == nm)
     return out
+
+
+def stereo_leg(args, ext, d_img, host, B, H, W, cap, mbf, mb, reps=30):
+    """Secondary measurement (SURVEY 8(f) row 1): Frame::ComputeStereoMatches on the step's B
+    pairs, device-resident, after one extraction of the 2B images (the pyramids it reads stay in
+    HBM). GPU: HIP events around `reps` launches of the 3-kernel sequence on the extraction stream;
+    roofline of that sequence (algorithmic bytes per pair: both sides' keypoints + descriptors,
+    2 x 16 B right-keypoint buckets, 12 B out per left keypoint). CPU: the oracle built with the
+    reference's flags on one core, on the same pairs. Parity: the GPU output of every pair is
+    compared with the oracle run on the GPU's keypoints and pyramid levels."""
+    import torch
+    from oracle import orbref
+    from orb_slam2_2021_amd import _lib as L
+    dev = d_img.device
+    n_img = 2 * B
+    kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
+    desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(n_img, dtype=torch.int32, device=dev)
+    ur = torch.empty(B * cap, dtype=torch.float32, device=dev)
+    dep = torch.empty(B * cap, dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev)
+    s = stream.cuda_stream
+
+    def run():
+        ext.compute_stereo_matches_batch_device(B, 0, B, kps.data_ptr(), desc.data_ptr(),
+                                                cnt.data_ptr(), cap, mbf, mb, ur.data_ptr(),
+                                                dep.data_ptr(), stream=s)
+
+    with torch.cuda.stream(stream):
+        ext.extract_batch_device(n_img, d_img.data_ptr(), H * W, H, W, W, kps.data_ptr(),
+                                 desc.data_ptr(), cap, cnt.data_ptr(), stream=s)
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            run()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    K = kps.cpu().numpy().view(L.KEYPOINT_DTYPE)
+    D = desc.cpu().numpy().reshape(-1, 32)
+    C = cnt.cpu().numpy()
+    UR, DEP = ur.cpu().numpy(), dep.cpu().numpy()
+    matches, same, cpu_s = 0, True, 0.0
+    scale, inv = ext.GetScaleFactors(), ext.GetInverseScaleFactors()
+    for p in range(B):
+        nl, nr = int(C[p]), int(C[B + p])
+        kl, dl = K[p * cap:p * cap + nl], D[p * cap:p * cap + nl]
+        kr, dr = K[(B + p) * cap:(B + p) * cap + nr], D[(B + p) * cap:(B + p) * cap + nr]
+        pl = [ext.level(lv, image=p) for lv in range(ext.nlevels)]
+        pr = [ext.level(lv, image=B + p) for lv in range(ext.nlevels)]
+        t0 = time.perf_counter()
+        wu, wd = orbref.compute_stereo_matches(kl, dl, kr, dr, pl, pr, scale, inv, mb, mbf,
+                                               kind="native")
+        cpu_s += time.perf_counter() - t0
+        gu, gd = UR[p * cap:p * cap + nl], DEP[p * cap:p * cap + nl]
+        same &= bool(np.array_equal(gu.view(np.uint32), wu.view(np.uint32))
+                     and np.array_equal(gd.view(np.uint32), wd.view(np.uint32)))
+        matches += int((gu >= 0).sum())
+    nkp = int(C.sum())
+    algo = 60 * nkp + 32 * nkp // 2 + 12 * nkp // 2  # bytes per launch sequence (B pairs)
+    achieved = algo / (us * 1e-6) / 1e9
+    return {
+        "pairs_per_s": round(B / (us * 1e-6), 1), "us_per_batch": round(us, 2), "batch_pairs": B,
+        "stereo_matches_per_pair": round(matches / B, 1),
+        "parity_all_pairs_bit_exact": same,
+        "roofline": {"kernel": "k_stereo_rows + k_stereo_match + k_stereo_median", "bound": "hbm",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "algorithmic_bytes_per_launch_sequence": algo},
+        "cpu_baseline": {"value": round(B / cpu_s, 1), "unit": "pairs/s", "cores": 1, "kind": "port",
+                         "sample": f"ComputeStereoMatches oracle (-O3 -march=native) on the same {B} "
+                                   f"pairs' keypoints and pyramids, 1 thread"},
+        "what": "device-resident batch after extraction; events around the 3 stereo launches",
+    }
 
 
 def host_boundary_rate(ext, host, reps=5):

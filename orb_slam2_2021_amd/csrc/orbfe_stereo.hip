@@ -2,8 +2,8 @@
 //
 // Three launches per batch of rectified pairs, all reading the pyramids and keypoints the
 // extractor left resident in HBM:
-//   k_stereo_rows    one block per pair: counting sort of the right keypoints by floor(y) into
-//                    row buckets (CSR) with each keypoint's packed row span (Frame.cc:532-548).
+//   k_stereo_rows    one block per pair: counting sort of the right keypoints into (octave,
+//                    floor(y)) buckets (CSR) with each keypoint's packed row span (Frame.cc:532-548).
 //   k_stereo_match   16 lanes per left keypoint: the Hamming search over the row band
 //                    (:557-607), then the 11x11 SAD sweep over 11 shifts -- lane = window row --
 //                    and the parabola fit / disparity test (:609-684).
@@ -47,12 +47,39 @@ struct StereoGeom {
 };
 
 // ---- k_stereo_rows ----------------------------------------------------------------------------
+constexpr int ROWS_THREADS = 1024;
+
+// exclusive scan of data[0..n) in LDS by the ROWS_THREADS threads of the block (wsum: 16 ints)
+__device__ inline void scan_excl_1024(int* data, int n, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int per = (n + ROWS_THREADS - 1) / ROWS_THREADS;
+  const int beg = min(t * per, n), end = min(beg + per, n);
+  int s = 0;
+  for (int i = beg; i < end; i++) s += data[i];
+  int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int run = inc - s;
+  for (int q = 0; q < w; q++) run += wsum[q];
+  for (int i = beg; i < end; i++) {
+    const int v = data[i];
+    data[i] = run;
+    run += v;
+  }
+  __syncthreads();
+}
+
 // Counting sort of pair p's right keypoints into buckets (octave, floor(y)); bucket entry
 // {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544.
-__global__ __launch_bounds__(256) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
-                                                     const int32_t* __restrict__ counts,
-                                                     int32_t* __restrict__ row_start,
-                                                     uint4* __restrict__ buckets) {
+__global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
+                                                              const int32_t* __restrict__ counts,
+                                                              int32_t* __restrict__ row_start,
+                                                              uint4* __restrict__ buckets) {
   extern __shared__ int s_hist[];  // nbk*(rows0+1) counters, then 16 ints of scan scratch
   const int ntab = g.nbk * (g.rows0 + 1);
   int* wsum = s_hist + ntab;
@@ -60,27 +87,98 @@ __global__ __launch_bounds__(256) void k_stereo_rows(StereoGeom g, const orbfe_k
   const int img = g.right0 + p;
   const int nR = min(counts[img], g.cap);
   const orbfe_keypoint* K = kps + (long long)img * g.cap;
-  for (int r = t; r < ntab; r += 256) s_hist[r] = 0;
+  for (int r = t; r < ntab; r += ROWS_THREADS) s_hist[r] = 0;
   __syncthreads();
-  auto bucket = [&](const orbfe_keypoint& kp) {
-    const int row = min(max((int)floorf(kp.y), 0), g.rows0 - 1);
-    return (g.nbk > 1 ? kp.octave * (g.rows0 + 1) : 0) + row;
+  auto bucket = [&](float y, int oct) {
+    const int row = min(max((int)floorf(y), 0), g.rows0 - 1);
+    return (g.nbk > 1 ? oct * (g.rows0 + 1) : 0) + row;
   };
-  for (int i = t; i < nR; i += 256) atomicAdd(&s_hist[bucket(K[i])], 1);
+  for (int i = t; i < nR; i += ROWS_THREADS) atomicAdd(&s_hist[bucket(K[i].y, K[i].octave)], 1);
   __syncthreads();
-  block_scan_excl(s_hist, ntab, wsum);
+  scan_excl_1024(s_hist, ntab, wsum);
   int32_t* rs = row_start + (long long)p * ntab;
-  for (int r = t; r < ntab; r += 256) rs[r] = s_hist[r];
+  for (int r = t; r < ntab; r += ROWS_THREADS) rs[r] = s_hist[r];
   __syncthreads();
   uint4* B = buckets + (long long)p * g.cap;
-  for (int i = t; i < nR; i += 256) {
-    const orbfe_keypoint kp = K[i];
-    const int slot = atomicAdd(&s_hist[bucket(kp)], 1);
-    const float r = 2.0f * g.scale[kp.octave];
-    const int maxr = (int)ceilf(kp.y + r);
-    const int minr = (int)floorf(kp.y - r);
-    B[slot] = make_uint4(__float_as_uint(kp.x), ((unsigned)minr & 0xffffu) | ((unsigned)maxr << 16),
-                         (unsigned)kp.octave, (unsigned)i);
+  for (int i = t; i < nR; i += ROWS_THREADS) {
+    const float x = K[i].x, y = K[i].y;
+    const int oct = K[i].octave;
+    const int slot = atomicAdd(&s_hist[bucket(y, oct)], 1);
+    const float r = 2.0f * g.scale[oct];
+    const int maxr = (int)ceilf(y + r);
+    const int minr = (int)floorf(y - r);
+    B[slot] = make_uint4(__float_as_uint(x), ((unsigned)minr & 0xffffu) | ((unsigned)maxr << 16),
+                         (unsigned)oct, (unsigned)i);
+  }
+}
+
+// ---- median filter ---------------------------------------------------------------------------
+// median = the (M/2)-th smallest SAD of the M matches (:686-688); SADs are < 2^16 (121 * 510), so
+// two 8-bit radix-select passes find it. Every match with SAD >= 1.5*1.4*median is dropped.
+__device__ __forceinline__ void select_bin(const int* hist, int k, int* s_out, int* wsum) {
+  // the bin b with prefix(b) <= k < prefix(b+1): block-wide inclusive scan of 256 bins
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int hv = hist[t];
+  int inc = hv;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  for (int q = 0; q < w; q++) inc += wsum[q];
+  const int exc = inc - hv;
+  if (exc <= k && k < inc) {
+    s_out[0] = t;
+    s_out[1] = k - exc;
+  }
+  __syncthreads();
+}
+
+struct MedianSmem {
+  int hist[256];
+  int wsum[4];
+  int sel[3];
+};
+
+// Runs on the 256 threads of one block over pair p's SADs (sad_in[i] < 0: no match).
+__device__ void median_filter(MedianSmem& sm, int nL, const int32_t* S, float* ur, float* dep) {
+  const int t = threadIdx.x;
+  if (t == 0) sm.sel[2] = 0;
+  sm.hist[t] = 0;
+  __syncthreads();
+  int m = 0;
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0) {
+      m++;
+      atomicAdd(&sm.hist[(s >> 8) & 255], 1);
+    }
+  }
+  m = wave_sum(m);
+  if (lane_id() == 0) atomicAdd(&sm.sel[2], m);
+  __syncthreads();
+  const int M = sm.sel[2];
+  if (M == 0) return;  // the reference indexes an empty vector here; nothing is rejected
+  select_bin(sm.hist, M / 2, sm.sel, sm.wsum);
+  const int hb = sm.sel[0], k2 = sm.sel[1];
+  sm.hist[t] = 0;
+  __syncthreads();
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0 && (s >> 8) == hb) atomicAdd(&sm.hist[s & 255], 1);
+  }
+  __syncthreads();
+  select_bin(sm.hist, k2, sm.sel, sm.wsum);
+  const float median = (float)((hb << 8) | sm.sel[0]);
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = t; i < nL; i += 256) {
+    const int s = S[i];
+    if (s >= 0 && !((float)s < thDist)) {
+      ur[i] = -1.0f;
+      dep[i] = -1.0f;
+    }
   }
 }
 
@@ -114,20 +212,11 @@ __device__ __forceinline__ unsigned pair_at(const uint32_t* a, int k) {
   return __builtin_amdgcn_perm(a[w + 1], a[w], 0x0c040c03u);
 }
 
-__global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
-                                                      const uint8_t* __restrict__ desc,
-                                                      const int32_t* __restrict__ counts,
-                                                      const int32_t* __restrict__ row_start,
-                                                      const uint4* __restrict__ buckets,
-                                                      float* __restrict__ u_right, float* __restrict__ depth,
-                                                      int32_t* __restrict__ sad_out) {
-  const int2 blk = xcd_block2d();
-  const int p = blk.y;
-  const int j = threadIdx.x & 15;
-  const int i = blk.x * 16 + (threadIdx.x >> 4);
-  const int imgL = g.left0 + p, imgR = g.right0 + p;
-  const int nL = min(counts[imgL], g.cap);
-  if (i >= nL) return;  // whole 16-lane group leaves together; no barriers below
+__device__ __forceinline__ void stereo_one(const StereoGeom& g, const orbfe_keypoint* __restrict__ kps,
+                                           const uint8_t* __restrict__ desc, const int32_t* __restrict__ row_start,
+                                           const uint4* __restrict__ buckets, float* __restrict__ u_right,
+                                           float* __restrict__ depth, int32_t* __restrict__ sad_out, int p, int i,
+                                           int j, int imgL, int imgR) {
   const orbfe_keypoint kpL = kps[(long long)imgL * g.cap + i];
   const long long o = (long long)p * g.cap + i;
   float ur_out = -1.0f, dep_out = -1.0f;
@@ -289,74 +378,32 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
   }
 }
 
-// ---- k_stereo_median ---------------------------------------------------------------------------
-// median = the (M/2)-th smallest SAD of the M matches (:686-688); SADs are < 2^16 (121 * 510), so
-// two 8-bit radix-select passes find it. Every match with SAD >= 1.5*1.4*median is dropped.
-__device__ __forceinline__ void select_bin(const int* hist, int k, int* s_out, int* wsum) {
-  // the bin b with prefix(b) <= k < prefix(b+1): block-wide inclusive scan of 256 bins
-  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int hv = hist[t];
-  int inc = hv;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  for (int q = 0; q < w; q++) inc += wsum[q];
-  const int exc = inc - hv;
-  if (exc <= k && k < inc) {
-    s_out[0] = t;
-    s_out[1] = k - exc;
-  }
-  __syncthreads();
+__global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
+                                                      const uint8_t* __restrict__ desc,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int32_t* __restrict__ row_start,
+                                                      const uint4* __restrict__ buckets,
+                                                      float* __restrict__ u_right, float* __restrict__ depth,
+                                                      int32_t* __restrict__ sad_out) {
+  const int2 blk = xcd_block2d();
+  const int p = blk.y;
+  const int j = threadIdx.x & 15;
+  const int i = blk.x * 16 + (threadIdx.x >> 4);
+  const int imgL = g.left0 + p, imgR = g.right0 + p;
+  const int nL = min(counts[imgL], g.cap);
+  if (i < nL) stereo_one(g, kps, desc, row_start, buckets, u_right, depth, sad_out, p, i, j, imgL, imgR);
 }
 
+// One block per pair. (A last-block-done tail in k_stereo_match would save this launch, but on
+// MI355X the agent-scope release/acquire it needs writes back and invalidates the per-XCD L2 in
+// every block: measured 413 us vs 30 + 8 us for the two launches.)
 __global__ __launch_bounds__(256) void k_stereo_median(int left0, int cap, const int32_t* __restrict__ counts,
                                                        const int32_t* __restrict__ sad_in,
                                                        float* __restrict__ u_right, float* __restrict__ depth) {
-  __shared__ int hist[256];
-  __shared__ int wsum[4];
-  __shared__ int s_sel[3];
-  const int p = blockIdx.x, t = threadIdx.x;
-  const int nL = min(counts[left0 + p], cap);
-  const int32_t* S = sad_in + (long long)p * cap;
-  if (t == 0) s_sel[2] = 0;
-  hist[t] = 0;
-  __syncthreads();
-  int m = 0;
-  for (int i = t; i < nL; i += 256) {
-    const int s = S[i];
-    if (s >= 0) {
-      m++;
-      atomicAdd(&hist[(s >> 8) & 255], 1);
-    }
-  }
-  m = wave_sum(m);
-  if (lane_id() == 0) atomicAdd(&s_sel[2], m);
-  __syncthreads();
-  const int M = s_sel[2];
-  if (M == 0) return;  // the reference indexes an empty vector here; nothing is rejected
-  select_bin(hist, M / 2, s_sel, wsum);
-  const int hb = s_sel[0], k2 = s_sel[1];
-  hist[t] = 0;
-  __syncthreads();
-  for (int i = t; i < nL; i += 256) {
-    const int s = S[i];
-    if (s >= 0 && (s >> 8) == hb) atomicAdd(&hist[s & 255], 1);
-  }
-  __syncthreads();
-  select_bin(hist, k2, s_sel, wsum);
-  const float median = (float)((hb << 8) | s_sel[0]);
-  const float thDist = 1.5f * 1.4f * median;
-  for (int i = t; i < nL; i += 256) {
-    const int s = S[i];
-    if (s >= 0 && !((float)s < thDist)) {
-      u_right[(long long)p * cap + i] = -1.0f;
-      depth[(long long)p * cap + i] = -1.0f;
-    }
-  }
+  __shared__ MedianSmem sm;
+  const int p = blockIdx.x;
+  const long long base = (long long)p * cap;
+  median_filter(sm, min(counts[left0 + p], cap), sad_in + base, u_right + base, depth + base);
 }
 
 }  // namespace
@@ -463,7 +510,7 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
   if (g.nbk == 1) g.rbo[0] = rb_all;
   hipStream_t s = stream ? (hipStream_t)stream : P.stream;
   const size_t lds = sizeof(int) * (g.nbk * (g.rows0 + 1) + 16);
-  hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(256), lds, s, g, d_kps, d_counts,
+  hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(ROWS_THREADS), lds, s, g, d_kps, d_counts,
                      S->d_row_start, S->d_buckets);
   ORBFE_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
