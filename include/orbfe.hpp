@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "orbfe.h"
+#include "orbfe_stereo.h"
 
 namespace orbfe {
 
@@ -180,6 +181,20 @@ class Matcher {
  private:
   orbfe_matcher* m_ = nullptr;
 };
+
+// Frame::ComputeStereoMatches (src/Frame.cc:522-700) with the reference's two extractors: the
+// pyramids are those of the last call of `left` and `right` (image 0 of each). uRight / depth get
+// one entry per left keypoint, -1 where unmatched (mvuRight / mvDepth). mb: see orbfe_stereo.h.
+inline void ComputeStereoMatches(Extractor& left, Extractor& right, const std::vector<KeyPoint>& kl,
+                                 const std::vector<uint8_t>& dl, const std::vector<KeyPoint>& kr,
+                                 const std::vector<uint8_t>& dr, float mbf, float mb,
+                                 std::vector<float>& uRight, std::vector<float>& depth) {
+  uRight.assign(kl.size(), -1.0f);
+  depth.assign(kl.size(), -1.0f);
+  check(orbfe_compute_stereo_matches(left.handle(), 0, right.handle(), 0, kl.data(), dl.data(), (int)kl.size(),
+                                     kr.data(), dr.data(), (int)kr.size(), mbf, mb, uRight.data(), depth.data()),
+        "orbfe_compute_stereo_matches");
+}
 
 }  // namespace orbfe
 #endif

@@ -44,9 +44,14 @@ int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const uint8_t* r
                        uint8_t* desc_l, int* n_l, orbfe_keypoint* kps_r, uint8_t* desc_r, int* n_r,
                        int cap, float* u_right, float* depth);
 
-/* Host-buffer ComputeStereoMatches over keypoints the caller already holds for images 0 (left)
- * and 1 (right) of the last extract call on h (e.g. after orbfe_extract_batch of {left, right}). */
-int orbfe_compute_stereo_matches(orbfe_extractor* h, const orbfe_keypoint* kps_l,
+/* Host-buffer ComputeStereoMatches = the drop-in for Frame::ComputeStereoMatches with the
+ * reference's two extractors (mpORBextractorLeft / mpORBextractorRight, Frame.cc:529,620-640):
+ * the left pyramid is image `image_left` of h_left's last extract call, the right pyramid image
+ * `image_right` of h_right's (h_left == h_right with images 0 / 1 after a two-image batch also
+ * works). kps_* / desc_* are mvKeys / mDescriptors and mvKeysRight / mDescriptorsRight
+ * (orbfe_keypoint has cv::KeyPoint's layout). Writes u_right / depth [n_l]. Blocking. */
+int orbfe_compute_stereo_matches(orbfe_extractor* h_left, int image_left, orbfe_extractor* h_right,
+                                 int image_right, const orbfe_keypoint* kps_l,
                                  const uint8_t* desc_l, int n_l, const orbfe_keypoint* kps_r,
                                  const uint8_t* desc_r, int n_r, float mbf, float mb,
                                  float* u_right, float* depth);

@@ -137,9 +137,9 @@ _SIGNATURES = {
     "orbfe_compute_stereo_matches_batch_device": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p,
                                                           c_void_p, c_void_p, c_int, c_float,
                                                           c_float, c_void_p, c_void_p, c_void_p]),
-    "orbfe_compute_stereo_matches": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                             c_void_p, c_int, c_float, c_float, c_void_p,
-                                             c_void_p]),
+    "orbfe_compute_stereo_matches": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_int, c_void_p, c_void_p, c_int, c_float,
+                                             c_float, c_void_p, c_void_p]),
     "orbfe_stereo_frame": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_size_t, c_float,
                                    c_float, c_void_p, c_void_p, POINTER(c_int), c_void_p, c_void_p,
                                    POINTER(c_int), c_int, c_void_p, c_void_p]),

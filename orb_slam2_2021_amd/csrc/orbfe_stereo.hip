@@ -34,9 +34,12 @@ constexpr int ST_TH_ORB = (100 + 50) / 2;  // thOrbDist = (TH_HIGH + TH_LOW) / 2
 constexpr int ST_TAB_MAX = 16384;          // LDS bucket table bound (ints)
 
 struct StereoGeom {
-  const uint8_t* pyr;
-  long long image_stride;
-  int left0, right0, cap, nlevels, rows0;
+  const uint8_t* pyrL;  // left / right pyramids (may be the same handle's)
+  const uint8_t* pyrR;
+  long long strideL, strideR;
+  int pL0, pR0;         // pair p: left pyramid image pL0 + p, right pyramid image pR0 + p
+  int kL0, kR0;         // pair p: keypoints / descriptors / counts of images kL0 + p, kR0 + p
+  int cap, nlevels, rows0;
   int nbk;  // octave buckets: nlevels (bucket per octave and row) or 1 (per row only)
   float mbf, maxD;
   int w[ORBFE_MAX_LEVELS], pitch[ORBFE_MAX_LEVELS];
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, cons
   const int ntab = g.nbk * (g.rows0 + 1);
   int* wsum = s_hist + ntab;
   const int p = blockIdx.x, t = threadIdx.x;
-  const int img = g.right0 + p;
+  const int img = g.kR0 + p;
   const int nR = min(counts[img], g.cap);
   const orbfe_keypoint* K = kps + (long long)img * g.cap;
   for (int r = t; r < ntab; r += ROWS_THREADS) s_hist[r] = 0;
@@ -217,6 +220,7 @@ __device__ __forceinline__ void stereo_one(const StereoGeom& g, const orbfe_keyp
                                            const uint4* __restrict__ buckets, float* __restrict__ u_right,
                                            float* __restrict__ depth, int32_t* __restrict__ sad_out, int p, int i,
                                            int j, int imgL, int imgR) {
+  const int pimgL = g.pL0 + p, pimgR = g.pR0 + p;
   const orbfe_keypoint kpL = kps[(long long)imgL * g.cap + i];
   const long long o = (long long)p * g.cap + i;
   float ur_out = -1.0f, dep_out = -1.0f;
@@ -287,9 +291,9 @@ __device__ __forceinline__ void stereo_one(const StereoGeom& g, const orbfe_keyp
       if (ok) {
         // lane j = window row j (lanes 11..15 re-read row 10 and contribute nothing)
         const int row = yL + min(j, 2 * ST_W) - ST_W;
-        const uint8_t* pl = g.pyr + (long long)imgL * g.image_stride + g.off[levelL] +
+        const uint8_t* pl = g.pyrL + (long long)pimgL * g.strideL + g.off[levelL] +
                             (long long)row * g.pitch[levelL] + (xL - ST_W);
-        const uint8_t* pr = g.pyr + (long long)imgR * g.image_stride + g.off[levelL] +
+        const uint8_t* pr = g.pyrR + (long long)pimgR * g.strideR + g.off[levelL] +
                             (long long)row * g.pitch[levelL] + (xR0 - ST_L - ST_W);
         const uint32_t* ql = reinterpret_cast<const uint32_t*>((uintptr_t)pl & ~(uintptr_t)3);
         const uint32_t* qr = reinterpret_cast<const uint32_t*>((uintptr_t)pr & ~(uintptr_t)3);
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
   const int p = blk.y;
   const int j = threadIdx.x & 15;
   const int i = blk.x * 16 + (threadIdx.x >> 4);
-  const int imgL = g.left0 + p, imgR = g.right0 + p;
+  const int imgL = g.kL0 + p, imgR = g.kR0 + p;
   const int nL = min(counts[imgL], g.cap);
   if (i < nL) stereo_one(g, kps, desc, row_start, buckets, u_right, depth, sad_out, p, i, j, imgL, imgR);
 }
@@ -444,23 +448,20 @@ static OrbfeStereoScratch* scratch_of(orbfe_extractor* h) {
   return *slot;
 }
 
-extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int n_pairs, int left0,
-                                                         int right0, const orbfe_keypoint* d_kps,
-                                                         const uint8_t* d_desc, const int32_t* d_counts,
-                                                         int cap, float mbf, float mb, float* d_u_right,
-                                                         float* d_depth, void* stream) {
-  if (!h || n_pairs < 0 || cap <= 0 || !d_kps || !d_desc || !d_counts || !d_u_right || !d_depth)
-    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_compute_stereo_matches_batch_device: bad argument");
-  if (n_pairs == 0) return ORBFE_OK;
-  OrbfePyramid P;
-  int st = orbfe_internal_pyramid(h, &P);
-  if (st != ORBFE_OK) return st;
-  if (left0 < 0 || right0 < 0 || left0 + n_pairs > P.n_images || right0 + n_pairs > P.n_images)
-    return orbfe_set_error(ORBFE_ERR_ARG, "stereo pair images outside the last extract call");
-  if (cap < P.total_key_slots) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
-  hipSetDevice(P.device);
-  OrbfeStereoScratch* S = scratch_of(h);
-  const size_t rs_n = (size_t)n_pairs * P.nlevels * (P.h[0] + 1), sl_n = (size_t)n_pairs * cap;
+// The three launches for n_pairs pairs: left pyramid image pl0 + p of PL, right pyramid image
+// pr0 + p of PR, keypoints / descriptors / counts of images kl0 + p and kr0 + p of d_kps (cap
+// slots per image), outputs at p*cap.
+static int launch_stereo(OrbfeStereoScratch* S, const OrbfePyramid& PL, int pl0, const OrbfePyramid& PR,
+                         int pr0, int n_pairs, int kl0, int kr0, const orbfe_keypoint* d_kps,
+                         const uint8_t* d_desc, const int32_t* d_counts, int cap, float mbf, float mb,
+                         float* d_u_right, float* d_depth, hipStream_t s) {
+  if (PL.nlevels != PR.nlevels)
+    return orbfe_set_error(ORBFE_ERR_ARG, "left and right extractors differ in levels");
+  for (int l = 0; l < PL.nlevels; l++)
+    if (PL.w[l] != PR.w[l] || PL.h[l] != PR.h[l] || PL.pitch[l] != PR.pitch[l] || PL.off[l] != PR.off[l] ||
+        PL.scale[l] != PR.scale[l])
+      return orbfe_set_error(ORBFE_ERR_ARG, "left and right pyramids differ in geometry");
+  const size_t rs_n = (size_t)n_pairs * PL.nlevels * (PL.h[0] + 1), sl_n = (size_t)n_pairs * cap;
   if (rs_n > S->row_start_n) {
     hipFree(S->d_row_start);
     S->d_row_start = nullptr;
@@ -478,37 +479,40 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
   }
   StereoGeom g;
   std::memset(&g, 0, sizeof(g));
-  g.pyr = P.base;
-  g.image_stride = P.image_stride;
-  g.left0 = left0;
-  g.right0 = right0;
+  g.pyrL = PL.base;
+  g.pyrR = PR.base;
+  g.strideL = PL.image_stride;
+  g.strideR = PR.image_stride;
+  g.pL0 = pl0;
+  g.pR0 = pr0;
+  g.kL0 = kl0;
+  g.kR0 = kr0;
   g.cap = cap;
-  g.nlevels = P.nlevels;
-  g.rows0 = P.h[0];
+  g.nlevels = PL.nlevels;
+  g.rows0 = PL.h[0];
   g.mbf = mbf;
   const float minZ = mb;
   g.maxD = mbf / minZ;  // :553
-  for (int l = 0; l < P.nlevels; l++) {
-    g.w[l] = P.w[l];
-    g.h[l] = P.h[l];
-    g.pitch[l] = P.pitch[l];
-    g.off[l] = P.off[l];
-    g.scale[l] = P.scale[l];
-    g.inv_scale[l] = P.inv_scale[l];
+  for (int l = 0; l < PL.nlevels; l++) {
+    g.w[l] = PL.w[l];
+    g.h[l] = PL.h[l];
+    g.pitch[l] = PL.pitch[l];
+    g.off[l] = PL.off[l];
+    g.scale[l] = PL.scale[l];
+    g.inv_scale[l] = PL.inv_scale[l];
   }
   // Row band of a bucket: a right keypoint at row floor(y) = b of octave o covers v only if
   // floor(y - r) <= v <= ceil(y + r), r = 2 scale[o] (:541-544), i.e. |b - v| <= ceil(r) + 1;
   // one more row absorbs the float rounding of y -+ r.
-  g.nbk = P.nlevels * (g.rows0 + 1) <= ST_TAB_MAX ? P.nlevels : 1;
+  g.nbk = PL.nlevels * (g.rows0 + 1) <= ST_TAB_MAX ? PL.nlevels : 1;
   if (g.nbk == 1 && g.rows0 + 1 > ST_TAB_MAX)
     return orbfe_set_error(ORBFE_ERR_ARG, "image taller than the stereo row table");
   int rb_all = 0;
-  for (int l = 0; l < P.nlevels; l++) {
-    g.rbo[l] = (int)std::ceil(2.0f * P.scale[l]) + 2;
+  for (int l = 0; l < PL.nlevels; l++) {
+    g.rbo[l] = (int)std::ceil(2.0f * PL.scale[l]) + 2;
     rb_all = std::max(rb_all, g.rbo[l]);
   }
   if (g.nbk == 1) g.rbo[0] = rb_all;
-  hipStream_t s = stream ? (hipStream_t)stream : P.stream;
   const size_t lds = sizeof(int) * (g.nbk * (g.rows0 + 1) + 16);
   hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(ROWS_THREADS), lds, s, g, d_kps, d_counts,
                      S->d_row_start, S->d_buckets);
@@ -516,10 +520,30 @@ extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int
   hipLaunchKernelGGL(k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
                      d_counts, S->d_row_start, S->d_buckets, d_u_right, d_depth, S->d_sad);
   ORBFE_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(256), 0, s, left0, cap, d_counts, S->d_sad,
+  hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(256), 0, s, kl0, cap, d_counts, S->d_sad,
                      d_u_right, d_depth);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
+}
+
+extern "C" int orbfe_compute_stereo_matches_batch_device(orbfe_extractor* h, int n_pairs, int left0,
+                                                         int right0, const orbfe_keypoint* d_kps,
+                                                         const uint8_t* d_desc, const int32_t* d_counts,
+                                                         int cap, float mbf, float mb, float* d_u_right,
+                                                         float* d_depth, void* stream) {
+  if (!h || n_pairs < 0 || cap <= 0 || !d_kps || !d_desc || !d_counts || !d_u_right || !d_depth)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_compute_stereo_matches_batch_device: bad argument");
+  if (n_pairs == 0) return ORBFE_OK;
+  OrbfePyramid P;
+  int st = orbfe_internal_pyramid(h, &P);
+  if (st != ORBFE_OK) return st;
+  if (left0 < 0 || right0 < 0 || left0 + n_pairs > P.n_images || right0 + n_pairs > P.n_images)
+    return orbfe_set_error(ORBFE_ERR_ARG, "stereo pair images outside the last extract call");
+  if (cap < P.total_key_slots) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
+  hipSetDevice(P.device);
+  hipStream_t s = stream ? (hipStream_t)stream : P.stream;
+  return launch_stereo(scratch_of(h), P, left0, P, right0, n_pairs, left0, right0, d_kps, d_desc, d_counts,
+                       cap, mbf, mb, d_u_right, d_depth, s);
 }
 
 static int ensure_io(OrbfeStereoScratch* S, size_t slots) {
@@ -544,24 +568,31 @@ static int ensure_io(OrbfeStereoScratch* S, size_t slots) {
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_compute_stereo_matches(orbfe_extractor* h, const orbfe_keypoint* kps_l,
-                                            const uint8_t* desc_l, int n_l, const orbfe_keypoint* kps_r,
-                                            const uint8_t* desc_r, int n_r, float mbf, float mb,
-                                            float* u_right, float* depth) {
-  if (!h || n_l < 0 || n_r < 0 || (n_l > 0 && (!kps_l || !desc_l || !u_right || !depth)) ||
+extern "C" int orbfe_compute_stereo_matches(orbfe_extractor* h_left, int image_left,
+                                            orbfe_extractor* h_right, int image_right,
+                                            const orbfe_keypoint* kps_l, const uint8_t* desc_l, int n_l,
+                                            const orbfe_keypoint* kps_r, const uint8_t* desc_r, int n_r,
+                                            float mbf, float mb, float* u_right, float* depth) {
+  if (!h_left || !h_right || n_l < 0 || n_r < 0 || (n_l > 0 && (!kps_l || !desc_l || !u_right || !depth)) ||
       (n_r > 0 && (!kps_r || !desc_r)))
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_compute_stereo_matches: bad argument");
+  for (int i = 0; i < n_l; i++) u_right[i] = depth[i] = -1.0f;  // :524-525
   if (n_l == 0) return ORBFE_OK;
-  OrbfePyramid P;
-  int st = orbfe_internal_pyramid(h, &P);
+  OrbfePyramid PL, PR;
+  int st = orbfe_internal_pyramid(h_left, &PL);
   if (st != ORBFE_OK) return st;
-  if (P.n_images < 2) return orbfe_set_error(ORBFE_ERR_STATE, "the last extract call held no stereo pair");
-  hipSetDevice(P.device);
-  const int cap = std::max(P.total_key_slots, std::max(n_l, n_r));
-  OrbfeStereoScratch* S = scratch_of(h);
+  st = orbfe_internal_pyramid(h_right, &PR);
+  if (st != ORBFE_OK) return st;
+  if (image_left < 0 || image_left >= PL.n_images || image_right < 0 || image_right >= PR.n_images)
+    return orbfe_set_error(ORBFE_ERR_ARG, "stereo image outside the last extract call");
+  if (PL.device != PR.device) return orbfe_set_error(ORBFE_ERR_ARG, "left and right handles on different devices");
+  hipSetDevice(PL.device);
+  if (h_right != h_left) ORBFE_HIP_CHECK(hipStreamSynchronize(PR.stream));  // right pyramid complete
+  const int cap = std::max(PL.total_key_slots, std::max(n_l, n_r));
+  OrbfeStereoScratch* S = scratch_of(h_left);
   st = ensure_io(S, (size_t)cap);
   if (st != ORBFE_OK) return st;
-  // stage both keypoint / descriptor sets (image 0 = left, image 1 = right) in one H2D burst each
+  // stage both keypoint / descriptor sets (slot 0 = left, slot 1 = right) in one H2D burst each
   orbfe_keypoint* hk = reinterpret_cast<orbfe_keypoint*>(S->h_stage);
   uint8_t* hd = S->h_stage + 2 * (size_t)cap * sizeof(orbfe_keypoint);
   std::memcpy(hk, kps_l, sizeof(orbfe_keypoint) * n_l);
@@ -571,14 +602,14 @@ extern "C" int orbfe_compute_stereo_matches(orbfe_extractor* h, const orbfe_keyp
   int32_t* hc = reinterpret_cast<int32_t*>(hd + 2 * (size_t)cap * 32);
   hc[0] = n_l;
   hc[1] = n_r;
-  hipStream_t s = P.stream;
+  hipStream_t s = PL.stream;
   ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_kps, hk, 2 * (size_t)cap * sizeof(orbfe_keypoint), hipMemcpyHostToDevice, s));
   ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_desc, hd, 2 * (size_t)cap * 32, hipMemcpyHostToDevice, s));
   ORBFE_HIP_CHECK(hipMemcpyAsync(S->d_counts, hc, 2 * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(s));  // hc is reused for the results below
-  st = orbfe_compute_stereo_matches_batch_device(h, 1, 0, 1, S->d_kps, S->d_desc, S->d_counts, cap, mbf, mb,
-                                                 S->d_out, S->d_out + cap, s);
+  st = launch_stereo(S, PL, image_left, PR, image_right, 1, 0, 1, S->d_kps, S->d_desc, S->d_counts, cap, mbf,
+                     mb, S->d_out, S->d_out + cap, s);
   if (st != ORBFE_OK) return st;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(s));  // the staging area is reused for the results
   float* ho = reinterpret_cast<float*>(hk);
   ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * n_l, hipMemcpyDeviceToHost, s));
   ORBFE_HIP_CHECK(hipMemcpyAsync(ho + n_l, S->d_out + cap, sizeof(float) * n_l, hipMemcpyDeviceToHost, s));
@@ -621,8 +652,8 @@ extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const
   OrbfeStereoScratch* S = scratch_of(h);
   st = ensure_io(S, (size_t)K);
   if (st != ORBFE_OK) return st;
-  st = orbfe_compute_stereo_matches_batch_device(h, 1, 0, 1, P.io_kps, P.io_desc, P.io_counts, K, mbf, mb,
-                                                 S->d_out, S->d_out + K, P.stream);
+  st = launch_stereo(S, P, 0, P, 1, 1, 0, 1, P.io_kps, P.io_desc, P.io_counts, K, mbf, mb, S->d_out,
+                     S->d_out + K, P.stream);
   if (st != ORBFE_OK) return st;
   float* ho = reinterpret_cast<float*>(S->h_stage);
   ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * counts[0], hipMemcpyDeviceToHost, P.stream));

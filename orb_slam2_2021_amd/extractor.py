@@ -153,12 +153,18 @@ class ORBextractor:
 
     # ---- Frame::ComputeStereoMatches (src/Frame.cc:522-700) -------------------------------
     def compute_stereo_matches(self, kps_l: KeyPoints, desc_l: np.ndarray, kps_r: KeyPoints,
-                               desc_r: np.ndarray, mbf: float, mb: float
+                               desc_r: np.ndarray, mbf: float, mb: float, right: "ORBextractor" = None,
+                               image_left: int = 0, image_right: Optional[int] = None
                                ) -> Tuple[np.ndarray, np.ndarray]:
-        """(mvuRight, mvDepth) of the left keypoints against the right ones, on the pyramids of
-        images 0 (left) and 1 (right) of the last extract call (e.g. extract_batch([l, r])).
+        """Frame::ComputeStereoMatches (Frame.cc:522-700): (mvuRight, mvDepth) of the left keypoints.
+        The left pyramid is image `image_left` of this extractor's last call; the right pyramid is
+        image `image_right` of `right`'s last call (default: this extractor, image 1 -- e.g. after
+        extract_batch([left, right]); with a separate right extractor, its image 0).
         mb: the reference uses the Frame's mb before assigning it (Frame.cc:125 vs :149); pass
         mbf / fx, or 0 for an unbounded disparity range."""
+        other = self if right is None else right
+        if image_right is None:
+            image_right = 1 if other is self else 0
         kl = np.ascontiguousarray(kps_l, L.KEYPOINT_DTYPE)
         kr = np.ascontiguousarray(kps_r, L.KEYPOINT_DTYPE)
         dl = np.ascontiguousarray(desc_l if desc_l is not None else np.zeros((0, 32)), np.uint8)
@@ -167,8 +173,9 @@ class ORBextractor:
         ur = np.full(n, -1.0, np.float32)
         dep = np.full(n, -1.0, np.float32)
         L.check(self._lib.orbfe_compute_stereo_matches(
-            self._h, L.ptr(kl), L.ptr(dl), n, L.ptr(kr), L.ptr(dr), len(kr), float(mbf), float(mb),
-            L.ptr(ur), L.ptr(dep)), "orbfe_compute_stereo_matches")
+            self._h, int(image_left), other._h, int(image_right), L.ptr(kl), L.ptr(dl), n,
+            L.ptr(kr), L.ptr(dr), len(kr), float(mbf), float(mb), L.ptr(ur), L.ptr(dep)),
+            "orbfe_compute_stereo_matches")
         return ur, dep
 
     def stereo_frame(self, left: np.ndarray, right: np.ndarray, mbf: float, mb: float):

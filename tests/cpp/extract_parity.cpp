@@ -93,6 +93,49 @@ int main() {
     }
   }
   orbref_extractor_destroy(ref);
+  // Frame::ComputeStereoMatches over the two extractors' pyramids vs the oracle on the oracle's
+  {
+    const float bf = 386.1448f, mb = bf / 718.856f;
+    std::vector<float> ur, dep;
+    orbfe::ComputeStereoMatches(el, er, kl, dl, kr, dr, bf, mb, ur, dep);
+    orbref_extractor* rl = orbref_extractor_create(2000, 1.2f, 8, 20, 7);
+    orbref_extractor* rr = orbref_extractor_create(2000, 1.2f, 8, 20, 7);
+    std::vector<orbfe_keypoint> k(4000);
+    std::vector<uint8_t> d(4000 * 32);
+    int n = 0;
+    orbref_extract(rl, left.data(), rows, cols, cols, k.data(), 4000, d.data(), &n);
+    orbref_extract(rr, right.data(), rows, cols, cols, k.data(), 4000, d.data(), &n);
+    std::vector<std::vector<uint8_t>> lvl(16);
+    orbref_level_view vl[8], vr[8];
+    for (int l = 0; l < 8; l++)
+      for (int side = 0; side < 2; side++) {
+        orbref_extractor* e = side ? rr : rl;
+        int r = 0, c = 0;
+        orbref_get_level(e, l, nullptr, 0, &r, &c);
+        std::vector<uint8_t>& buf = lvl[2 * l + side];
+        buf.resize((size_t)r * c);
+        orbref_get_level(e, l, buf.data(), (int)buf.size(), &r, &c);
+        (side ? vr : vl)[l] = orbref_level_view{buf.data(), r, c, c};
+      }
+    std::vector<float> scale(8), inv(8), s2(8), is2(8);
+    std::vector<int32_t> fpl(8), umax(16);
+    orbref_get_tables(rl, scale.data(), inv.data(), s2.data(), is2.data(), fpl.data(), umax.data());
+    std::vector<float> wu(kl.size()), wd(kl.size());
+    orbref_compute_stereo_matches(kl.data(), dl.data(), (int)kl.size(), kr.data(), dr.data(), (int)kr.size(), vl,
+                                  vr, 8, scale.data(), inv.data(), mb, bf, wu.data(), wd.data());
+    int matched = 0;
+    for (size_t i = 0; i < kl.size(); i++) {
+      if (std::memcmp(&ur[i], &wu[i], 4) != 0 || std::memcmp(&dep[i], &wd[i], 4) != 0) {
+        std::printf("stereo: keypoint %zu differs (%g %g vs %g %g)\n", i, ur[i], dep[i], wu[i], wd[i]);
+        fails++;
+        break;
+      }
+      matched += ur[i] >= 0;
+    }
+    std::printf("stereo: %d of %zu left keypoints matched\n", matched, kl.size());
+    orbref_extractor_destroy(rl);
+    orbref_extractor_destroy(rr);
+  }
   // DescriptorDistance on the extracted descriptors
   for (size_t i = 0; i + 1 < kl.size() && i < 64; i++)
     if (orbfe::Matcher::DescriptorDistance(&dl[i * 32], &dl[(i + 1) * 32]) !=
