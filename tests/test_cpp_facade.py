@@ -1,5 +1,6 @@
 """The C++ facade (include/orbfe.hpp) as a reference-side adapter would use it: two extractor
-instances on two threads (Frame.cc:113-116), pyramid level views, DescriptorDistance -- checked
+instances on two threads (Frame.cc:113-116), pyramid level views, ComputeStereoMatches over the
+two extractors, DescriptorDistance -- checked
 against the oracle's C API inside the C++ program (tests/cpp/extract_parity.cpp)."""
 import os
 import subprocess
@@ -31,4 +32,6 @@ def test_cpp_facade_parity(require_gpu):
     exe = _build()
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert out.stdout.startswith("OK")
+    lines = out.stdout.strip().splitlines()
+    assert lines[-1].startswith("OK"), out.stdout
+    assert any(l.startswith("stereo: ") for l in lines), out.stdout
