@@ -1187,3 +1187,93 @@ extern "C" int orbref_compute_stereo_matches(const orbfe_keypoint* kl, const uin
   }
   return ORBFE_OK;
 }
+
+// =============================================================================================
+// Frame::isInFrustum (src/Frame.cc:318-374) with MapPoint::PredictScale (MapPoint.cc:432-447) and
+// Get{Min,Max}DistanceInvariance (:403-413), over a MapPoint set; Tracking::SearchLocalPoints'
+// skip rules (Tracking.cc:1186-1201). cv::Mat CV_32F algebra per SURVEY Appendix A.9.
+extern "C" int orbref_is_in_frustum(const orbfe_frame_view* F, const orbfe_mappoint_geometry* G,
+                                    const float* T, float log_scale_factor, float viewing_cos_limit,
+                                    const orbfe_frustum_out* out, int* n_in_view) {
+  if (!F || !G || !T || !out || !out->flags || G->m < 0) return ORBFE_ERR_ARG;
+  const float Rcw[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+  const float tcw[3] = {T[3], T[7], T[11]};
+  float Ow[3];  // mOw = -mRcw.t() * mtcw (Frame.cc:314)
+  for (int i = 0; i < 3; i++) {
+    const float col[3] = {Rcw[i], Rcw[3 + i], Rcw[6 + i]};
+    Ow[i] = -gemv_row(col, tcw, nullptr);
+  }
+  int nv = 0;
+  for (int i = 0; i < G->m; i++) {
+    uint8_t fl = (uint8_t)(G->flags[i] & ~ORBFE_MPF_TRACK_IN_VIEW);  // mbTrackInView = false (:320)
+    out->flags[i] = fl;
+    if (fl & (ORBFE_MPF_BAD | ORBFE_MPF_SEEN)) continue;  // Tracking.cc:1193-1196
+    const float* P = G->world_pos + 3 * (size_t)i;
+    const float PcX = gemv_row(Rcw, P, &tcw[0]);  // Pc = mRcw * P + mtcw (:326)
+    const float PcY = gemv_row(Rcw + 3, P, &tcw[1]);
+    const float PcZ = gemv_row(Rcw + 6, P, &tcw[2]);
+    if (PcZ < 0.0f) continue;  // :332
+    const float invz = 1.0f / PcZ;
+    const float u = F->fx * PcX * invz + F->cx;
+    const float v = F->fy * PcY * invz + F->cy;
+    if (u < F->min_x || u > F->max_x) continue;
+    if (v < F->min_y || v > F->max_y) continue;
+    const float maxDistance = 1.2f * G->max_distance[i];
+    const float minDistance = 0.8f * G->min_distance[i];
+    const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+    double ss = 0.0;  // cv::norm: squares accumulated in double, sqrt in double (:350)
+    for (int k = 0; k < 3; k++) ss += (double)PO[k] * (double)PO[k];
+    const float dist = (float)std::sqrt(ss);
+    if (dist < minDistance || dist > maxDistance) continue;
+    const float* Pn = G->normal + 3 * (size_t)i;
+    double dot = 0.0;  // Mat::dot: products accumulated in double (:358)
+    for (int k = 0; k < 3; k++) dot += (double)PO[k] * (double)Pn[k];
+    const float viewCos = (float)(dot / (double)dist);
+    if (viewCos < viewing_cos_limit) continue;
+    // PredictScale: ratio in float, ceil(log(ratio) / mfLogScaleFactor) in double
+    const float ratio = G->max_distance[i] / dist;
+    int nScale = (int)std::ceil(std::log((double)ratio) / (double)log_scale_factor);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
+    out->flags[i] = (uint8_t)(fl | ORBFE_MPF_TRACK_IN_VIEW);
+    if (out->proj_x) out->proj_x[i] = u;
+    if (out->proj_xr) out->proj_xr[i] = u - F->bf * invz;
+    if (out->proj_y) out->proj_y[i] = v;
+    if (out->level) out->level[i] = nScale;
+    if (out->view_cos) out->view_cos[i] = viewCos;
+    nv++;
+  }
+  if (n_in_view) *n_in_view = nv;
+  return ORBFE_OK;
+}
+
+extern "C" int orbref_search_local_points(const orbfe_frame_view* F, const orbfe_mappoint_geometry* G,
+                                          const float* T, float log_scale_factor,
+                                          float viewing_cos_limit, float th, float nnratio,
+                                          int32_t* best_idx, int* nmatches,
+                                          const orbfe_frustum_out* out, int* n_in_view) {
+  if (!F || !G || !T || !best_idx || !nmatches || G->m < 0) return ORBFE_ERR_ARG;
+  const size_t M = (size_t)G->m;
+  std::vector<uint8_t> fl(M);
+  std::vector<float> px(M, 0.f), py(M, 0.f), pxr(M, 0.f), vc(M, 0.f);
+  std::vector<int32_t> lvl(M, 0);
+  orbfe_frustum_out o{fl.data(), px.data(), py.data(), pxr.data(), lvl.data(), vc.data()};
+  int nv = 0;
+  int st = orbref_is_in_frustum(F, G, T, log_scale_factor, viewing_cos_limit, &o, &nv);
+  if (st) return st;
+  if (out) {
+    if (out->flags) std::memcpy(out->flags, fl.data(), M);
+    if (out->proj_x) std::memcpy(out->proj_x, px.data(), 4 * M);
+    if (out->proj_y) std::memcpy(out->proj_y, py.data(), 4 * M);
+    if (out->proj_xr) std::memcpy(out->proj_xr, pxr.data(), 4 * M);
+    if (out->level) std::memcpy(out->level, lvl.data(), 4 * M);
+    if (out->view_cos) std::memcpy(out->view_cos, vc.data(), 4 * M);
+  }
+  if (n_in_view) *n_in_view = nv;
+  *nmatches = 0;
+  for (size_t i = 0; i < M; i++) best_idx[i] = -1;
+  if (nv == 0) return ORBFE_OK;  // if (nToMatch > 0) (Tracking.cc:1204)
+  orbfe_local_mappoints mp{G->m, fl.data(), px.data(), py.data(), pxr.data(), lvl.data(), vc.data(),
+                           G->descriptors};
+  return orbref_search_by_projection_local(F, &mp, th, nnratio, best_idx, nmatches);
+}

@@ -20,6 +20,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include "../include/orbfe.h"
+#include "../include/orbfe_frustum.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -70,6 +71,15 @@ int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* node_desc,
                            const int32_t* first_child, const int32_t* n_children,
                            const float* weights, const uint8_t* desc, int n, int levelsup,
                            uint32_t* node_ids, int32_t* offsets, int32_t* indices, int* n_out);
+/* Frame::isInFrustum over a MapPoint set (Frame.cc:318-374, MapPoint.cc:403-447) and
+ * Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:1186-1213). */
+int orbref_is_in_frustum(const orbfe_frame_view* frame, const orbfe_mappoint_geometry* geom,
+                         const float* tcw, float log_scale_factor, float viewing_cos_limit,
+                         const orbfe_frustum_out* out, int* n_in_view);
+int orbref_search_local_points(const orbfe_frame_view* frame, const orbfe_mappoint_geometry* geom,
+                               const float* tcw, float log_scale_factor, float viewing_cos_limit,
+                               float th, float nnratio, int32_t* best_idx, int* nmatches,
+                               const orbfe_frustum_out* out, int* n_in_view);
 /* One pyramid level (ORBextractor::mvImagePyramid[l]): rows x cols bytes, row stride. */
 typedef struct orbref_level_view {
   const uint8_t* data;

@@ -5,9 +5,9 @@ package is its host-side mirror of the reference's ORBextractor / ORBmatcher int
 """
 from ._lib import (KEYPOINT_DTYPE, LIB_PATH, LibraryMissing, OrbfeError, ORBFE_MP_NONE,
                    ORBFE_MP_OBSERVED, ORBFE_MP_PRESENT, ORBFE_RESIZE_SCALAR, ORBFE_RESIZE_SIMD128,
-                   MPF_BAD, MPF_OBSERVED, MPF_OUTLIER, MPF_PRESENT, MPF_TRACK_IN_VIEW)
+                   MPF_BAD, MPF_OBSERVED, MPF_OUTLIER, MPF_PRESENT, MPF_SEEN, MPF_TRACK_IN_VIEW)
 from .extractor import ORBextractor, synth_frame
-from .frames import FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints
+from .frames import FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints, MapPointGeometry
 from .matcher import ORBmatcher
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "FeatureVector", "LocalMapPoints",

@@ -1,5 +1,5 @@
 """ctypes binding of liborbfe.so (include/orbfe.h, orbfe_match_batch.h, orbfe_debug.h, orbfe_synth.h,
-orbfe_vocab.h, orbfe_stereo.h).
+orbfe_vocab.h, orbfe_stereo.h, orbfe_frustum.h).
 
 The shared library is the product: every compute call below runs the HIP kernels in it. There is
 no CPU fallback -- if the library is missing, or no HIP device is present when a compute handle is
@@ -26,6 +26,7 @@ ORBFE_RESIZE_SIMD128 = 0
 ORBFE_RESIZE_SCALAR = 1
 ORBFE_MP_NONE, ORBFE_MP_PRESENT, ORBFE_MP_OBSERVED = 0, 1, 2
 MPF_TRACK_IN_VIEW, MPF_BAD, MPF_OBSERVED, MPF_PRESENT, MPF_OUTLIER = 1, 2, 4, 8, 16
+MPF_SEEN = 32  # orbfe_frustum.h: mnLastFrameSeen == CurrentFrame.mnId
 
 # cv::KeyPoint field order (28 bytes), = orbfe_keypoint
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -68,6 +69,16 @@ class lastframe_mappoints(Structure):
     _fields_ = [("n", c_int32), ("flags", c_void_p), ("world_pos", c_void_p),
                 ("descriptors", c_void_p), ("octave", c_void_p), ("angle", c_void_p),
                 ("tcw_last", c_float * 12)]
+
+
+class mappoint_geometry(Structure):
+    _fields_ = [("m", c_int32), ("flags", c_void_p), ("world_pos", c_void_p), ("normal", c_void_p),
+                ("min_distance", c_void_p), ("max_distance", c_void_p), ("descriptors", c_void_p)]
+
+
+class frustum_out(Structure):
+    _fields_ = [("flags", c_void_p), ("proj_x", c_void_p), ("proj_y", c_void_p),
+                ("proj_xr", c_void_p), ("level", c_void_p), ("view_cos", c_void_p)]
 
 
 class sft_pair(Structure):
@@ -143,6 +154,13 @@ _SIGNATURES = {
     "orbfe_stereo_frame": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_size_t, c_float,
                                    c_float, c_void_p, c_void_p, POINTER(c_int), c_void_p, c_void_p,
                                    POINTER(c_int), c_int, c_void_p, c_void_p]),
+    "orbfe_is_in_frustum": (c_int, [c_void_p, POINTER(frame_view), POINTER(mappoint_geometry),
+                                    c_void_p, c_float, c_float, POINTER(frustum_out),
+                                    POINTER(c_int)]),
+    "orbfe_search_local_points": (c_int, [c_void_p, POINTER(frame_view),
+                                          POINTER(mappoint_geometry), c_void_p, c_float, c_float,
+                                          c_float, c_void_p, POINTER(c_int), POINTER(frustum_out),
+                                          POINTER(c_int)]),
     "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
 }
 

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/orbfe.h"
+#include "../../include/orbfe_frustum.h"
 #include "../../include/orbfe_match_batch.h"
 #include "orbfe_device.h"
 
@@ -792,6 +793,82 @@ __global__ void k_sbp_local_queries(LocalQueryArgs a) {
   a.q[i] = q;
 }
 
+// Frame::isInFrustum (Frame.cc:318-374) + PredictScale (MapPoint.cc:432-447), thread per
+// MapPoint; skip rules of Tracking::SearchLocalPoints (Tracking.cc:1193-1196).
+struct FrustumArgs {
+  int m;
+  const uint8_t* flags_in;
+  const float* pos;
+  const float* normal;
+  const float* min_d;
+  const float* max_d;
+  orbfe_frustum_out out;  // device pointers (all set)
+  int32_t* n_in_view;     // device counter (zeroed before the launch)
+  float rcw[9], tcw[3], ow[3];
+  float fx, fy, cx, cy, bf, min_x, max_x, min_y, max_y;
+  float log_sf, cos_limit;
+  int nlevels;
+};
+__device__ __forceinline__ float gemv3_d(const float* r, float x, float y, float z, float add) {
+  double s = (double)r[0] * (double)x;  // cv::Mat CV_32F gemm: double accumulation, one rounding
+  s += (double)r[1] * (double)y;
+  s += (double)r[2] * (double)z;
+  s = s + (double)add;
+  return (float)s;
+}
+__global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  bool in = false;
+  if (i < a.m) {
+    const uint8_t fl = (uint8_t)(a.flags_in[i] & ~ORBFE_MPF_TRACK_IN_VIEW);  // :320
+    float u = 0.f, v = 0.f, xr = 0.f, viewCos = 0.f;
+    int nScale = 0;
+    if (!(fl & (ORBFE_MPF_BAD | ORBFE_MPF_SEEN))) {
+      const float Px = a.pos[3 * i], Py = a.pos[3 * i + 1], Pz = a.pos[3 * i + 2];
+      const float PcX = gemv3_d(a.rcw, Px, Py, Pz, a.tcw[0]);
+      const float PcY = gemv3_d(a.rcw + 3, Px, Py, Pz, a.tcw[1]);
+      const float PcZ = gemv3_d(a.rcw + 6, Px, Py, Pz, a.tcw[2]);
+      if (!(PcZ < 0.0f)) {
+        const float invz = 1.0f / PcZ;
+        u = a.fx * PcX * invz + a.cx;
+        v = a.fy * PcY * invz + a.cy;
+        if (!(u < a.min_x || u > a.max_x) && !(v < a.min_y || v > a.max_y)) {
+          const float maxDistance = 1.2f * a.max_d[i];
+          const float minDistance = 0.8f * a.min_d[i];
+          const float POx = Px - a.ow[0], POy = Py - a.ow[1], POz = Pz - a.ow[2];
+          double ss = (double)POx * (double)POx;  // cv::norm (:350)
+          ss += (double)POy * (double)POy;
+          ss += (double)POz * (double)POz;
+          const float dist = (float)sqrt(ss);
+          if (!(dist < minDistance || dist > maxDistance)) {
+            double dot = (double)POx * (double)a.normal[3 * i];  // Mat::dot (:358)
+            dot += (double)POy * (double)a.normal[3 * i + 1];
+            dot += (double)POz * (double)a.normal[3 * i + 2];
+            viewCos = (float)(dot / (double)dist);
+            if (!(viewCos < a.cos_limit)) {
+              const float ratio = a.max_d[i] / dist;
+              nScale = (int)ceil(log((double)ratio) / (double)a.log_sf);
+              nScale = nScale < 0 ? 0 : (nScale >= a.nlevels ? a.nlevels - 1 : nScale);
+              xr = u - a.bf * invz;
+              in = true;
+            }
+          }
+        }
+      }
+    }
+    a.out.flags[i] = (uint8_t)(fl | (in ? ORBFE_MPF_TRACK_IN_VIEW : 0u));
+    if (in) {
+      a.out.proj_x[i] = u;
+      a.out.proj_y[i] = v;
+      a.out.proj_xr[i] = xr;
+      a.out.level[i] = nScale;
+      a.out.view_cos[i] = viewCos;
+    }
+  }
+  const uint64_t b = wave_ballot(in);
+  if (lane_id() == 0 && b) atomicAdd(a.n_in_view, __popcll(b));
+}
+
 // Queries of SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1358-1410):
 // projection with cv::Mat float algebra accumulated in double.
 struct LastQueryArgs {
@@ -1379,4 +1456,169 @@ extern "C" int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* seri
   if (rounds) *rounds = m->last_rounds;
   if (serial_used) *serial_used = m->last_serial;
   return ORBFE_OK;
+}
+
+// ---- isInFrustum / SearchLocalPoints ------------------------------------------------------------
+static bool geom_ok(const orbfe_mappoint_geometry* g, bool need_desc) {
+  return g && g->m >= 0 &&
+         (g->m == 0 || (g->flags && g->world_pos && g->normal && g->min_distance && g->max_distance &&
+                        (!need_desc || g->descriptors)));
+}
+
+static void fill_frustum_args(FrustumArgs& fa, const orbfe_frame_view* F, const float* T, float log_sf,
+                              float cos_limit) {
+  std::memset(&fa, 0, sizeof(fa));
+  const float Rcw[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+  const float tcw[3] = {T[3], T[7], T[11]};
+  std::memcpy(fa.rcw, Rcw, sizeof(Rcw));
+  std::memcpy(fa.tcw, tcw, sizeof(tcw));
+  for (int i = 0; i < 3; i++) {  // mOw = -mRcw.t() * mtcw (Frame.cc:314), double-accumulated
+    double s = (double)Rcw[i] * (double)tcw[0];
+    s += (double)Rcw[3 + i] * (double)tcw[1];
+    s += (double)Rcw[6 + i] * (double)tcw[2];
+    fa.ow[i] = -(float)s;
+  }
+  fa.fx = F->fx;
+  fa.fy = F->fy;
+  fa.cx = F->cx;
+  fa.cy = F->cy;
+  fa.bf = F->bf;
+  fa.min_x = F->min_x;
+  fa.max_x = F->max_x;
+  fa.min_y = F->min_y;
+  fa.max_y = F->max_y;
+  fa.log_sf = log_sf;
+  fa.cos_limit = cos_limit;
+  fa.nlevels = F->nlevels;
+}
+
+struct FrustumPlan {
+  size_t flags_in, pos, normal, mind, maxd, o_flags, o_px, o_py, o_pxr, o_lvl, o_vc, counter;
+};
+static FrustumPlan plan_frustum(Arena& ar, int M) {
+  const size_t m1 = (size_t)std::max(M, 1);
+  FrustumPlan p;
+  p.flags_in = ar.add(m1);
+  p.pos = ar.add(12 * m1);
+  p.normal = ar.add(12 * m1);
+  p.mind = ar.add(4 * m1);
+  p.maxd = ar.add(4 * m1);
+  p.o_flags = ar.add(m1);
+  p.o_px = ar.add(4 * m1);
+  p.o_py = ar.add(4 * m1);
+  p.o_pxr = ar.add(4 * m1);
+  p.o_lvl = ar.add(4 * m1);
+  p.o_vc = ar.add(4 * m1);
+  p.counter = ar.add(4);
+  return p;
+}
+// stages the geometry, launches k_frustum; outputs stay in the arena
+static int launch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, const orbfe_mappoint_geometry* G,
+                          FrustumArgs fa) {
+  const size_t M = (size_t)G->m;
+  stage_h2d(m, A + p.flags_in, G->flags, M);
+  stage_h2d(m, A + p.pos, G->world_pos, 12 * M);
+  stage_h2d(m, A + p.normal, G->normal, 12 * M);
+  stage_h2d(m, A + p.mind, G->min_distance, 4 * M);
+  stage_h2d(m, A + p.maxd, G->max_distance, 4 * M);
+  int st = flush_h2d(m);
+  if (st) return st;
+  ORBFE_HIP_CHECK(hipMemsetAsync(A + p.counter, 0, 4, m->stream));
+  fa.m = G->m;
+  fa.flags_in = A + p.flags_in;
+  fa.pos = (const float*)(A + p.pos);
+  fa.normal = (const float*)(A + p.normal);
+  fa.min_d = (const float*)(A + p.mind);
+  fa.max_d = (const float*)(A + p.maxd);
+  fa.out.flags = A + p.o_flags;
+  fa.out.proj_x = (float*)(A + p.o_px);
+  fa.out.proj_y = (float*)(A + p.o_py);
+  fa.out.proj_xr = (float*)(A + p.o_pxr);
+  fa.out.level = (int32_t*)(A + p.o_lvl);
+  fa.out.view_cos = (float*)(A + p.o_vc);
+  fa.n_in_view = (int32_t*)(A + p.counter);
+  if (G->m > 0) hipLaunchKernelGGL(k_frustum, dim3((G->m + 255) / 256), dim3(256), 0, m->stream, fa);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  return ORBFE_OK;
+}
+// D2H of the per-MapPoint outputs the caller asked for, and the in-view count
+static int fetch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, int M, const orbfe_frustum_out* out,
+                         int* n_in_view) {
+  const size_t n = (size_t)M;
+  if (out && M > 0) {
+    if (out->flags) ORBFE_HIP_CHECK(hipMemcpyAsync(out->flags, A + p.o_flags, n, hipMemcpyDeviceToHost, m->stream));
+    if (out->proj_x) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_x, A + p.o_px, 4 * n, hipMemcpyDeviceToHost, m->stream));
+    if (out->proj_y) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_y, A + p.o_py, 4 * n, hipMemcpyDeviceToHost, m->stream));
+    if (out->proj_xr) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_xr, A + p.o_pxr, 4 * n, hipMemcpyDeviceToHost, m->stream));
+    if (out->level) ORBFE_HIP_CHECK(hipMemcpyAsync(out->level, A + p.o_lvl, 4 * n, hipMemcpyDeviceToHost, m->stream));
+    if (out->view_cos) ORBFE_HIP_CHECK(hipMemcpyAsync(out->view_cos, A + p.o_vc, 4 * n, hipMemcpyDeviceToHost, m->stream));
+  }
+  int32_t nv = 0;
+  ORBFE_HIP_CHECK(hipMemcpyAsync(&nv, A + p.counter, 4, hipMemcpyDeviceToHost, m->stream));
+  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  if (n_in_view) *n_in_view = nv;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_is_in_frustum(orbfe_matcher* m, const orbfe_frame_view* F, const orbfe_mappoint_geometry* G,
+                                   const float* tcw, float log_scale_factor, float viewing_cos_limit,
+                                   const orbfe_frustum_out* out, int* n_in_view) {
+  if (!m || !F || !tcw || !geom_ok(G, false) || F->nlevels <= 0)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_is_in_frustum: bad argument");
+  hipSetDevice(m->device);
+  Arena ar;
+  const FrustumPlan p = plan_frustum(ar, G->m);
+  int st = ensure_arena(m, ar.total);
+  if (st) return st;
+  FrustumArgs fa;
+  fill_frustum_args(fa, F, tcw, log_scale_factor, viewing_cos_limit);
+  if ((st = launch_frustum(m, m->arena, p, G, fa))) return st;
+  return fetch_frustum(m, m->arena, p, G->m, out, n_in_view);
+}
+
+extern "C" int orbfe_search_local_points(orbfe_matcher* m, const orbfe_frame_view* F,
+                                         const orbfe_mappoint_geometry* G, const float* tcw,
+                                         float log_scale_factor, float viewing_cos_limit, float th,
+                                         int32_t* best_idx, int* nmatches, const orbfe_frustum_out* out,
+                                         int* n_in_view) {
+  if (!m || !frame_ok(F) || !tcw || !geom_ok(G, true) || !nmatches || (G->m > 0 && !best_idx))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_local_points: bad argument");
+  hipSetDevice(m->device);
+  const int M = G->m;
+  FrustumPlan fp;
+  FrustumArgs fa;
+  fill_frustum_args(fa, F, tcw, log_scale_factor, viewing_cos_limit);
+  uint8_t* A_used = nullptr;
+  auto plan = [&](Arena& ar) -> int {
+    fp = plan_frustum(ar, M);
+    return 0;
+  };
+  auto make = [&](uint8_t* A, const orbfe_frame_view& dF, SbpQuery* dq) -> int {
+    A_used = A;
+    int st = launch_frustum(m, A, fp, G, fa);
+    if (st) return st;
+    // SearchByProjection's queries straight from the isInFrustum outputs (no host round trip);
+    // with nothing in view every query is empty and the result is the skipped matcher's
+    LocalQueryArgs qa;
+    std::memset(&qa, 0, sizeof(qa));
+    qa.mp.m = M;
+    qa.mp.flags = A + fp.o_flags;
+    qa.mp.proj_x = (const float*)(A + fp.o_px);
+    qa.mp.proj_y = (const float*)(A + fp.o_py);
+    qa.mp.proj_xr = (const float*)(A + fp.o_pxr);
+    qa.mp.level = (const int32_t*)(A + fp.o_lvl);
+    qa.mp.view_cos = (const float*)(A + fp.o_vc);
+    qa.scale_factors = dF.scale_factors;
+    qa.th = th;
+    qa.q = dq;
+    hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
+    return ORBFE_OK;
+  };
+  int st = run_sbp(m, F, M, 0, G->descriptors, nullptr, 0, plan, make, best_idx, nmatches);
+  if (st) return st;
+  if (M == 0) {
+    if (n_in_view) *n_in_view = 0;
+    return ORBFE_OK;
+  }
+  return fetch_frustum(m, A_used, fp, M, out, n_in_view);
 }

@@ -163,6 +163,39 @@ class LocalMapPoints:
 
 
 @dataclass
+class MapPointGeometry:
+    """Local-map MapPoints as Frame::isInFrustum reads them (Frame.cc:318-374)."""
+
+    flags: np.ndarray         # MPF_BAD | MPF_SEEN (| MPF_OBSERVED, passed to SearchByProjection)
+    world_pos: np.ndarray     # (M, 3) GetWorldPos()
+    normal: np.ndarray        # (M, 3) GetNormal()
+    min_distance: np.ndarray  # mfMinDistance
+    max_distance: np.ndarray  # mfMaxDistance
+    descriptors: np.ndarray   # (M, 32) GetDescriptor()
+
+    def __post_init__(self):
+        m = len(self.flags)
+        self.flags = np.ascontiguousarray(self.flags, np.uint8)
+        self.world_pos = np.ascontiguousarray(self.world_pos, np.float32).reshape(m, 3)
+        self.normal = np.ascontiguousarray(self.normal, np.float32).reshape(m, 3)
+        self.min_distance = np.ascontiguousarray(self.min_distance, np.float32).reshape(m)
+        self.max_distance = np.ascontiguousarray(self.max_distance, np.float32).reshape(m)
+        self.descriptors = np.ascontiguousarray(self.descriptors, np.uint8).reshape(m, 32)
+
+    def view(self) -> L.mappoint_geometry:
+        v = L.mappoint_geometry()
+        v.m = len(self.flags)
+        for f in ("flags", "world_pos", "normal", "min_distance", "max_distance", "descriptors"):
+            setattr(v, f, L.ptr(getattr(self, f)))
+        return v
+
+
+def log_scale_factor(scale_factor: float) -> np.float32:
+    """Frame::mfLogScaleFactor = log(mfScaleFactor) (Frame.cc:106), rounded to float."""
+    return np.float32(np.log(np.float64(np.float32(scale_factor))))
+
+
+@dataclass
 class LastFrameMapPoints:
     """LastFrame.mvpMapPoints and the per-keypoint data SearchByProjection reads from it."""
 

@@ -15,7 +15,8 @@ from typing import List, Optional, Tuple, Union
 import numpy as np
 
 from . import _lib as L
-from .frames import FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints, epipole
+from .frames import (FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints, MapPointGeometry,
+                     epipole, log_scale_factor)
 
 
 class ORBmatcher:
@@ -80,6 +81,56 @@ class ORBmatcher:
                 L.ptr(best), byref(nm)), "SearchByProjection(last frame)")
             return nm.value, best
         raise TypeError("points must be LocalMapPoints or LastFrameMapPoints")
+
+    # ---- Frame::isInFrustum / Tracking::SearchLocalPoints (orbfe_frustum.h) -----------------
+    @staticmethod
+    def _frustum_out(m: int):
+        arrs = {"flags": np.zeros(m, np.uint8), "proj_x": np.zeros(m, np.float32),
+                "proj_y": np.zeros(m, np.float32), "proj_xr": np.zeros(m, np.float32),
+                "level": np.zeros(m, np.int32), "view_cos": np.zeros(m, np.float32)}
+        o = L.frustum_out()
+        for k, a in arrs.items():
+            setattr(o, k, L.ptr(a))
+        return o, arrs
+
+    def isInFrustum(self, F: Frame, mps: MapPointGeometry, viewingCosLimit: float = 0.5,
+                    scale_factor: Optional[float] = None) -> Tuple[int, LocalMapPoints]:
+        """Frame::isInFrustum (Frame.cc:318-374) for every MapPoint (not BAD, not SEEN) with the
+        frame's pose F.tcw. Returns (nToMatch, LocalMapPoints carrying mbTrackInView and the
+        mTrackProj* / mnTrackScaleLevel / mTrackViewCos members it writes)."""
+        if F.tcw is None:
+            raise ValueError("F.tcw (mTcw) is required")
+        sf = scale_factor if scale_factor is not None else float(F.scale_factors[1])
+        fv, gv = F.view(), mps.view()
+        o, arrs = self._frustum_out(len(mps.flags))
+        n = c_int()
+        L.check(self._lib.orbfe_is_in_frustum(self._h, byref(fv), byref(gv), L.ptr(F.tcw),
+                                              float(log_scale_factor(sf)), float(viewingCosLimit),
+                                              byref(o), byref(n)), "isInFrustum")
+        return n.value, LocalMapPoints(arrs["flags"], arrs["proj_x"], arrs["proj_y"],
+                                       arrs["proj_xr"], arrs["level"], arrs["view_cos"],
+                                       mps.descriptors)
+
+    def SearchLocalPoints(self, F: Frame, mps: MapPointGeometry, th: float,
+                          viewingCosLimit: float = 0.5, scale_factor: Optional[float] = None
+                          ) -> Tuple[int, np.ndarray, int, LocalMapPoints]:
+        """Tracking::SearchLocalPoints' projection + matching (Tracking.cc:1186-1213) in one
+        device pass: isInFrustum(pMP, 0.5) then SearchByProjection(F, vpLocalMapPoints, th).
+        Returns (nmatches, best_idx, nToMatch, LocalMapPoints as isInFrustum left them)."""
+        if F.tcw is None:
+            raise ValueError("F.tcw (mTcw) is required")
+        sf = scale_factor if scale_factor is not None else float(F.scale_factors[1])
+        fv, gv = F.view(), mps.view()
+        o, arrs = self._frustum_out(len(mps.flags))
+        best = np.full(len(mps.flags), -1, np.int32)
+        nm, nv = c_int(), c_int()
+        L.check(self._lib.orbfe_search_local_points(
+            self._h, byref(fv), byref(gv), L.ptr(F.tcw), float(log_scale_factor(sf)),
+            float(viewingCosLimit), float(th), L.ptr(best), byref(nm), byref(o), byref(nv)),
+            "SearchLocalPoints")
+        lm = LocalMapPoints(arrs["flags"], arrs["proj_x"], arrs["proj_y"], arrs["proj_xr"],
+                            arrs["level"], arrs["view_cos"], mps.descriptors)
+        return nm.value, best, nv.value, lm
 
     def set_max_rounds(self, rounds: int) -> None:
         L.check(self._lib.orbfe_matcher_set_max_rounds(self._h, int(rounds)), "set_max_rounds")

@@ -164,6 +164,55 @@ def make_local_mappoints(F: Frame, m: int, rng: np.random.Generator, match_frac:
     return LocalMapPoints(flags, px, py, pxr, level, vc, desc)
 
 
+def make_local_map(C: Frame, m: int, rng: np.random.Generator, match_frac: float = 0.5,
+                   max_flips: int = 30) -> "MapPointGeometry":
+    """Local-map MapPoints for isInFrustum + SearchByProjection (Tracking.cc:1186-1213): most lie
+    in front of C near one of its keypoints, with MapPoint::UpdateNormalAndDepth-style distance
+    bounds (MapPoint.cc:376-400) around C's keypoint level; the rest fail each isInFrustum test
+    (behind the camera, outside the image, outside the scale-invariance range, oblique normal)."""
+    from .frames import MapPointGeometry
+    K = C.N
+    Rcw = C.tcw[:, :3].astype(np.float64)
+    tcw = C.tcw[:, 3].astype(np.float64)
+    Ow = -Rcw.T @ tcw
+    src = rng.integers(0, max(K, 1), m)
+    z = rng.uniform(1.0, 30.0, m)
+    u = (C.keys_un["x"][src] if K else rng.uniform(C.min_x, C.max_x, m)) + rng.normal(0, 1.0, m)
+    v = (C.keys_un["y"][src] if K else rng.uniform(C.min_y, C.max_y, m)) + rng.normal(0, 1.0, m)
+    kind = rng.random(m)
+    u[kind < 0.05] = rng.uniform(-200, -10, int((kind < 0.05).sum()))  # outside the image
+    pc = np.stack([(u - C.cx) / C.fx * z, (v - C.cy) / C.fy * z, z], axis=1)
+    behind = (kind >= 0.05) & (kind < 0.08)
+    pc[behind] *= -1.0
+    pw = (Rcw.T @ (pc - tcw).T).T
+    dist = np.linalg.norm(pw - Ow, axis=1)
+    oct_ = C.keys_un["octave"][src] if K else np.zeros(m, np.int32)
+    sf = np.float64(C.scale_factors[1]) if len(C.scale_factors) > 1 else 1.2
+    nl = len(C.scale_factors)
+    maxd = dist * sf ** (oct_ + rng.uniform(-0.45, 0.45, m))
+    far = (kind >= 0.08) & (kind < 0.12)
+    maxd[far] = dist[far] / 1.5                 # dist > 1.2 * mfMaxDistance
+    mind = maxd / np.float64(C.scale_factors[nl - 1])
+    near = (kind >= 0.12) & (kind < 0.15)
+    mind[near] = dist[near] * 1.5               # dist < 0.8 * mfMinDistance
+    nrm = (pw - Ow) / dist[:, None]
+    nrm += rng.normal(0, 0.1, nrm.shape)
+    oblique = (kind >= 0.15) & (kind < 0.2)
+    nrm[oblique] = -nrm[oblique]
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    desc = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+    sel = np.nonzero(rng.random(m) < match_frac)[0]
+    if K and len(sel):
+        desc[sel] = flip_bits(C.descriptors[src[sel]], rng.integers(0, max_flips + 1, len(sel)), rng)
+    flags = np.full(m, L.MPF_OBSERVED, np.uint8)
+    flags[rng.random(m) < 0.05] |= np.uint8(L.MPF_BAD)
+    flags[rng.random(m) < 0.1] |= np.uint8(L.MPF_SEEN)
+    flags[rng.random(m) < 0.2] &= ~np.uint8(L.MPF_OBSERVED)
+    flags[rng.random(m) < 0.3] |= np.uint8(L.MPF_TRACK_IN_VIEW)  # stale: isInFrustum resets it
+    return MapPointGeometry(flags, pw.astype(np.float32), nrm.astype(np.float32),
+                            mind.astype(np.float32), maxd.astype(np.float32), desc)
+
+
 def make_lastframe(C: Frame, n: int, rng: np.random.Generator, motion: np.ndarray,
                    match_frac: float = 0.6, max_flips: int = 30) -> LastFrameMapPoints:
     """Last-frame MapPoints that re-project near current keypoints after a small motion."""

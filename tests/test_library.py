@@ -10,7 +10,7 @@ import pytest
 from conftest import gpu_available
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = ["orbfe.h", "orbfe_match_batch.h", "orbfe_debug.h", "orbfe_synth.h", "orbfe_vocab.h",
+HEADERS = ["orbfe.h", "orbfe_match_batch.h", "orbfe_debug.h", "orbfe_synth.h", "orbfe_vocab.h", "orbfe_frustum.h",
            "orbfe_stereo.h"]
 
 
