@@ -334,7 +334,7 @@ def main():
     if rank == 0 and world == 1:
         out["host_boundary"] = host_boundary_rate(ext, host)
         if not args.no_legs:
-            out["legs"] = {"c5_search_by_projection": sbp_leg(args),
+            out["legs"] = {"c5_search_local_points": sbp_leg(args),
                            "compute_stereo_matches": stereo_leg(args, ext, d_img, host, B, H, W, cap,
                                                                 cam["bf"], float(dummy.mb))}
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -427,33 +427,40 @@ def pipeline_bytes_per_stereo_frame(geo, counts, B):
 
 
 def sbp_leg(args, m_points=50000, reps=20):
-    """Secondary measurement (BASELINE config C5 shape): ORBmatcher::SearchByProjection(Frame,
-    50k local MapPoints, th=3) on a 640x480 frame, through the host-buffer C ABI (frame and
-    MapPoint SoA uploaded every call, so PCIe is included), beside the CPU oracle on the same
-    input. Reported, not `value`."""
+    """Secondary measurement (BASELINE config C5 shape): Tracking::SearchLocalPoints' hot part on a
+    640x480 frame against 50k local MapPoints -- Frame::isInFrustum(pMP, 0.5) for every MapPoint,
+    then ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th=3) (Tracking.cc:1186-1213) --
+    through the host-buffer C ABI orbfe_search_local_points (frame and MapPoint SoA uploaded every
+    call, so PCIe is included), beside the CPU oracle on the same input (one core, -O3
+    -march=native) and a bit-exact check of the two. Reported, not `value`."""
     from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame
     from orb_slam2_2021_amd import synthetic as S
+    from orb_slam2_2021_amd.frames import log_scale_factor
     ext = ORBextractor(args.nfeatures, 1.2, 8, 12, 7)  # arducam.yaml:126-127
     k, d = ext(synth_frame(7, 480, 640))
     rng = np.random.default_rng(0x50C0DE)
     F = S.make_frame(k, d, ext.GetScaleFactors(), ext.GetScaleSigmaSquares(), 480, 640,
-                     S.ARDUCAM_CAM, rng, mp_frac=0.0)
-    mps = S.make_local_mappoints(F, m_points, rng)
-    m = ORBmatcher(0.8, True)  # Tracking.cc:1207
-    nm, _ = m.SearchByProjection(F, mps, 3.0)
+                     S.ARDUCAM_CAM, rng, mp_frac=0.0, tcw=S.pose(tx=0.1, yaw=0.02))
+    G = S.make_local_map(F, m_points, rng)
+    m = ORBmatcher(0.8, True)  # Tracking.cc:1206
+    nm, best, nv, _ = m.SearchLocalPoints(F, G, 3.0)
     t0 = time.perf_counter()
     for _ in range(reps):
-        m.SearchByProjection(F, mps, 3.0)
+        m.SearchLocalPoints(F, G, 3.0)
     gpu_s = (time.perf_counter() - t0) / reps
     out = {"frames_per_s": round(1.0 / gpu_s, 1), "ms_per_frame": round(1e3 * gpu_s, 3),
-           "map_points": m_points, "keypoints": int(len(k)), "matches": int(nm),
-           "what": "host C ABI per call (H2D of frame + MapPoints, kernels, D2H), 1 GPU"}
+           "map_points": m_points, "in_view": int(nv), "keypoints": int(len(k)),
+           "matches": int(nm),
+           "what": "orbfe_search_local_points per call (H2D of frame + MapPoints, isInFrustum + "
+                   "SearchByProjection kernels, D2H), 1 GPU"}
     if not args.no_cpu:
         from oracle import orbref
+        lsf = log_scale_factor(1.2)
+        orbref.lib("native")
         t0 = time.perf_counter()
-        nr, _ = orbref.search_by_projection_local(F, mps, 3.0, 0.8)
+        nr, br, nvr, _ = orbref.search_local_points(F, G, lsf, 3.0, 0.8, kind="native")
         out["cpu_oracle_ms_per_frame"] = round(1e3 * (time.perf_counter() - t0), 3)
-        out["cpu_matches_equal"] = bool(nr == nm)
+        out["cpu_bit_exact"] = bool(nr == nm and nvr == nv and np.array_equal(br, best))
     return out
 
 

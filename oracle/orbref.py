@@ -291,10 +291,11 @@ def is_in_frustum(F, mps, log_sf: float, cos_limit: float = 0.5):
     return n.value, arrs
 
 
-def search_local_points(F, mps, log_sf: float, th: float, nnratio: float, cos_limit: float = 0.5):
+def search_local_points(F, mps, log_sf: float, th: float, nnratio: float, cos_limit: float = 0.5,
+                        kind: str = "checker"):
     """Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:1186-1213).
     Returns (nmatches, best_idx, n_in_view, arrays)."""
-    L = lib()
+    L = lib(kind)
     fv, gv = F.view(), mps.view()
     o, arrs = _frustum_out(len(mps.flags))
     best = np.full(len(mps.flags), -1, np.int32)

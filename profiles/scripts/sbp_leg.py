@@ -1,4 +1,4 @@
-"""Run the C5-shape SearchByProjection leg alone (for rocprofv3 traces)."""
+"""Run the C5-shape SearchLocalPoints leg (isInFrustum + SearchByProjection) alone, for rocprofv3."""
 import argparse
 import os
 import sys
