@@ -286,7 +286,7 @@ def main():
     frames = world * B * args.steps
     value = frames / elapsed
     counts = sets[0].cnt.cpu().numpy()
-    cand = sum(len(ext.debug_candidates(l, image=i)) for i in range(n_img) for l in range(8))
+    cand = ext.debug_candidate_total()
     nm = sets[0].nm.cpu().numpy()
     geo = ext.geometry(H, W)
     roof = roofline(timed if dominant in timed else probe, dominant, geo, counts, cand, n_img,

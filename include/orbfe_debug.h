@@ -13,6 +13,8 @@ extern "C" {
  * coordinates relative to minBorder (16). */
 int orbfe_debug_get_candidates(orbfe_extractor* h, int image, int level, uint32_t* out, int cap,
                                int* n);
+/* FAST candidates of every image and level of the last extract call (one D2H of the cell counts). */
+int orbfe_debug_candidate_total(orbfe_extractor* h, long long* total);
 /* Octree survivors of (image, level) in output order, level coordinates. */
 int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level, uint32_t* out, int cap,
                                int* n);

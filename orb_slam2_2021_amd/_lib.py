@@ -132,6 +132,7 @@ _SIGNATURES = {
     "orbfe_search_for_triangulation_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_int,
                                                             c_void_p]),
     "orbfe_debug_get_candidates": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
+    "orbfe_debug_candidate_total": (c_int, [c_void_p, POINTER(ctypes.c_longlong)]),
     "orbfe_debug_get_level_keys": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, POINTER(c_int)]),
     "orbfe_debug_get_blurred": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),
     "orbfe_debug_geometry": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int]),

@@ -175,6 +175,31 @@ __device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum
   return tot;
 }
 
+// Exclusive scan of data[0..n) in LDS by the 1024 threads of the block (wsum: 16 ints).
+__device__ inline void block_scan_excl_1024(int* data, int n, int* wsum) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int per = (n + 1023) / 1024;
+  const int beg = min(t * per, n), end = min(beg + per, n);
+  int s = 0;
+  for (int i = beg; i < end; i++) s += data[i];
+  int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int run = inc - s;
+  for (int q = 0; q < w; q++) run += wsum[q];
+  for (int i = beg; i < end; i++) {
+    const int v = data[i];
+    data[i] = run;
+    run += v;
+  }
+  __syncthreads();
+}
+
 #define ORBFE_HIP_CHECK(expr)                                     \
   do {                                                            \
     hipError_t _e = (expr);                                       \

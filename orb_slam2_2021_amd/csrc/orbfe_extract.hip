@@ -2439,6 +2439,17 @@ extern "C" int orbfe_debug_get_candidates(orbfe_extractor* h, int image, int lev
   return (out && tot > cap) ? ORBFE_ERR_CAPACITY : ORBFE_OK;
 }
 
+extern "C" int orbfe_debug_candidate_total(orbfe_extractor* h, long long* total) {
+  if (!h || !total || h->last_n <= 0) return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
+  std::vector<int32_t> cnt((size_t)h->last_n * h->cells.size());
+  ORBFE_HIP_CHECK(hipMemcpy(cnt.data(), h->d_cellcnt, sizeof(int32_t) * cnt.size(), hipMemcpyDeviceToHost));
+  long long t = 0;
+  for (int32_t c : cnt) t += c;
+  *total = t;
+  return ORBFE_OK;
+}
+
 extern "C" int orbfe_debug_get_level_keys(orbfe_extractor* h, int image, int level,
                                           uint32_t* out, int cap, int* n) {
   if (!h || !n || image < 0 || image >= h->last_n || level < 0 || level >= h->nlevels)

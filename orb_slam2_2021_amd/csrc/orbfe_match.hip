@@ -447,48 +447,53 @@ struct GridArgs {
   int32_t* items;
 };
 
-__global__ __launch_bounds__(256) void k_grid(GridArgs g) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t skeys[];
+// Counting sort by cell (1024 threads): cell histogram, scan, scatter, then each cell's few
+// items put back in ascending keypoint order (mGrid[i][j] is filled in index order, Frame.cc:286-293,
+// and GetFeaturesInArea's candidate order decides ties).
+__global__ __launch_bounds__(1024) void k_grid(GridArgs g) {
+  extern __shared__ int s_grid[];  // GRID_CELLS + 1 counters, 16 scan ints, then n items
+  int* cnt = s_grid;
+  int* wsum = s_grid + GRID_CELLS + 1;
+  int* items = wsum + 16;
   const int t = threadIdx.x;
-  int P2 = 1;
-  while (P2 < g.n) P2 <<= 1;
-  for (int i = t; i < P2; i += 256) {
-    uint32_t key = 0xffffffffu;
-    if (i < g.n) {
-      const orbfe_keypoint kp = g.keys[i];
-      // PosInGrid (Frame.cc:435-445): round() half away from zero on the float product
-      const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
-      const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
-      if (px >= 0 && px < GRID_COLS && py >= 0 && py < GRID_ROWS)
-        key = ((uint32_t)(px * GRID_ROWS + py) << 16) | (uint32_t)i;
-    }
-    skeys[i] = key;
+  auto cell_of = [&](int i) {
+    const orbfe_keypoint kp = g.keys[i];
+    // PosInGrid (Frame.cc:435-445): round() half away from zero on the float product
+    const int px = (int)roundf((kp.x - g.min_x) * g.inv_w);
+    const int py = (int)roundf((kp.y - g.min_y) * g.inv_h);
+    return (px >= 0 && px < GRID_COLS && py >= 0 && py < GRID_ROWS) ? px * GRID_ROWS + py : -1;
+  };
+  for (int c = t; c <= GRID_CELLS; c += 1024) cnt[c] = 0;
+  __syncthreads();
+  for (int i = t; i < g.n; i += 1024) {
+    const int c = cell_of(i);
+    if (c >= 0) atomicAdd(&cnt[c], 1);
   }
   __syncthreads();
-  for (int k = 2; k <= P2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
-        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
-        const uint32_t x = skeys[i], y = skeys[ixj];
-        if ((i & k) == 0 ? (x > y) : (x < y)) {
-          skeys[i] = y;
-          skeys[ixj] = x;
-        }
+  block_scan_excl_1024(cnt, GRID_CELLS + 1, wsum);
+  for (int c = t; c <= GRID_CELLS; c += 1024) g.start[c] = cnt[c];  // start[GRID_CELLS] = keys in grid
+  __syncthreads();
+  for (int i = t; i < g.n; i += 1024) {
+    const int c = cell_of(i);
+    if (c >= 0) items[atomicAdd(&cnt[c], 1)] = i;
+  }
+  __syncthreads();
+  // cnt[c] is now the end of cell c; its start is the end of cell c - 1
+  for (int c = t; c < GRID_CELLS; c += 1024) {
+    const int b = c ? cnt[c - 1] : 0, e = cnt[c];
+    for (int x = b + 1; x < e; x++) {  // insertion sort of the cell's items (a handful)
+      const int v = items[x];
+      int y = x - 1;
+      while (y >= b && items[y] > v) {
+        items[y + 1] = items[y];
+        y--;
       }
-      __syncthreads();
+      items[y + 1] = v;
     }
   }
-  for (int i = t; i < g.n; i += 256) g.items[i] = (int32_t)(skeys[i] & 0xffffu);
-  for (int c = t; c <= GRID_CELLS; c += 256) {
-    const uint32_t probe = (uint32_t)c << 16;
-    int lo = 0, hi = g.n;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (skeys[mid] < probe) lo = mid + 1;
-      else hi = mid;
-    }
-    g.start[c] = lo;  // start[GRID_CELLS] = number of keys inside the grid
-  }
+  __syncthreads();
+  const int total = cnt[GRID_CELLS - 1];
+  for (int i = t; i < total; i += 1024) g.items[i] = items[i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1255,9 +1260,8 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   g.inv_h = F->grid_inv_h;
   g.start = (int32_t*)(A + og_start);
   g.items = (int32_t*)(A + og_items);
-  int P2 = 1;
-  while (P2 < F->n) P2 <<= 1;
-  hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sizeof(uint32_t) * P2, m->stream, g);
+  hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), sizeof(int) * (GRID_CELLS + 1 + 16 + std::max(F->n, 1)),
+                     m->stream, g);
   {
     SbpInit in;
     in.res0 = (int32_t*)(A + ores0);

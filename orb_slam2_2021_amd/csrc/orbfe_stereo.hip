@@ -52,31 +52,6 @@ struct StereoGeom {
 // ---- k_stereo_rows ----------------------------------------------------------------------------
 constexpr int ROWS_THREADS = 1024;
 
-// exclusive scan of data[0..n) in LDS by the ROWS_THREADS threads of the block (wsum: 16 ints)
-__device__ inline void scan_excl_1024(int* data, int n, int* wsum) {
-  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int per = (n + ROWS_THREADS - 1) / ROWS_THREADS;
-  const int beg = min(t * per, n), end = min(beg + per, n);
-  int s = 0;
-  for (int i = beg; i < end; i++) s += data[i];
-  int inc = s;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  int run = inc - s;
-  for (int q = 0; q < w; q++) run += wsum[q];
-  for (int i = beg; i < end; i++) {
-    const int v = data[i];
-    data[i] = run;
-    run += v;
-  }
-  __syncthreads();
-}
-
 // Counting sort of pair p's right keypoints into buckets (octave, floor(y)); bucket entry
 // {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544.
 __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
@@ -98,7 +73,7 @@ __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, cons
   };
   for (int i = t; i < nR; i += ROWS_THREADS) atomicAdd(&s_hist[bucket(K[i].y, K[i].octave)], 1);
   __syncthreads();
-  scan_excl_1024(s_hist, ntab, wsum);
+  block_scan_excl_1024(s_hist, ntab, wsum);
   int32_t* rs = row_start + (long long)p * ntab;
   for (int r = t; r < ntab; r += ROWS_THREADS) rs[r] = s_hist[r];
   __syncthreads();

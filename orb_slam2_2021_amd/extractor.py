@@ -276,6 +276,12 @@ class ORBextractor:
                                                      byref(n)), "debug_candidates")
         return out[:n.value]
 
+    def debug_candidate_total(self) -> int:
+        """FAST candidates over every image and level of the last call."""
+        t = ctypes.c_longlong()
+        L.check(self._lib.orbfe_debug_candidate_total(self._h, byref(t)), "debug_candidate_total")
+        return t.value
+
     def debug_level_keys(self, level: int, image: int = 0) -> np.ndarray:
         n = c_int()
         L.check(self._lib.orbfe_debug_get_level_keys(self._h, image, level, None, 0, byref(n)),

@@ -147,3 +147,11 @@ def test_repeatable(require_gpu):
     a = ext(img)
     b = ext(img)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_candidate_total_matches_per_level_lists(require_gpu):
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    imgs = [synth_frame(i, 376, 1241) for i in range(3)]
+    ext.extract_batch(imgs)
+    want = sum(len(ext.debug_candidates(l, image=i)) for i in range(3) for l in range(8))
+    assert ext.debug_candidate_total() == want > 0
