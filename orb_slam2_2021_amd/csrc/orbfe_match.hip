@@ -441,10 +441,11 @@ __global__ __launch_bounds__(256) void k_sft_finish(const orbfe_sft_pair* pairs,
 // Frame grid (AssignFeaturesToGrid) as CSR: start[GRID_CELLS + 1], items[n]
 struct GridArgs {
   const orbfe_keypoint* keys;
+  const float* u_right;
   int n;
   float min_x, min_y, inv_w, inv_h;
   int32_t* start;
-  int32_t* items;
+  uint4* recs;  // per grid item: {x, y, uRight (float bits), index | octave << 16}
 };
 
 // Counting sort by cell (1024 threads): cell histogram, scan, scatter, then each cell's few
@@ -493,7 +494,12 @@ __global__ __launch_bounds__(1024) void k_grid(GridArgs g) {
   }
   __syncthreads();
   const int total = cnt[GRID_CELLS - 1];
-  for (int i = t; i < total; i += 1024) g.items[i] = items[i];
+  for (int i = t; i < total; i += 1024) {  // the fields the window walks read, in one 16-B record
+    const int k = items[i];
+    const orbfe_keypoint kp = g.keys[k];
+    g.recs[i] = make_uint4(__float_as_uint(kp.x), __float_as_uint(kp.y), __float_as_uint(g.u_right[k]),
+                           (unsigned)k | ((unsigned)kp.octave << 16));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -508,7 +514,7 @@ struct SbpQuery {
 struct SbpArgs {
   orbfe_frame_view F;        // device pointers
   const int32_t* grid_start;
-  const int32_t* grid_items;
+  const uint4* grid_recs;
   const SbpQuery* q;
   const uint8_t* qdesc;       // m x 32
   int m;
@@ -600,8 +606,12 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
       const int c = ix * GRID_ROWS + iy;
       const int e = a.grid_start[c + 1];
       for (int j = a.grid_start[c]; j < e; j++) {
-        const int k = a.grid_items[j];
-        const orbfe_keypoint kp = F.keys_un[k];
+        const uint4 rec = a.grid_recs[j];
+        const int k = (int)(rec.w & 0xffffu);
+        struct {
+          float x, y;
+          int octave;
+        } kp = {__uint_as_float(rec.x), __uint_as_float(rec.y), (int)(rec.w >> 16)};
         if (checkLevels) {
           if (kp.octave < q.min_level) continue;
           if (q.max_level >= 0 && kp.octave > q.max_level) continue;
@@ -609,7 +619,7 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
         const float distx = kp.x - x, disty = kp.y - y;
         if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
         if (!RECORD && blocked(k)) continue;
-        const float ur = F.u_right[k];
+        const float ur = __uint_as_float(rec.z);
         if (ur > 0) {
           const float er = fabsf(q.xr - ur);
           if (er > q.er_lim) continue;
@@ -664,20 +674,171 @@ __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = a.round + 1;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < a.F.n) a.owner_next[i] = 0x7fffffff;
-  if (i >= a.m) return;
-  auto blocked = [&](int k) { return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i; };
-  int res;
-  if (!a.cand_n) {
-    res = sbp_one(a, i, blocked);
-  } else if (a.round == 0) {
-    res = sbp_one<decltype(blocked), true>(a, i, blocked);
-  } else {
-    const int n = a.cand_n[i];
-    res = n >= 0 ? sbp_cached(a, i, n, blocked) : sbp_one(a, i, blocked);
+  bool changed = false;
+  if (i < a.m) {
+    auto blocked = [&](int k) { return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i; };
+    int res;
+    if (!a.cand_n) {
+      res = sbp_one(a, i, blocked);
+    } else if (a.round == 0) {
+      res = sbp_one<decltype(blocked), true>(a, i, blocked);
+    } else {
+      const int n = a.cand_n[i];
+      res = n >= 0 ? sbp_cached(a, i, n, blocked) : sbp_one(a, i, blocked);
+    }
+    a.res_cur[i] = res;
+    if (res >= 0 && (a.q[i].flags & 2)) atomicMin(&a.owner_cur[res], i);
+    changed = res != a.res_prev[i];
+  }
+  // "some result changed": a plain store of 1 (every writer stores the same value). A device-scope
+  // atomic on one address is serialised at the coherence point across the XCDs (~10 ns each):
+  // one per query or per wavefront was most of this kernel's time.
+  if (wave_ballot(changed) && lane_id() == 0) a.state[2 + a.round] = 1;
+}
+
+// Round 0 with the candidate cache, 16 lanes (one DPP row) per MapPoint. The window's grid cells
+// are taken 16 at a time in GetFeaturesInArea order (ix outer, iy inner, Frame.cc:394-430), one
+// cell per lane: a counting pass and a 16-lane scan place each lane's candidates in that order in
+// the cache, then a second pass computes their distances. The sequential best / second-best
+// bookkeeping of :106-118 / :1417-1450 equals the two smallest (dist, position) keys over the
+// unblocked candidates with dist < 256, so each lane keeps its two smallest and the row merges.
+__device__ __forceinline__ unsigned long long min_u64(unsigned long long a, unsigned long long b) {
+  return a < b ? a : b;
+}
+__device__ __forceinline__ unsigned long long max_u64(unsigned long long a, unsigned long long b) {
+  return a < b ? b : a;
+}
+#define SBP_FLAT 128  // flattened grid items per 16-lane row and pass (LDS)
+__global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
+  __shared__ int s_flat[16][SBP_FLAT];
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = 1;
+  if (t < a.F.n) a.owner_next[t] = 0x7fffffff;
+  const int j = threadIdx.x & 15, row = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + row;
+  if (i >= a.m) return;  // the 16 lanes of a row leave together; rows sync with wave_sync only
+  int* flat = s_flat[row];
+  const SbpQuery q = a.q[i];
+  const orbfe_frame_view& F = a.F;
+  const float x = q.x, y = q.y, r = q.r;
+  int nMinCellX = 0, nMaxCellX = -1, nMinCellY = 0, nMaxCellY = -1;
+  if (q.flags & 1) {  // GetFeaturesInArea's cell range (Frame.cc:383-397); empty when out of grid
+    nMinCellX = max(0, (int)floorf((x - F.min_x - r) * F.grid_inv_w));
+    nMaxCellX = min(GRID_COLS - 1, (int)ceilf((x - F.min_x + r) * F.grid_inv_w));
+    nMinCellY = max(0, (int)floorf((y - F.min_y - r) * F.grid_inv_h));
+    nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((y - F.min_y + r) * F.grid_inv_h));
+    if (nMinCellX >= GRID_COLS || nMaxCellX < 0 || nMinCellY >= GRID_ROWS || nMaxCellY < 0)
+      nMaxCellX = nMinCellX - 1;
+  }
+  const int ny = nMaxCellY - nMinCellY + 1;
+  const int ncell = nMaxCellX >= nMinCellX && ny > 0 ? (nMaxCellX - nMinCellX + 1) * ny : 0;
+  const bool checkLevels = (q.min_level > 0) || (q.max_level >= 0);
+  uint4 dq0 = make_uint4(0, 0, 0, 0), dq1 = dq0;
+  if (ncell) load_desc(a.qdesc + (size_t)i * 32, dq0, dq1);
+  int16_t* ck = a.cand_k + (size_t)i * SBP_CAND;
+  uint8_t* cd = a.cand_d + (size_t)i * SBP_CAND;
+  uint8_t* cl = a.cand_l + (size_t)i * SBP_CAND;
+  const unsigned long long NONE = ~0ull;
+  unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
+  int kb1 = -1;                             // keypoint of k1
+  int total = 0;                            // candidates so far, in GetFeaturesInArea order
+  const int rowbase = (threadIdx.x & 63) & ~15;  // first lane of this row in the wavefront
+  for (int o0 = 0; o0 < ncell; o0 += 16) {
+    // 16 cells, one per lane: item ranges and their offsets in the flattened list
+    const int o = o0 + j;
+    int b = 0, e = 0;
+    if (o < ncell) {
+      const int c = (nMinCellX + o / ny) * GRID_ROWS + nMinCellY + o % ny;
+      b = a.grid_start[c];
+      e = a.grid_start[c + 1];
+    }
+    const int cnt = e - b;
+    int inc = cnt;
+#pragma unroll
+    for (int s2 = 1; s2 < 16; s2 <<= 1) {
+      const int y2 = __shfl_up(inc, s2, 16);
+      if (j >= s2) inc += y2;
+    }
+    const int nflat = __shfl(inc, 15, 16), off = inc - cnt;
+    for (int f0 = 0; f0 < nflat; f0 += SBP_FLAT) {
+      for (int u = max(off, f0); u < min(off + cnt, f0 + SBP_FLAT); u++) flat[u - f0] = b + (u - off);
+      wave_sync();
+      const int nf = min(nflat - f0, SBP_FLAT);
+      for (int u0 = 0; u0 < nf; u0 += 16) {
+        const int u = u0 + j;
+        bool pass = false;
+        int k = 0, oct = 0;
+        if (u < nf) {  // window / level / stereo gates of :86-103, :1412-1427
+          const uint4 rec = a.grid_recs[flat[u]];
+          k = (int)(rec.w & 0xffffu);
+          oct = (int)(rec.w >> 16);
+          pass = true;
+          if (checkLevels) {
+            if (oct < q.min_level) pass = false;
+            if (q.max_level >= 0 && oct > q.max_level) pass = false;
+          }
+          const float distx = __uint_as_float(rec.x) - x, disty = __uint_as_float(rec.y) - y;
+          if (!(fabsf(distx) < r && fabsf(disty) < r)) pass = false;
+          const float ur = __uint_as_float(rec.z);
+          if (ur > 0 && fabsf(q.xr - ur) > q.er_lim) pass = false;
+        }
+        const uint64_t bm = (wave_ballot(pass) >> rowbase) & 0xffffull;
+        if (pass) {
+          const int pos = total + __popcll(bm & ((1ull << j) - 1));
+          uint4 d0, d1;
+          load_desc(F.descriptors + (size_t)k * 32, d0, d1);
+          const int dist = hamming256(dq0, dq1, d0, d1);
+          if (pos < SBP_CAND) {
+            ck[pos] = (int16_t)k;
+            cd[pos] = (uint8_t)dist;
+            cl[pos] = (uint8_t)oct;
+          }
+          if (dist < 256 && F.mp_state[k] != ORBFE_MP_OBSERVED) {  // blocked(k) in round 0
+            const unsigned long long key =
+                ((unsigned long long)dist << 40) | ((unsigned long long)pos << 8) | (unsigned)oct;
+            if (key < k1) {
+              k2 = k1;
+              k1 = key;
+              kb1 = k;
+            } else if (key < k2) {
+              k2 = key;
+            }
+          }
+        }
+        total += __popcll(bm);
+      }
+      wave_sync();  // the row's flat list is rewritten by the next pass
+    }
+  }
+  // top-2 over the row (the keypoint of the smallest key travels with it)
+#pragma unroll
+  for (int s2 = 8; s2 > 0; s2 >>= 1) {
+    const unsigned long long o1 = __shfl_xor(k1, s2, 16), o2 = __shfl_xor(k2, s2, 16);
+    const int ob = __shfl_xor(kb1, s2, 16);
+    k2 = min_u64(max_u64(k1, o1), min_u64(k2, o2));
+    if (o1 < k1) {
+      k1 = o1;
+      kb1 = ob;
+    }
+  }
+  if (j != 0) return;
+  a.cand_n[i] = total <= SBP_CAND ? total : -1;
+  int res = -1;
+  if (k1 != NONE) {
+    SbpBest bb;
+    bb.bestDist = (int)(k1 >> 40);
+    bb.bestLevel = (int)(k1 & 0xff);
+    bb.bestIdx = kb1;
+    if (k2 != NONE) {
+      bb.bestDist2 = (int)(k2 >> 40);
+      bb.bestLevel2 = (int)(k2 & 0xff);
+    }
+    res = bb.result(a.mode, a.nnratio);
   }
   a.res_cur[i] = res;
-  if (res >= 0 && (a.q[i].flags & 2)) atomicMin(&a.owner_cur[res], i);
-  if (res != a.res_prev[i]) atomicOr(&a.state[2 + a.round], 1);
+  if (res >= 0 && (q.flags & 2)) atomicMin(&a.owner_cur[res], i);
+  const uint64_t changed = wave_ballot(res != a.res_prev[i]);  // plain store, see k_sbp_round
+  if (changed && lane_id() == __ffsll((long long)wave_ballot(true)) - 1) a.state[2] = 1;
 }
 
 struct SbpFinishArgs {
@@ -710,8 +871,12 @@ __global__ __launch_bounds__(256) void k_sbp_collect(SbpFinishArgs f) {
     f.best_out[i] = r;
     c = r >= 0;
   }
+  // one atomic per block (same-address device atomics serialise across the XCDs)
+  __shared__ int s_c[4];
   c = wave_sum(c);
-  if (lane_id() == 0 && c) atomicAdd(f.nmatches, c);
+  if (lane_id() == 0) s_c[wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0 && s_c[0] + s_c[1] + s_c[2] + s_c[3]) atomicAdd(f.nmatches, s_c[0] + s_c[1] + s_c[2] + s_c[3]);
 }
 
 __global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* blocked_scratch) {
@@ -870,8 +1035,11 @@ __global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
       a.out.view_cos[i] = viewCos;
     }
   }
+  __shared__ int s_n[4];  // one atomic per block (same-address device atomics serialise)
   const uint64_t b = wave_ballot(in);
-  if (lane_id() == 0 && b) atomicAdd(a.n_in_view, __popcll(b));
+  if (lane_id() == 0) s_n[wave_id()] = __popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_n[0] + s_n[1] + s_n[2] + s_n[3]) atomicAdd(a.n_in_view, s_n[0] + s_n[1] + s_n[2] + s_n[3]);
 }
 
 // Queries of SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1358-1410):
@@ -1222,7 +1390,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   const size_t oqd = ar.add(32 * (size_t)std::max(nq, 1));
   const size_t oqa = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t og_start = ar.add(4 * (GRID_CELLS + 1));
-  const size_t og_items = ar.add(4 * (size_t)std::max(F->n, 1));
+  const size_t og_items = ar.add(16 * (size_t)std::max(F->n, 1));
   const size_t oq = ar.add(sizeof(SbpQuery) * std::max(nq, 1));
   const size_t ores0 = ar.add(4 * (size_t)std::max(nq, 1));
   const size_t ores1 = ar.add(4 * (size_t)std::max(nq, 1));
@@ -1259,7 +1427,8 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   g.inv_w = F->grid_inv_w;
   g.inv_h = F->grid_inv_h;
   g.start = (int32_t*)(A + og_start);
-  g.items = (int32_t*)(A + og_items);
+  g.recs = (uint4*)(A + og_items);
+  g.u_right = dF.u_right;
   hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), sizeof(int) * (GRID_CELLS + 1 + 16 + std::max(F->n, 1)),
                      m->stream, g);
   {
@@ -1279,7 +1448,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   std::memset(&a, 0, sizeof(a));
   a.F = dF;
   a.grid_start = g.start;
-  a.grid_items = g.items;
+  a.grid_recs = g.recs;
   a.q = dq;
   a.qdesc = A + oqd;
   a.m = nq;
@@ -1303,7 +1472,11 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
     a.owner_cur = own[r % 3];
     a.owner_prev = own[(r + 2) % 3];
     a.owner_next = own[(r + 1) % 3];
-    hipLaunchKernelGGL(k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
+    if (r == 0 && cache)
+      hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+                         m->stream, a);
+    else
+      hipLaunchKernelGGL(k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
   }
   SbpFinishArgs f;
   std::memset(&f, 0, sizeof(f));
