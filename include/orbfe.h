@@ -138,6 +138,11 @@ typedef struct orbfe_frame_view {
   float min_x, max_x, min_y, max_y;  /* mnMinX, mnMaxX, mnMinY, mnMaxY */
   float grid_inv_w, grid_inv_h;      /* mfGridElementWidthInv, mfGridElementHeightInv */
   float fx, fy, cx, cy, bf, b;       /* camera; bf = mbf, b = mb */
+  /* KeyFrame views (orbfe_keyframe.h): the grid origin when it differs from min_x/min_y (the
+   * Frame's float mnMinX/mnMinY that built mGrid; KeyFrame.h:202-205 keeps int bounds).
+   * grid_origin_set = 0 (zero-initialised views): the grid origin is (min_x, min_y). */
+  int32_t grid_origin_set;
+  float grid_min_x, grid_min_y;
 } orbfe_frame_view;
 
 /* DBoW2::FeatureVector as CSR: node ids ascending, indices of node k in

@@ -695,113 +695,9 @@ extern "C" int orbref_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 }
 
 // =============================================================================================
-// Matchers
-namespace {
-const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;  // ORBmatcher.cc:37-39
-const int GRID_COLS = 64, GRID_ROWS = 48;                   // Frame.h:38-39
-
-struct Grid {  // Frame::mGrid as CSR, cell = ix * GRID_ROWS + iy
-  std::vector<int32_t> start, items;
-};
-
-// Frame::AssignFeaturesToGrid + PosInGrid (Frame.cc:279-294, 435-445)
-Grid build_grid(const orbfe_frame_view* f) {
-  Grid g;
-  std::vector<std::vector<int32_t>> cells(GRID_COLS * GRID_ROWS);
-  for (int i = 0; i < f->n; i++) {
-    const orbfe_keypoint& kp = f->keys_un[i];
-    int px = (int)std::round((kp.x - f->min_x) * f->grid_inv_w);
-    int py = (int)std::round((kp.y - f->min_y) * f->grid_inv_h);
-    if (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) continue;
-    cells[px * GRID_ROWS + py].push_back(i);
-  }
-  g.start.assign(GRID_COLS * GRID_ROWS + 1, 0);
-  for (int c = 0; c < GRID_COLS * GRID_ROWS; c++) {
-    g.start[c + 1] = g.start[c] + (int)cells[c].size();
-    g.items.insert(g.items.end(), cells[c].begin(), cells[c].end());
-  }
-  return g;
-}
-
-// Frame::GetFeaturesInArea (Frame.cc:376-433)
-void features_in_area(const orbfe_frame_view* f, const Grid& g, float x, float y, float r,
-                      int minLevel, int maxLevel, std::vector<int>& out) {
-  out.clear();
-  const int nMinCellX = std::max(0, (int)std::floor((x - f->min_x - r) * f->grid_inv_w));
-  if (nMinCellX >= GRID_COLS) return;
-  const int nMaxCellX = std::min(GRID_COLS - 1, (int)std::ceil((x - f->min_x + r) * f->grid_inv_w));
-  if (nMaxCellX < 0) return;
-  const int nMinCellY = std::max(0, (int)std::floor((y - f->min_y - r) * f->grid_inv_h));
-  if (nMinCellY >= GRID_ROWS) return;
-  const int nMaxCellY = std::min(GRID_ROWS - 1, (int)std::ceil((y - f->min_y + r) * f->grid_inv_h));
-  if (nMaxCellY < 0) return;
-  const bool checkLevels = (minLevel > 0) || (maxLevel >= 0);
-  for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
-    for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
-      int c = ix * GRID_ROWS + iy;
-      for (int j = g.start[c]; j < g.start[c + 1]; j++) {
-        const orbfe_keypoint& kp = f->keys_un[g.items[j]];
-        if (checkLevels) {
-          if (kp.octave < minLevel) continue;
-          if (maxLevel >= 0 && kp.octave > maxLevel) continue;
-        }
-        const float distx = kp.x - x, disty = kp.y - y;
-        if (std::fabs(distx) < r && std::fabs(disty) < r) out.push_back(g.items[j]);
-      }
-    }
-}
-
-// ORBmatcher::ComputeThreeMaxima (ORBmatcher.cc:1627-1668)
-void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, int& ind3) {
-  int max1 = 0, max2 = 0, max3 = 0;
-  for (int i = 0; i < L; i++) {
-    const int s = (int)histo[i].size();
-    if (s > max1) {
-      max3 = max2; max2 = max1; max1 = s;
-      ind3 = ind2; ind2 = ind1; ind1 = i;
-    } else if (s > max2) {
-      max3 = max2; max2 = s;
-      ind3 = ind2; ind2 = i;
-    } else if (s > max3) {
-      max3 = s; ind3 = i;
-    }
-  }
-  if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-  else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-}
-
-inline int rot_bin(float a1, float a2) {  // ORBmatcher.cc:781-786 (bins 0..12 only, kept as is)
-  const float factor = 1.0f / HISTO_LENGTH;
-  float rot = a1 - a2;
-  if (rot < 0.0) rot += 360.0f;
-  int bin = (int)std::round(rot * factor);
-  if (bin == HISTO_LENGTH) bin = 0;
-  return bin;
-}
-
-// ORBmatcher::CheckDistEpipolarLine (ORBmatcher.cc:143-163)
-bool epipolar_ok(const orbfe_keypoint& k1, const orbfe_keypoint& k2, const float* F,
-                 const float* sigma2) {
-  const float a = k1.x * F[0] + k1.y * F[3] + F[6];
-  const float b = k1.x * F[1] + k1.y * F[4] + F[7];
-  const float c = k1.x * F[2] + k1.y * F[5] + F[8];
-  const float num = a * k2.x + b * k2.y + c;
-  const float den = a * a + b * b;
-  if (den == 0) return false;
-  const float dsqr = num * num / den;
-  return dsqr < 3.84 * sigma2[k2.octave];
-}
-
-// 3x3 (row-major, from a 3x4 [R|t]) times 3-vector plus optional 3-vector, accumulated in
-// double and rounded once (cv::Mat CV_32F gemm).
-inline float gemv_row(const float* r, const float* v, const float* add) {
-  double s = (double)r[0] * (double)v[0];
-  s += (double)r[1] * (double)v[1];
-  s += (double)r[2] * (double)v[2];
-  if (add) s = s + (double)*add;
-  return (float)s;
-}
-}  // namespace
+// Matchers (shared helpers in orbref_match.h, also used by orbref_kf.cpp)
+#include "orbref_match.h"
+using namespace orbref_m;
 
 extern "C" int orbref_build_grid(const orbfe_frame_view* frame, int32_t* cell_start,
                                  int32_t* cell_items) {
@@ -1230,11 +1126,7 @@ extern "C" int orbref_is_in_frustum(const orbfe_frame_view* F, const orbfe_mappo
     for (int k = 0; k < 3; k++) dot += (double)PO[k] * (double)Pn[k];
     const float viewCos = (float)(dot / (double)dist);
     if (viewCos < viewing_cos_limit) continue;
-    // PredictScale: ratio in float, ceil(log(ratio) / mfLogScaleFactor) in double
-    const float ratio = G->max_distance[i] / dist;
-    int nScale = (int)std::ceil(std::log((double)ratio) / (double)log_scale_factor);
-    if (nScale < 0) nScale = 0;
-    else if (nScale >= F->nlevels) nScale = F->nlevels - 1;
+    const int nScale = predict_scale(G->max_distance[i], dist, log_scale_factor, F->nlevels);
     out->flags[i] = (uint8_t)(fl | ORBFE_MPF_TRACK_IN_VIEW);
     if (out->proj_x) out->proj_x[i] = u;
     if (out->proj_xr) out->proj_xr[i] = u - F->bf * invz;

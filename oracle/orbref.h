@@ -95,6 +95,39 @@ int orbref_compute_stereo_matches(const orbfe_keypoint* kl, const uint8_t* dl, i
 /* Frame::AssignFeaturesToGrid as CSR (64 x 48 cells, cell = ix*48 + iy): cell_start[3073]. */
 int orbref_build_grid(const orbfe_frame_view* frame, int32_t* cell_start, int32_t* cell_items);
 
+/* Keyframe matchers and ComputeDistinctiveDescriptors (orbref_kf.cpp; encodings as
+ * include/orbfe_keyframe.h). */
+int orbref_search_by_bow_kf_frame(const orbfe_frame_view* kf, const orbfe_feature_vector* kf_fv,
+                                  const orbfe_frame_view* frame, const orbfe_feature_vector* frame_fv,
+                                  float nnratio, int check_ori, int32_t* match_f, int* nmatches);
+int orbref_search_by_bow_kf_kf(const orbfe_frame_view* kf1, const orbfe_feature_vector* fv1,
+                               const orbfe_frame_view* kf2, const orbfe_feature_vector* fv2,
+                               float nnratio, int check_ori, int32_t* match12, int* nmatches);
+int orbref_search_by_projection_keyframe(const orbfe_frame_view* current, const float* tcw,
+                                         const orbfe_mappoint_geometry* kf_points,
+                                         const float* kf_angle, float log_scale_factor, float th,
+                                         int orb_dist, int check_ori, int32_t* best_idx,
+                                         int* nmatches);
+int orbref_search_by_projection_sim3(const orbfe_frame_view* kf, const float* scw,
+                                     const orbfe_mappoint_geometry* points, float log_scale_factor,
+                                     int th, int32_t* best_idx, int* nmatches);
+int orbref_fuse(const orbfe_frame_view* kf, const float* tcw, const float* ow,
+                const orbfe_mappoint_geometry* points, float log_scale_factor, float th,
+                int32_t* best_idx, int* n_candidates);
+int orbref_fuse_sim3(const orbfe_frame_view* kf, const float* scw,
+                     const orbfe_mappoint_geometry* points, float log_scale_factor, float th,
+                     int32_t* best_idx, int* nfused);
+int orbref_search_by_sim3(const orbfe_frame_view* kf1, const orbfe_frame_view* kf2,
+                          const orbfe_mappoint_geometry* mps1, const orbfe_mappoint_geometry* mps2,
+                          const float* t1w, const float* t2w, float s12, const float* r12,
+                          const float* t12, float lsf1, float lsf2, float th, int32_t* match12,
+                          int* nfound);
+int orbref_search_for_initialization(const orbfe_frame_view* f1, const orbfe_frame_view* f2,
+                                     float* prev_matched, int window, float nnratio, int check_ori,
+                                     int32_t* match12, int* nmatches);
+int orbref_compute_distinctive_descriptors(int n_points, const int32_t* offsets,
+                                           const uint8_t* descriptors, int32_t* best_index);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,7 +51,8 @@ class frame_view(Structure):
                 ("min_x", c_float), ("max_x", c_float), ("min_y", c_float), ("max_y", c_float),
                 ("grid_inv_w", c_float), ("grid_inv_h", c_float),
                 ("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float),
-                ("bf", c_float), ("b", c_float)]
+                ("bf", c_float), ("b", c_float),
+                ("grid_origin_set", c_int32), ("grid_min_x", c_float), ("grid_min_y", c_float)]
 
 
 class feature_vector(Structure):

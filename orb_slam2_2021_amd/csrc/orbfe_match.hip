@@ -28,50 +28,12 @@
 
 #include "../../include/orbfe.h"
 #include "../../include/orbfe_frustum.h"
+#include "../../include/orbfe_keyframe.h"
 #include "../../include/orbfe_match_batch.h"
 #include "orbfe_device.h"
+#include "orbfe_match_internal.h"
 
-#define TH_HIGH 100
-#define TH_LOW 50
-#define HISTO_LENGTH 30
-#define GRID_COLS 64
-#define GRID_ROWS 48
-#define GRID_CELLS (GRID_COLS * GRID_ROWS)
-#define SBP_MAX_ROUNDS 12
-#define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
-#define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
-
-// ---------------------------------------------------------------------------------------------
-// shared helpers
-__device__ __forceinline__ int rot_bin_dev(float a1, float a2) {
-  // ORBmatcher.cc:781-786 (only bins 0..12 are reachable: round(rot * 1/30); kept as is)
-  const float factor = 1.0f / HISTO_LENGTH;
-  float rot = a1 - a2;
-  if (rot < 0.0) rot += 360.0f;
-  int bin = (int)roundf(rot * factor);
-  if (bin == HISTO_LENGTH) bin = 0;
-  return bin;
-}
-
-// ComputeThreeMaxima (ORBmatcher.cc:1627-1668) on 30 counts
-__device__ void three_maxima_dev(const int* h, int& ind1, int& ind2, int& ind3) {
-  int max1 = 0, max2 = 0, max3 = 0;
-  ind1 = ind2 = ind3 = -1;
-  for (int i = 0; i < HISTO_LENGTH; i++) {
-    const int s = h[i];
-    if (s > max1) {
-      max3 = max2; max2 = max1; max1 = s;
-      ind3 = ind2; ind2 = ind1; ind1 = i;
-    } else if (s > max2) {
-      max3 = max2; max2 = s;
-      ind3 = ind2; ind2 = i;
-    } else if (s > max3) {
-      max3 = s; ind3 = i;
-    }
-  }
-  if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-  else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-}
+using namespace orbfe_mi;
 
 // ---------------------------------------------------------------------------------------------
 // SearchForTriangulation: k_sft_init (match12 = -1), k_sft_nodes (one wavefront per common
@@ -504,12 +466,6 @@ __global__ __launch_bounds__(1024) void k_grid(GridArgs g) {
 
 // ---------------------------------------------------------------------------------------------
 // SearchByProjection (both overloads): queries + fixpoint rounds + finish
-struct SbpQuery {
-  float x, y, r;      // search window centre and half-size (GetFeaturesInArea's x, y, r)
-  float xr, er_lim;   // stereo gate: |xr - uRight| > er_lim rejects
-  int min_level, max_level;
-  int flags;          // bit0 valid query, bit1 claims block (Observations() > 0)
-};
 
 struct SbpArgs {
   orbfe_frame_view F;        // device pointers
@@ -518,8 +474,11 @@ struct SbpArgs {
   const SbpQuery* q;
   const uint8_t* qdesc;       // m x 32
   int m;
-  int mode;                   // 0 local (best + second + ratio), 1 last frame (best only)
+  int mode;                   // 0 local (best + second + ratio), 1 first minimum (other overloads)
   float nnratio;
+  int dist_th;                // accept bestDist <= dist_th (TH_HIGH, TH_LOW or ORBdist)
+  int block_any;              // pre-blocked keypoints: mp_state != NONE (1) or == OBSERVED (0)
+  int cand_cap;               // per-query candidate cache entries
   int32_t* res_prev;
   int32_t* res_cur;
   const int32_t* owner_prev;  // INT_MAX = unclaimed in the previous round
@@ -529,13 +488,38 @@ struct SbpArgs {
   int round;
   // per-query candidate cache filled in round 0 (keypoints passing the window, level and stereo
   // gates, in GetFeaturesInArea order, with their distances); later rounds only re-apply the
-  // claims. cand_n[i] < 0: more than SBP_CAND candidates, the query re-searches every round.
+  // claims. cand_n[i] < 0: more than cand_cap candidates, the query re-searches every round.
+  // Candidates at distance 256 are left out: they can be neither best nor second (:106-118).
   int16_t* cand_k;
   uint8_t* cand_d;
   uint8_t* cand_l;
   int32_t* cand_n;
 };
-#define SBP_CAND 48
+
+// Keypoint taken before the search starts: Frame::mvpMapPoints with Observations() > 0 (:91-93,
+// :1420-1422) or any non-NULL entry (:384, :1567).
+__device__ __forceinline__ bool sbp_pre_blocked(const SbpArgs& a, int k) {
+  const uint8_t st = a.F.mp_state[k];
+  return a.block_any ? st != ORBFE_MP_NONE : st == ORBFE_MP_OBSERVED;
+}
+
+// Window candidate test that precedes the distance (rec = {x, y, uRight, index | octave << 16}).
+__device__ __forceinline__ bool sbp_gate(const SbpQuery& q, const uint4& rec, const float* level_sigma2) {
+  const float ur = __uint_as_float(rec.z);
+  if (q.gate == SBP_GATE_STEREO) return !(ur > 0 && fabsf(q.xr - ur) > q.er_lim);
+  if (q.gate == SBP_GATE_FUSE) {  // Fuse (:930-954): reprojection error against chi2 bounds
+    const float inv = 1.0f / level_sigma2[rec.w >> 16];  // mvInvLevelSigma2 (ORBextractor.cc:433)
+    const float ex = q.x - __uint_as_float(rec.x), ey = q.y - __uint_as_float(rec.y);
+    if (ur >= 0) {
+      const float er = q.xr - ur;
+      const float e2 = ex * ex + ey * ey + er * er;
+      return !((double)(e2 * inv) > 7.8);
+    }
+    const float e2 = ex * ex + ey * ey;
+    return !((double)(e2 * inv) > 5.99);
+  }
+  return true;
+}
 
 // One MapPoint's search given a predicate blocked(k). Returns the keypoint index or -1.
 // Best / second-best bookkeeping of the reference loop (:106-118 local; :1417-1450 last frame).
@@ -558,8 +542,8 @@ struct SbpBest {
       bestIdx = k;
     }
   }
-  __device__ __forceinline__ int result(int mode, float nnratio) const {
-    if (bestDist > TH_HIGH) return -1;
+  __device__ __forceinline__ int result(int mode, float nnratio, int dist_th) const {
+    if (bestDist > dist_th) return -1;
     if (mode == 0 && bestLevel == bestLevel2 && (float)bestDist > nnratio * (float)bestDist2) return -1;
     return bestIdx;
   }
@@ -569,15 +553,15 @@ struct SbpBest {
 template <class Blocked>
 __device__ int sbp_cached(const SbpArgs& a, int i, int n, Blocked blocked) {
   SbpBest b;
-  const int16_t* ck = a.cand_k + (size_t)i * SBP_CAND;
-  const uint8_t* cd = a.cand_d + (size_t)i * SBP_CAND;
-  const uint8_t* cl = a.cand_l + (size_t)i * SBP_CAND;
+  const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
+  const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
+  const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
   for (int c = 0; c < n; c++) {
     const int k = ck[c];
     if (blocked(k)) continue;
     b.add(a.mode, cd[c], cl[c], k);
   }
-  return b.result(a.mode, a.nnratio);
+  return b.result(a.mode, a.nnratio, a.dist_th);
 }
 
 template <class Blocked, bool RECORD = false>
@@ -619,19 +603,16 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
         const float distx = kp.x - x, disty = kp.y - y;
         if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
         if (!RECORD && blocked(k)) continue;
-        const float ur = __uint_as_float(rec.z);
-        if (ur > 0) {
-          const float er = fabsf(q.xr - ur);
-          if (er > q.er_lim) continue;
-        }
+        if (!sbp_gate(q, rec, F.level_sigma2)) continue;
         uint4 d0, d1;
         load_desc(F.descriptors + (size_t)k * 32, d0, d1);
         const int dist = hamming256(dq0, dq1, d0, d1);
         if (RECORD) {
-          if (nc < SBP_CAND) {
-            a.cand_k[(size_t)i * SBP_CAND + nc] = (int16_t)k;
-            a.cand_d[(size_t)i * SBP_CAND + nc] = (uint8_t)dist;
-            a.cand_l[(size_t)i * SBP_CAND + nc] = (uint8_t)kp.octave;
+          if (dist == 256) continue;
+          if (nc < a.cand_cap) {
+            a.cand_k[(size_t)i * a.cand_cap + nc] = (int16_t)k;
+            a.cand_d[(size_t)i * a.cand_cap + nc] = (uint8_t)dist;
+            a.cand_l[(size_t)i * a.cand_cap + nc] = (uint8_t)kp.octave;
           }
           nc++;
           if (blocked(k)) continue;
@@ -640,8 +621,8 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
       }
     }
   }
-  if (RECORD) a.cand_n[i] = nc <= SBP_CAND ? nc : -1;
-  return b.result(a.mode, a.nnratio);
+  if (RECORD) a.cand_n[i] = nc <= a.cand_cap ? nc : -1;
+  return b.result(a.mode, a.nnratio, a.dist_th);
 }
 
 struct SbpInit {
@@ -676,7 +657,7 @@ __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
   if (i < a.F.n) a.owner_next[i] = 0x7fffffff;
   bool changed = false;
   if (i < a.m) {
-    auto blocked = [&](int k) { return a.F.mp_state[k] == ORBFE_MP_OBSERVED || a.owner_prev[k] < i; };
+    auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || a.owner_prev[k] < i; };
     int res;
     if (!a.cand_n) {
       res = sbp_one(a, i, blocked);
@@ -735,9 +716,9 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   const bool checkLevels = (q.min_level > 0) || (q.max_level >= 0);
   uint4 dq0 = make_uint4(0, 0, 0, 0), dq1 = dq0;
   if (ncell) load_desc(a.qdesc + (size_t)i * 32, dq0, dq1);
-  int16_t* ck = a.cand_k + (size_t)i * SBP_CAND;
-  uint8_t* cd = a.cand_d + (size_t)i * SBP_CAND;
-  uint8_t* cl = a.cand_l + (size_t)i * SBP_CAND;
+  int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
+  uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
+  uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
   const unsigned long long NONE = ~0ull;
   unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
   int kb1 = -1;                             // keypoint of k1
@@ -767,7 +748,7 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
       for (int u0 = 0; u0 < nf; u0 += 16) {
         const int u = u0 + j;
         bool pass = false;
-        int k = 0, oct = 0;
+        int k = 0, oct = 0, dist = 256;
         if (u < nf) {  // window / level / stereo gates of :86-103, :1412-1427
           const uint4 rec = a.grid_recs[flat[u]];
           k = (int)(rec.w & 0xffffu);
@@ -779,21 +760,23 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
           }
           const float distx = __uint_as_float(rec.x) - x, disty = __uint_as_float(rec.y) - y;
           if (!(fabsf(distx) < r && fabsf(disty) < r)) pass = false;
-          const float ur = __uint_as_float(rec.z);
-          if (ur > 0 && fabsf(q.xr - ur) > q.er_lim) pass = false;
+          if (pass && !sbp_gate(q, rec, F.level_sigma2)) pass = false;
         }
-        const uint64_t bm = (wave_ballot(pass) >> rowbase) & 0xffffull;
         if (pass) {
-          const int pos = total + __popcll(bm & ((1ull << j) - 1));
           uint4 d0, d1;
           load_desc(F.descriptors + (size_t)k * 32, d0, d1);
-          const int dist = hamming256(dq0, dq1, d0, d1);
-          if (pos < SBP_CAND) {
+          dist = hamming256(dq0, dq1, d0, d1);
+        }
+        const bool keep = pass && dist < 256;  // a distance of 256 is never best or second
+        const uint64_t bm = (wave_ballot(keep) >> rowbase) & 0xffffull;
+        if (keep) {
+          const int pos = total + __popcll(bm & ((1ull << j) - 1));
+          if (pos < a.cand_cap) {
             ck[pos] = (int16_t)k;
             cd[pos] = (uint8_t)dist;
             cl[pos] = (uint8_t)oct;
           }
-          if (dist < 256 && F.mp_state[k] != ORBFE_MP_OBSERVED) {  // blocked(k) in round 0
+          if (!sbp_pre_blocked(a, k)) {  // blocked(k) in round 0
             const unsigned long long key =
                 ((unsigned long long)dist << 40) | ((unsigned long long)pos << 8) | (unsigned)oct;
             if (key < k1) {
@@ -822,7 +805,7 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
     }
   }
   if (j != 0) return;
-  a.cand_n[i] = total <= SBP_CAND ? total : -1;
+  a.cand_n[i] = total <= a.cand_cap ? total : -1;
   int res = -1;
   if (k1 != NONE) {
     SbpBest bb;
@@ -833,7 +816,7 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
       bb.bestDist2 = (int)(k2 >> 40);
       bb.bestLevel2 = (int)(k2 & 0xff);
     }
-    res = bb.result(a.mode, a.nnratio);
+    res = bb.result(a.mode, a.nnratio, a.dist_th);
   }
   a.res_cur[i] = res;
   if (res >= 0 && (q.flags & 2)) atomicMin(&a.owner_cur[res], i);
@@ -891,7 +874,7 @@ __global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* bl
   if (!converged) {
     if (t == 0) {
       *f.serial_used = 1;
-      for (int k = 0; k < a.F.n; k++) blocked_scratch[k] = a.F.mp_state[k] == ORBFE_MP_OBSERVED;
+      for (int k = 0; k < a.F.n; k++) blocked_scratch[k] = sbp_pre_blocked(a, k);
       for (int i = 0; i < a.m; i++) {
         const int r = sbp_one(a, i, [&](int k) { return blocked_scratch[k] != 0; });
         f.best_out[i] = r;
@@ -976,16 +959,10 @@ struct FrustumArgs {
   int32_t* n_in_view;     // device counter (zeroed before the launch)
   float rcw[9], tcw[3], ow[3];
   float fx, fy, cx, cy, bf, min_x, max_x, min_y, max_y;
-  float log_sf, cos_limit;
+  float cos_limit;
   int nlevels;
+  float scale_thr[ORBFE_MAX_LEVELS_M];  // PredictScale table (predict_scale_table)
 };
-__device__ __forceinline__ float gemv3_d(const float* r, float x, float y, float z, float add) {
-  double s = (double)r[0] * (double)x;  // cv::Mat CV_32F gemm: double accumulation, one rounding
-  s += (double)r[1] * (double)y;
-  s += (double)r[2] * (double)z;
-  s = s + (double)add;
-  return (float)s;
-}
 __global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   bool in = false;
@@ -1016,9 +993,7 @@ __global__ __launch_bounds__(256) void k_frustum(FrustumArgs a) {
             dot += (double)POz * (double)a.normal[3 * i + 2];
             viewCos = (float)(dot / (double)dist);
             if (!(viewCos < a.cos_limit)) {
-              const float ratio = a.max_d[i] / dist;
-              nScale = (int)ceil(log((double)ratio) / (double)a.log_sf);
-              nScale = nScale < 0 ? 0 : (nScale >= a.nlevels ? a.nlevels - 1 : nScale);
+              nScale = predict_scale_dev(a.max_d[i], dist, a.scale_thr, a.nlevels);
               xr = u - a.bf * invz;
               in = true;
             }
@@ -1100,37 +1075,7 @@ __global__ void k_hamming_batch(const uint8_t* a, const uint8_t* b, int n, int32
 
 // =============================================================================================
 // host side
-struct orbfe_matcher {
-  int device = 0;
-  float nnratio;
-  int check_ori;
-  hipStream_t stream = nullptr;
-  // device arena (grown on demand)
-  uint8_t* arena = nullptr;
-  size_t arena_bytes = 0;
-  orbfe_sft_pair* d_pairs = nullptr;
-  int pairs_cap = 0;
-  std::vector<orbfe_sft_pair> pairs_uploaded;  // host copy of d_pairs (skip identical uploads)
-  int32_t* d_serial = nullptr;
-  // pinned mirror of the arena: host inputs are staged at their arena offsets and uploaded in one
-  // H2D copy per call instead of one pageable copy per array
-  uint8_t* pinned = nullptr;
-  size_t pinned_bytes = 0;
-  size_t stage_lo = SIZE_MAX, stage_hi = 0;
-  int last_rounds = 0, last_serial = 0;
-  int max_rounds = SBP_MAX_ROUNDS;
-};
-
-namespace {
-struct Arena {
-  size_t total = 0;
-  size_t add(size_t bytes) {
-    const size_t off = total;
-    total += (bytes + 255) & ~(size_t)255;
-    return off;
-  }
-};
-
+namespace orbfe_mi {
 int ensure_arena(orbfe_matcher* m, size_t bytes) {
   m->stage_lo = SIZE_MAX;
   m->stage_hi = 0;
@@ -1168,10 +1113,7 @@ int flush_h2d(orbfe_matcher* m) {
   return ORBFE_OK;
 }
 
-// Layout of one frame view in the arena
-struct FrameOffsets {
-  size_t keys, ur, desc, mp, scale, sigma2;
-};
+// Layout of one frame view in the arena (FrameOffsets)
 FrameOffsets plan_frame(Arena& ar, const orbfe_frame_view* f) {
   FrameOffsets o;
   o.keys = ar.add(sizeof(orbfe_keypoint) * std::max(f->n, 1));
@@ -1206,7 +1148,7 @@ int upload_frame(orbfe_matcher* m, const FrameOffsets& o, const orbfe_frame_view
 }
 bool frame_ok(const orbfe_frame_view* f) {
   return f && f->n >= 0 && f->n <= GRID_MAX_KEYS && (f->n == 0 || (f->keys_un && f->u_right && f->descriptors && f->mp_state)) &&
-         f->nlevels > 0 && f->scale_factors;
+         f->nlevels > 0 && f->nlevels <= ORBFE_MAX_LEVELS_M && f->scale_factors;
 }
 bool levels_ok(const orbfe_keypoint* k, int n, int nlevels) {
   for (int i = 0; i < n; i++)
@@ -1376,95 +1318,148 @@ extern "C" int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_fram
 }
 
 // ---- SearchByProjection -----------------------------------------------------------------------
-static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode,
-                   const uint8_t* h_qdesc, const float* h_qangle, int check_ori,
-                   const std::function<int(Arena&)>& plan_q,
-                   const std::function<int(uint8_t*, const orbfe_frame_view&, SbpQuery*)>& make_q,
-                   int32_t* best_idx, int* nmatches) {
-  Arena ar;
-  // host-staged inputs first (frame, query inputs, query descriptors/angles): one contiguous
-  // span for the single H2D copy; device-only scratch after
-  const FrameOffsets fo = plan_frame(ar, F);
-  const size_t extra = plan_q(ar);
-  (void)extra;
-  const size_t oqd = ar.add(32 * (size_t)std::max(nq, 1));
-  const size_t oqa = ar.add(4 * (size_t)std::max(nq, 1));
-  const size_t og_start = ar.add(4 * (GRID_CELLS + 1));
-  const size_t og_items = ar.add(16 * (size_t)std::max(F->n, 1));
-  const size_t oq = ar.add(sizeof(SbpQuery) * std::max(nq, 1));
-  const size_t ores0 = ar.add(4 * (size_t)std::max(nq, 1));
-  const size_t ores1 = ar.add(4 * (size_t)std::max(nq, 1));
-  const size_t oown0 = ar.add(4 * (size_t)std::max(F->n, 1));
-  const size_t oown1 = ar.add(4 * (size_t)std::max(F->n, 1));
-  const size_t oown2 = ar.add(4 * (size_t)std::max(F->n, 1));
-  const size_t oblk = ar.add(4 * (size_t)std::max(F->n, 1));
-  const size_t ostate = ar.add(4 * (SBP_MAX_ROUNDS + 4));
-  const size_t obest = ar.add(4 * (size_t)std::max(nq, 1));
-  const bool cache = F->n <= 32767;  // candidate keypoint indices are int16
-  const size_t ocand_k = ar.add(cache ? 2 * (size_t)SBP_CAND * std::max(nq, 1) : 0);
-  const size_t ocand_d = ar.add(cache ? (size_t)SBP_CAND * std::max(nq, 1) : 0);
-  const size_t ocand_l = ar.add(cache ? (size_t)SBP_CAND * std::max(nq, 1) : 0);
-  const size_t ocand_n = ar.add(cache ? 4 * (size_t)std::max(nq, 1) : 0);
-  const size_t onm = ar.add(4);
-  int st = ensure_arena(m, ar.total);
-  if (st) return st;
+namespace orbfe_mi {
+// host-staged inputs (frame, query descriptors / angles) ...
+void sbp_plan_inputs(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap, SbpPlan& p) {
+  p.nq = nq;
+  p.cand_cap = cand_cap;
+  p.fo = plan_frame(ar, F);
+  const size_t q1 = (size_t)std::max(nq, 1);
+  p.oqd = ar.add(32 * q1);
+  p.oqa = ar.add(4 * q1);
+}
+// ... and device-only scratch, planned after every staged input of the call so that the staged
+// bytes form one contiguous span (one H2D copy)
+void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
+  const size_t q1 = (size_t)std::max(p.nq, 1), f1 = (size_t)std::max(F->n, 1);
+  const int cand_cap = p.cand_cap;
+  p.og_start = ar.add(4 * (GRID_CELLS + 1));
+  p.og_items = ar.add(16 * f1);
+  p.oq = ar.add(sizeof(SbpQuery) * q1);
+  p.ores0 = ar.add(4 * q1);
+  p.ores1 = ar.add(4 * q1);
+  p.oown0 = ar.add(4 * f1);
+  p.oown1 = ar.add(4 * f1);
+  p.oown2 = ar.add(4 * f1);
+  p.oblk = ar.add(4 * f1);
+  p.ostate = ar.add(4 * (SBP_MAX_ROUNDS + 4));
+  p.obest = ar.add(4 * q1);
+  p.cache = F->n <= 32767;  // candidate keypoint indices are int16
+  const size_t cq = p.cache ? (size_t)cand_cap * q1 : 0;
+  p.ocand_k = ar.add(2 * cq);
+  p.ocand_d = ar.add(cq);
+  p.ocand_l = ar.add(cq);
+  p.ocand_n = ar.add(p.cache ? 4 * q1 : 0);
+  p.onm = ar.add(4);
+}
+SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap) {
+  SbpPlan p;
+  sbp_plan_inputs(ar, F, nq, cand_cap, p);
+  sbp_plan_scratch(ar, F, p);
+  return p;
+}
+
+int sbp_stage(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const uint8_t* h_qdesc,
+              const float* h_qangle, orbfe_frame_view* dF) {
   uint8_t* A = m->arena;
-  orbfe_frame_view dF;
-  if ((st = upload_frame(m, fo, F, &dF))) return st;
-  SbpQuery* dq = (SbpQuery*)(A + oq);
-  if (nq > 0) {
-    stage_h2d(m, A + oqd, h_qdesc, 32 * (size_t)nq);
-    if (h_qangle) stage_h2d(m, A + oqa, h_qangle, 4 * (size_t)nq);
-    if ((st = make_q(A, dF, dq))) return st;  // stages the query inputs, flushes, builds queries
+  int st = upload_frame(m, p.fo, F, dF);
+  if (st) return st;
+  if (p.nq > 0) {
+    if (h_qdesc) stage_h2d(m, A + p.oqd, h_qdesc, 32 * (size_t)p.nq);
+    if (h_qangle) stage_h2d(m, A + p.oqa, h_qangle, 4 * (size_t)p.nq);
   }
-  if ((st = flush_h2d(m))) return st;
-  // grid
+  return ORBFE_OK;
+}
+
+static GridArgs grid_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF) {
   GridArgs g;
   g.keys = dF.keys_un;
   g.n = F->n;
-  g.min_x = F->min_x;
-  g.min_y = F->min_y;
+  g.min_x = F->grid_origin_set ? F->grid_min_x : F->min_x;  // mGrid was built with these bounds
+  g.min_y = F->grid_origin_set ? F->grid_min_y : F->min_y;
   g.inv_w = F->grid_inv_w;
   g.inv_h = F->grid_inv_h;
-  g.start = (int32_t*)(A + og_start);
-  g.recs = (uint4*)(A + og_items);
+  g.start = (int32_t*)(A + p.og_start);
+  g.recs = (uint4*)(A + p.og_items);
   g.u_right = dF.u_right;
+  return g;
+}
+
+void sbp_launch_grid(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF) {
+  const GridArgs g = grid_args(m->arena, p, F, dF);
   hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), sizeof(int) * (GRID_CELLS + 1 + 16 + std::max(F->n, 1)),
                      m->stream, g);
-  {
-    SbpInit in;
-    in.res0 = (int32_t*)(A + ores0);
-    in.res1 = (int32_t*)(A + ores1);
-    in.own0 = (int32_t*)(A + oown0);
-    in.own2 = (int32_t*)(A + oown2);
-    in.state = (int32_t*)(A + ostate);
-    in.nmatches = (int32_t*)(A + onm);
-    in.serial = m->d_serial;
-    in.nq = std::max(nq, 1);
-    in.nf = std::max(F->n, 1);
-    hipLaunchKernelGGL(k_sbp_init, dim3((std::max(in.nq, in.nf) + 255) / 256), dim3(256), 0, m->stream, in);
-  }
+}
+
+static SbpArgs sbp_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
+                        const SbpMode& md, float nnratio) {
   SbpArgs a;
   std::memset(&a, 0, sizeof(a));
   a.F = dF;
-  a.grid_start = g.start;
-  a.grid_recs = g.recs;
-  a.q = dq;
-  a.qdesc = A + oqd;
-  a.m = nq;
-  a.mode = mode;
-  a.nnratio = m->nnratio;
-  a.state = (int32_t*)(A + ostate);
-  if (cache) {
-    a.cand_k = (int16_t*)(A + ocand_k);
-    a.cand_d = A + ocand_d;
-    a.cand_l = A + ocand_l;
-    a.cand_n = (int32_t*)(A + ocand_n);
+  a.grid_start = (const int32_t*)(A + p.og_start);
+  a.grid_recs = (const uint4*)(A + p.og_items);
+  a.q = (const SbpQuery*)(A + p.oq);
+  a.qdesc = A + p.oqd;
+  a.m = p.nq;
+  a.mode = md.mode;
+  a.nnratio = nnratio;
+  a.dist_th = md.dist_th;
+  a.block_any = md.block_any;
+  a.cand_cap = p.cand_cap;
+  a.state = (int32_t*)(A + p.ostate);
+  if (p.cache) {
+    a.cand_k = (int16_t*)(A + p.ocand_k);
+    a.cand_d = A + p.ocand_d;
+    a.cand_l = A + p.ocand_l;
+    a.cand_n = (int32_t*)(A + p.ocand_n);
   }
-  int32_t* res[2] = {(int32_t*)(A + ores0), (int32_t*)(A + ores1)};
+  (void)F;
+  return a;
+}
+
+static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F) {
+  uint8_t* A = m->arena;
+  SbpInit in;
+  in.res0 = (int32_t*)(A + p.ores0);
+  in.res1 = (int32_t*)(A + p.ores1);
+  in.own0 = (int32_t*)(A + p.oown0);
+  in.own2 = (int32_t*)(A + p.oown2);
+  in.state = (int32_t*)(A + p.ostate);
+  in.nmatches = (int32_t*)(A + p.onm);
+  in.serial = m->d_serial;
+  in.nq = std::max(p.nq, 1);
+  in.nf = std::max(F->n, 1);
+  hipLaunchKernelGGL(k_sbp_init, dim3((std::max(in.nq, in.nf) + 255) / 256), dim3(256), 0, m->stream, in);
+}
+
+void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
+                       const SbpMode& md) {
+  uint8_t* A = m->arena;
+  sbp_launch_grid(m, p, F, dF);
+  sbp_launch_init(m, p, F);
+  SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
+  a.round = 0;
+  a.res_cur = (int32_t*)(A + p.ores0);
+  a.res_prev = (int32_t*)(A + p.ores1);
+  a.owner_cur = (int32_t*)(A + p.oown0);
+  a.owner_prev = (int32_t*)(A + p.oown2);
+  a.owner_next = (int32_t*)(A + p.oown1);
+  if (p.nq > 0)
+    hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((p.nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+                       m->stream, a);
+}
+
+int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
+               const SbpMode& md) {
+  uint8_t* A = m->arena;
+  const int nq = p.nq;
+  sbp_launch_grid(m, p, F, dF);
+  sbp_launch_init(m, p, F);
+  SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
+  int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
   // owner buffers rotate over three: round r claims into own[r % 3], reads own[(r + 2) % 3] and
   // clears own[(r + 1) % 3] for round r + 1 (nobody reads it during round r)
-  int32_t* own[3] = {(int32_t*)(A + oown0), (int32_t*)(A + oown1), (int32_t*)(A + oown2)};
+  int32_t* own[3] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2)};
   for (int r = 0; r < m->max_rounds && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
@@ -1472,7 +1467,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
     a.owner_cur = own[r % 3];
     a.owner_prev = own[(r + 2) % 3];
     a.owner_next = own[(r + 1) % 3];
-    if (r == 0 && cache)
+    if (r == 0 && p.cache)
       hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                          m->stream, a);
     else
@@ -1483,28 +1478,91 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, int mode
   f.s = a;
   f.res_final[0] = res[0];
   f.res_final[1] = res[1];
-  f.best_out = (int32_t*)(A + obest);
-  f.nmatches = (int32_t*)(A + onm);
-  f.check_ori = check_ori;
-  f.q_angle = (const float*)(A + oqa);
+  f.best_out = (int32_t*)(A + p.obest);
+  f.nmatches = (int32_t*)(A + p.onm);
+  f.check_ori = md.check_ori;
+  f.q_angle = (const float*)(A + p.oqa);
   f.serial_used = m->d_serial;
   if (nq > 0) {
     hipLaunchKernelGGL(k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
-    hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + oblk));
+    hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
   }
   ORBFE_HIP_CHECK(hipGetLastError());
+  return ORBFE_OK;
+}
+
+int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatches) {
+  uint8_t* A = m->arena;
   int32_t nm = 0, state[2] = {0, 0}, serial = 0;
-  if (nq > 0) {
-    ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, f.best_out, 4 * (size_t)nq, hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, f.nmatches, 4, hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(state, a.state, 8, hipMemcpyDeviceToHost, m->stream));
+  if (p.nq > 0) {
+    if (best_idx)
+      ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, A + p.obest, 4 * (size_t)p.nq, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, A + p.onm, 4, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipMemcpyAsync(state, A + p.ostate, 8, hipMemcpyDeviceToHost, m->stream));
     ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
   }
   ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
   m->last_rounds = state[1];
   m->last_serial = serial;
-  *nmatches = nm;
+  if (nmatches) *nmatches = nm;
   return ORBFE_OK;
+}
+
+// PredictScale's ceil(logf(ratio) / log_scale_factor) (MapPoint.cc:415-447, float overloads under
+// `using namespace std`) is non-decreasing in ratio, so nScale >= k  <=>  ratio >= thr[k-1], the
+// smallest float with ceilf(logf(thr) / lsf) >= k. Found by bisection over the ordered bit
+// patterns of positive floats, with the host's own logf -- the device never evaluates a log.
+void predict_scale_table(float lsf, int nlevels, float* thr) {
+  auto level = [&](uint32_t bits) {
+    float r;
+    std::memcpy(&r, &bits, 4);
+    return (int)std::ceil(std::log(r) / lsf);
+  };
+  for (int k = 1; k < nlevels; k++) {
+    uint32_t lo = 1u, hi = 0x7f800000u;  // level(hi = +inf) is huge; level(lo) is very negative
+    if (!(lsf > 0)) {                    // degenerate scale factor: nothing reaches level k
+      thr[k - 1] = INFINITY;
+      continue;
+    }
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (level(mid) >= k) hi = mid;
+      else lo = mid + 1;
+    }
+    std::memcpy(&thr[k - 1], &lo, 4);
+  }
+  for (int k = std::max(nlevels, 1); k < ORBFE_MAX_LEVELS_M; k++) thr[k - 1] = INFINITY;
+}
+}  // namespace orbfe_mi
+
+extern "C" int orbfe_predict_scale_thresholds(float log_scale_factor, int nlevels, float* thresholds) {
+  if (!thresholds || nlevels < 1 || nlevels > ORBFE_MAX_LEVELS_M)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_predict_scale_thresholds: bad argument");
+  float t[ORBFE_MAX_LEVELS_M];
+  predict_scale_table(log_scale_factor, nlevels, t);
+  for (int k = 1; k < nlevels; k++) thresholds[k - 1] = t[k - 1];
+  return ORBFE_OK;
+}
+
+static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, const SbpMode& md,
+                   const uint8_t* h_qdesc, const float* h_qangle,
+                   const std::function<int(Arena&)>& plan_q,
+                   const std::function<int(uint8_t*, const orbfe_frame_view&, SbpQuery*)>& make_q,
+                   int32_t* best_idx, int* nmatches) {
+  Arena ar;
+  SbpPlan p;
+  sbp_plan_inputs(ar, F, nq, SBP_CAND, p);
+  plan_q(ar);
+  sbp_plan_scratch(ar, F, p);
+  int st = ensure_arena(m, ar.total);
+  if (st) return st;
+  uint8_t* A = m->arena;
+  orbfe_frame_view dF;
+  if ((st = sbp_stage(m, p, F, h_qdesc, h_qangle, &dF))) return st;
+  if (nq > 0 && (st = make_q(A, dF, (SbpQuery*)(A + p.oq)))) return st;  // stages, flushes, builds queries
+  if ((st = flush_h2d(m))) return st;
+  if ((st = sbp_launch(m, p, F, dF, md))) return st;
+  return sbp_fetch(m, p, best_idx, nmatches);
 }
 
 extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_frame_view* F,
@@ -1554,7 +1612,7 @@ extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_fr
     hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
-  return run_sbp(m, F, M, 0, mps->descriptors, nullptr, 0, plan, make, best_idx, nmatches);
+  return run_sbp(m, F, M, SbpMode{0, TH_HIGH, 0, 0}, mps->descriptors, nullptr, plan, make, best_idx, nmatches);
 }
 
 extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
@@ -1619,7 +1677,8 @@ extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
     hipLaunchKernelGGL(k_sbp_last_queries, dim3((N + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
-  return run_sbp(m, C, N, 1, L->descriptors, L->angle, m->check_ori, plan, make, best_idx, nmatches);
+  return run_sbp(m, C, N, SbpMode{1, TH_HIGH, 0, m->check_ori}, L->descriptors, L->angle, plan, make, best_idx,
+                 nmatches);
 }
 
 extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
@@ -1664,9 +1723,9 @@ static void fill_frustum_args(FrustumArgs& fa, const orbfe_frame_view* F, const 
   fa.max_x = F->max_x;
   fa.min_y = F->min_y;
   fa.max_y = F->max_y;
-  fa.log_sf = log_sf;
   fa.cos_limit = cos_limit;
   fa.nlevels = F->nlevels;
+  predict_scale_table(log_sf, F->nlevels, fa.scale_thr);
 }
 
 struct FrustumPlan {
@@ -1740,7 +1799,7 @@ static int fetch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, int
 extern "C" int orbfe_is_in_frustum(orbfe_matcher* m, const orbfe_frame_view* F, const orbfe_mappoint_geometry* G,
                                    const float* tcw, float log_scale_factor, float viewing_cos_limit,
                                    const orbfe_frustum_out* out, int* n_in_view) {
-  if (!m || !F || !tcw || !geom_ok(G, false) || F->nlevels <= 0)
+  if (!m || !F || !tcw || !geom_ok(G, false) || F->nlevels <= 0 || F->nlevels > ORBFE_MAX_LEVELS_M)
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_is_in_frustum: bad argument");
   hipSetDevice(m->device);
   Arena ar;
@@ -1791,7 +1850,7 @@ extern "C" int orbfe_search_local_points(orbfe_matcher* m, const orbfe_frame_vie
     hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
-  int st = run_sbp(m, F, M, 0, G->descriptors, nullptr, 0, plan, make, best_idx, nmatches);
+  int st = run_sbp(m, F, M, SbpMode{0, TH_HIGH, 0, 0}, G->descriptors, nullptr, plan, make, best_idx, nmatches);
   if (st) return st;
   if (M == 0) {
     if (n_in_view) *n_in_view = 0;

@@ -190,9 +190,21 @@ class MapPointGeometry:
         return v
 
 
+_libm = None
+
+
 def log_scale_factor(scale_factor: float) -> np.float32:
-    """Frame::mfLogScaleFactor = log(mfScaleFactor) (Frame.cc:106), rounded to float."""
-    return np.float32(np.log(np.float64(np.float32(scale_factor))))
+    """Frame::mfLogScaleFactor = log(mfScaleFactor) (Frame.cc:106). mfScaleFactor is a float and
+    the translation unit sees `using namespace std` (TemplatedVocabulary.h:36), so this is the
+    float overload: the C library's logf."""
+    global _libm
+    if _libm is None:
+        import ctypes
+        import ctypes.util
+        _libm = ctypes.CDLL(ctypes.util.find_library("m") or "libm.so.6")
+        _libm.logf.restype = ctypes.c_float
+        _libm.logf.argtypes = [ctypes.c_float]
+    return np.float32(_libm.logf(float(np.float32(scale_factor))))
 
 
 @dataclass
