@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "orbfe.h"
+#include "orbfe_keyframe.h"
 #include "orbfe_stereo.h"
 
 namespace orbfe {
@@ -174,6 +175,97 @@ class Matcher {
     for (int i = 0; i < kf1.n; i++)
       if (m12[i] >= 0) pairs.emplace_back((size_t)i, (size_t)m12[i]);
     return nm;
+  }
+
+  // ---- the remaining searches (orbfe_keyframe.h); outputs as documented there ----------------
+  // SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.h:64): match_f[k] = KF keypoint or -1.
+  int SearchByBoW(const orbfe_frame_view& kf, const orbfe_feature_vector& kf_fv, const orbfe_frame_view& F,
+                  const orbfe_feature_vector& f_fv, std::vector<int32_t>& match_f) {
+    match_f.assign(F.n > 0 ? F.n : 1, -1);
+    int nm = 0;
+    check(orbfe_search_by_bow_kf_frame(m_, &kf, &kf_fv, &F, &f_fv, match_f.data(), &nm), "SearchByBoW(KF, F)");
+    match_f.resize(F.n > 0 ? F.n : 0);
+    return nm;
+  }
+  // SearchByBoW(pKF1, pKF2, vpMatches12) (ORBmatcher.h:65): match12[i] = KF2 keypoint or -1.
+  int SearchByBoW12(const orbfe_frame_view& kf1, const orbfe_feature_vector& fv1, const orbfe_frame_view& kf2,
+                    const orbfe_feature_vector& fv2, std::vector<int32_t>& match12) {
+    match12.assign(kf1.n > 0 ? kf1.n : 1, -1);
+    int nm = 0;
+    check(orbfe_search_by_bow_kf_kf(m_, &kf1, &fv1, &kf2, &fv2, match12.data(), &nm), "SearchByBoW(KF, KF)");
+    match12.resize(kf1.n > 0 ? kf1.n : 0);
+    return nm;
+  }
+  // SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (ORBmatcher.h:56)
+  int SearchByProjection(const orbfe_frame_view& current, const float tcw_cur[12],
+                         const orbfe_mappoint_geometry& kf_points, const float* kf_angle, float log_scale_factor,
+                         float th, int orb_dist, std::vector<int32_t>& best_idx) {
+    best_idx.assign(kf_points.m > 0 ? kf_points.m : 1, -1);
+    int nm = 0;
+    check(orbfe_search_by_projection_keyframe(m_, &current, tcw_cur, &kf_points, kf_angle, log_scale_factor, th,
+                                              orb_dist, best_idx.data(), &nm),
+          "SearchByProjection(F, KF)");
+    best_idx.resize(kf_points.m > 0 ? kf_points.m : 0);
+    return nm;
+  }
+  // SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.h:60)
+  int SearchByProjectionSim3(const orbfe_frame_view& kf, const float scw[12], const orbfe_mappoint_geometry& pts,
+                             float log_scale_factor, int th, std::vector<int32_t>& best_idx) {
+    best_idx.assign(pts.m > 0 ? pts.m : 1, -1);
+    int nm = 0;
+    check(orbfe_search_by_projection_sim3(m_, &kf, scw, &pts, log_scale_factor, th, best_idx.data(), &nm),
+          "SearchByProjection(KF, Scw)");
+    best_idx.resize(pts.m > 0 ? pts.m : 0);
+    return nm;
+  }
+  // Fuse(pKF, vpMapPoints, th) (ORBmatcher.h:88): candidates; the caller applies and counts.
+  int Fuse(const orbfe_frame_view& kf, const float tcw[12], const float ow[3], const orbfe_mappoint_geometry& pts,
+           float log_scale_factor, float th, std::vector<int32_t>& best_idx) {
+    best_idx.assign(pts.m > 0 ? pts.m : 1, -1);
+    int n = 0;
+    check(orbfe_fuse(m_, &kf, tcw, ow, &pts, log_scale_factor, th, best_idx.data(), &n), "Fuse(KF)");
+    best_idx.resize(pts.m > 0 ? pts.m : 0);
+    return n;
+  }
+  // Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (ORBmatcher.h:91)
+  int FuseSim3(const orbfe_frame_view& kf, const float scw[12], const orbfe_mappoint_geometry& pts,
+               float log_scale_factor, float th, std::vector<int32_t>& best_idx) {
+    best_idx.assign(pts.m > 0 ? pts.m : 1, -1);
+    int n = 0;
+    check(orbfe_fuse_sim3(m_, &kf, scw, &pts, log_scale_factor, th, best_idx.data(), &n), "Fuse(KF, Scw)");
+    best_idx.resize(pts.m > 0 ? pts.m : 0);
+    return n;
+  }
+  // SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.h:69)
+  int SearchBySim3(const orbfe_frame_view& kf1, const orbfe_frame_view& kf2, const orbfe_mappoint_geometry& mps1,
+                   const orbfe_mappoint_geometry& mps2, const float t1w[12], const float t2w[12], float s12,
+                   const float r12[9], const float t12[3], float lsf1, float lsf2, float th,
+                   std::vector<int32_t>& match12) {
+    match12.assign(kf1.n > 0 ? kf1.n : 1, -1);
+    int n = 0;
+    check(orbfe_search_by_sim3(m_, &kf1, &kf2, &mps1, &mps2, t1w, t2w, s12, r12, t12, lsf1, lsf2, th,
+                               match12.data(), &n),
+          "SearchBySim3");
+    match12.resize(kf1.n > 0 ? kf1.n : 0);
+    return n;
+  }
+  // SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) (ORBmatcher.h:77)
+  int SearchForInitialization(const orbfe_frame_view& f1, const orbfe_frame_view& f2, std::vector<float>& prev_xy,
+                              std::vector<int32_t>& match12, int window_size = 10) {
+    match12.assign(f1.n > 0 ? f1.n : 1, -1);
+    int nm = 0;
+    check(orbfe_search_for_initialization(m_, &f1, &f2, prev_xy.data(), window_size, match12.data(), &nm),
+          "SearchForInitialization");
+    match12.resize(f1.n > 0 ? f1.n : 0);
+    return nm;
+  }
+  // MapPoint::ComputeDistinctiveDescriptors for many MapPoints (MapPoint.cc:272-337)
+  void ComputeDistinctiveDescriptors(const std::vector<int32_t>& offsets, const std::vector<uint8_t>& desc,
+                                     std::vector<int32_t>& best_index) {
+    const int n = offsets.empty() ? 0 : (int)offsets.size() - 1;
+    best_index.assign(n, -1);
+    check(orbfe_compute_distinctive_descriptors(m_, n, offsets.data(), desc.data(), best_index.data()),
+          "ComputeDistinctiveDescriptors");
   }
 
   orbfe_matcher* handle() const { return m_; }

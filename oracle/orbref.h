@@ -125,6 +125,8 @@ int orbref_search_by_sim3(const orbfe_frame_view* kf1, const orbfe_frame_view* k
 int orbref_search_for_initialization(const orbfe_frame_view* f1, const orbfe_frame_view* f2,
                                      float* prev_matched, int window, float nnratio, int check_ori,
                                      int32_t* match12, int* nmatches);
+long long orbref_check_predict_scale(float lsf, int nlevels, const float* thr, uint32_t lo_bits,
+                                     uint32_t hi_bits, long long* non_monotone);
 int orbref_compute_distinctive_descriptors(int n_points, const int32_t* offsets,
                                            const uint8_t* descriptors, int32_t* best_index);
 

@@ -574,3 +574,27 @@ extern "C" int orbref_compute_distinctive_descriptors(int n_points, const int32_
   }
   return ORBFE_OK;
 }
+
+// Exhaustive check of a PredictScale threshold table (orbfe_predict_scale_thresholds) against the
+// reference formula over every float ratio with bit pattern in [lo_bits, hi_bits]: returns the
+// number of ratios where #{k : ratio >= thr[k-1]} differs from clamp(ceil(logf(r) / lsf)), and
+// (in *non_monotone) how many times the reference formula decreased between neighbouring floats.
+extern "C" long long orbref_check_predict_scale(float lsf, int nlevels, const float* thr, uint32_t lo_bits,
+                                                uint32_t hi_bits, long long* non_monotone) {
+  long long bad = 0, nm = 0;
+  int last = INT_MIN;
+  for (uint64_t b = lo_bits; b <= hi_bits; b++) {
+    const uint32_t bits = (uint32_t)b;
+    float r;
+    std::memcpy(&r, &bits, 4);
+    const int raw = (int)std::ceil(std::log(r) / lsf);  // MapPoint.cc:424 (float overloads)
+    const int want = raw < 0 ? 0 : (raw >= nlevels ? nlevels - 1 : raw);
+    int got = 0;
+    for (int k = 1; k < nlevels; k++) got += r >= thr[k - 1];
+    bad += got != want;
+    if (raw < last) nm++;
+    last = raw;
+  }
+  if (non_monotone) *non_monotone = nm;
+  return bad;
+}

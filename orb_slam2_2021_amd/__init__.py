@@ -3,12 +3,15 @@
 The product is liborbfe.so (HIP kernels for gfx950 behind the C ABI in include/orbfe.h); this
 package is its host-side mirror of the reference's ORBextractor / ORBmatcher interfaces.
 """
-from ._lib import (KEYPOINT_DTYPE, LIB_PATH, LibraryMissing, OrbfeError, ORBFE_MP_NONE,
+from ._lib import (KEYPOINT_DTYPE, LIB_PATH, LibraryMissing, OrbfeError, ORBFE_MP_BAD, ORBFE_MP_NONE,
                    ORBFE_MP_OBSERVED, ORBFE_MP_PRESENT, ORBFE_RESIZE_SCALAR, ORBFE_RESIZE_SIMD128,
-                   MPF_BAD, MPF_OBSERVED, MPF_OUTLIER, MPF_PRESENT, MPF_SEEN, MPF_TRACK_IN_VIEW)
+                   MPF_BAD, MPF_OBSERVED, MPF_OUTLIER, MPF_PRESENT, MPF_SEEN, MPF_SKIP,
+                   MPF_TRACK_IN_VIEW)
 from .extractor import ORBextractor, synth_frame
-from .frames import FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints, MapPointGeometry
+from .frames import (FeatureVector, Frame, KeyFrame, KeyFrameMapPoints, LastFrameMapPoints,
+                     LocalMapPoints, MapPointGeometry)
 from .matcher import ORBmatcher
 
-__all__ = ["ORBextractor", "ORBmatcher", "Frame", "FeatureVector", "LocalMapPoints",
-           "LastFrameMapPoints", "KEYPOINT_DTYPE", "synth_frame", "OrbfeError", "LibraryMissing"]
+__all__ = ["ORBextractor", "ORBmatcher", "Frame", "KeyFrame", "FeatureVector", "LocalMapPoints",
+           "LastFrameMapPoints", "MapPointGeometry", "KeyFrameMapPoints", "KEYPOINT_DTYPE",
+           "synth_frame", "OrbfeError", "LibraryMissing"]

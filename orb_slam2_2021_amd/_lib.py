@@ -25,8 +25,10 @@ ORBFE_ERR_STATE = -4
 ORBFE_RESIZE_SIMD128 = 0
 ORBFE_RESIZE_SCALAR = 1
 ORBFE_MP_NONE, ORBFE_MP_PRESENT, ORBFE_MP_OBSERVED = 0, 1, 2
+ORBFE_MP_BAD = 3  # orbfe_keyframe.h: non-NULL MapPoint with isBad()
 MPF_TRACK_IN_VIEW, MPF_BAD, MPF_OBSERVED, MPF_PRESENT, MPF_OUTLIER = 1, 2, 4, 8, 16
 MPF_SEEN = 32  # orbfe_frustum.h: mnLastFrameSeen == CurrentFrame.mnId
+MPF_SKIP = 64  # orbfe_keyframe.h: already found / in the KeyFrame / already matched
 
 # cv::KeyPoint field order (28 bytes), = orbfe_keypoint
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -164,6 +166,36 @@ _SIGNATURES = {
                                           c_float, c_void_p, POINTER(c_int), POINTER(frustum_out),
                                           POINTER(c_int)]),
     "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
+    # orbfe_keyframe.h
+    "orbfe_search_by_bow_kf_frame": (c_int, [c_void_p, POINTER(frame_view), POINTER(feature_vector),
+                                             POINTER(frame_view), POINTER(feature_vector), c_void_p,
+                                             POINTER(c_int)]),
+    "orbfe_search_by_bow_kf_frame_multi": (c_int, [c_void_p, c_int, c_void_p, c_void_p,
+                                                   POINTER(frame_view), POINTER(feature_vector),
+                                                   c_void_p, c_void_p]),
+    "orbfe_search_by_bow_kf_kf": (c_int, [c_void_p, POINTER(frame_view), POINTER(feature_vector),
+                                          POINTER(frame_view), POINTER(feature_vector), c_void_p,
+                                          POINTER(c_int)]),
+    "orbfe_search_by_projection_keyframe": (c_int, [c_void_p, POINTER(frame_view), c_void_p,
+                                                    POINTER(mappoint_geometry), c_void_p, c_float,
+                                                    c_float, c_int, c_void_p, POINTER(c_int)]),
+    "orbfe_search_by_projection_sim3": (c_int, [c_void_p, POINTER(frame_view), c_void_p,
+                                                POINTER(mappoint_geometry), c_float, c_int,
+                                                c_void_p, POINTER(c_int)]),
+    "orbfe_fuse": (c_int, [c_void_p, POINTER(frame_view), c_void_p, c_void_p,
+                           POINTER(mappoint_geometry), c_float, c_float, c_void_p, POINTER(c_int)]),
+    "orbfe_fuse_sim3": (c_int, [c_void_p, POINTER(frame_view), c_void_p, POINTER(mappoint_geometry),
+                                c_float, c_float, c_void_p, POINTER(c_int)]),
+    "orbfe_search_by_sim3": (c_int, [c_void_p, POINTER(frame_view), POINTER(frame_view),
+                                     POINTER(mappoint_geometry), POINTER(mappoint_geometry),
+                                     c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_float,
+                                     c_float, c_float, c_void_p, POINTER(c_int)]),
+    "orbfe_search_for_initialization": (c_int, [c_void_p, POINTER(frame_view), POINTER(frame_view),
+                                                c_void_p, c_int, c_void_p, POINTER(c_int)]),
+    "orbfe_compute_distinctive_descriptors": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "orbfe_compute_distinctive_descriptors_device": (c_int, [c_void_p, c_int, c_void_p, c_void_p,
+                                                             c_void_p, c_void_p]),
+    "orbfe_predict_scale_thresholds": (c_int, [c_float, c_int, c_void_p]),
 }
 
 # symbols declared in include/*.h (checked by tests/test_library.py)

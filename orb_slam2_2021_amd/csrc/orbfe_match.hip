@@ -477,7 +477,7 @@ struct SbpArgs {
   int mode;                   // 0 local (best + second + ratio), 1 first minimum (other overloads)
   float nnratio;
   int dist_th;                // accept bestDist <= dist_th (TH_HIGH, TH_LOW or ORBdist)
-  int block_any;              // pre-blocked keypoints: mp_state != NONE (1) or == OBSERVED (0)
+  int block_any;              // pre-blocked keypoints: SBP_BLOCK_*
   int cand_cap;               // per-query candidate cache entries
   int32_t* res_prev;
   int32_t* res_cur;
@@ -499,8 +499,9 @@ struct SbpArgs {
 // Keypoint taken before the search starts: Frame::mvpMapPoints with Observations() > 0 (:91-93,
 // :1420-1422) or any non-NULL entry (:384, :1567).
 __device__ __forceinline__ bool sbp_pre_blocked(const SbpArgs& a, int k) {
+  if (a.block_any == SBP_BLOCK_NONE) return false;  // Fuse, SearchBySim3: nothing is skipped
   const uint8_t st = a.F.mp_state[k];
-  return a.block_any ? st != ORBFE_MP_NONE : st == ORBFE_MP_OBSERVED;
+  return a.block_any == SBP_BLOCK_ANY ? st != ORBFE_MP_NONE : st == ORBFE_MP_OBSERVED;
 }
 
 // Window candidate test that precedes the distance (rec = {x, y, uRight, index | octave << 16}).

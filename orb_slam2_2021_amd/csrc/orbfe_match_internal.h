@@ -111,10 +111,14 @@ struct SbpQuery {
   int gate;           // SBP_GATE_*
 };
 
+#define SBP_BLOCK_OBSERVED 0  // mp_state == ORBFE_MP_OBSERVED (Observations() > 0: :91-93, :1420-1422)
+#define SBP_BLOCK_ANY 1       // mp_state != ORBFE_MP_NONE (any non-NULL entry: :384, :1567)
+#define SBP_BLOCK_NONE 2      // nothing (Fuse, SearchBySim3 never skip a keypoint)
+
 struct SbpMode {
   int mode;       // 0 best + second + ratio (local map), 1 first minimum (all other overloads)
   int dist_th;    // accept bestDist <= dist_th
-  int block_any;  // 1: a keypoint whose mp_state != NONE is taken; 0: only ORBFE_MP_OBSERVED
+  int block_any;  // SBP_BLOCK_*: which keypoints are taken before the search starts
   int check_ori;  // rotation-consistency filter over q_angle (mode 1)
 };
 

@@ -89,6 +89,52 @@ class Frame:
         return v
 
 
+class KeyFrame(Frame):
+    """KeyFrame(F, pMap, pKFDB) as the keyframe matchers read it (KeyFrame.cc:29-64): the Frame's
+    keypoints, descriptors and tables, with the image bounds narrowed to the KeyFrame's
+    `const int` mnMinX.. (KeyFrame.h:202-205) while mGrid stays the Frame's grid (built with the
+    Frame's float bounds and cell sizes). mp_state is GetMapPointMatches() (ORBFE_MP_BAD for a
+    MapPoint with isBad())."""
+
+    grid_origin: Optional[tuple] = None  # the Frame's (mnMinX, mnMinY) that built mGrid
+    grid_inv: Optional[tuple] = None     # the Frame's (mfGridElementWidthInv, ...HeightInv)
+
+    @staticmethod
+    def from_frame(F: "Frame", tcw: Optional[np.ndarray] = None,
+                   mp_state: Optional[np.ndarray] = None) -> "KeyFrame":
+        kf = KeyFrame(keys_un=F.keys_un, descriptors=F.descriptors, u_right=F.u_right,
+                      mp_state=F.mp_state if mp_state is None else mp_state,
+                      scale_factors=F.scale_factors, level_sigma2=F.level_sigma2,
+                      min_x=float(int(F.min_x)), max_x=float(int(F.max_x)),
+                      min_y=float(int(F.min_y)), max_y=float(int(F.max_y)),
+                      fx=F.fx, fy=F.fy, cx=F.cx, cy=F.cy, bf=F.bf,
+                      tcw=F.tcw if tcw is None else tcw, feat_vec=F.feat_vec)
+        kf.grid_origin = (float(F.min_x), float(F.min_y))
+        kf.grid_inv = (float(F.grid_inv_w), float(F.grid_inv_h))
+        return kf
+
+    @property
+    def grid_inv_w(self) -> np.float32:
+        return _f32(self.grid_inv[0]) if self.grid_inv else Frame.grid_inv_w.fget(self)
+
+    @property
+    def grid_inv_h(self) -> np.float32:
+        return _f32(self.grid_inv[1]) if self.grid_inv else Frame.grid_inv_h.fget(self)
+
+    @property
+    def camera_center(self) -> np.ndarray:
+        """GetCameraCenter(): Ow = -Rcw^T tcw (gemm, double accumulation)."""
+        R, t = self.tcw[:, :3], self.tcw[:, 3]
+        return np.array([-gemv_f32_double(R.T[i:i + 1], t)[0] for i in range(3)], np.float32)
+
+    def view(self) -> L.frame_view:
+        v = Frame.view(self)
+        if self.grid_origin is not None:
+            v.grid_origin_set = 1
+            v.grid_min_x, v.grid_min_y = self.grid_origin
+        return v
+
+
 @dataclass
 class FeatureVector:
     """DBoW2::FeatureVector (node id -> ascending feature indices) as CSR."""
@@ -188,6 +234,19 @@ class MapPointGeometry:
         for f in ("flags", "world_pos", "normal", "min_distance", "max_distance", "descriptors"):
             setattr(v, f, L.ptr(getattr(self, f)))
         return v
+
+
+@dataclass
+class KeyFrameMapPoints:
+    """pKF->GetMapPointMatches() by KeyFrame keypoint with the KeyFrame's mvKeysUn angles, as
+    SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) reads them
+    (ORBmatcher.cc:1511-1595). geometry.flags: MPF_PRESENT, MPF_BAD, MPF_SKIP (in sAlreadyFound)."""
+
+    geometry: MapPointGeometry
+    angle: np.ndarray
+
+    def __post_init__(self):
+        self.angle = np.ascontiguousarray(self.angle, np.float32).reshape(len(self.geometry.flags))
 
 
 _libm = None

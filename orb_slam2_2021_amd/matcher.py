@@ -1,22 +1,32 @@
 """ORBmatcher on MI355X -- host mirror of include/ORBmatcher.h over liborbfe.so.
 
-ORBmatcher(nnratio=0.6, checkOri=True) with DescriptorDistance, both SearchByProjection overloads
-used by Tracking and SearchForTriangulation used by LocalMapping (include/ORBmatcher.h:41-85).
-The reference mutates the Frame it is given; the mirror returns what it would have written:
-  SearchByProjection(F, LocalMapPoints, th)      -> (nmatches, best_idx per MapPoint)
-  SearchByProjection(F, LastFrameMapPoints, th, bMono) -> (nmatches, best_idx per last-frame kp)
+ORBmatcher(nnratio=0.6, checkOri=True) with DescriptorDistance and every search of
+include/ORBmatcher.h:41-85. The reference mutates the Frame / KeyFrame / MapPoints it is given;
+the mirror returns what it would have written (overloads dispatch on argument types, as in C++):
+  SearchByProjection(F, LocalMapPoints, th)             -> (nmatches, best_idx per MapPoint)
+  SearchByProjection(F, LastFrameMapPoints, th, bMono)  -> (nmatches, best_idx per last-frame kp)
+  SearchByProjection(F, KeyFrame, KeyFrameMapPoints, th, ORBdist) -> (nmatches, best_idx per KF kp)
+  SearchByProjection(KeyFrame, Scw, MapPointGeometry, th) -> (nmatches, best_idx per point)
+  SearchByBoW(KeyFrame, Frame)     -> (nmatches, KF keypoint per Frame keypoint)
+  SearchByBoW(KeyFrame, KeyFrame)  -> (nmatches, KF2 keypoint per KF1 keypoint)
+  SearchForInitialization(F1, F2, vbPrevMatched, windowSize) -> (nmatches, vnMatches12, prev)
   SearchForTriangulation(KF1, KF2, F12, bOnlyStereo) -> (nmatches, [(idx1, idx2), ...])
+  Fuse(KeyFrame, MapPointGeometry, th) / Fuse(KeyFrame, Scw, MapPointGeometry, th)
+                                   -> (count, best_idx per point)
+  SearchBySim3(KF1, KF2, mps1, mps2, s12, R12, t12, th) -> (nfound, match12)
+  ComputeDistinctiveDescriptors([descriptors per MapPoint]) -> BestIdx per MapPoint
 """
 from __future__ import annotations
 
+import ctypes
 from ctypes import byref, c_int, c_void_p
 from typing import List, Optional, Tuple, Union
 
 import numpy as np
 
 from . import _lib as L
-from .frames import (FeatureVector, Frame, LastFrameMapPoints, LocalMapPoints, MapPointGeometry,
-                     epipole, log_scale_factor)
+from .frames import (FeatureVector, Frame, KeyFrame, KeyFrameMapPoints, LastFrameMapPoints,
+                     LocalMapPoints, MapPointGeometry, epipole, log_scale_factor)
 
 
 class ORBmatcher:
@@ -58,8 +68,20 @@ class ORBmatcher:
                                                           L.ptr(out)), "distance_batch")
         return out
 
-    def SearchByProjection(self, F: Frame, points: Union[LocalMapPoints, LastFrameMapPoints],
-                           th: float = 3, bMono: Optional[bool] = None) -> Tuple[int, np.ndarray]:
+    def SearchByProjection(self, F: Frame, points, *args, **kw) -> Tuple[int, np.ndarray]:
+        """The four overloads of ORBmatcher.h:48-60, by argument types:
+        (F, LocalMapPoints, th=3); (F, LastFrameMapPoints, th, bMono);
+        (F, KeyFrame, KeyFrameMapPoints, th, ORBdist); (KeyFrame, Scw, MapPointGeometry, th)."""
+        if isinstance(points, KeyFrame):
+            return self.SearchByProjectionKeyFrame(F, points, *args, **kw)
+        if isinstance(F, KeyFrame) and isinstance(points, np.ndarray):
+            return self.SearchByProjectionSim3(F, points, *args, **kw)
+        th = args[0] if len(args) > 0 else kw.get("th", 3)
+        bMono = args[1] if len(args) > 1 else kw.get("bMono")
+        return self._search_by_projection_frame(F, points, th, bMono)
+
+    def _search_by_projection_frame(self, F: Frame, points: Union[LocalMapPoints, LastFrameMapPoints],
+                                    th: float, bMono: Optional[bool]) -> Tuple[int, np.ndarray]:
         fv = F.view()
         nm = c_int()
         if isinstance(points, LocalMapPoints):
@@ -139,6 +161,152 @@ class ORBmatcher:
         r, s = c_int(), c_int()
         L.check(self._lib.orbfe_matcher_last_stats(self._h, byref(r), byref(s)), "last_stats")
         return r.value, s.value
+
+    # ---- keyframe matchers (orbfe_keyframe.h) -----------------------------------------------
+    @staticmethod
+    def _lsf(F: Frame) -> float:
+        sf = float(F.scale_factors[1]) if len(F.scale_factors) > 1 else 1.0
+        return float(log_scale_factor(sf))
+
+    def SearchByBoW(self, pKF: KeyFrame, other: Frame) -> Tuple[int, np.ndarray]:
+        """SearchByBoW(pKF, F, vpMapPointMatches) (ORBmatcher.cc:165-293) when `other` is a Frame:
+        returns (nmatches, KF keypoint index per Frame keypoint or -1).
+        SearchByBoW(pKF1, pKF2, vpMatches12) (:536-669) when `other` is a KeyFrame:
+        returns (nmatches, KF2 keypoint index per KF1 keypoint or -1)."""
+        if pKF.feat_vec is None or other.feat_vec is None:
+            raise ValueError("SearchByBoW needs mFeatVec on both sides")
+        v1, f1 = pKF.view(), pKF.feat_vec.view()
+        v2, f2 = other.view(), other.feat_vec.view()
+        nm = c_int()
+        if isinstance(other, KeyFrame):
+            out = np.full(max(pKF.N, 1), -1, np.int32)
+            L.check(self._lib.orbfe_search_by_bow_kf_kf(self._h, byref(v1), byref(f1), byref(v2),
+                                                        byref(f2), L.ptr(out), byref(nm)),
+                    "SearchByBoW(KF, KF)")
+            return nm.value, out[:pKF.N]
+        out = np.full(max(other.N, 1), -1, np.int32)
+        L.check(self._lib.orbfe_search_by_bow_kf_frame(self._h, byref(v1), byref(f1), byref(v2),
+                                                       byref(f2), L.ptr(out), byref(nm)),
+                "SearchByBoW(KF, F)")
+        return nm.value, out[:other.N]
+
+    def SearchByBoWMulti(self, kfs: List[KeyFrame], F: Frame) -> Tuple[np.ndarray, np.ndarray]:
+        """Tracking::Relocalization's SearchByBoW(vpCandidateKFs[i], mCurrentFrame, ...) loop in
+        one launch: (nmatches per KF, (n_kf, F.N) KF keypoint per Frame keypoint)."""
+        n = len(kfs)
+        views = (L.frame_view * max(n, 1))()
+        fvs = (L.feature_vector * max(n, 1))()
+        for i, kf in enumerate(kfs):
+            views[i] = kf.view()
+            fvs[i] = kf.feat_vec.view()
+        fv, ff = F.view(), F.feat_vec.view()
+        out = np.full((max(n, 1), max(F.N, 1)), -1, np.int32)
+        counts = np.zeros(max(n, 1), np.int32)
+        L.check(self._lib.orbfe_search_by_bow_kf_frame_multi(
+            self._h, n, ctypes.addressof(views), ctypes.addressof(fvs), byref(fv), byref(ff),
+            L.ptr(out), L.ptr(counts)), "SearchByBoW(KFs, F)")
+        return counts[:n], out[:n, :F.N]
+
+    def SearchByProjectionKeyFrame(self, F: Frame, pKF: KeyFrame, pts: KeyFrameMapPoints,
+                                   th: float, ORBdist: int) -> Tuple[int, np.ndarray]:
+        """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+        (ORBmatcher.cc:1493-1625): best_idx per KF keypoint, encoded as for the last-frame
+        overload (k >= 0 assigned, k <= -2 assigned then undone by the rotation filter)."""
+        if F.tcw is None:
+            raise ValueError("CurrentFrame.tcw (mTcw) is required")
+        fv, gv = F.view(), pts.geometry.view()
+        best = np.full(max(len(pts.angle), 1), -1, np.int32)
+        nm = c_int()
+        L.check(self._lib.orbfe_search_by_projection_keyframe(
+            self._h, byref(fv), L.ptr(F.tcw), byref(gv), L.ptr(pts.angle), self._lsf(F), float(th),
+            int(ORBdist), L.ptr(best), byref(nm)), "SearchByProjection(F, KF)")
+        return nm.value, best[:len(pts.angle)]
+
+    def SearchByProjectionSim3(self, pKF: KeyFrame, Scw: np.ndarray, pts: MapPointGeometry,
+                               th: int) -> Tuple[int, np.ndarray]:
+        """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:295-412);
+        pKF.mp_state encodes vpMatched. best_idx[i] = keypoint for vpPoints[i] or -1."""
+        kv, gv = pKF.view(), pts.view()
+        scw = np.ascontiguousarray(np.asarray(Scw, np.float32).reshape(-1, 4)[:3], np.float32)
+        best = np.full(max(len(pts.flags), 1), -1, np.int32)
+        nm = c_int()
+        L.check(self._lib.orbfe_search_by_projection_sim3(
+            self._h, byref(kv), L.ptr(scw), byref(gv), self._lsf(pKF), int(th), L.ptr(best),
+            byref(nm)), "SearchByProjection(KF, Scw)")
+        return nm.value, best[:len(pts.flags)]
+
+    def Fuse(self, pKF: KeyFrame, *args) -> Tuple[int, np.ndarray]:
+        """Fuse(pKF, vpMapPoints, th=3.0) (ORBmatcher.cc:841-991) or Fuse(pKF, Scw, vpPoints, th)
+        (:993-1120): the keypoint each MapPoint is fused into (or -1). For the first overload the
+        count is the number of candidates (the adapter re-tests isBad / IsInKeyFrame as it
+        applies them); for the Scw overload it is the reference's return value."""
+        kv = pKF.view()
+        if len(args) and isinstance(args[0], np.ndarray) and args[0].size in (12, 16):
+            scw = np.ascontiguousarray(np.asarray(args[0], np.float32).reshape(-1, 4)[:3])
+            pts, th = args[1], float(args[2])
+            gv = pts.view()
+            best = np.full(max(len(pts.flags), 1), -1, np.int32)
+            n = c_int()
+            L.check(self._lib.orbfe_fuse_sim3(self._h, byref(kv), L.ptr(scw), byref(gv),
+                                              self._lsf(pKF), th, L.ptr(best), byref(n)),
+                    "Fuse(KF, Scw)")
+            return n.value, best[:len(pts.flags)]
+        pts = args[0]
+        th = float(args[1]) if len(args) > 1 else 3.0
+        if pKF.tcw is None:
+            raise ValueError("pKF.tcw (GetPose) is required")
+        gv = pts.view()
+        ow = pKF.camera_center
+        best = np.full(max(len(pts.flags), 1), -1, np.int32)
+        n = c_int()
+        L.check(self._lib.orbfe_fuse(self._h, byref(kv), L.ptr(pKF.tcw), L.ptr(ow), byref(gv),
+                                     self._lsf(pKF), th, L.ptr(best), byref(n)), "Fuse(KF)")
+        return n.value, best[:len(pts.flags)]
+
+    def SearchBySim3(self, pKF1: KeyFrame, pKF2: KeyFrame, mps1: MapPointGeometry,
+                     mps2: MapPointGeometry, s12: float, R12: np.ndarray, t12: np.ndarray,
+                     th: float) -> Tuple[int, np.ndarray]:
+        """SearchBySim3 (ORBmatcher.cc:1122-1346): (nFound, KF2 keypoint per KF1 keypoint where
+        both directions agree, else -1). mps1 / mps2 flags: MPF_PRESENT, MPF_BAD, MPF_SKIP
+        (vbAlreadyMatched)."""
+        v1, v2, g1, g2 = pKF1.view(), pKF2.view(), mps1.view(), mps2.view()
+        r12 = np.ascontiguousarray(R12, np.float32).reshape(9)
+        t = np.ascontiguousarray(t12, np.float32).reshape(3)
+        out = np.full(max(pKF1.N, 1), -1, np.int32)
+        n = c_int()
+        L.check(self._lib.orbfe_search_by_sim3(
+            self._h, byref(v1), byref(v2), byref(g1), byref(g2), L.ptr(pKF1.tcw), L.ptr(pKF2.tcw),
+            float(s12), L.ptr(r12), L.ptr(t), self._lsf(pKF1), self._lsf(pKF2), float(th),
+            L.ptr(out), byref(n)), "SearchBySim3")
+        return n.value, out[:pKF1.N]
+
+    def SearchForInitialization(self, F1: Frame, F2: Frame, vbPrevMatched: np.ndarray,
+                                windowSize: int = 10) -> Tuple[int, np.ndarray, np.ndarray]:
+        """SearchForInitialization (ORBmatcher.cc:414-534): (nmatches, vnMatches12, updated
+        vbPrevMatched as an (N1, 2) float32 array)."""
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).reshape(F1.N, 2).copy()
+        v1, v2 = F1.view(), F2.view()
+        out = np.full(max(F1.N, 1), -1, np.int32)
+        nm = c_int()
+        L.check(self._lib.orbfe_search_for_initialization(self._h, byref(v1), byref(v2), L.ptr(prev),
+                                                          int(windowSize), L.ptr(out), byref(nm)),
+                "SearchForInitialization")
+        return nm.value, out[:F1.N], prev
+
+    def ComputeDistinctiveDescriptors(self, descriptor_sets: List[np.ndarray]) -> np.ndarray:
+        """MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:272-337) for many MapPoints at
+        once: BestIdx into each MapPoint's (n_i, 32) descriptor rows (-1 when n_i == 0)."""
+        counts = np.array([len(d) for d in descriptor_sets], np.int64)
+        offsets = np.zeros(len(descriptor_sets) + 1, np.int32)
+        offsets[1:] = np.cumsum(counts)
+        desc = (np.ascontiguousarray(np.concatenate([np.asarray(d, np.uint8).reshape(-1, 32)
+                                                     for d in descriptor_sets]), np.uint8)
+                if len(descriptor_sets) and offsets[-1] else np.zeros((1, 32), np.uint8))
+        out = np.full(max(len(descriptor_sets), 1), -1, np.int32)
+        L.check(self._lib.orbfe_compute_distinctive_descriptors(
+            self._h, len(descriptor_sets), L.ptr(offsets), L.ptr(desc), L.ptr(out)),
+            "ComputeDistinctiveDescriptors")
+        return out[:len(descriptor_sets)]
 
     def SearchForTriangulation(self, pKF1: Frame, pKF2: Frame, F12: np.ndarray,
                                bOnlyStereo: bool = False,

@@ -239,3 +239,159 @@ def make_lastframe(C: Frame, n: int, rng: np.random.Generator, motion: np.ndarra
     flags[rng.random(n) < 0.05] |= np.uint8(L.MPF_OUTLIER)
     flags[rng.random(n) < 0.2] &= ~np.uint8(L.MPF_OBSERVED)
     return LastFrameMapPoints(flags, pw, desc, octave.astype(np.int32), angle, tl)
+
+
+# ---- keyframe scenes (SearchByBoW, Fuse, SearchBySim3, relocalisation / loop-closing projections) ---
+@dataclass
+class KeyFrameScene:
+    """Two KeyFrames observing one set of world points, with the MapPoints by keypoint."""
+
+    kf1: "KeyFrame"
+    kf2: "KeyFrame"
+    mps1: "MapPointGeometry"   # KF1's GetMapPointMatches() by keypoint (flags 0 = NULL)
+    mps2: "MapPointGeometry"
+    point_of_kp1: np.ndarray   # world point index per KF1 keypoint (-1 = clutter)
+    point_of_kp2: np.ndarray
+    world: np.ndarray          # (P, 3) world points
+    f1: Optional[Frame] = None  # the Frames the KeyFrames were made from (Frame-typed arguments)
+    f2: Optional[Frame] = None
+
+
+def scale_tables(sf: float, nlevels: int) -> Tuple[np.ndarray, np.ndarray]:
+    """ORBextractor's mvScaleFactor / mvLevelSigma2 (ORBextractor.cc:419-426): float products."""
+    scale = np.ones(nlevels, np.float32)
+    for i in range(1, nlevels):
+        scale[i] = np.float32(scale[i - 1] * np.float32(sf))
+    return scale, (scale * scale).astype(np.float32)
+
+
+def _keypoints(x, y, octave, angle, scale) -> np.ndarray:
+    k = np.zeros(len(x), L.KEYPOINT_DTYPE)
+    k["x"], k["y"], k["octave"] = x, y, octave
+    k["size"] = np.float32(31) * scale[octave]
+    k["angle"] = np.mod(angle, 360.0)
+    k["response"] = 20.0
+    k["class_id"] = -1
+    return k
+
+
+def make_keyframe_scene(rng: np.random.Generator, rows: int = 376, cols: int = 1241,
+                        cam: Optional[dict] = None, n_points: int = 1200, n_clutter: int = 500,
+                        t1: Optional[np.ndarray] = None, t2: Optional[np.ndarray] = None,
+                        nlevels: int = 8, sf: float = 1.2, max_flips: int = 30,
+                        rot_noise: float = 4.0, wild_frac: float = 0.15, bad_frac: float = 0.05,
+                        stereo_frac: float = 0.4, vocab: Optional["Vocabulary"] = None,
+                        levelsup: int = 0, bounds: Optional[Tuple[float, float, float, float]] = None
+                        ) -> KeyFrameScene:
+    """World points in front of KF1 (pixel uniform, depth 2..30 m) re-observed by KF2 where they
+    project inside its image, plus clutter keypoints. Octaves follow each point's scale-invariance
+    range (MapPoint::UpdateNormalAndDepth, MapPoint.cc:376-400) up to +-1; KF2 descriptors are KF1's
+    with random bit flips; angles rotate by a few degrees (some wild). `bounds` = the Frame's float
+    (mnMinX, mnMaxX, mnMinY, mnMaxY) of a distorted camera (KeyFrames keep their int parts)."""
+    from .frames import KeyFrame, MapPointGeometry
+    cam = cam or KITTI_CAM
+    t1 = pose() if t1 is None else t1
+    t2 = pose(tx=-0.3, tz=0.4, yaw=0.03) if t2 is None else t2
+    scale, sigma2 = scale_tables(sf, nlevels)
+    mnx, mxx, mny, mxy = bounds if bounds is not None else (0.0, float(cols), 0.0, float(rows))
+    fx, fy, cx, cy = cam["fx"], cam["fy"], cam["cx"], cam["cy"]
+    R1, p1 = t1[:, :3].astype(np.float64), t1[:, 3].astype(np.float64)
+    R2, p2 = t2[:, :3].astype(np.float64), t2[:, 3].astype(np.float64)
+    O1, O2 = -R1.T @ p1, -R2.T @ p2
+    P = n_points
+    u1 = rng.uniform(mnx + 1, mxx - 1, P)
+    v1 = rng.uniform(mny + 1, mxy - 1, P)
+    z = rng.uniform(2.0, 30.0, P)
+    Xc1 = np.stack([(u1 - cx) / fx * z, (v1 - cy) / fy * z, z], 1)
+    Xw = (R1.T @ (Xc1 - p1).T).T
+    Xc2 = (R2 @ Xw.T).T + p2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        u2 = fx * Xc2[:, 0] / Xc2[:, 2] + cx
+        v2 = fy * Xc2[:, 1] / Xc2[:, 2] + cy
+    in2 = (Xc2[:, 2] > 0.1) & (u2 > mnx + 1) & (u2 < mxx - 1) & (v2 > mny + 1) & (v2 < mxy - 1)
+    octave = rng.integers(0, nlevels, P)
+    dist1 = np.linalg.norm(Xw - O1, axis=1)
+    maxd = dist1 * np.float64(sf) ** (octave + rng.uniform(-0.4, 0.4, P))
+    mind = maxd / np.float64(scale[nlevels - 1])
+    nrm = (Xw - O1) / dist1[:, None] + rng.normal(0, 0.05, (P, 3))
+    oblique = rng.random(P) < 0.05
+    nrm[oblique] = -nrm[oblique]
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    desc = rng.integers(0, 256, (P, 32), dtype=np.uint8)
+    ang = rng.uniform(0, 360, P)
+
+    def side(sel_pts, u, v, oct_, ang_, d_, clutter):
+        idx = np.nonzero(sel_pts)[0]
+        n = len(idx) + clutter
+        x = np.concatenate([u[idx] + rng.normal(0, 0.7, len(idx)), rng.uniform(mnx, mxx, clutter)])
+        y = np.concatenate([v[idx] + rng.normal(0, 0.7, len(idx)), rng.uniform(mny, mxy, clutter)])
+        o = np.concatenate([oct_[idx], rng.integers(0, nlevels, clutter)]).astype(np.int32)
+        a = np.concatenate([ang_[idx], rng.uniform(0, 360, clutter)])
+        d = np.concatenate([d_[idx], rng.integers(0, 256, (clutter, 32), dtype=np.uint8)])
+        pid = np.concatenate([idx, np.full(clutter, -1)]).astype(np.int64)
+        perm = rng.permutation(n)
+        x, y, o, a, d, pid = x[perm], y[perm], o[perm], a[perm], d[perm], pid[perm]
+        x = np.clip(x, mnx, mxx - 1e-3).astype(np.float32)
+        y = np.clip(y, mny, mxy - 1e-3).astype(np.float32)
+        return _keypoints(x, y, o, a.astype(np.float32), scale), d, pid
+
+    k1, d1, pid1 = side(np.ones(P, bool), u1, v1, octave, ang, desc, n_clutter)
+    oct2 = np.clip(octave + rng.integers(-1, 2, P), 0, nlevels - 1)
+    ang2 = ang + rng.normal(0, rot_noise, P)
+    wild = rng.random(P) < wild_frac
+    ang2[wild] = rng.uniform(0, 360, int(wild.sum()))
+    d2src = flip_bits(desc, rng.integers(0, max_flips + 1, P), rng)
+    k2, d2, pid2 = side(in2, u2, v2, oct2, ang2, d2src, n_clutter)
+
+    def frame(k, d, pid, tcw, depth):
+        n = len(k)
+        disp = np.where(pid >= 0, np.float32(cam["bf"]) / np.maximum(depth[np.maximum(pid, 0)], 0.1), 10.0)
+        ur = np.where(rng.random(n) < stereo_frac, k["x"] - disp, -1.0).astype(np.float32)
+        mp = np.where(pid >= 0, np.where(rng.random(n) < 0.7, L.ORBFE_MP_OBSERVED, L.ORBFE_MP_PRESENT),
+                      L.ORBFE_MP_NONE).astype(np.uint8)
+        mp[(pid >= 0) & (rng.random(n) < bad_frac)] = L.ORBFE_MP_BAD
+        F = Frame(keys_un=k, descriptors=d, u_right=ur, mp_state=mp, scale_factors=scale,
+                  level_sigma2=sigma2, min_x=mnx, max_x=mxx, min_y=mny, max_y=mxy, tcw=tcw, **cam)
+        if vocab is not None:
+            F.feat_vec = vocab.feature_vector(d, levelsup)
+        return F, KeyFrame.from_frame(F)
+
+    f1, kf1 = frame(k1, d1, pid1, t1, z)
+    f2, kf2 = frame(k2, d2, pid2, t2, np.where(in2, Xc2[:, 2], 1.0))
+
+    def geometry(kf, pid, dsrc):
+        n = kf.N
+        has = pid >= 0
+        j = np.maximum(pid, 0)
+        flags = np.where(has, L.MPF_PRESENT, 0).astype(np.uint8)
+        flags[kf.mp_state == L.ORBFE_MP_BAD] |= np.uint8(L.MPF_BAD)
+        pos = np.where(has[:, None], Xw[j], 0.0).astype(np.float32)
+        return MapPointGeometry(flags, pos, nrm[j].astype(np.float32), mind[j].astype(np.float32),
+                                maxd[j].astype(np.float32), np.where(has[:, None], dsrc[j], kf.descriptors))
+
+    return KeyFrameScene(kf1, kf2, geometry(kf1, pid1, desc), geometry(kf2, pid2, d2src), pid1, pid2,
+                         Xw.astype(np.float32), f1, f2)
+
+
+def sim3_between(t1: np.ndarray, t2: np.ndarray, s12: float = 1.0):
+    """(s12, R12, t12) of S12 = T1w * T2w^-1 with the scale set to s12 (LoopClosing::ComputeSim3)."""
+    R1, p1 = t1[:, :3].astype(np.float64), t1[:, 3].astype(np.float64)
+    R2, p2 = t2[:, :3].astype(np.float64), t2[:, 3].astype(np.float64)
+    R12 = R1 @ R2.T
+    t12 = p1 - s12 * R12 @ p2
+    return np.float32(s12), R12.astype(np.float32), t12.astype(np.float32)
+
+
+def distinctive_sets(rng: np.random.Generator, n: int, max_obs: int = 40) -> list:
+    """Per-MapPoint observation descriptors: a base descriptor with a few bit flips per
+    observation, some outliers, some empty sets (ComputeDistinctiveDescriptors, MapPoint.cc:272-337)."""
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(0, max_obs + 1))
+        base = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+        d = flip_bits(np.repeat(base, k, 0), rng.integers(0, 25, k), rng) if k else np.zeros((0, 32), np.uint8)
+        if k > 2:
+            out_idx = rng.random(k) < 0.2
+            d[out_idx] = rng.integers(0, 256, (int(out_idx.sum()), 32), dtype=np.uint8)
+        out.append(d)
+    return out
