@@ -335,6 +335,7 @@ def main():
         out["host_boundary"] = host_boundary_rate(ext, host)
         if not args.no_legs:
             out["legs"] = {"c5_search_local_points": sbp_leg(args),
+                           "keyframe_searches": keyframe_leg(args),
                            "compute_stereo_matches": stereo_leg(args, ext, d_img, host, B, H, W, cap,
                                                                 cam["bf"], float(dummy.mb))}
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -461,6 +462,106 @@ def sbp_leg(args, m_points=50000, reps=20):
         nr, br, nvr, _ = orbref.search_local_points(F, G, lsf, 3.0, 0.8, kind="native")
         out["cpu_oracle_ms_per_frame"] = round(1e3 * (time.perf_counter() - t0), 3)
         out["cpu_bit_exact"] = bool(nr == nm and nvr == nv and np.array_equal(br, best))
+    return out
+
+
+def keyframe_leg(args, reps=20):
+    """Secondary measurement: the remaining ORBmatcher searches and
+    MapPoint::ComputeDistinctiveDescriptors on a KITTI-shaped keyframe scene (two KeyFrames of
+    ~2000 keypoints over 1500 shared world points, synthetic vocabulary k=10, L=2), each through
+    its host-buffer C ABI entry (inputs uploaded and results returned every call: PCIe included),
+    beside the CPU oracle (-O3 -march=native, one core) on the same inputs and a bit-exact check.
+    Wall-clock per call on both sides; reported, not `value`."""
+    from orb_slam2_2021_amd import ORBmatcher, MPF_SKIP
+    from orb_slam2_2021_amd import synthetic as S
+    from orb_slam2_2021_amd.frames import KeyFrameMapPoints
+    from oracle import orbref
+    rng = np.random.default_rng(0x0B0C)
+    voc = S.Vocabulary.synthetic()
+    sc = S.make_keyframe_scene(rng, n_points=1500, n_clutter=500, vocab=voc)
+    kfs = [sc.kf2] + [S.make_keyframe_scene(np.random.default_rng(s), n_points=1500, n_clutter=500,
+                                            vocab=voc).kf2 for s in range(1, 8)]
+    cur = sc.f1
+    cur_state = cur.mp_state.copy()
+    sparse = np.where(rng.random(cur.N) < 0.2, 1, 0).astype(np.uint8)
+    pts = KeyFrameMapPoints(sc.mps2, sc.kf2.keys_un["angle"])
+    Scw = np.vstack([sc.kf1.tcw, [0, 0, 0, 1]]).astype(np.float32)
+    Scw[:3] *= np.float32(0.9)
+    s12, R12, t12 = S.sim3_between(sc.kf1.tcw, sc.kf2.tcw, 1.0)
+    prev = np.stack([cur.keys_un["x"], cur.keys_un["y"]], 1).astype(np.float32)
+    sets = S.distinctive_sets(rng, 2000, max_obs=20)
+    m = ORBmatcher(0.75, True)
+    mi = ORBmatcher(0.9, True)  # Initializer's matcher (Tracking::MonocularInitialization)
+
+    def with_state(state, fn):
+        def run():
+            cur.mp_state = state
+            try:
+                return fn()
+            finally:
+                cur.mp_state = cur_state
+        return run
+
+    cases = {
+        "SearchByBoW(KF,F)": (lambda: m.SearchByBoW(sc.kf2, cur),
+                              lambda k: orbref.search_by_bow(sc.kf2, cur, 0.75, True, False, kind=k)),
+        "SearchByBoW(KF,KF)": (lambda: m.SearchByBoW(sc.kf1, sc.kf2),
+                               lambda k: orbref.search_by_bow(sc.kf1, sc.kf2, 0.75, True, True, kind=k)),
+        "SearchByBoW x8 KFs (relocalisation)": (
+            lambda: m.SearchByBoWMulti(kfs, cur),
+            lambda k: [orbref.search_by_bow(kf, cur, 0.75, True, False, kind=k) for kf in kfs]),
+        "SearchByProjection(F,KF)": (
+            with_state(sparse, lambda: m.SearchByProjection(cur, sc.kf2, pts, 10, 100)),
+            lambda k: with_state(sparse, lambda: orbref.search_by_projection_keyframe(cur, pts, 10, 100, True,
+                                                                                     kind=k))()),
+        "SearchByProjection(KF,Scw)": (lambda: m.SearchByProjection(sc.kf1, Scw, sc.mps2, 10),
+                                       lambda k: orbref.search_by_projection_sim3(sc.kf1, Scw, sc.mps2, 10,
+                                                                                  kind=k)),
+        "Fuse(KF)": (lambda: m.Fuse(sc.kf1, sc.mps2, 3.0), lambda k: orbref.fuse(sc.kf1, sc.mps2, 3.0, kind=k)),
+        "Fuse(KF,Scw)": (lambda: m.Fuse(sc.kf1, Scw, sc.mps2, 4.0),
+                         lambda k: orbref.fuse_sim3(sc.kf1, Scw, sc.mps2, 4.0, kind=k)),
+        "SearchBySim3": (lambda: m.SearchBySim3(sc.kf1, sc.kf2, sc.mps1, sc.mps2, s12, R12, t12, 7.5),
+                         lambda k: orbref.search_by_sim3(sc.kf1, sc.kf2, sc.mps1, sc.mps2, s12, R12, t12, 7.5,
+                                                         kind=k)),
+        "SearchForInitialization": (lambda: mi.SearchForInitialization(cur, sc.f2, prev, 100),
+                                    lambda k: orbref.search_for_initialization(cur, sc.f2, prev, 100, 0.9, True,
+                                                                               kind=k)),
+        "ComputeDistinctiveDescriptors x2000": (lambda: m.ComputeDistinctiveDescriptors(sets),
+                                               lambda k: orbref.compute_distinctive_descriptors(sets, kind=k)),
+    }
+
+    def canon(r):  # (count, array) tuples / lists of them -> comparable arrays
+        if isinstance(r, list):
+            return [canon(x) for x in r]
+        if isinstance(r, tuple):
+            return tuple(np.asarray(x).tolist() if isinstance(x, np.ndarray) else x for x in r)
+        return np.asarray(r).tolist()
+
+    out = {}
+    for name, (gpu, cpu) in cases.items():
+        g = gpu()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            gpu()
+        gms = 1e3 * (time.perf_counter() - t0) / reps
+        row = {"gpu_ms_per_call": round(gms, 3)}
+        if not args.no_cpu:
+            t0 = time.perf_counter()
+            c = cpu("native")
+            row["cpu_oracle_ms_per_call"] = round(1e3 * (time.perf_counter() - t0), 3)
+            if name.startswith("SearchByBoW x8"):
+                gc, go = g
+                same = all(int(gc[i]) == c[i][0] and np.array_equal(go[i], c[i][1]) for i in range(len(kfs)))
+            elif name.startswith("SearchForInitialization"):
+                same = g[0] == c[0] and np.array_equal(g[1], c[1]) and np.array_equal(g[2], c[2])
+            elif name.startswith("ComputeDistinctive"):
+                same = np.array_equal(g, c)
+            else:
+                same = g[0] == c[0] and np.array_equal(g[1], c[1])
+            row["cpu_bit_exact"] = bool(same)
+        out[name] = row
+    out["what"] = ("host-buffer C ABI call per search (upload, kernels, download) on a KITTI-shaped keyframe "
+                   "scene (~2000 keypoints per KeyFrame), 1 GPU; CPU oracle one core")
     return out
 
 

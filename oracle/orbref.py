@@ -331,91 +331,91 @@ def _addr(struct):
     return ctypes.addressof(struct)
 
 
-def search_by_bow(K, other, nnratio: float, check_ori: bool, kf_kf: bool):
+def search_by_bow(K, other, nnratio: float, check_ori: bool, kf_kf: bool, kind: str = "checker"):
     """SearchByBoW (ORBmatcher.cc:165-293 / :536-669): (nmatches, per-Frame KF index or per-KF1
     KF2 index)."""
     v1, f1, v2, f2 = K.view(), K.feat_vec.view(), other.view(), other.feat_vec.view()
     nm = c_int()
     if kf_kf:
         out = np.full(max(K.N, 1), -1, np.int32)
-        st = lib().orbref_search_by_bow_kf_kf(_addr(v1), _addr(f1), _addr(v2), _addr(f2), nnratio,
+        st = lib(kind).orbref_search_by_bow_kf_kf(_addr(v1), _addr(f1), _addr(v2), _addr(f2), nnratio,
                                               int(check_ori), _p(out), byref(nm))
         assert st == 0
         return nm.value, out[:K.N]
     out = np.full(max(other.N, 1), -1, np.int32)
-    st = lib().orbref_search_by_bow_kf_frame(_addr(v1), _addr(f1), _addr(v2), _addr(f2), nnratio,
+    st = lib(kind).orbref_search_by_bow_kf_frame(_addr(v1), _addr(f1), _addr(v2), _addr(f2), nnratio,
                                              int(check_ori), _p(out), byref(nm))
     assert st == 0
     return nm.value, out[:other.N]
 
 
-def search_by_projection_keyframe(F, pts, th: float, orb_dist: int, check_ori: bool):
+def search_by_projection_keyframe(F, pts, th: float, orb_dist: int, check_ori: bool, kind: str = "checker"):
     fv, gv = F.view(), pts.geometry.view()
     best = np.full(max(len(pts.angle), 1), -1, np.int32)
     nm = c_int()
-    st = lib().orbref_search_by_projection_keyframe(_addr(fv), _p(F.tcw), _addr(gv), _p(pts.angle), _lsf(F),
+    st = lib(kind).orbref_search_by_projection_keyframe(_addr(fv), _p(F.tcw), _addr(gv), _p(pts.angle), _lsf(F),
                                                     float(th), int(orb_dist), int(check_ori), _p(best),
                                                     byref(nm))
     assert st == 0
     return nm.value, best[:len(pts.angle)]
 
 
-def search_by_projection_sim3(K, Scw, pts, th: int):
+def search_by_projection_sim3(K, Scw, pts, th: int, kind: str = "checker"):
     kv, gv = K.view(), pts.view()
     scw = np.ascontiguousarray(np.asarray(Scw, np.float32).reshape(-1, 4)[:3], np.float32)
     best = np.full(max(len(pts.flags), 1), -1, np.int32)
     nm = c_int()
-    st = lib().orbref_search_by_projection_sim3(_addr(kv), _p(scw), _addr(gv), _lsf(K), int(th), _p(best),
+    st = lib(kind).orbref_search_by_projection_sim3(_addr(kv), _p(scw), _addr(gv), _lsf(K), int(th), _p(best),
                                                 byref(nm))
     assert st == 0
     return nm.value, best[:len(pts.flags)]
 
 
-def fuse(K, pts, th: float):
+def fuse(K, pts, th: float, kind: str = "checker"):
     kv, gv = K.view(), pts.view()
     ow = np.ascontiguousarray(K.camera_center, np.float32)
     best = np.full(max(len(pts.flags), 1), -1, np.int32)
     n = c_int()
-    st = lib().orbref_fuse(_addr(kv), _p(K.tcw), _p(ow), _addr(gv), _lsf(K), float(th), _p(best), byref(n))
+    st = lib(kind).orbref_fuse(_addr(kv), _p(K.tcw), _p(ow), _addr(gv), _lsf(K), float(th), _p(best), byref(n))
     assert st == 0
     return n.value, best[:len(pts.flags)]
 
 
-def fuse_sim3(K, Scw, pts, th: float):
+def fuse_sim3(K, Scw, pts, th: float, kind: str = "checker"):
     kv, gv = K.view(), pts.view()
     scw = np.ascontiguousarray(np.asarray(Scw, np.float32).reshape(-1, 4)[:3], np.float32)
     best = np.full(max(len(pts.flags), 1), -1, np.int32)
     n = c_int()
-    st = lib().orbref_fuse_sim3(_addr(kv), _p(scw), _addr(gv), _lsf(K), float(th), _p(best), byref(n))
+    st = lib(kind).orbref_fuse_sim3(_addr(kv), _p(scw), _addr(gv), _lsf(K), float(th), _p(best), byref(n))
     assert st == 0
     return n.value, best[:len(pts.flags)]
 
 
-def search_by_sim3(K1, K2, m1, m2, s12, R12, t12, th: float):
+def search_by_sim3(K1, K2, m1, m2, s12, R12, t12, th: float, kind: str = "checker"):
     v1, v2, g1, g2 = K1.view(), K2.view(), m1.view(), m2.view()
     r12 = np.ascontiguousarray(R12, np.float32).reshape(9)
     t = np.ascontiguousarray(t12, np.float32).reshape(3)
     out = np.full(max(K1.N, 1), -1, np.int32)
     n = c_int()
-    st = lib().orbref_search_by_sim3(_addr(v1), _addr(v2), _addr(g1), _addr(g2), _p(K1.tcw), _p(K2.tcw),
+    st = lib(kind).orbref_search_by_sim3(_addr(v1), _addr(v2), _addr(g1), _addr(g2), _p(K1.tcw), _p(K2.tcw),
                                      float(s12), _p(r12), _p(t), _lsf(K1), _lsf(K2), float(th), _p(out),
                                      byref(n))
     assert st == 0
     return n.value, out[:K1.N]
 
 
-def search_for_initialization(F1, F2, prev, window: int, nnratio: float, check_ori: bool):
+def search_for_initialization(F1, F2, prev, window: int, nnratio: float, check_ori: bool, kind: str = "checker"):
     v1, v2 = F1.view(), F2.view()
     pm = np.ascontiguousarray(prev, np.float32).reshape(F1.N, 2).copy()
     out = np.full(max(F1.N, 1), -1, np.int32)
     n = c_int()
-    st = lib().orbref_search_for_initialization(_addr(v1), _addr(v2), _p(pm), int(window), float(nnratio),
+    st = lib(kind).orbref_search_for_initialization(_addr(v1), _addr(v2), _p(pm), int(window), float(nnratio),
                                                 int(check_ori), _p(out), byref(n))
     assert st == 0
     return n.value, out[:F1.N], pm
 
 
-def compute_distinctive_descriptors(descriptor_sets):
+def compute_distinctive_descriptors(descriptor_sets, kind: str = "checker"):
     counts = np.array([len(d) for d in descriptor_sets], np.int64)
     offsets = np.zeros(len(descriptor_sets) + 1, np.int32)
     offsets[1:] = np.cumsum(counts)
@@ -423,5 +423,5 @@ def compute_distinctive_descriptors(descriptor_sets):
                                                  for d in descriptor_sets]), np.uint8)
             if len(descriptor_sets) and offsets[-1] else np.zeros((1, 32), np.uint8))
     out = np.full(max(len(descriptor_sets), 1), -1, np.int32)
-    assert lib().orbref_compute_distinctive_descriptors(len(descriptor_sets), _p(offsets), _p(desc), _p(out)) == 0
+    assert lib(kind).orbref_compute_distinctive_descriptors(len(descriptor_sets), _p(offsets), _p(desc), _p(out)) == 0
     return out[:len(descriptor_sets)]

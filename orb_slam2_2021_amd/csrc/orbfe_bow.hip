@@ -50,7 +50,7 @@ struct BowPair {
 __device__ __forceinline__ bool good_mp(uint8_t st) { return st != ORBFE_MP_NONE && st != ORBFE_MP_BAD; }
 
 __global__ __launch_bounds__(256) void k_bow_init(const BowPair* pairs) {
-  const BowPair& P = pairs[blockIdx.x];
+  const BowPair P = pairs[blockIdx.x];  // a private copy: stores through P.match_a cannot alias it
   for (int i = threadIdx.x; i < P.A.n; i += 256) P.match_a[i] = -1;
   if (P.out_b)
     for (int i = threadIdx.x; i < P.B.n; i += 256) P.out_b[i] = -1;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_bow_init(const BowPair* pairs) {
 __global__ __launch_bounds__(256) void k_bow_nodes(const BowPair* pairs, float nnratio) {
   __shared__ uint4 s_desc[4][BOW_LDS_CAND * 2];
   __shared__ uint32_t s_taken[4][BOW_MAX_NODE / 32];  // unusable or claimed candidates
-  const BowPair& P = pairs[blockIdx.y];
+  const BowPair P = pairs[blockIdx.y];
   const int w = wave_id(), lane = lane_id();
   const int a = blockIdx.x * 4 + w;
   if (a >= P.fa.n_nodes) return;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(const BowPair* pairs, float n
 __global__ __launch_bounds__(256) void k_bow_finish(const BowPair* pairs, int check_ori) {
   __shared__ int s_hist[HISTO_LENGTH];
   __shared__ int s_misc[8];
-  const BowPair& P = pairs[blockIdx.x];
+  const BowPair P = pairs[blockIdx.x];  // a private copy: stores through P.match_a cannot alias it
   const int t = threadIdx.x;
   if (t < HISTO_LENGTH) s_hist[t] = 0;
   if (t == 0) s_misc[4] = 0;
@@ -196,16 +196,40 @@ __global__ __launch_bounds__(256) void k_bow_finish(const BowPair* pairs, int ch
 }
 
 // ---- SearchForInitialization ----------------------------------------------------------------------
+// The order dependence of :431-501 as a fixpoint (k_init_round). Feature i1's decision D(i1) -- the
+// accepted bestIdx2, or none -- depends only on vMatchedDistance as the features before it left it,
+// and vMatchedDistance[i2] is then the smallest accepted distance among the earlier features that
+// chose i2 (an assignment needs a strictly smaller distance, :458). Round r recomputes every
+// decision against the choosers of round r-1 (per i2 up to INIT_SLOTS (i1, dist) entries); two equal
+// consecutive rounds with complete chooser lists are the sequential result (D(i) = f(D(j < i)) has a
+// single solution, and round r has the first r features right). Otherwise k_init_seq walks the
+// features in order.
+#define INIT_SLOTS 16
+#define INIT_MAX_ROUNDS 16
+#define INIT_STATE_INTS (2 + 2 * INIT_MAX_ROUNDS)  // settled, rounds run, changed[r], overflow[r]
+#define INIT_CHANGED(r) (2 + (r))
+#define INIT_OVF(r) (2 + INIT_MAX_ROUNDS + (r))
+
 struct InitQueryArgs {
-  int n1;
+  int n1, n2;
   const orbfe_keypoint* keys1;
   const float* prev;
   float r;
   SbpQuery* q;
+  int32_t* dec_init;  // round 0's "previous" decisions: never computed
+  int32_t* cnt0;      // chooser counts written by round 0 and read as round -1's: zero
+  int32_t* cnt2;
+  int32_t* state;
 };
 __global__ __launch_bounds__(256) void k_init_queries(InitQueryArgs a) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < a.n2) {
+    a.cnt0[i] = 0;
+    a.cnt2[i] = 0;
+  }
+  if (i < INIT_STATE_INTS) a.state[i] = 0;
   if (i >= a.n1) return;
+  a.dec_init[i] = (int32_t)0xfefefefe;
   SbpQuery q = {};
   q.gate = SBP_GATE_NONE;
   const int level1 = a.keys1[i].octave;
@@ -220,6 +244,91 @@ __global__ __launch_bounds__(256) void k_init_queries(InitQueryArgs a) {
   a.q[i] = q;
 }
 
+struct InitFixArgs {
+  int n1, n2, cand_cap, round;
+  float nnratio;
+  const int16_t* cand_k;
+  const uint8_t* cand_d;
+  const int32_t* cand_n;
+  const int32_t* dec_prev;
+  int32_t* dec_cur;          // accepted i2, or -1
+  const int2* slots_prev;    // choosers of round r-1: per i2, INIT_SLOTS (i1, dist)
+  const int32_t* cnt_prev;
+  int2* slots_cur;
+  int32_t* cnt_cur;
+  int32_t* cnt_next;         // cleared here for round r+1
+  int32_t* state;
+};
+
+// after `rounds` rounds: the last reproduced the one before it, and neither chooser list overflowed
+__device__ __forceinline__ bool init_settled(const int32_t* st, int rounds) {
+  return rounds >= 2 && st[INIT_CHANGED(rounds - 1)] == 0 && st[INIT_OVF(rounds - 1)] == 0 &&
+         st[INIT_OVF(rounds - 2)] == 0;
+}
+
+__global__ __launch_bounds__(256) void k_init_round(InitFixArgs a) {
+  if (a.state[0] != 0 || init_settled(a.state, a.round)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.state[0] = 1;
+    return;
+  }
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t == 0) a.state[1] = a.round + 1;
+  if (t < a.n2) a.cnt_next[t] = 0;
+  const int j = threadIdx.x & 15, row = threadIdx.x >> 4;
+  const int i1 = blockIdx.x * 16 + row;
+  if (i1 >= a.n1) return;  // the 16 lanes of a row leave together
+  const int n = a.cand_n[i1];
+  const int16_t* ck = a.cand_k + (size_t)i1 * a.cand_cap;
+  const uint8_t* cd = a.cand_d + (size_t)i1 * a.cand_cap;
+  const unsigned NONE = 0xffffffffu;
+  unsigned k1 = NONE;  // (distance << 16 | position)
+  int d2 = INT_MAX;
+  for (int c = j; c < n; c += 16) {
+    const int i2 = ck[c];
+    const int dist = cd[c];
+    int vmd = INT_MAX;  // vMatchedDistance[i2] before i1, per the previous round's choosers
+    const int cc = min(a.cnt_prev[i2], INIT_SLOTS);
+    for (int s = 0; s < cc; s++) {
+      const int2 e = a.slots_prev[(size_t)i2 * INIT_SLOTS + s];
+      if (e.x < i1) vmd = min(vmd, e.y);
+    }
+    if (vmd <= dist) continue;  // :458-459
+    const unsigned key = ((unsigned)dist << 16) | (unsigned)c;
+    if (key < k1) {
+      if (k1 != NONE) d2 = min(d2, (int)(k1 >> 16));
+      k1 = key;
+    } else if (dist < d2) {
+      d2 = dist;
+    }
+  }
+  unsigned kmin = k1;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    const unsigned other = (unsigned)__shfl_xor((int)kmin, o, 16);
+    kmin = other < kmin ? other : kmin;
+  }
+  int second = k1 == kmin ? d2 : (k1 == NONE ? INT_MAX : (int)(k1 >> 16));
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) second = min(second, __shfl_xor(second, o, 16));
+  int dec = -1;
+  if (kmin != NONE) {
+    const int bestDist = (int)(kmin >> 16);
+    if (bestDist <= TH_LOW && (float)bestDist < (float)second * a.nnratio) dec = ck[kmin & 0xffffu];  // :473-475
+  }
+  bool changed = false;
+  if (j == 0) {
+    a.dec_cur[i1] = dec;
+    changed = dec != a.dec_prev[i1];
+    if (dec >= 0) {
+      const int s = atomicAdd(&a.cnt_cur[dec], 1);
+      if (s < INIT_SLOTS) a.slots_cur[(size_t)dec * INIT_SLOTS + s] = make_int2(i1, (int)(kmin >> 16));
+      else a.state[INIT_OVF(a.round)] = 1;
+    }
+  }
+  if (wave_ballot(changed) && lane_id() == __ffsll((long long)wave_ballot(true)) - 1)
+    a.state[INIT_CHANGED(a.round)] = 1;  // plain store: every writer stores 1
+}
+
 struct InitSeqArgs {
   int n1, n2, cand_cap, check_ori;
   float nnratio;
@@ -232,10 +341,17 @@ struct InitSeqArgs {
   int32_t* bin_of;   // rotation bin of every feature pushed into rotHist, else -1
   float* prev;
   int32_t* nmatches;
+  // the fixpoint's outcome: decisions by round parity, choosers by round mod 3
+  const int32_t* state;
+  const int32_t* dec[2];
+  const int2* slots[3];
+  const int32_t* cnt[3];
 };
 
-// One wavefront: the reference's loop over i1 in order (:431-501), then the rotation filter
-// (:503-526) and the vbPrevMatched update (:528-531).
+// One wavefront: the fixpoint's result when it settled (the last accepted chooser of an i2 keeps
+// it, :477-481; every accepted feature was pushed into rotHist, :496), else the reference's loop
+// over i1 in order (:431-501); then the rotation filter (:503-526) and the vbPrevMatched update
+// (:528-531).
 __global__ __launch_bounds__(64) void k_init_seq(InitSeqArgs a) {
   extern __shared__ int s_init[];  // vMatchedDistance[n2], vnMatches21[n2], hist[30], misc[4]
   int* mdist = s_init;
@@ -243,18 +359,34 @@ __global__ __launch_bounds__(64) void k_init_seq(InitSeqArgs a) {
   int* hist = m21 + a.n2;
   int* misc = hist + HISTO_LENGTH;
   const int lane = lane_id();
-  for (int k = lane; k < a.n2; k += 64) {
-    mdist[k] = INT_MAX;
-    m21[k] = -1;
-  }
   if (lane < HISTO_LENGTH) hist[lane] = 0;
-  for (int i = lane; i < a.n1; i += 64) {
-    a.match12[i] = -1;
-    a.bin_of[i] = -1;
+  const int rounds = a.state[1];
+  const bool settled = a.state[0] != 0 || init_settled(a.state, rounds);
+  if (settled) {
+    const int32_t* D = a.dec[(rounds - 1) & 1];
+    const int2* S = a.slots[(rounds - 1) % 3];
+    const int32_t* C = a.cnt[(rounds - 1) % 3];
+    for (int i = lane; i < a.n1; i += 64) {
+      const int d = D[i];
+      int last = -1;  // the last feature that chose d keeps it
+      if (d >= 0)
+        for (int s = 0; s < C[d]; s++) last = max(last, S[(size_t)d * INIT_SLOTS + s].x);
+      a.match12[i] = (d >= 0 && last == i) ? d : -1;
+      a.bin_of[i] = (d >= 0 && a.check_ori) ? rot_bin_dev(a.keys1[i].angle, a.keys2[d].angle) : -1;
+    }
+  } else {
+    for (int k = lane; k < a.n2; k += 64) {
+      mdist[k] = INT_MAX;
+      m21[k] = -1;
+    }
+    for (int i = lane; i < a.n1; i += 64) {
+      a.match12[i] = -1;
+      a.bin_of[i] = -1;
+    }
   }
   wave_sync();
   const unsigned NONE = 0xffffffffu;
-  for (int i1 = 0; i1 < a.n1; i1++) {
+  for (int i1 = 0; i1 < a.n1 && !settled; i1++) {
     const int n = a.cand_n[i1];
     if (n <= 0) continue;  // not level 0, or vIndices2.empty()
     const int16_t* ck = a.cand_k + (size_t)i1 * a.cand_cap;
@@ -556,7 +688,8 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   // as large as that set never overflows
   int cap = 1;
   for (int k = 0; k < f2->n; k++) cap += f2->keys_un[k].octave == 0;
-  const int n1 = f1->n;
+  const int n1 = f1->n, n2 = f2->n;
+  const size_t n2s = (size_t)std::max(n2, 1);
   Arena ar;
   SbpPlan p;
   sbp_plan_inputs(ar, f2, n1, cap, p);
@@ -564,6 +697,11 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   const size_t oprev = ar.add(8 * (size_t)n1);
   sbp_plan_scratch(ar, f2, p);
   const size_t om = ar.add(4 * (size_t)n1), obin = ar.add(4 * (size_t)n1), onm = ar.add(4);
+  size_t odec[2], oslot[3], ocnt[3];
+  for (int k = 0; k < 2; k++) odec[k] = ar.add(4 * (size_t)n1);
+  for (int k = 0; k < 3; k++) oslot[k] = ar.add(8 * INIT_SLOTS * n2s);
+  for (int k = 0; k < 3; k++) ocnt[k] = ar.add(4 * n2s);
+  const size_t ostate = ar.add(4 * INIT_STATE_INTS);
   int st = ensure_arena(m, ar.total);
   if (st) return st;
   uint8_t* A = m->arena;
@@ -572,26 +710,67 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   if ((st = upload_frame(m, o1, f1, &d1))) return st;
   stage_h2d(m, A + oprev, prev_matched, 8 * (size_t)n1);
   if ((st = flush_h2d(m))) return st;
-  InitQueryArgs qa{n1, d1.keys_un, (const float*)(A + oprev), (float)window_size, (SbpQuery*)(A + p.oq)};
-  hipLaunchKernelGGL(k_init_queries, dim3((n1 + 255) / 256), dim3(256), 0, m->stream, qa);
   if (!p.cache) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_for_initialization: F2 too large");
-  sbp_launch_round0(m, p, f2, d2, SbpMode{1, TH_LOW, SBP_BLOCK_NONE, 0});
+  int32_t* dec[2] = {(int32_t*)(A + odec[0]), (int32_t*)(A + odec[1])};
+  int2* slots[3];
+  int32_t* cnt[3];
+  for (int k = 0; k < 3; k++) {
+    slots[k] = (int2*)(A + oslot[k]);
+    cnt[k] = (int32_t*)(A + ocnt[k]);
+  }
+  int32_t* state = (int32_t*)(A + ostate);
+  InitQueryArgs qa{n1, n2, d1.keys_un, (const float*)(A + oprev), (float)window_size, (SbpQuery*)(A + p.oq),
+                   dec[1], cnt[0], cnt[2], state};
+  const int qn = std::max(std::max(n1, n2), INIT_STATE_INTS);
+  hipLaunchKernelGGL(k_init_queries, dim3((qn + 255) / 256), dim3(256), 0, m->stream, qa);
+  sbp_launch_round0(m, p, f2, d2, SbpMode{1, TH_LOW, SBP_BLOCK_NONE, 0, 0});
+  // the claim order: fixpoint rounds (each exits at once after convergence), then the finish
+  InitFixArgs fa;
+  std::memset(&fa, 0, sizeof(fa));
+  fa.n1 = n1;
+  fa.n2 = n2;
+  fa.cand_cap = cap;
+  fa.nnratio = m->nnratio;
+  fa.cand_k = (const int16_t*)(A + p.ocand_k);
+  fa.cand_d = A + p.ocand_d;
+  fa.cand_n = (const int32_t*)(A + p.ocand_n);
+  fa.state = state;
+  const int gx = std::max((n1 + 15) / 16, (n2 + 255) / 256);
+  for (int r = 0; r < INIT_MAX_ROUNDS; r++) {
+    fa.round = r;
+    fa.dec_prev = dec[(r + 1) & 1];
+    fa.dec_cur = dec[r & 1];
+    fa.slots_prev = slots[(r + 2) % 3];
+    fa.cnt_prev = cnt[(r + 2) % 3];
+    fa.slots_cur = slots[r % 3];
+    fa.cnt_cur = cnt[r % 3];
+    fa.cnt_next = cnt[(r + 1) % 3];
+    hipLaunchKernelGGL(k_init_round, dim3(gx), dim3(256), 0, m->stream, fa);
+  }
   InitSeqArgs sa;
+  std::memset(&sa, 0, sizeof(sa));
   sa.n1 = n1;
-  sa.n2 = f2->n;
+  sa.n2 = n2;
   sa.cand_cap = cap;
   sa.check_ori = m->check_ori;
   sa.nnratio = m->nnratio;
-  sa.cand_k = (const int16_t*)(A + p.ocand_k);
-  sa.cand_d = A + p.ocand_d;
-  sa.cand_n = (const int32_t*)(A + p.ocand_n);
+  sa.cand_k = fa.cand_k;
+  sa.cand_d = fa.cand_d;
+  sa.cand_n = fa.cand_n;
   sa.keys1 = d1.keys_un;
   sa.keys2 = d2.keys_un;
   sa.match12 = (int32_t*)(A + om);
   sa.bin_of = (int32_t*)(A + obin);
   sa.prev = (float*)(A + oprev);
   sa.nmatches = (int32_t*)(A + onm);
-  const size_t lds = sizeof(int) * (2 * (size_t)std::max(f2->n, 1) + HISTO_LENGTH + 4);
+  sa.state = state;
+  sa.dec[0] = dec[0];
+  sa.dec[1] = dec[1];
+  for (int k = 0; k < 3; k++) {
+    sa.slots[k] = slots[k];
+    sa.cnt[k] = cnt[k];
+  }
+  const size_t lds = sizeof(int) * (2 * n2s + HISTO_LENGTH + 4);
   if (lds > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_for_initialization: F2 too large");
   hipLaunchKernelGGL(k_init_seq, dim3(1), dim3(64), lds, m->stream, sa);
   ORBFE_HIP_CHECK(hipGetLastError());

@@ -479,6 +479,7 @@ struct SbpArgs {
   int dist_th;                // accept bestDist <= dist_th (TH_HIGH, TH_LOW or ORBdist)
   int block_any;              // pre-blocked keypoints: SBP_BLOCK_*
   int cand_cap;               // per-query candidate cache entries
+  int no_claims;              // no query blocks a keypoint: round 0 is the result
   int32_t* res_prev;
   int32_t* res_cur;
   const int32_t* owner_prev;  // INT_MAX = unclaimed in the previous round
@@ -694,7 +695,10 @@ __device__ __forceinline__ unsigned long long max_u64(unsigned long long a, unsi
 __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   __shared__ int s_flat[16][SBP_FLAT];
   const int t = blockIdx.x * 256 + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    a.state[1] = 1;
+    if (a.no_claims) a.state[0] = 1;  // nothing to iterate: converged after this round
+  }
   if (t < a.F.n) a.owner_next[t] = 0x7fffffff;
   const int j = threadIdx.x & 15, row = threadIdx.x >> 4;
   const int i = blockIdx.x * 16 + row;
@@ -1407,6 +1411,7 @@ static SbpArgs sbp_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* F,
   a.dist_th = md.dist_th;
   a.block_any = md.block_any;
   a.cand_cap = p.cand_cap;
+  a.no_claims = md.no_claims;
   a.state = (int32_t*)(A + p.ostate);
   if (p.cache) {
     a.cand_k = (int16_t*)(A + p.ocand_k);
@@ -1461,7 +1466,8 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   // owner buffers rotate over three: round r claims into own[r % 3], reads own[(r + 2) % 3] and
   // clears own[(r + 1) % 3] for round r + 1 (nobody reads it during round r)
   int32_t* own[3] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2)};
-  for (int r = 0; r < m->max_rounds && nq > 0; r++) {
+  const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
+  for (int r = 0; r < rounds && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];

@@ -120,6 +120,7 @@ struct SbpMode {
   int dist_th;    // accept bestDist <= dist_th
   int block_any;  // SBP_BLOCK_*: which keypoints are taken before the search starts
   int check_ori;  // rotation-consistency filter over q_angle (mode 1)
+  int no_claims;  // 1: no assignment blocks a keypoint (Fuse, SearchBySim3): one round suffices
 };
 
 namespace orbfe_mi {

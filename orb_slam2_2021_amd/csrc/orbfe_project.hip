@@ -314,7 +314,7 @@ extern "C" int orbfe_fuse(orbfe_matcher* m, const orbfe_frame_view* kf, const fl
   Pose p = pose_from(tcw);
   std::memcpy(p.Ow, ow, sizeof(p.Ow));  // pKF->GetCameraCenter() (:852)
   set_pose(qa, p);
-  const SbpMode md{1, TH_LOW, SBP_BLOCK_NONE, 0};  // no claims: nothing blocks
+  const SbpMode md{1, TH_LOW, SBP_BLOCK_NONE, 0, 1};  // no claims: nothing blocks
   return run_projection(m, kf, points, true, nullptr, qa, md, kf, log_scale_factor, th, best_idx, n_candidates);
 }
 
@@ -327,7 +327,7 @@ extern "C" int orbfe_fuse_sim3(orbfe_matcher* m, const orbfe_frame_view* kf, con
   std::memset(&qa, 0, sizeof(qa));
   qa.kind = PQ_FUSE_SIM3;
   set_pose(qa, pose_from_sim3(scw));
-  const SbpMode md{1, TH_LOW, SBP_BLOCK_NONE, 0};
+  const SbpMode md{1, TH_LOW, SBP_BLOCK_NONE, 0, 1};
   return run_projection(m, kf, points, true, nullptr, qa, md, kf, log_scale_factor, th, best_idx, nfused);
 }
 
@@ -389,7 +389,7 @@ extern "C" int orbfe_search_by_sim3(orbfe_matcher* m, const orbfe_frame_view* kf
   set_camera(q2, kf1, kf1, d1, lsf1, th);
   launch_queries(m, p1, q1);
   launch_queries(m, p2, q2);
-  const SbpMode md{1, TH_HIGH, SBP_BLOCK_NONE, 0};
+  const SbpMode md{1, TH_HIGH, SBP_BLOCK_NONE, 0, 1};
   if ((st = sbp_launch(m, p1, kf2, d2, md))) return st;
   if ((st = sbp_launch(m, p2, kf1, d1, md))) return st;
   if (kf1->n > 0)
