@@ -14,8 +14,10 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return (1ull << (unsigned)lane_id()) - 1ull;
 }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return (uint64_t)__ballot(p ? 1 : 0); }
+// set bits of `mask` below this lane: v_mbcnt_lo + v_mbcnt_hi (2 VALU ops, mask from SGPRs)
 __device__ __forceinline__ int prefix_in_wave(uint64_t mask) {
-  return __popcll(mask & lanemask_lt());
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 __device__ __forceinline__ int wave_sum(int v) {

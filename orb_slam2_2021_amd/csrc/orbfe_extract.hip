@@ -490,9 +490,9 @@ __device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
 }
 
-// Two pixels at once (pa -> low 16 bits, pb -> high 16 bits): OpenCV's full antipodal quick test
-// at tlow, then the arc strength M for the pixels passing it; returns the packed M (0 where the
-// pixel is no corner at tlow), the same values arc_strength_nq gives.
+// Arc strength of two pixels (pa -> low 16 bits, pb -> high 16 bits): M where M >= tlow + 1
+// (exactly the FAST corners at tlow; see arc_strength_nq), else 0. The callers' prefilter has
+// already dropped most non-corners, so OpenCV's full antipodal quick test is not repeated here.
 typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 typedef short i16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
@@ -504,21 +504,18 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2v, a), __builtin_bit_cast(i16x2v, b)));
 }
+// two LDS bytes into the halves of a dword (ds_read_u8 + ds_read_u8_d16_hi, no packing op)
+__device__ __forceinline__ uint32_t lds_pair(const uint8_t* a, const uint8_t* b) {
+  u16x2v v;
+  v.x = a[0];
+  v.y = b[0];
+  return __builtin_bit_cast(uint32_t, v);
+}
 __device__ __forceinline__ uint32_t arc_strength_pk(const uint8_t* pa, const uint8_t* pb, int s, int tlow) {
-  const uint32_t c = (uint32_t)pa[0] | ((uint32_t)pb[0] << 16);
+  const uint32_t c = lds_pair(pa, pb);
   uint32_t x[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) x[k] = (uint32_t)pa[ring_off(k, s)] | ((uint32_t)pb[ring_off(k, s)] << 16);
-  const uint32_t T2 = (uint32_t)tlow * 0x10001u;
-  const uint32_t lo = pk_sub16(c, T2), hi = pk_add16(c, T2);
-  uint32_t dark = 0xffffffffu, brt = 0xffffffffu;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    dark &= pk_sub16(x[k], lo) | pk_sub16(x[k + 8], lo);
-    brt &= pk_sub16(hi, x[k]) | pk_sub16(hi, x[k + 8]);
-  }
-  const uint32_t pass = (dark | brt) & 0x80008000u;
-  if (pass == 0) return 0;
+  for (int k = 0; k < 16; k++) x[k] = lds_pair(pa + ring_off(k, s), pb + ring_off(k, s));
   // A = min over the 16 arcs of 9 of the arc max, then B = max over arcs of the arc min (one
   // network at a time keeps 32 values live instead of 64)
   uint32_t A = 0x00ff00ffu, B = 0;
@@ -544,9 +541,79 @@ __device__ __forceinline__ uint32_t arc_strength_pk(const uint8_t* pa, const uin
   }
   const uint32_t m = pk_max_i16(pk_sub16(c, A), pk_sub16(B, c));  // max(v - A, B - v), signed
   const int ma = (int)(short)(m & 0xffffu), mb = (int)(short)(m >> 16);
-  const uint32_t ra = (pass & 0x8000u) && ma >= tlow + 1 ? (uint32_t)ma : 0u;
-  const uint32_t rb = (pass & 0x80000000u) && mb >= tlow + 1 ? (uint32_t)mb : 0u;
+  const uint32_t ra = ma >= tlow + 1 ? (uint32_t)ma : 0u;
+  const uint32_t rb = mb >= tlow + 1 ? (uint32_t)mb : 0u;
   return ra | (rb << 16);
+}
+
+// 2a on the constant-stride path: four horizontally adjacent detection pixels per lane from dword
+// LDS reads. ROI row i holds global column x0a + j at byte j, so detection pixel (rr, cc) of a
+// cell with xo = x0 & 3 sits at byte XO + 3 + cc of ROI row rr + 3; for cc = 4g the ten bytes
+// XO + 4g .. XO + 4g + 9 (left ring point .. right ring point) lie in the four dwords from byte
+// 4g, the up / down ring points in two dwords of rows rr and rr + 6. Bytes are split into the two
+// packed-u16 pairs (0, 2) and (1, 3) by v_perm. Survivors go to `list` in row-major order (lane
+// prefix of the per-lane counts from three ballots of the count bits).
+__device__ __forceinline__ uint32_t pk_even(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c020c00u); }
+__device__ __forceinline__ uint32_t pk_odd(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0c030c01u); }
+__device__ __forceinline__ uint32_t quick2(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
+                                           uint32_t T2) {
+  const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
+  const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
+  return pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
+}
+template <int RSC, int XO>
+__device__ __forceinline__ int fast_prefilter4(const uint8_t* roi, int dw, int dh, uint32_t T2, uint16_t* list) {
+  static_assert(RSC % 4 == 0, "dword rows");
+  constexpr int RD = RSC / 4;                         // row stride in dwords
+  constexpr int OC = XO + 3, OR = XO + 6;             // centre / right byte offsets from 4g
+  const int gw = (dw + 3) >> 2;
+  const uint32_t gmagic = ((1u << 20) + gw - 1) / gw;
+  const int items = gw * dh;
+  int nlist = 0;
+  for (int q0 = 0; q0 < items; q0 += 64) {
+    const int q = q0 + lane_id();
+    uint32_t m4 = 0;
+    int px = 0;
+    if (q < items) {
+      const int rr = (int)(((uint32_t)q * gmagic) >> 20), g = q - rr * gw;
+      px = rr * dw + 4 * g;
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(roi) + (rr + 3) * RD + g;
+      const uint32_t* up = row - 3 * RD;
+      const uint32_t* dn = row + 3 * RD;
+      const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+      const uint32_t w3 = XO == 3 ? row[3] : 0u;
+      const uint32_t l = XO == 0 ? w0 : __builtin_amdgcn_alignbyte(w1, w0, XO);
+      uint32_t c, r, u, d;
+      if constexpr (OC < 4) c = __builtin_amdgcn_alignbyte(w1, w0, OC);
+      else if constexpr (OC == 4) c = w1;
+      else c = __builtin_amdgcn_alignbyte(w2, w1, OC - 4);
+      if constexpr (OR < 8) r = __builtin_amdgcn_alignbyte(w2, w1, OR - 4);
+      else if constexpr (OR == 8) r = w2;
+      else r = __builtin_amdgcn_alignbyte(w3, w2, OR - 8);
+      if constexpr ((OC & 3) == 0) {
+        u = up[OC >> 2];
+        d = dn[OC >> 2];
+      } else {
+        u = __builtin_amdgcn_alignbyte(up[(OC >> 2) + 1], up[OC >> 2], OC & 3);
+        d = __builtin_amdgcn_alignbyte(dn[(OC >> 2) + 1], dn[OC >> 2], OC & 3);
+      }
+      const uint32_t re = quick2(pk_even(c), pk_even(u), pk_even(d), pk_even(l), pk_even(r), T2);
+      const uint32_t ro = quick2(pk_odd(c), pk_odd(u), pk_odd(d), pk_odd(l), pk_odd(r), T2);
+      m4 = ((re >> 15) & 1u) | ((ro >> 14) & 2u) | ((re >> 29) & 4u) | ((ro >> 28) & 8u);
+      const int nv = dw - 4 * g;
+      if (nv < 4) m4 &= (1u << nv) - 1u;
+    }
+    const int n = __popc(m4);
+    const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
+    int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (m4 & (1u << k)) list[pos] = (uint16_t)(px + k);
+      pos += (m4 >> k) & 1u;
+    }
+    nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  }
+  return nlist;
 }
 
 __device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
@@ -685,36 +752,45 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
   // 2a. OpenCV's first two antipodal pairs (ring 0/8 = dy +-3, ring 4/12 = dx +-3) at the lower
-  //     threshold, two horizontally adjacent pixels per lane in packed 16-bit halves:
-  //     dark <=> max(min(u,d), min(l,r)) < v - t, bright <=> min(max(u,d), max(l,r)) > v + t.
-  //     Survivors (about 1 in 8 pixels) are compacted in row-major order.
-  const int pw = (dw + 1) >> 1;
-  const uint32_t pmagic = ((1u << 20) + pw - 1) / pw;
+  //     threshold in packed 16-bit halves (four pixels per lane on the constant-stride path, two
+  //     otherwise): dark <=> max(min(u,d), min(l,r)) < v - t, bright <=> min(max(u,d), max(l,r))
+  //     > v + t. Survivors (about 1 in 8 pixels) are compacted in row-major order.
   const uint32_t T2 = (uint32_t)a.tlow * 0x10001u;
   int nlist = 0;
-  for (int q0 = 0; q0 < pw * dh; q0 += 64) {
-    const int q = q0 + lane;
-    bool p0 = false, p1 = false;
-    int px = 0;
-    if (q < pw * dh) {
-      const int rr = RSC != 0 ? (int)(((uint32_t)q * pmagic) >> 20) : q / pw;
-      const int cc = 2 * (q - rr * pw);
-      px = rr * dw + cc;
-      const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
-      const uint32_t c = pack2(p[0], p[1]);
-      const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
-      const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
-      const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
-      const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
-      const uint32_t res = pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
-      p0 = (res & 0x8000u) != 0;
-      p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
+  if constexpr (RSC != 0) {
+    switch (xo) {
+      case 0: nlist = fast_prefilter4<RSC, 0>(roi, dw, dh, T2, list); break;
+      case 1: nlist = fast_prefilter4<RSC, 1>(roi, dw, dh, T2, list); break;
+      case 2: nlist = fast_prefilter4<RSC, 2>(roi, dw, dh, T2, list); break;
+      default: nlist = fast_prefilter4<RSC, 3>(roi, dw, dh, T2, list); break;
     }
-    const uint64_t b0 = wave_ballot(p0), b1 = wave_ballot(p1);
-    const int pos = nlist + prefix_in_wave(b0) + prefix_in_wave(b1);
-    if (p0) list[pos] = (uint16_t)px;
-    if (p1) list[pos + (p0 ? 1 : 0)] = (uint16_t)(px + 1);
-    nlist += __popcll(b0) + __popcll(b1);
+  } else {
+    const int pw = (dw + 1) >> 1;
+    const uint32_t pmagic = ((1u << 20) + pw - 1) / pw;
+    for (int q0 = 0; q0 < pw * dh; q0 += 64) {
+      const int q = q0 + lane;
+      bool p0 = false, p1 = false;
+      int px = 0;
+      if (q < pw * dh) {
+        const int rr = RSC != 0 ? (int)(((uint32_t)q * pmagic) >> 20) : q / pw;
+        const int cc = 2 * (q - rr * pw);
+        px = rr * dw + cc;
+        const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
+        const uint32_t c = pack2(p[0], p[1]);
+        const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
+        const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
+        const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
+        const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
+        const uint32_t res = pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
+        p0 = (res & 0x8000u) != 0;
+        p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
+      }
+      const uint64_t b0 = wave_ballot(p0), b1 = wave_ballot(p1);
+      const int pos = nlist + prefix_in_wave(b0) + prefix_in_wave(b1);
+      if (p0) list[pos] = (uint16_t)px;
+      if (p1) list[pos + (p0 ? 1 : 0)] = (uint16_t)(px + 1);
+      nlist += __popcll(b0) + __popcll(b1);
+    }
   }
   wave_sync();
   // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the full antipodal
