@@ -28,6 +28,9 @@ int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
 /* 1 (default): build the pyramid with one k_resize launch per level; 0: one banded k_pyramid
  * launch when its row bands fit in LDS (currently slower on MI355X; kept for comparison). */
 int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
+/* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the
+ * rest in one launch after the resize chain (k <= 0: the default, level 0 only). */
+int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
 #ifdef __cplusplus
 }
 #endif

@@ -1526,8 +1526,8 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
     const f32x2 sc = {sb, ca}, cs = {ca, -sb}, magic = {12582912.0f, 12582912.0f};
     const f32x2 q0 = (f32x2){P.x, P.x} * sc + (f32x2){P.y, P.y} * cs + magic;
     const f32x2 q1 = (f32x2){P.z, P.z} * sc + (f32x2){P.w, P.w} * cs + magic;
-    const int i0 = __float_as_int(q0.x) * 40 + __float_as_int(q0.y) - 0x4B400000 * 41;
-    const int i1 = __float_as_int(q1.x) * 40 + __float_as_int(q1.y) - 0x4B400000 * 41;
+    const int i0 = (int)((uint32_t)__float_as_int(q0.x) * 40u + (uint32_t)__float_as_int(q0.y) - 0x4B400000u * 41u);
+    const int i1 = (int)((uint32_t)__float_as_int(q1.x) * 40u + (uint32_t)__float_as_int(q1.y) - 0x4B400000u * 41u);
     const int t0 = wb[i0];
     const int t1 = wb[i1];
     const uint32_t hv = (uint32_t)(wave_ballot(t0 < t1) >> (16 * grp)) & 0xffffu;
@@ -1572,6 +1572,11 @@ struct KernelTimer {
 
 }  // namespace
 
+// Fork/join events between the extractor's two streams order device work only (nothing on the
+// host waits on them), so they skip the system-scope fence: without it the record + wait pair
+// costs less queue time between the dependent launches.
+static const unsigned kForkJoinEvent = hipEventDisableTiming | hipEventDisableSystemFence;
+
 struct orbfe_extractor {
   int device = 0;
   int nfeatures, nlevels, ini_th, min_th;
@@ -1582,9 +1587,11 @@ struct orbfe_extractor {
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level)
+  int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: level 0 only)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
+  std::vector<hipEvent_t> ev_lvl;           // level l built (per-level FAST on the side stream)
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
   std::vector<LevelDesc> levels;
@@ -1970,6 +1977,15 @@ static size_t fast_lds(const orbfe_extractor* h) {
     }                                                              \
   } while (0)
 
+// How many levels, from level 0 up, get their FAST launch on the side stream as soon as the main
+// stream has built them; the rest run in one launch on the main stream after the resize chain.
+// Measured on MI355X (C3, 64 images): k = 4 shortens a lone extraction by ~3 % but in the
+// benchmark's pipelined steps the side-stream FAST launches only stretch the resize chain and
+// their own duration (no throughput change), so the default stays at level 0 alone.
+static int fast_side_split(const orbfe_extractor* h) {
+  return h->fast_side_levels > 0 ? std::min(h->fast_side_levels, h->nlevels) : 1;
+}
+
 static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long long img_stride,
                           int pitch, orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
                           int32_t* d_counts, hipStream_t st) {
@@ -2034,7 +2050,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
     return ORBFE_OK;
   };
-  const int lv1_cells = h->nlevels > 1 ? h->levels[1].cell_begin : a.ncells;
   if (h->nbands > 0 && !h->force_level_launches) {
     dim3 grid(h->nbands, n);
     LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), h->pyramid_lds, st, a));
@@ -2045,12 +2060,25 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       dim3 grid((d.w + 1023) / 1024, (d.h + 3) / 4, n), block(64, 4);
       LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
     }
-    // level 0's FAST cells run on the side stream while the main stream builds levels 1..L-1
-    // (a chain of small, dependent resize launches that leaves most CUs idle)
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
-    ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_l0, 0));
-    launch_fast(h->side, 0, lv1_cells);
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
+    // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
+    // stream has built it, beside the chain of small dependent resize launches that leaves most
+    // CUs idle; levels k..L-1 follow the chain on the main stream
+    const int k_side = fast_side_split(h);
+    if ((int)h->ev_lvl.size() < h->nlevels) {
+      for (int l = (int)h->ev_lvl.size(); l < h->nlevels; l++) {
+        hipEvent_t e = nullptr;
+        ORBFE_HIP_CHECK(hipEventCreateWithFlags(&e, kForkJoinEvent));
+        h->ev_lvl.push_back(e);
+      }
+    }
+    auto side_fast = [&](int l) -> int {
+      const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
+      ORBFE_HIP_CHECK(hipEventRecord(e, st));
+      ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, e, 0));
+      const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
+      return launch_fast(h->side, h->levels[l].cell_begin, c1);
+    };
+    side_fast(0);
     for (int l = 1; l < h->nlevels; l++) {
       const LevelDesc& d = h->levels[l];
       if (d.rwin_ok) {
@@ -2060,8 +2088,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
         dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
         LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
       }
+      if (l < k_side) side_fast(l);
     }
-    launch_fast(st, lv1_cells, a.ncells);
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
+    if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
     ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   }
   // fork: GaussianBlur needs only the pyramid, so it runs on the side stream beside k_octree (a
@@ -2158,10 +2188,10 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       create_side_stream(&h->side) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_l0, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_f0, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&h->ev_fork, kForkJoinEvent) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_join, kForkJoinEvent) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_l0, kForkJoinEvent) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_f0, kForkJoinEvent) != hipSuccess) {
     delete h;
     return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: stream creation failed");
   }
@@ -2228,6 +2258,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->ev_l0) hipEventDestroy(h->ev_l0);
   if (h->ev_f0) hipEventDestroy(h->ev_f0);
+  for (hipEvent_t e : h->ev_lvl) hipEventDestroy(e);
   delete h;
   return ORBFE_OK;
 }
@@ -2552,6 +2583,12 @@ extern "C" int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level,
   ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   ORBFE_HIP_CHECK(hipMemcpy2D(out, d.w, h->d_blur + (size_t)image * h->pyr_stride + d.pyr_off, d.pitch,
                               d.w, d.h, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->fast_side_levels = k > 0 ? k : -1;
   return ORBFE_OK;
 }
 

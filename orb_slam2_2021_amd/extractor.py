@@ -302,6 +302,10 @@ class ORBextractor:
         """Limit the keys DistributeOctTree keeps in LDS (0: global-memory path; <0: auto)."""
         L.check(self._lib.orbfe_debug_set_octree_key_cap(self._h, int(cap)), "set_octree_key_cap")
 
+    def debug_set_fast_side_levels(self, k: int) -> None:
+        """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: level 0 only)."""
+        L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
+
     def debug_force_level_launches(self, on: bool = True) -> None:
         """True (default): one k_resize launch per level; False: the banded k_pyramid launch."""
         L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),

@@ -1,5 +1,5 @@
 """Extraction only, C3 shape (64 images of 1241x376 per call), for PMC passes on the extractor
-kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel]"""
+kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel] [--side=K]"""
 import os
 import sys
 import time
@@ -21,6 +21,9 @@ def main():
     dev = torch.device("cuda", 0)
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(2000, 1.2, 8, 20, 7, device=0)
+    for a in sys.argv:
+        if a.startswith("--side="):
+            ext.debug_set_fast_side_levels(int(a.split("=")[1]))
     cap = ext.max_keypoints(H, W)
     kps = torch.empty(2 * B * cap * 28, dtype=torch.uint8, device=dev)
     desc = torch.empty(2 * B * cap * 32, dtype=torch.uint8, device=dev)
