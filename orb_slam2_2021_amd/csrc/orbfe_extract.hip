@@ -504,6 +504,20 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2v, a), __builtin_bit_cast(i16x2v, b)));
 }
+// 3-input packed min / max of byte pairs viewed as f16 (v_pk_minimum3_f16 / v_pk_maximum3_f16)
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f16_max3(uint32_t a, uint32_t b, uint32_t c) {
+  const f16x2v r = __builtin_elementwise_maximum(
+      __builtin_elementwise_maximum(__builtin_bit_cast(f16x2v, a), __builtin_bit_cast(f16x2v, b)),
+      __builtin_bit_cast(f16x2v, c));
+  return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t f16_min3(uint32_t a, uint32_t b, uint32_t c) {
+  const f16x2v r = __builtin_elementwise_minimum(
+      __builtin_elementwise_minimum(__builtin_bit_cast(f16x2v, a), __builtin_bit_cast(f16x2v, b)),
+      __builtin_bit_cast(f16x2v, c));
+  return __builtin_bit_cast(uint32_t, r);
+}
 // two LDS bytes into the halves of a dword (ds_read_u8 + ds_read_u8_d16_hi, no packing op)
 __device__ __forceinline__ uint32_t lds_pair(const uint8_t* a, const uint8_t* b) {
   u16x2v v;
@@ -516,28 +530,29 @@ __device__ __forceinline__ uint32_t arc_strength_pk(const uint8_t* pa, const uin
   uint32_t x[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) x[k] = lds_pair(pa + ring_off(k, s), pb + ring_off(k, s));
-  // A = min over the 16 arcs of 9 of the arc max, then B = max over arcs of the arc min (one
-  // network at a time keeps 32 values live instead of 64)
-  uint32_t A = 0x00ff00ffu, B = 0;
+  // A = min over the 16 arcs of 9 of the arc max, B = max over the arcs of the arc min, by the
+  // gfx950 3-input packed f16 ops: a zero-extended byte is an f16 denormal whose order is the
+  // integer order (f16 denormals are preserved, .amdhsa_float_denorm_mode_16_64 3), and min / max
+  // return one of their inputs bit for bit, so A and B come out as the integer bytes.
+  // Arc max over x[k..k+8] = max3 of three 3-wide maxima: 16 + 16 ops, then a min3 tree.
+  uint32_t A, B;
   {
-    uint32_t m4[16];
+    uint32_t t3[16], t9[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = pk_max_u16(x[k], x[(k + 1) & 15]);
+    for (int k = 0; k < 16; k++) t3[k] = f16_max3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = pk_max_u16(m4[k], pk_max_u16(x[(k + 2) & 15], x[(k + 3) & 15]));
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      A = pk_min_u16(A, pk_max_u16(pk_max_u16(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]));
+    for (int k = 0; k < 16; k++) t9[k] = f16_max3(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]);
+    A = f16_min3(f16_min3(f16_min3(t9[0], t9[1], t9[2]), f16_min3(t9[3], t9[4], t9[5]), f16_min3(t9[6], t9[7], t9[8])),
+                 f16_min3(t9[9], t9[10], t9[11]), f16_min3(f16_min3(t9[12], t9[13], t9[14]), t9[15], t9[15]));
   }
   {
-    uint32_t m4[16];
+    uint32_t t3[16], t9[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = pk_min_u16(x[k], x[(k + 1) & 15]);
+    for (int k = 0; k < 16; k++) t3[k] = f16_min3(x[k], x[(k + 1) & 15], x[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = pk_min_u16(m4[k], pk_min_u16(x[(k + 2) & 15], x[(k + 3) & 15]));
-#pragma unroll
-    for (int k = 0; k < 16; k++)
-      B = pk_max_u16(B, pk_min_u16(pk_min_u16(m4[k], m4[(k + 4) & 15]), x[(k + 8) & 15]));
+    for (int k = 0; k < 16; k++) t9[k] = f16_min3(t3[k], t3[(k + 3) & 15], t3[(k + 6) & 15]);
+    B = f16_max3(f16_max3(f16_max3(t9[0], t9[1], t9[2]), f16_max3(t9[3], t9[4], t9[5]), f16_max3(t9[6], t9[7], t9[8])),
+                 f16_max3(t9[9], t9[10], t9[11]), f16_max3(f16_max3(t9[12], t9[13], t9[14]), t9[15], t9[15]));
   }
   const uint32_t m = pk_max_i16(pk_sub16(c, A), pk_sub16(B, c));  // max(v - A, B - v), signed
   const int ma = (int)(short)(m & 0xffffu), mb = (int)(short)(m >> 16);
