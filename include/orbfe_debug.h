@@ -31,6 +31,11 @@ int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
 /* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the
  * rest in one launch after the resize chain (k <= 0: the default, level 0 only). */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
+/* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe
+ * computes them (a port of glibc's cosf / sinf), for the float degree values with bit patterns
+ * deg_bits_begin .. deg_bits_begin + n - 1, into device buffers (NULL stream = default stream;
+ * synchronous). Used by the exhaustive glibc check, tests/test_gpu_trig.py. */
+int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float* d_cos, float* d_sin, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -12,7 +12,8 @@
 // Deterministic rules where the reference is not:
 //   C.1 octree refinement ties between equal-size nodes break on node creation order (latest
 //       created node divides first), standing in for the reference's heap-address order;
-//   A.10 descriptor cos/sin are (float)cos((double)a), (float)sin((double)a).
+//   A.10 descriptor cos/sin are glibc's cosf / sinf, as the reference's std::cos(float) resolves
+//        (the earlier (float)cos((double)a) reading differs on 0.13 % of the angles).
 #include "orbref.h"
 
 #include <algorithm>
@@ -398,7 +399,9 @@ float ic_angle(const uint8_t* img, int step, int cx, int cy, const int* umax) {
 const float kFactorPI = (float)(M_PI / 180.f);
 void orb_descriptor(const uint8_t* img, int step, int cx, int cy, float angle_deg, uint8_t* desc) {
   float angle = angle_deg * kFactorPI;
-  float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+  // :110 `(float)cos(angle)` with a float angle and `using namespace std` (:66) is
+  // std::cos(float) = glibc cosf / sinf, which are not correctly rounded (trig_check.cpp)
+  float a = cosf(angle), b = sinf(angle);
   const uint8_t* center = img + (size_t)cy * step + cx;
   const signed char* pat = kOrbPattern31;
   auto sample = [&](int idx) -> int {

@@ -82,12 +82,42 @@ def lib(kind: str = "checker") -> ctypes.CDLL:
         L.orbref_search_for_initialization.argtypes = [c_void_p] * 3 + [c_int, c_float, c_int, c_void_p,
                                                                        POINTER(c_int)]
         L.orbref_compute_distinctive_descriptors.argtypes = [c_int, c_void_p, c_void_p, c_void_p]
+        # trig_check.cpp
+        L.orbref_trig_mismatch.restype = ctypes.c_uint64
+        L.orbref_trig_mismatch.argtypes = [c_uint32, c_uint32, c_uint32, c_int, POINTER(c_uint32)]
+        L.orbref_trig_compare.restype = ctypes.c_uint64
+        L.orbref_trig_compare.argtypes = [c_uint32, ctypes.c_uint64, c_void_p, c_void_p, c_int,
+                                          POINTER(ctypes.c_uint64)]
         _libs[kind] = L
     return _libs[kind]
 
 
 def _p(a):
     return c_void_p(a.ctypes.data) if a is not None else c_void_p(0)
+
+
+DEG_360_BITS = 0x43B40000  # 360.0f: fastAtan2's degrees lie in [0, 360) (ORBextractor.cc:109)
+
+
+def trig_mismatch(bits_begin: int = 0, bits_end: int = DEG_360_BITS, stride: int = 1,
+                  threads: int = 8) -> Tuple[int, int]:
+    """glibc cosf / sinf vs (float)cos / sin((double)x) of the steering angle x = deg * factorPI,
+    for the float degree values with bit patterns [bits_begin, bits_end) (trig_check.cpp).
+    Returns (mismatches, smallest mismatching bit pattern or 0xffffffff)."""
+    first = c_uint32()
+    n = lib().orbref_trig_mismatch(bits_begin, bits_end, stride, threads, byref(first))
+    return int(n), int(first.value)
+
+
+def trig_compare(bits_begin: int, cos_vals: np.ndarray, sin_vals: np.ndarray,
+                 threads: int = 8) -> Tuple[int, int]:
+    """Mismatches of cos_vals / sin_vals (float32, computed elsewhere for the degree bit patterns
+    bits_begin + i) against glibc cosf / sinf of the steering angle, and the first index."""
+    c = np.ascontiguousarray(cos_vals, np.float32)
+    s = np.ascontiguousarray(sin_vals, np.float32)
+    first = ctypes.c_uint64()
+    n = lib().orbref_trig_compare(bits_begin, len(c), _p(c), _p(s), threads, byref(first))
+    return int(n), int(first.value)
 
 
 class RefExtractor:

@@ -1452,6 +1452,58 @@ __device__ __forceinline__ int group16_sum(int v) {  // sum over the 16-lane gro
   return v;
 }
 
+// computeOrbDescriptor's cos / sin of the steering angle (ORBextractor.cc:109-110). With `using
+// namespace std` (:66) `cos(angle)` on a float is std::cos(float) = glibc cosf / sinf, which are
+// not correctly rounded ((float)cos((double)x) differs on 0.13 % of the reachable angles), so this
+// is a port of glibc 2.35's sinf / cosf for |x| < 120 (sysdeps/ieee754/flt-32, the FMA ifunc
+// variant x86-64 CPUs with FMA run): double polynomials on __sincosf_table with the same fma /
+// multiply sequence. test_gpu_trig.py checks it against glibc on every float degree in [0, 360).
+__device__ __forceinline__ double glibc_cos_poly(double x2) {
+  const double x4 = x2 * x2;
+  const double c1 = fma(x2, -0x1.ffffffd0c621cp-2, 1.0);
+  const double c2 = fma(x2, 0x1.99343027bf8c3p-16, -0x1.6c087e89a359dp-10);
+  const double x6 = x2 * x4;
+  const double c = fma(x4, 0x1.55553e1068f19p-5, c1);
+  return fma(c2, x6, c);
+}
+__device__ __forceinline__ double glibc_sin_poly(double x, double x2) {
+  const double s1 = fma(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+  const double x3 = x2 * x;
+  const double x5 = x3 * x2;
+  const double s = fma(x3, -0x1.555545995a603p-3, x);
+  return fma(s1, x5, s);
+}
+__device__ __forceinline__ void steer_cos_sin(float angle_deg, float factor_pi, float& c, float& s) {
+  const float y = angle_deg * factor_pi;  // 0 <= y < 2 pi
+  const uint32_t top12 = (__float_as_uint(y) >> 20) & 0x7ffu;
+  const double x = (double)y;
+  if (top12 <= 0x3f3u) {  // y < 0.75: no reduction; y < 2^-12: cosf = 1, sinf = y
+    const double x2 = x * x;
+    c = top12 <= 0x397u ? 1.0f : (float)glibc_cos_poly(x2);
+    s = top12 <= 0x397u ? y : (float)glibc_sin_poly(x, x2);
+    return;
+  }
+  const int n = ((int)(x * 0x1.45f306dc9c883p+23) + 0x800000) >> 24;  // reduce_fast
+  const double r = fma(-(double)n, 0x1.921fb54442d18p+0, x);
+  const double r2 = r * r;
+  const double sp = glibc_sin_poly((n & 3) == 1 || (n & 3) == 2 ? -r : r, r2);  // r * sign[n & 3]
+  const double cp = (n & 2) ? -glibc_cos_poly(r2) : glibc_cos_poly(r2);  // table 1 negates c0..c4
+  // cosf: sin branch for odd n; sinf: sin branch for even n
+  c = (float)((n & 1) ? sp : cp);
+  s = (float)((n & 1) ? cp : sp);
+}
+
+// orbfe_debug_steer_trig: steer_cos_sin for the float degree values bits0 .. bits0 + n - 1
+__global__ __launch_bounds__(256) void k_steer_trig(uint32_t bits0, uint32_t n, float factor_pi, float* c,
+                                                     float* s) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  float cv, sv;
+  steer_cos_sin(__uint_as_float(bits0 + i), factor_pi, cv, sv);
+  c[i] = cv;
+  s[i] = sv;
+}
+
 // Four keypoints per wavefront, 16 lanes each, so the per-keypoint scalar work (level lookup,
 // fastAtan2, the double-precision cos/sin of computeOrbDescriptor) is shared by 4 keypoints.
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
@@ -1523,8 +1575,8 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   m01 = group16_sum(m01);
   m10 = group16_sum(m10);
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
-  const float ang = angle * a.factor_pi;
-  const float ca = (float)cos((double)ang), sb = (float)sin((double)ang);
+  float ca, sb;
+  steer_cos_sin(angle, a.factor_pi, ca, sb);
   wave_sync();
   // 3. the 256 steered tests (:105-151) on the LDS window, pixel (dy, dx) at byte
   //    (dy + 18) * 40 + (dx + cx - xb); test p = 16 j + l16 lands in bit l16 of the group's
@@ -2598,6 +2650,18 @@ extern "C" int orbfe_debug_get_blurred(orbfe_extractor* h, int image, int level,
   ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
   ORBFE_HIP_CHECK(hipMemcpy2D(out, d.w, h->d_blur + (size_t)image * h->pyr_stride + d.pyr_off, d.pitch,
                               d.w, d.h, hipMemcpyDeviceToHost));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float* d_cos, float* d_sin,
+                                      void* stream) {
+  if (n > 0 && (!d_cos || !d_sin)) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_steer_trig: bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0)
+    hipLaunchKernelGGL(k_steer_trig, dim3((n + 255) / 256), dim3(256), 0, st, deg_bits_begin, n,
+                       (float)(M_PI / 180.f), d_cos, d_sin);
+  ORBFE_HIP_CHECK(hipGetLastError());
+  ORBFE_HIP_CHECK(hipStreamSynchronize(st));
   return ORBFE_OK;
 }
 
