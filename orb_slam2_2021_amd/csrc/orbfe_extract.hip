@@ -851,18 +851,12 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
         cc = q - rr * dw;
         const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
         const int m = mp[0];
-        if (m >= t + 1) {
-          sc = m - 1;
-          keep = true;
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            const int o = k == 0 ? -mw - 1 : k == 1 ? -mw : k == 2 ? -mw + 1 : k == 3 ? -1 :
-                          k == 4 ? 1 : k == 5 ? mw - 1 : k == 6 ? mw : mw + 1;
-            const int mn = mp[o];
-            const int sn = mn >= t + 1 ? mn - 1 : 0;
-            keep = keep && (sc > sn);
-          }
-        }
+        // score m - 1 beats every neighbour's (mn >= t + 1 ? mn - 1 : 0) exactly when m > mn for
+        // all 8 neighbours and m >= 2: a neighbour below t + 1 is below m too, and scores 0
+        const int mn = max(max(max(max((int)mp[-mw - 1], (int)mp[-mw]), max((int)mp[-mw + 1], (int)mp[-1])),
+                               max(max((int)mp[1], (int)mp[mw - 1]), (int)mp[mw])), (int)mp[mw + 1]);
+        sc = m - 1;
+        keep = m >= max(t + 1, 2) && m > mn;
       }
       const uint64_t bal = wave_ballot(keep);
       if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, sc);
@@ -940,23 +934,41 @@ __device__ void wave_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, ui
 
 // Thread-serial forms for small nodes (count <= OCT_SMALL): one lane walks the whole segment.
 #define OCT_SMALL 48
+// Four keys per step (four independent loads in flight); the four counts / offsets are packed in
+// the bytes of one register (count <= OCT_SMALL < 256), not a dynamically indexed array.
 __device__ __forceinline__ int4 serial_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
   const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
-  int c[4] = {0, 0, 0, 0};
-  for (int i = 0; i < nd.count; i++) c[child_of(src[i], mx, my)]++;
-  return make_int4(c[0], c[1], c[2], c[3]);
+  uint32_t c = 0;
+  int i = 0;
+  for (; i + 4 <= nd.count; i += 4) {
+    const uint32_t k0 = src[i], k1 = src[i + 1], k2 = src[i + 2], k3 = src[i + 3];
+    c += (1u << (8 * child_of(k0, mx, my))) + (1u << (8 * child_of(k1, mx, my))) +
+         (1u << (8 * child_of(k2, mx, my))) + (1u << (8 * child_of(k3, mx, my)));
+  }
+  for (; i < nd.count; i++) c += 1u << (8 * child_of(src[i], mx, my));
+  return make_int4((int)(c & 255u), (int)((c >> 8) & 255u), (int)((c >> 16) & 255u), (int)(c >> 24));
 }
 
 __device__ __forceinline__ void serial_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, uint32_t* kb) {
   const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
   uint32_t* dst = ((nd.flags & 1) ? ka : kb) + nd.begin;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
-  int o[4] = {0, cnt.x, cnt.x + cnt.y, cnt.x + cnt.y + cnt.z};
-  for (int i = 0; i < nd.count; i++) {
-    const uint32_t key = src[i];
-    dst[o[child_of(key, mx, my)]++] = key;
+  uint32_t o = ((uint32_t)cnt.x << 8) | ((uint32_t)(cnt.x + cnt.y) << 16) | ((uint32_t)(cnt.x + cnt.y + cnt.z) << 24);
+  auto put = [&](uint32_t key) {
+    const int sh = 8 * child_of(key, mx, my);
+    dst[(o >> sh) & 255u] = key;
+    o += 1u << sh;
+  };
+  int i = 0;
+  for (; i + 4 <= nd.count; i += 4) {
+    const uint32_t k0 = src[i], k1 = src[i + 1], k2 = src[i + 2], k3 = src[i + 3];
+    put(k0);
+    put(k1);
+    put(k2);
+    put(k3);
   }
+  for (; i < nd.count; i++) put(src[i]);
 }
 
 __device__ __forceinline__ ONode make_child(const ONode& p, int c, int begin, int count, int seq) {
@@ -1505,8 +1517,21 @@ __global__ __launch_bounds__(256) void k_steer_trig(uint32_t bits0, uint32_t n, 
 }
 
 // Four keypoints per wavefront, 16 lanes each, so the per-keypoint scalar work (level lookup,
-// fastAtan2, the double-precision cos/sin of computeOrbDescriptor) is shared by 4 keypoints.
+// fastAtan2, the cos/sin of computeOrbDescriptor) is shared by 4 keypoints. A wavefront issues all
+// of its global loads before their first use (the IC_Angle window as 12-byte pieces, the blurred
+// window as 8-byte pieces); the test pattern and the circle masks are copied to LDS once per
+// block, so the moments and the 256 tests read no global memory.
+struct DwX3 {
+  uint32_t x, y, z;
+};
+
 __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
+  __shared__ float4 s_pat[256];
+  __shared__ uint32_t s_mom[4 * 279];
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[16][37 * 10];
+  s_pat[threadIdx.x] = c_patf[threadIdx.x];
+  for (int k = threadIdx.x; k < 4 * 279; k += 256) s_mom[k] = (&c_momask[0][0][0])[k];
+  __syncthreads();  // before any wavefront may leave
   const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
   const int img = blk.y;
@@ -1533,47 +1558,65 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   // origin is minBorder - 3 = 16), so both windows below stay inside the padded rows
   const long long lbase = (long long)img * a.pyr_stride + ld.pyr_off;
   const int pitch = ld.pitch;
-  // 1. blurred window rows cy-18..cy+18, dword columns from xb = (cx-18) & ~3 (10 per row) -> LDS
-  __shared__ uint32_t s_win[16][37 * 10];
-  uint32_t* win = s_win[w * 4 + grp];
-  const int xb = (cx - 18) & ~3;
-  const uint8_t* bsrc = a.blur + lbase + (long long)(cy - 18) * pitch + xb;
-  // (370 dwords: two batches of 12 loads per lane, landing in LDS before the moments start)
-#pragma unroll
-  for (int b = 0; b < 2; b++) {
-    uint32_t bw[12];
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-      const int i = l16 + 16 * (12 * b + k);
-      const int r = i / 10, c = i - 10 * r;
-      bw[k] = i < 370 ? *reinterpret_cast<const uint32_t*>(bsrc + r * pitch + 4 * c) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-      const int i = l16 + 16 * (12 * b + k);
-      if (i < 370) win[i] = bw[k];
-    }
-  }
-  // 2. IC_Angle moments (:75-102) over the 749-pixel circle of the unblurred level: dwords of rows
-  //    cy-15..cy+15 (9 per row from xa = (cx-15) & ~3), bytes masked to |u| <= umax[|v|], sums of
-  //    I and col*I by byte dot products
-  const int xa = (cx - 15) & ~3;
+  // 1. every global load in flight at once. IC_Angle window: rows cy-15..cy+15, 9 dwords per row
+  //    from xa = (cx-15) & ~3, as three 12-byte pieces; piece i = l16 + 16 k lies in row i / 3,
+  //    16 rows further every 3 k. Blurred window: rows cy-18..cy+18, 10 dwords from
+  //    xb = (cx-18) & ~3, as five 8-byte pieces (row i / 5, 16 rows further every 5 k).
+  const int xa = (cx - 15) & ~3, xb = (cx - 18) & ~3;
   const uint8_t* usrc = a.pyr + lbase + (long long)(cy - 15) * pitch + xa;
-  int m01 = 0, m10 = 0;
-  const uint32_t* mtab = &c_momask[(cx - 15) & 3][0][0];
+  const uint8_t* bsrc = a.blur + lbase + (long long)(cy - 18) * pitch + xb;
+  const int step16 = 16 * pitch;
+  int ur[3], uc[3], br[5], bc[5];
 #pragma unroll
-  for (int k = 0; k < 18; k++) {
-    const int i = l16 + 16 * k;  // 279 dwords
-    const int r = i / 9, c = i - 9 * r, v = r - 15;
-    const uint32_t d = i < 279 ? *reinterpret_cast<const uint32_t*>(usrc + r * pitch + 4 * c) : 0u;
-    const uint32_t px = i < 279 ? d & mtab[i] : 0u;  // bytes on the circle (|u| <= umax[|v|])
-    const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
-    const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
-    m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
-    m01 += v * sI;
+  for (int q = 0; q < 3; q++) {
+    ur[q] = (l16 + 16 * q) / 3;
+    uc[q] = l16 + 16 * q - 3 * ur[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    br[q] = (l16 + 16 * q) / 5;
+    bc[q] = l16 + 16 * q - 5 * br[q];
+  }
+  DwX3 mu[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    mu[k] = DwX3{0u, 0u, 0u};
+    if (l16 + 16 * k < 93) __builtin_memcpy(&mu[k], usrc + (k / 3) * step16 + ur[k % 3] * pitch + 12 * uc[k % 3], 12);
+  }
+  uint2 bw[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+    bw[k] = make_uint2(0u, 0u);
+    if (l16 + 16 * k < 185) __builtin_memcpy(&bw[k], bsrc + (k / 5) * step16 + br[k % 5] * pitch + 8 * bc[k % 5], 8);
+  }
+  // 2. IC_Angle moments (:75-102) over the 749-pixel circle: bytes with |u| <= umax[|v|] (masks in
+  //    LDS), sums of I and col * I by byte dot products
+  const uint32_t* mt = s_mom + ((cx - 15) & 3) * 279;
+  int m01 = 0, m10 = 0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    if (l16 + 16 * k < 93) {
+      const int r = ur[k % 3] + 16 * (k / 3), v = r - 15;
+      const uint32_t d3[3] = {mu[k].x, mu[k].y, mu[k].z};
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const int c = 3 * uc[k % 3] + d;  // dword of the row
+        const uint32_t px = d3[d] & mt[r * 9 + c];
+        const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
+        const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
+        m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
+        m01 += v * sI;
+      }
+    }
   }
   m01 = group16_sum(m01);
   m10 = group16_sum(m10);
+  // the blurred pieces -> LDS (rows of 40 bytes), ahead of the angle arithmetic
+  uint8_t* winb = reinterpret_cast<uint8_t*>(s_win[w * 4 + grp]);
+#pragma unroll
+  for (int k = 0; k < 12; k++)
+    if (l16 + 16 * k < 185)
+      *reinterpret_cast<uint2*>(winb + (br[k % 5] + 16 * (k / 5)) * 40 + 8 * bc[k % 5]) = bw[k];
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
   float ca, sb;
   steer_cos_sin(angle, a.factor_pi, ca, sb);
@@ -1581,7 +1624,7 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   // 3. the 256 steered tests (:105-151) on the LDS window, pixel (dy, dx) at byte
   //    (dy + 18) * 40 + (dx + cx - xb); test p = 16 j + l16 lands in bit l16 of the group's
   //    16-bit slice of ballot j = descriptor bytes 2j, 2j+1
-  const uint8_t* wb = reinterpret_cast<const uint8_t*>(win) + 18 * 40 + (cx - xb);
+  const uint8_t* wb = winb + 18 * 40 + (cx - xb);
   uint32_t dv = 0;  // lane l16 < 8 collects descriptor dword l16 = bytes 4 l16 .. 4 l16 + 3
 #pragma unroll
   for (int j = 0; j < 16; j++) {
@@ -1589,7 +1632,7 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
     // row = cvRound(x sin + y cos), col = cvRound(x cos - y sin) (:115-117): the products and the
     // sum in packed fp32 (separately rounded, as the reference), cvRound's half-even by adding
     // 1.5 * 2^23 and reading the integer out of the mantissa
-    const float4 P = c_patf[p];
+    const float4 P = s_pat[p];
     const f32x2 sc = {sb, ca}, cs = {ca, -sb}, magic = {12582912.0f, 12582912.0f};
     const f32x2 q0 = (f32x2){P.x, P.x} * sc + (f32x2){P.y, P.y} * cs + magic;
     const f32x2 q1 = (f32x2){P.z, P.z} * sc + (f32x2){P.w, P.w} * cs + magic;
