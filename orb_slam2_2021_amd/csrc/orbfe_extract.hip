@@ -71,6 +71,7 @@ struct LevelDesc {
   int xmax, simd_end;        // resize: first column using the clamped path / end of SIMD columns
   int tile_begin, tiles_x;   // k_blur tiles of this level
   int rgrp_begin, rwin_ok;   // k_resize 4-column group tables; 1 when every group's taps fit 8 bytes
+  int ini_thr[8];            // smallest x with (int)(x / hx) >= b, b = 1..7 (initial node of key x)
 };
 
 struct CellDesc {
@@ -971,6 +972,83 @@ __device__ __forceinline__ void serial_child_partition(const ONode& nd, int4 cnt
   for (; i < nd.count; i++) put(src[i]);
 }
 
+// Count + stable partition in one walk for the full passes, the keys read once into registers:
+// a wavefront for a large node (up to 64 * OCT_WJ keys), a thread for a small one (up to OCT_SJ).
+#define OCT_WJ 16
+#define OCT_SJ 16
+__device__ int4 wave_child_split(const ONode& nd, uint32_t* ka, uint32_t* kb) {
+  if (nd.count > 64 * OCT_WJ) {
+    const int4 c4 = wave_child_counts(nd, ka, kb);
+    wave_child_partition(nd, c4, ka, kb);
+    return c4;
+  }
+  const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
+  uint32_t* dst = ((nd.flags & 1) ? ka : kb) + nd.begin;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  const int lane = lane_id();
+  uint32_t key[OCT_WJ];
+  int ch[OCT_WJ];
+#pragma unroll
+  for (int j = 0; j < OCT_WJ; j++) {
+    const int i = 64 * j + lane;
+    key[j] = i < nd.count ? src[i] : 0u;
+  }
+  int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+  for (int j = 0; j < OCT_WJ; j++) {
+    if (64 * j >= nd.count) break;
+    ch[j] = 64 * j + lane < nd.count ? child_of(key[j], mx, my) : -1;
+    c0 += __popcll(wave_ballot(ch[j] == 0));
+    c1 += __popcll(wave_ballot(ch[j] == 1));
+    c2 += __popcll(wave_ballot(ch[j] == 2));
+    c3 += __popcll(wave_ballot(ch[j] == 3));
+  }
+  int o0 = 0, o1 = c0, o2 = c0 + c1, o3 = c0 + c1 + c2;
+#pragma unroll
+  for (int j = 0; j < OCT_WJ; j++) {
+    if (64 * j >= nd.count) break;
+    const uint64_t b0 = wave_ballot(ch[j] == 0), b1 = wave_ballot(ch[j] == 1), b2 = wave_ballot(ch[j] == 2),
+                   b3 = wave_ballot(ch[j] == 3);
+    if (ch[j] == 0) dst[o0 + prefix_in_wave(b0)] = key[j];
+    if (ch[j] == 1) dst[o1 + prefix_in_wave(b1)] = key[j];
+    if (ch[j] == 2) dst[o2 + prefix_in_wave(b2)] = key[j];
+    if (ch[j] == 3) dst[o3 + prefix_in_wave(b3)] = key[j];
+    o0 += __popcll(b0);
+    o1 += __popcll(b1);
+    o2 += __popcll(b2);
+    o3 += __popcll(b3);
+  }
+  return make_int4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ int4 serial_child_split(const ONode& nd, uint32_t* ka, uint32_t* kb) {
+  if (nd.count > OCT_SJ) {
+    const int4 c4 = serial_child_counts(nd, ka, kb);
+    serial_child_partition(nd, c4, ka, kb);
+    return c4;
+  }
+  const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
+  uint32_t* dst = ((nd.flags & 1) ? ka : kb) + nd.begin;
+  const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
+  uint32_t key[OCT_SJ];
+#pragma unroll
+  for (int j = 0; j < OCT_SJ; j++) key[j] = j < nd.count ? src[j] : 0u;
+  uint32_t c = 0;  // four 8-bit counts
+#pragma unroll
+  for (int j = 0; j < OCT_SJ; j++)
+    if (j < nd.count) c += 1u << (8 * child_of(key[j], mx, my));
+  const uint32_t c0 = c & 255u, c1 = (c >> 8) & 255u, c2 = (c >> 16) & 255u;
+  uint32_t o = (c0 << 8) | ((c0 + c1) << 16) | ((c0 + c1 + c2) << 24);
+#pragma unroll
+  for (int j = 0; j < OCT_SJ; j++)
+    if (j < nd.count) {
+      const int sh = 8 * child_of(key[j], mx, my);
+      dst[(o >> sh) & 255u] = key[j];
+      o += 1u << sh;
+    }
+  return make_int4((int)c0, (int)c1, (int)c2, (int)(c >> 24));
+}
+
 __device__ __forceinline__ ONode make_child(const ONode& p, int c, int begin, int count, int seq) {
   const int mx = p.x0 + ((p.x1 - p.x0 + 1) >> 1), my = p.y0 + ((p.y1 - p.y0 + 1) >> 1);
   ONode n;
@@ -1016,30 +1094,21 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   int32_t* out_n = a.lvlcnt + (long long)img * a.nlevels + l;
 
   // 1. gather this level's FAST candidates in cell order (ComputeKeyPointsOctTree :821-829):
-  //    sa = exclusive prefix of the cell counts, sx = cell slots (filled by the caller); key i
-  //    belongs to the last cell whose prefix is <= i. Loads batched 4 per thread.
+  //    sa = exclusive prefix of the cell counts, sx = cell slots (filled by the caller); a thread
+  //    per cell copies the cell's keys, four loads in flight
   const int ncells = ld.ncells;
-  for (int i0 = 0; i0 < n; i0 += 1024) {
-    uint32_t v[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = i0 + t + 256 * k;
-      if (i < n) {
-        int lo = 0, hi = ncells;  // upper_bound(sa, i) - 1
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sa[mid] <= i) lo = mid + 1;
-          else hi = mid;
-        }
-        const int c = lo - 1;
-        v[k] = cand[sx[c] + i - sa[c]];
-      }
+  for (int c = t; c < ncells; c += 256) {
+    const int b0 = sa[c], cnt = (c + 1 < ncells ? sa[c + 1] : n) - b0;
+    const uint32_t* src = cand + sx[c];
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {
+      const uint32_t v0 = src[k], v1 = src[k + 1], v2 = src[k + 2], v3 = src[k + 3];
+      ka[b0 + k] = v0;
+      ka[b0 + k + 1] = v1;
+      ka[b0 + k + 2] = v2;
+      ka[b0 + k + 3] = v3;
     }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = i0 + t + 256 * k;
-      if (i < n) ka[i] = v[k];
-    }
+    for (; k < cnt; k++) ka[b0 + k] = src[k];
   }
   __syncthreads();
 
@@ -1047,16 +1116,43 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   //    wave w counts then places the keys of its quarter; bucket offsets in between
   const int nini = ld.nini;
   const float hx = ld.hx;
+  auto ini_node = [&](uint32_t key) -> int {  // (size_t)(kp.pt.x / hX) (:575)
+    const int x = key_x(key);
+    if (nini > 8) return (int)((float)x / hx);
+    int b = 0;
+#pragma unroll
+    for (int k = 1; k < 8; k++) b += (k < nini && x >= ld.ini_thr[k]) ? 1 : 0;
+    return b;
+  };
   int* bcnt = reinterpret_cast<int*>(sk);  // [4][nini] counts, then [4][nini] offsets
   int* boff = bcnt + 4 * nini;
   const int R = ((n + 3) / 4 + 63) & ~63;
   const int wbeg = min(w * R, n), wend = min(wbeg + R, n);
+  // the wave's keys and their initial nodes stay in registers for both walks (one LDS read and one
+  // bucket per key) when the quarter has at most 64 * INI_J keys
+  constexpr int INI_J = 24;
+  const bool cached = wend - wbeg <= 64 * INI_J;
+  uint32_t kr[INI_J];
+  int br[INI_J];
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < INI_J; j++) {
+      const int i = wbeg + 64 * j + lane;
+      kr[j] = i < wend ? ka[i] : 0u;
+      br[j] = i < wend ? ini_node(kr[j]) : -1;
+    }
+  }
   for (int bkt = 0; bkt < nini; bkt++) {
     int cnt = 0;
-    for (int i0 = wbeg; i0 < wend; i0 += 64) {
-      const int i = i0 + lane;
-      const bool in = i < wend && (int)((float)key_x(ka[i]) / hx) == bkt;
-      cnt += __popcll(wave_ballot(in));
+    if (cached) {
+#pragma unroll
+      for (int j = 0; j < INI_J; j++) cnt += __popcll(wave_ballot(br[j] == bkt));
+    } else {
+      for (int i0 = wbeg; i0 < wend; i0 += 64) {
+        const int i = i0 + lane;
+        const bool in = i < wend && ini_node(ka[i]) == bkt;
+        cnt += __popcll(wave_ballot(in));
+      }
     }
     if (lane == 0) bcnt[w * nini + bkt] = cnt;
   }
@@ -1075,17 +1171,27 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   __syncthreads();
   for (int bkt = 0; bkt < nini; bkt++) {
     int run = boff[w * nini + bkt];
-    for (int i0 = wbeg; i0 < wend; i0 += 64) {
-      const int i = i0 + lane;
-      uint32_t key = 0;
-      bool in = false;
-      if (i < wend) {
-        key = ka[i];
-        in = (int)((float)key_x(key) / hx) == bkt;
+    if (cached) {
+#pragma unroll
+      for (int j = 0; j < INI_J; j++) {
+        const bool in = br[j] == bkt;
+        const uint64_t bal = wave_ballot(in);
+        if (in) kb[run + prefix_in_wave(bal)] = kr[j];
+        run += __popcll(bal);
       }
-      const uint64_t bal = wave_ballot(in);
-      if (in) kb[run + prefix_in_wave(bal)] = key;
-      run += __popcll(bal);
+    } else {
+      for (int i0 = wbeg; i0 < wend; i0 += 64) {
+        const int i = i0 + lane;
+        uint32_t key = 0;
+        bool in = false;
+        if (i < wend) {
+          key = ka[i];
+          in = ini_node(key) == bkt;
+        }
+        const uint64_t bal = wave_ballot(in);
+        if (in) kb[run + prefix_in_wave(bal)] = key;
+        run += __popcll(bal);
+      }
     }
   }
   __syncthreads();
@@ -1122,17 +1228,12 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       // ---- full pass (:603-668) ----
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
-        if (nd.count > 1 && nd.count <= OCT_SMALL) {
-          const int4 c4 = serial_child_counts(nd, ka, kb);
-          serial_child_partition(nd, c4, ka, kb);
-          cc[i] = c4;
-        }
+        if (nd.count > 1 && nd.count <= OCT_SMALL) cc[i] = serial_child_split(nd, ka, kb);
       }
       for (int i = w; i < S; i += 4) {
         const ONode nd = Lc[i];
         if (nd.count > OCT_SMALL) {
-          const int4 c4 = wave_child_counts(nd, ka, kb);
-          wave_child_partition(nd, c4, ka, kb);
+          const int4 c4 = wave_child_split(nd, ka, kb);
           if (lane == 0) cc[i] = c4;
         }
       }
@@ -1203,7 +1304,19 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
           rk[r] = 0;
         }
         const int per = (nR + 255) >> 8;
-        for (int j = 0; j < nR; j++) {
+        int j = 0;
+        for (; j + 8 <= nR; j += 8) {  // eight broadcast reads in flight
+          unsigned long long y[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) y[q] = sk[j + q];
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+            if (r == 0 || per > r) {
+#pragma unroll
+              for (int q = 0; q < 8; q++) rk[r] += y[q] > kk[r];
+            }
+        }
+        for (; j < nR; j++) {
           const unsigned long long y = sk[j];
           rk[0] += y > kk[0];
           if (per > 1) rk[1] += y > kk[1];
@@ -1793,6 +1906,13 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     if (d.nini < 1 || d.nini > 64)
       return orbfe_set_error(ORBFE_ERR_ARG, "unsupported aspect ratio (DistributeOctTree nIni)");
     d.hx = (float)bw / d.nini;
+    // initial node of a key = (int)(x / hX) (:575) as compares against host thresholds (the key
+    // x are integers in [0, bw]; the same IEEE float division as the reference)
+    for (int b = 0; b < 8; b++) {
+      int x = 0;
+      while (x <= bw + 1 && (int)((float)x / d.hx) < b) x++;
+      d.ini_thr[b] = x;
+    }
     d.rel_w = bw;
     d.rel_h = bh;
     d.budget = h->nfeat[l];
