@@ -1460,7 +1460,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 #define BS_W 248  // output columns per wavefront strip: lanes 1..62, 4 each (lanes 0 and 63 halo)
-#define BS_H 32   // output rows per strip
+#define BS_H 16   // output rows per strip
 __device__ __forceinline__ int reflect101(int i, int n) {
   return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i);
 }
@@ -1959,9 +1959,9 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
-    d.tiles_x = (d.w + 247) / 248;  // k_blur strips of 248 x 32
+    d.tiles_x = (d.w + BS_W - 1) / BS_W;  // k_blur strips of BS_W x BS_H
     d.tile_begin = tiles;
-    tiles += d.tiles_x * ((d.h + 31) / 32);
+    tiles += d.tiles_x * ((d.h + BS_H - 1) / BS_H);
     d.key_begin = keys;
     d.key_cap = std::max(d.budget + 3, 4 * d.nini);
     keys += d.key_cap;
