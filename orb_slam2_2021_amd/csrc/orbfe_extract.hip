@@ -711,17 +711,23 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
     // 16-byte loads, 4 lanes per ROI row (<= 61 columns + 3 alignment bytes = 16 dwords); the last
     // quad of a row may read up to 12 bytes past the ROI (row padding / next row / the +256 slack)
     const int nq4 = (nw + 3) >> 2;
+    uint4 v[3];  // rh <= 48 rows: 192 quads; unconditional loads (idle lanes re-read quad 0) so
+                 // that the three are in flight together
 #pragma unroll
-    for (int k = 0; k < 3; k++) {  // rh <= 48 rows: 192 quads
+    for (int k = 0; k < 3; k++) {
+      const int i = lane + 64 * k, r = i >> 2, q = i & 3;
+      const bool in = r < rh && q < nq4;
+      __builtin_memcpy(&v[k], lev + (long long)(cd.y0 + (in ? r : 0)) * pitch + x0a + 16 * (in ? q : 0), 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
       const int i = lane + 64 * k, r = i >> 2, q = i & 3;
       if (r < rh && q < nq4) {
-        uint4 v;
-        __builtin_memcpy(&v, lev + (long long)(cd.y0 + r) * pitch + x0a + 16 * q, 16);
         uint32_t* d = reinterpret_cast<uint32_t*>(roi + r * RSC + 16 * q);
-        d[0] = v.x;
-        d[1] = v.y;
-        d[2] = v.z;
-        d[3] = v.w;
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
       }
     }
     for (int i = lane + 192; i < 4 * rh; i += 64) {  // taller ROIs (rh > 48)
