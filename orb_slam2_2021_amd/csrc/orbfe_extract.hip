@@ -947,6 +947,15 @@ __device__ __forceinline__ int4 serial_child_counts(const ONode& nd, const uint3
   const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
   uint32_t c = 0;
+  if (nd.count <= 16) {  // every load in flight at once
+    uint32_t key[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) key[j] = j < nd.count ? src[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (j < nd.count) c += 1u << (8 * child_of(key[j], mx, my));
+    return make_int4((int)(c & 255u), (int)((c >> 8) & 255u), (int)((c >> 16) & 255u), (int)(c >> 24));
+  }
   int i = 0;
   for (; i + 4 <= nd.count; i += 4) {
     const uint32_t k0 = src[i], k1 = src[i + 1], k2 = src[i + 2], k3 = src[i + 3];
@@ -967,6 +976,15 @@ __device__ __forceinline__ void serial_child_partition(const ONode& nd, int4 cnt
     dst[(o >> sh) & 255u] = key;
     o += 1u << sh;
   };
+  if (nd.count <= 16) {  // every load in flight at once
+    uint32_t key[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) key[j] = j < nd.count ? src[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+      if (j < nd.count) put(key[j]);
+    return;
+  }
   int i = 0;
   for (; i + 4 <= nd.count; i += 4) {
     const uint32_t k0 = src[i], k1 = src[i + 1], k2 = src[i + 2], k3 = src[i + 3];
