@@ -592,7 +592,7 @@ __device__ __forceinline__ int fast_prefilter4(const uint8_t* roi, int dw, int d
     int px = 0;
     if (q < items) {
       const int rr = (int)(((uint32_t)q * gmagic) >> 20), g = q - rr * gw;
-      px = rr * dw + 4 * g;
+      px = (rr << 6) + 4 * g;  // list entry r << 6 | c (c < 64 on this path)
       const uint32_t* row = reinterpret_cast<const uint32_t*>(roi) + (rr + 3) * RD + g;
       const uint32_t* up = row - 3 * RD;
       const uint32_t* dn = row + 3 * RD;
@@ -763,12 +763,16 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
       }
     }
   }
-  // row of detection index q: q / dw, as (q * magic) >> 20 on the constant-stride path
-  // (exact while q * dw < 2^20, which the host guarantees by the ROI bounds)
-  const uint32_t magic = ((1u << 20) + dw - 1) / dw;
-  auto row_of = [&](int q) -> int {
-    if constexpr (RSC != 0) return (int)(((uint32_t)q * magic) >> 20);
-    else return q / dw;
+  // list entries: detection pixel (r, c) as r << 6 | c on the constant-stride path (every ROI
+  // there is at most 61 columns wide), as r * dw + c on the generic one
+  auto dec_rc = [&](int q, int& r, int& c) {
+    if constexpr (RSC != 0) {
+      r = q >> 6;
+      c = q & 63;
+    } else {
+      r = q / dw;
+      c = q - r * dw;
+    }
   };
   for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
   wave_sync();
@@ -826,7 +830,9 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
     if (ja < nlist) {
       qa = list[ja];
       qb = jb < nlist ? list[jb] : qa;
-      const int ra = row_of(qa), ca = qa - ra * dw, rb = row_of(qb), cb = qb - rb * dw;
+      int ra, ca, rb, cb;
+      dec_rc(qa, ra, ca);
+      dec_rc(qb, rb, cb);
       const uint8_t* pa = R + (ra + 3) * RS + (ca + 3);
       const uint8_t* pb = R + (rb + 3) * RS + (cb + 3);
       m = arc_strength_pk(pa, pb, RS, a.tlow);
@@ -854,8 +860,7 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
       int rr = 0, cc = 0, sc = 0;
       if (j < ncorner) {
         const int q = list[j];
-        rr = row_of(q);
-        cc = q - rr * dw;
+        dec_rc(q, rr, cc);
         const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
         const int m = mp[0];
         // score m - 1 beats every neighbour's (mn >= t + 1 ? mn - 1 : 0) exactly when m > mn for
