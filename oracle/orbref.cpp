@@ -922,51 +922,6 @@ extern "C" int orbref_search_for_triangulation(const orbfe_frame_view* K1,
   return ORBFE_OK;
 }
 
-// TemplatedVocabulary::transform -> FeatureVector (TemplatedVocabulary.h:1140-1207, 1231-1272).
-// Tree in DBoW2 layout: node 0 root, children contiguous at first_child[node], n_children == 0
-// marks a word. Output CSR: node ids ascending, features ascending inside a node.
-extern "C" int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* node_desc,
-                                      const int32_t* first_child, const int32_t* n_children,
-                                      const float* weights, const uint8_t* desc, int n,
-                                      int levelsup, uint32_t* node_ids, int32_t* offsets,
-                                      int32_t* indices, int* n_out) {
-  if (!node_desc || !first_child || !n_children || !weights || !n_out || n < 0 || n_nodes <= 0)
-    return ORBFE_ERR_ARG;
-  const int nid_level = levels - levelsup;
-  std::vector<std::pair<uint32_t, int>> fv;  // (node, feature) in addFeature order
-  for (int i = 0; i < n; i++) {
-    uint32_t nid = 0, final_id = 0;
-    int level = 0;
-    do {
-      ++level;
-      const int f = first_child[final_id], nc = n_children[final_id];
-      uint32_t best = (uint32_t)f;
-      int best_d = hamming32(desc + (size_t)i * 32, node_desc + (size_t)f * 32);
-      for (int c = 1; c < nc; c++) {
-        const int d = hamming32(desc + (size_t)i * 32, node_desc + (size_t)(f + c) * 32);
-        if (d < best_d) { best_d = d; best = (uint32_t)(f + c); }
-      }
-      final_id = best;
-      if (level == nid_level) nid = final_id;
-    } while (n_children[final_id] > 0);
-    if (weights[final_id] > 0) fv.push_back({nid, i});
-  }
-  std::stable_sort(fv.begin(), fv.end(), [](const std::pair<uint32_t, int>& a,
-                                            const std::pair<uint32_t, int>& b) { return a.first < b.first; });
-  int nodes = 0;
-  for (size_t k = 0; k < fv.size(); k++) {
-    if (k == 0 || fv[k].first != fv[k - 1].first) {
-      node_ids[nodes] = fv[k].first;
-      offsets[nodes] = (int32_t)k;
-      nodes++;
-    }
-    indices[k] = fv[k].second;
-  }
-  offsets[nodes] = (int32_t)fv.size();
-  *n_out = nodes;
-  return ORBFE_OK;
-}
-
 // =============================================================================================
 // Frame::ComputeStereoMatches (src/Frame.cc:522-700), restated. Keypoints are the extractor's
 // output (level-0 coordinates, octave = level); the pyramids are the left / right extractors'

@@ -66,11 +66,22 @@ int orbref_search_for_triangulation(const orbfe_frame_view* kf1, const orbfe_fra
                                     const orbfe_feature_vector* fv2, const float* f12, float ex,
                                     float ey, int only_stereo, int check_ori, int32_t* match12,
                                     int* nmatches);
-/* TemplatedVocabulary::transform -> FeatureVector CSR (see orbfe_vocab.h for the tree layout). */
-int orbref_vocab_transform(int n_nodes, int levels, const uint8_t* node_desc,
-                           const int32_t* first_child, const int32_t* n_children,
-                           const float* weights, const uint8_t* desc, int n, int levelsup,
-                           uint32_t* node_ids, int32_t* offsets, int32_t* indices, int* n_out);
+/* The DBoW2 vocabulary (orbref_vocab.cpp): the reference's loaders and transform with its own
+ * containers (std::map BowVector / FeatureVector, child-id vectors, double weights). */
+typedef struct orbref_vocab orbref_vocab;
+int orbref_vocab_load_text(const char* path, orbref_vocab** out);
+int orbref_vocab_load_binary(const char* path, orbref_vocab** out);
+int orbref_vocab_from_table(int n_nodes, int k, int levels, int scoring, int weighting,
+                            const int32_t* parent, const uint8_t* is_leaf, const uint8_t* node_desc,
+                            const double* weights, orbref_vocab** out);
+void orbref_vocab_free(orbref_vocab* v);
+int orbref_vocab_info(const orbref_vocab* v, int* info6);
+int orbref_vocab_tables(const orbref_vocab* v, int32_t* parent, uint8_t* is_word, uint8_t* desc,
+                        double* weight, uint32_t* word_id);
+int orbref_vocab_transform_full(const orbref_vocab* v, const uint8_t* desc, int n, int levelsup,
+                                uint32_t* bow_words, double* bow_weights, int* n_words,
+                                uint32_t* node_ids, int32_t* offsets, int32_t* indices,
+                                int* n_nodes);
 /* Frame::isInFrustum over a MapPoint set (Frame.cc:318-374, MapPoint.cc:403-447) and
  * Tracking::SearchLocalPoints' projection + SearchByProjection (Tracking.cc:1186-1213). */
 int orbref_is_in_frustum(const orbfe_frame_view* frame, const orbfe_mappoint_geometry* geom,

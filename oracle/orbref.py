@@ -67,8 +67,17 @@ def lib(kind: str = "checker") -> ctypes.CDLL:
         L.orbref_search_local_points.argtypes = [c_void_p] * 3 + [c_float] * 4 + \
             [c_void_p, POINTER(c_int), c_void_p, POINTER(c_int)]
         L.orbref_build_grid.argtypes = [c_void_p, c_void_p, c_void_p]
-        L.orbref_vocab_transform.argtypes = [c_int, c_int] + [c_void_p] * 5 + [c_int, c_int] + \
-            [c_void_p] * 3 + [POINTER(c_int)]
+        # orbref_vocab.cpp
+        L.orbref_vocab_load_text.argtypes = [ctypes.c_char_p, POINTER(c_void_p)]
+        L.orbref_vocab_load_binary.argtypes = [ctypes.c_char_p, POINTER(c_void_p)]
+        L.orbref_vocab_from_table.argtypes = [c_int] * 5 + [c_void_p] * 4 + [POINTER(c_void_p)]
+        L.orbref_vocab_free.argtypes = [c_void_p]
+        L.orbref_vocab_free.restype = None
+        L.orbref_vocab_info.argtypes = [c_void_p, c_void_p]
+        L.orbref_vocab_tables.argtypes = [c_void_p] * 6
+        L.orbref_vocab_transform_full.argtypes = [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                                  POINTER(c_int), c_void_p, c_void_p, c_void_p,
+                                                  POINTER(c_int)]
         # orbref_kf.cpp
         L.orbref_search_by_bow_kf_frame.argtypes = [c_void_p] * 4 + [c_float, c_int, c_void_p, POINTER(c_int)]
         L.orbref_search_by_bow_kf_kf.argtypes = [c_void_p] * 4 + [c_float, c_int, c_void_p, POINTER(c_int)]
@@ -265,20 +274,70 @@ def build_grid(F):
     return start, items[:start[-1]]
 
 
-def vocab_transform(voc, desc: np.ndarray, levelsup: int):
-    """(node_ids, offsets, indices) of TemplatedVocabulary::transform's FeatureVector."""
-    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
-    n = len(desc)
-    ids = np.zeros(max(n, 1), np.uint32)
-    offs = np.zeros(n + 1, np.int32)
-    idx = np.zeros(max(n, 1), np.int32)
-    nn = c_int()
-    st = lib().orbref_vocab_transform(len(voc.descriptors), voc.levels, _p(voc.descriptors),
-                                      _p(voc.first_child), _p(voc.n_children), _p(voc.weights),
-                                      _p(desc), n, levelsup, _p(ids), _p(offs), _p(idx), byref(nn))
-    assert st == 0
-    k = nn.value
-    return ids[:k], offs[:k + 1], idx[:offs[k]]
+class RefVocabulary:
+    """TemplatedVocabulary restated with the reference's containers (orbref_vocab.cpp): built from
+    a node table, or by the reference's text / binary loaders."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @staticmethod
+    def from_table(k, levels, scoring, weighting, parent, is_leaf, descriptors, weights):
+        parent = np.ascontiguousarray(parent, np.int32)
+        is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        descriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(-1, 32)
+        weights = np.ascontiguousarray(weights, np.float64)
+        h = c_void_p()
+        st = lib().orbref_vocab_from_table(len(parent), k, levels, scoring, weighting, _p(parent),
+                                           _p(is_leaf), _p(descriptors), _p(weights), byref(h))
+        assert st == 0, st
+        return RefVocabulary(h)
+
+    @staticmethod
+    def load(path: str, binary: bool = False) -> Optional["RefVocabulary"]:
+        h = c_void_p()
+        fn = lib().orbref_vocab_load_binary if binary else lib().orbref_vocab_load_text
+        if fn(str(path).encode(), byref(h)) != 0:
+            return None
+        return RefVocabulary(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbref_vocab_free(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def info(self) -> dict:
+        a = np.zeros(6, np.int32)
+        lib().orbref_vocab_info(self._h, _p(a))
+        return dict(zip(("n_nodes", "n_words", "k", "levels", "scoring", "weighting"), a.tolist()))
+
+    def tables(self) -> dict:
+        n = self.info()["n_nodes"]
+        t = {"parent": np.zeros(n, np.int32), "is_leaf": np.zeros(n, np.uint8),
+             "descriptors": np.zeros((n, 32), np.uint8), "weights": np.zeros(n, np.float64),
+             "word_id": np.zeros(n, np.uint32)}
+        lib().orbref_vocab_tables(self._h, _p(t["parent"]), _p(t["is_leaf"]), _p(t["descriptors"]),
+                                  _p(t["weights"]), _p(t["word_id"]))
+        return t
+
+    def transform(self, desc: np.ndarray, levelsup: int = 4):
+        """TemplatedVocabulary::transform: (bow_words, bow_weights, FeatureVector CSR
+        (node_ids, offsets, indices))."""
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(desc)
+        words = np.zeros(max(n, 1), np.uint32)
+        weights = np.zeros(max(n, 1), np.float64)
+        ids = np.zeros(max(n, 1), np.uint32)
+        offs = np.zeros(n + 1, np.int32)
+        idx = np.zeros(max(n, 1), np.int32)
+        nw, nn = c_int(), c_int()
+        st = lib().orbref_vocab_transform_full(self._h, _p(desc), n, levelsup, _p(words), _p(weights),
+                                               byref(nw), _p(ids), _p(offs), _p(idx), byref(nn))
+        assert st == 0
+        k = nn.value
+        return words[:nw.value], weights[:nw.value], (ids[:k], offs[:k + 1], idx[:offs[k]])
 
 
 class _LevelView(ctypes.Structure):

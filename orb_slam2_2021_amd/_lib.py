@@ -143,14 +143,18 @@ _SIGNATURES = {
     "orbfe_debug_force_level_launches": (c_int, [c_void_p, c_int]),
     "orbfe_debug_set_fast_side_levels": (c_int, [c_void_p, c_int]),
     "orbfe_debug_steer_trig": (c_int, [c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]),
-    "orbfe_vocab_create": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                   POINTER(c_void_p)]),
+    "orbfe_vocab_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_int, POINTER(c_void_p)]),
+    "orbfe_vocab_load_text": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
+    "orbfe_vocab_load_binary": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
+    "orbfe_vocab_get_info": (c_int, [c_void_p, c_void_p]),
+    "orbfe_vocab_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "orbfe_vocab_destroy": (c_int, [c_void_p]),
     "orbfe_vocab_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                      c_void_p, POINTER(c_int)]),
+                                      POINTER(c_int), c_void_p, c_void_p, c_void_p, POINTER(c_int)]),
     "orbfe_vocab_transform_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p,
                                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                                   c_int, c_void_p]),
+                                                   c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "orbfe_compute_stereo_matches_batch_device": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p,
                                                           c_void_p, c_void_p, c_int, c_float,
                                                           c_float, c_void_p, c_void_p, c_void_p]),

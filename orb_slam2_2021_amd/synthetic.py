@@ -31,14 +31,36 @@ def hamming_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 @dataclass
 class Vocabulary:
-    """A DBoW2 vocabulary tree: nodes in BFS order, children contiguous, node 0 = root."""
+    """A DBoW2 vocabulary tree: nodes in BFS order, children contiguous, node 0 = root.
+
+    The reference's node table (TemplatedVocabulary::m_nodes) is `parent` / `is_leaf` /
+    `descriptors` / `weights` (WordValue = double; internal nodes carry weight 0, words their idf)."""
 
     k: int
     levels: int
     descriptors: np.ndarray   # (n_nodes, 32) uint8 (row 0 unused: root)
     first_child: np.ndarray   # int32, -1 for leaves
     n_children: np.ndarray    # int32
-    weights: np.ndarray       # float32 word weight per node (> 0 for every leaf here)
+    weights: np.ndarray       # float64 weight per node (word weight at the leaves)
+    scoring: int = 0          # L1_NORM (ORBvoc)
+    weighting: int = 0        # TF_IDF (ORBvoc)
+
+    @property
+    def n_nodes(self) -> int:
+        return len(self.descriptors)
+
+    @property
+    def parent(self) -> np.ndarray:
+        p = np.full(self.n_nodes, -1, np.int32)
+        for node in np.nonzero(self.n_children > 0)[0]:
+            p[self.first_child[node]:self.first_child[node] + self.n_children[node]] = node
+        return p
+
+    @property
+    def is_leaf(self) -> np.ndarray:
+        leaf = (self.n_children == 0).astype(np.uint8)
+        leaf[0] = 0
+        return leaf
 
     @staticmethod
     def synthetic(k: int = 10, levels: int = 2, seed: int = 0x0B0C0AB) -> "Vocabulary":
@@ -60,10 +82,49 @@ class Vocabulary:
                 first[node] = nxt
                 nch[node] = k
                 nxt += k
-        return Vocabulary(k, levels, desc, first, nch, np.ones(n_nodes, np.float32))
+        return Vocabulary(k, levels, desc, first, nch, np.ones(n_nodes, np.float64))
+
+    @staticmethod
+    def synthetic_orbvoc(k: int = 10, levels: int = 6, seed: int = 0x0B0C6, stop_frac: float = 0.01,
+                         scoring: int = 0, weighting: int = 0) -> "Vocabulary":
+        """A tree shaped like ORBvoc (k = 10, L = 6: 1,111,111 nodes, 10^6 words). Centroids are
+        hierarchical -- a child differs from its parent in about 256 / 2^level bits -- so the
+        descent follows real nearest-centroid paths; word weights are idf-like doubles in
+        [0.5, 10), `stop_frac` of the words stopped (weight 0), internal nodes 0 (DBoW2 weights
+        words only)."""
+        rng = np.random.default_rng(seed)
+        counts = [k ** d for d in range(levels + 1)]
+        n_nodes = sum(counts)
+        desc = np.zeros((n_nodes, 32), np.uint8)
+        first = np.full(n_nodes, -1, np.int32)
+        nch = np.zeros(n_nodes, np.int32)
+        start = 1
+        desc[0] = 0
+        prev = slice(0, 1)
+        for d in range(1, levels + 1):
+            n = counts[d]
+            par = np.repeat(np.arange(prev.start, prev.stop), k)
+            first[prev] = start + np.arange(prev.stop - prev.start, dtype=np.int64) * k
+            nch[prev] = k
+            mask = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+            for _ in range(min(d, 5) - 1):  # P(bit flips) = 2^-min(d,5)
+                mask &= rng.integers(0, 256, (n, 32), dtype=np.uint8)
+            desc[start:start + n] = desc[par] ^ mask
+            prev = slice(start, start + n)
+            start += n
+        w = np.zeros(n_nodes, np.float64)
+        leaves = np.arange(prev.start, prev.stop)
+        w[leaves] = rng.uniform(0.5, 10.0, len(leaves))
+        w[leaves[rng.random(len(leaves)) < stop_frac]] = 0.0
+        return Vocabulary(k, levels, desc, first, nch, w, scoring, weighting)
 
     def node_at_level(self, desc: np.ndarray, levelsup: int) -> np.ndarray:
         """TemplatedVocabulary::transform's nid for every descriptor (strict '<': first best)."""
+        return self.descend(desc, levelsup)[0]
+
+    def descend(self, desc: np.ndarray, levelsup: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(nid, final node) of TemplatedVocabulary::transform for every descriptor
+        (TemplatedVocabulary.h:1231-1272; complete trees only)."""
         nid_level = self.levels - levelsup
         cur = np.zeros(len(desc), np.int64)
         nid = np.zeros(len(desc), np.int64)
@@ -79,10 +140,34 @@ class Vocabulary:
             cur = best
             if level == nid_level:
                 nid = cur.copy()
-        return nid
+        return nid, cur
 
     def feature_vector(self, desc: np.ndarray, levelsup: int) -> FeatureVector:
         return FeatureVector.from_assignment(self.node_at_level(desc, levelsup))
+
+    # ---- the reference's file formats (TemplatedVocabulary.h:1441-1461, 1516-1537) ----
+    def save_text(self, path: str) -> None:
+        """saveToTextFile: "k L  scoring weighting", then per node i >= 1
+        "parent isLeaf d0 .. d31  weight" with the weight in ostream's default format (%g)."""
+        par, leaf = self.parent, (self.n_children == 0)
+        with open(path, "w") as f:
+            f.write(f"{self.k} {self.levels}  {self.scoring} {self.weighting}\n")
+            for i in range(1, self.n_nodes):
+                d = " ".join(str(int(x)) for x in self.descriptors[i])
+                f.write(f"{par[i]} {1 if leaf[i] else 0} {d}  {self.weights[i]:g}\n")
+
+    def save_binary(self, path: str) -> None:
+        """saveToBinaryFile: nb_nodes, size_node = 41, k, L, scoring, weighting; per node i >= 1
+        int32 parent, 32 descriptor bytes, float32 weight, bool isLeaf."""
+        n = self.n_nodes
+        rec = np.zeros(n - 1, np.dtype([("p", "<i4"), ("d", "u1", 32), ("w", "<f4"), ("l", "u1")]))
+        rec["p"] = self.parent[1:]
+        rec["d"] = self.descriptors[1:]
+        rec["w"] = self.weights[1:].astype(np.float32)
+        rec["l"] = (self.n_children[1:] == 0)
+        with open(path, "wb") as f:
+            f.write(np.array([n, 41, self.k, self.levels, self.scoring, self.weighting], "<u4").tobytes())
+            f.write(rec.tobytes())
 
 
 def skew(t: np.ndarray) -> np.ndarray:
