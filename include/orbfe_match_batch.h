@@ -43,8 +43,11 @@ void* orbfe_matcher_stream(orbfe_matcher* m);
  * fallback kernel had to finish the claim order. */
 int orbfe_matcher_last_stats(orbfe_matcher* m, int* rounds, int* serial_used);
 
-/* Cap the fixpoint rounds of SearchByProjection (1..12, default 12). With too few rounds the
- * serial kernel finishes the claim order; tests use this to exercise that path. */
+/* The SearchByProjection claim-order fixpoint runs 12 rounds in its first launch; a host-buffer
+ * search whose fixpoint has not settled then continues in doubling chunks (up to 1024 rounds)
+ * before the serial kernel would finish the claim order. This call fixes the budget to `rounds`
+ * (1..12) with no continuation, so that the serial kernel runs past it; tests use it to exercise
+ * that path. */
 int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds);
 
 #ifdef __cplusplus

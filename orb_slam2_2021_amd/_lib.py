@@ -150,6 +150,10 @@ _SIGNATURES = {
     "orbfe_vocab_get_info": (c_int, [c_void_p, c_void_p]),
     "orbfe_vocab_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "orbfe_vocab_destroy": (c_int, [c_void_p]),
+    # orbfe_pack.h
+    "orbfe_packed_bytes": (c_size_t, [c_int, ctypes.c_longlong]),
+    "orbfe_pack_keypoints_device": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                            c_size_t, c_void_p, c_void_p]),
     "orbfe_vocab_transform": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                       POINTER(c_int), c_void_p, c_void_p, c_void_p, POINTER(c_int)]),
     "orbfe_vocab_transform_batch_device": (c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p,

@@ -642,7 +642,7 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
     in.own0[i] = 0x7fffffff;
     in.own2[i] = 0x7fffffff;
   }
-  if (i < SBP_MAX_ROUNDS + 4) in.state[i] = 0;
+  if (i < SBP_ROUND_CAP + 4) in.state[i] = 0;
   if (i == 0) {
     *in.nmatches = 0;
     *in.serial = 0;
@@ -836,7 +836,8 @@ struct SbpFinishArgs {
   int32_t* nmatches;
   int check_ori;
   const float* q_angle;  // last-frame keypoint angles (mode 1)
-  int32_t* serial_used;
+  int32_t* serial_used;  // 1: the serial walk ran; 2: unsettled, deferred to more rounds
+  int defer;
 };
 
 // Sequential fallback (the reference loop verbatim) when the fixpoint did not settle in
@@ -876,6 +877,10 @@ __global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* bl
   const bool converged = sbp_converged(a);
   if (converged && !f.check_ori) return;  // done by k_sbp_collect
   const int32_t* res = f.res_final[(rounds - 1) & 1];
+  if (!converged && f.defer) {  // the host continues the rounds (sbp_fetch)
+    if (t == 0) *f.serial_used = 2;
+    return;
+  }
   if (!converged) {
     if (t == 0) {
       *f.serial_used = 1;
@@ -1347,7 +1352,7 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
   p.oown1 = ar.add(4 * f1);
   p.oown2 = ar.add(4 * f1);
   p.oblk = ar.add(4 * f1);
-  p.ostate = ar.add(4 * (SBP_MAX_ROUNDS + 4));
+  p.ostate = ar.add(4 * (SBP_ROUND_CAP + 4));
   p.obest = ar.add(4 * q1);
   p.cache = F->n <= 32767;  // candidate keypoint indices are int16
   const size_t cq = p.cache ? (size_t)cand_cap * q1 : 0;
@@ -1435,7 +1440,8 @@ static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_fram
   in.serial = m->d_serial;
   in.nq = std::max(p.nq, 1);
   in.nf = std::max(F->n, 1);
-  hipLaunchKernelGGL(k_sbp_init, dim3((std::max(in.nq, in.nf) + 255) / 256), dim3(256), 0, m->stream, in);
+  const int nthreads = std::max(std::max(in.nq, in.nf), SBP_ROUND_CAP + 4);
+  hipLaunchKernelGGL(k_sbp_init, dim3((nthreads + 255) / 256), dim3(256), 0, m->stream, in);
 }
 
 void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
@@ -1455,19 +1461,17 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
                        m->stream, a);
 }
 
-int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
-               const SbpMode& md) {
+// Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over three:
+// round r claims into own[r % 3], reads own[(r + 2) % 3] and clears own[(r + 1) % 3] for round
+// r + 1, which nobody reads during round r).
+static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
+                       const SbpMode& md, int r0, int r1, bool defer) {
   uint8_t* A = m->arena;
   const int nq = p.nq;
-  sbp_launch_grid(m, p, F, dF);
-  sbp_launch_init(m, p, F);
   SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
   int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
-  // owner buffers rotate over three: round r claims into own[r % 3], reads own[(r + 2) % 3] and
-  // clears own[(r + 1) % 3] for round r + 1 (nobody reads it during round r)
   int32_t* own[3] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2)};
-  const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
-  for (int r = 0; r < rounds && nq > 0; r++) {
+  for (int r = r0; r < r1 && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];
@@ -1490,17 +1494,43 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   f.check_ori = md.check_ori;
   f.q_angle = (const float*)(A + p.oqa);
   f.serial_used = m->d_serial;
+  f.defer = defer ? 1 : 0;
   if (nq > 0) {
     hipLaunchKernelGGL(k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
     hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
   }
+}
+
+int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
+               const SbpMode& md, bool defer) {
+  sbp_launch_grid(m, p, F, dF);
+  sbp_launch_init(m, p, F);
+  const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
+  sbp_rounds(m, p, F, dF, md, 0, rounds, defer && m->round_cap > rounds);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }
 
-int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatches) {
+int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatches, const orbfe_frame_view* F,
+              const orbfe_frame_view* dF, const SbpMode* md) {
   uint8_t* A = m->arena;
   int32_t nm = 0, state[2] = {0, 0}, serial = 0;
+  if (p.nq > 0 && F && dF && md && !(md->no_claims && p.cache)) {
+    // a fixpoint still unsettled continues in doubling chunks of rounds (a rare case: one sync
+    // per chunk), the serial walk only past round_cap
+    ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
+    ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+    int done = m->max_rounds;
+    while (serial == 2) {
+      const int next = std::min(std::max(2 * done, done + 1), m->round_cap);
+      ORBFE_HIP_CHECK(hipMemsetAsync(m->d_serial, 0, 4, m->stream));
+      sbp_rounds(m, p, F, *dF, *md, done, next, next < m->round_cap);
+      ORBFE_HIP_CHECK(hipGetLastError());
+      done = next;
+      ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
+      ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+    }
+  }
   if (p.nq > 0) {
     if (best_idx)
       ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, A + p.obest, 4 * (size_t)p.nq, hipMemcpyDeviceToHost, m->stream));
@@ -1568,8 +1598,8 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, const Sb
   if ((st = sbp_stage(m, p, F, h_qdesc, h_qangle, &dF))) return st;
   if (nq > 0 && (st = make_q(A, dF, (SbpQuery*)(A + p.oq)))) return st;  // stages, flushes, builds queries
   if ((st = flush_h2d(m))) return st;
-  if ((st = sbp_launch(m, p, F, dF, md))) return st;
-  return sbp_fetch(m, p, best_idx, nmatches);
+  if ((st = sbp_launch(m, p, F, dF, md, true))) return st;
+  return sbp_fetch(m, p, best_idx, nmatches, F, &dF, &md);
 }
 
 extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_frame_view* F,
@@ -1691,6 +1721,7 @@ extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
 extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
   if (!m || rounds < 1 || rounds > SBP_MAX_ROUNDS) return ORBFE_ERR_ARG;
   m->max_rounds = rounds;
+  m->round_cap = rounds;  // a fixed budget: the serial walk past it (tests of the fallback)
   return ORBFE_OK;
 }
 

@@ -20,7 +20,8 @@
 #define GRID_COLS 64
 #define GRID_ROWS 48
 #define GRID_CELLS (GRID_COLS * GRID_ROWS)
-#define SBP_MAX_ROUNDS 12
+#define SBP_MAX_ROUNDS 12      // rounds of the first launch (no host sync)
+#define SBP_ROUND_CAP 1024     // rounds a host-synchronous search may continue to before the serial walk
 #define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
 #define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
 #define SBP_CAND 48          // default per-query candidate cache of the projection searches
@@ -45,6 +46,7 @@ struct orbfe_matcher {
   size_t stage_lo = SIZE_MAX, stage_hi = 0;
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
+  int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
 };
 
 // ---- device helpers shared by the matcher kernels ---------------------------------------------
@@ -161,10 +163,15 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p);
 int sbp_stage(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const uint8_t* h_qdesc,
               const float* h_qangle, orbfe_frame_view* dF);
 // grid, init, fixpoint rounds, collect / finish on the matcher's stream (queries at p.oq)
+// With `defer`, a fixpoint still unsettled after the first launch's rounds leaves its results for
+// sbp_fetch to continue (more rounds) instead of running the serial walk.
 int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
-               const SbpMode& md);
-// D2H of best_idx and the count, stream sync, round statistics
-int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatches);
+               const SbpMode& md, bool defer = false);
+// D2H of best_idx and the count, stream sync, round statistics. With F / dF / md (a search launched
+// with defer), an unsettled fixpoint continues with doubling round chunks up to m->round_cap.
+int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatches,
+              const orbfe_frame_view* F = nullptr, const orbfe_frame_view* dF = nullptr,
+              const SbpMode* md = nullptr);
 // grid only (CSR of the frame's keypoints, 16-B records) -- used by SearchForInitialization
 void sbp_launch_grid(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF);
 // round 0 only (candidate cache + first result), for callers that consume the cache

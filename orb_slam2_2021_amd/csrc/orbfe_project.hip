@@ -264,8 +264,8 @@ int run_projection(orbfe_matcher* m, const orbfe_frame_view* target, const orbfe
   if ((st = flush_h2d(m))) return st;
   set_camera(qa, cam, target, dT, lsf, th);
   launch_queries(m, p, qa);
-  if ((st = sbp_launch(m, p, target, dT, md))) return st;
-  return sbp_fetch(m, p, best_idx, count);
+  if ((st = sbp_launch(m, p, target, dT, md, true))) return st;
+  return sbp_fetch(m, p, best_idx, count, target, &dT, &md);
 }
 
 bool target_ok(const orbfe_frame_view* f) { return frame_ok(f) && levels_ok(f->keys_un, f->n, f->nlevels); }

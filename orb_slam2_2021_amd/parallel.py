@@ -1,18 +1,24 @@
-"""Frame sharding and result gathering across GPUs (one process per GPU, torch.distributed).
+"""Frame sharding and the exchange steps across GPUs (one process per GPU, torch.distributed).
 
 Extraction is independent per image (ORBextractor::operator(), ORBextractor.cc:1041-1103) and
-SearchForTriangulation per KeyFrame pair, so frames shard embarrassingly: rank r owns a
-contiguous block of frames and no collective touches the data path. The one exchange step the
-north star names -- gathering every rank's keypoints and descriptors to rank 0 (BASELINE config
-C4) -- is a fixed-capacity gather of (counts, keypoints, descriptors) buffers over RCCL (xGMI),
-unpacked into per-frame results on the destination.
+SearchForTriangulation per KeyFrame pair, so frames shard embarrassingly: rank r owns a block of
+frames and no collective touches the data path. The exchange steps BASELINE.json names:
+
+* C4: every rank's keypoints and descriptors gathered to rank 0. Each rank packs only its used
+  slots on the device (orbfe_pack_keypoints_device, include/orbfe_pack.h), the packed sizes are
+  all-gathered (8 bytes per rank), then rank 0 receives each payload point-to-point over RCCL
+  (xGMI: one link per peer) -- no fixed-capacity buffers cross the links.
+* C5: the local map (the MapPoint SoA Tracking::SearchLocalPoints projects, Tracking.cc:1164-1216)
+  is replicated: broadcast once from rank 0, then every rank matches its own frames against it.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from ctypes import c_size_t, c_void_p
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import _lib as L
 from ._lib import KEYPOINT_DTYPE
 
 
@@ -25,48 +31,110 @@ def shard_frames(n_frames: int, world: int, rank: int) -> range:
     return range(start, start + base + (1 if rank < extra else 0))
 
 
-def gather_to_root(counts, kps_bytes, desc_bytes, dst: int = 0):
-    """Gather fixed-capacity per-image buffers of every rank to `dst`.
+# ---- the packed form of a batch's keypoints + descriptors (include/orbfe_pack.h) ----
 
-    counts: int32 tensor [n_img]; kps_bytes / desc_bytes: uint8 tensors [n_img * cap * 28 / 32].
-    Returns lists of per-rank tensors on `dst` (None elsewhere). Works on any backend: RCCL
-    ("nccl") on GPUs, gloo on CPU tensors."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size()
-    rank = dist.get_rank()
-    out = None
-    if rank == dst:
-        out = ([torch.empty_like(counts) for _ in range(world)],
-               [torch.empty_like(kps_bytes) for _ in range(world)],
-               [torch.empty_like(desc_bytes) for _ in range(world)])
-    dist.gather(counts, out[0] if out else None, dst=dst)
-    dist.gather(kps_bytes, out[1] if out else None, dst=dst)
-    dist.gather(desc_bytes, out[2] if out else None, dst=dst)
+def _align16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+def packed_bytes(n_images: int, total_keypoints: int) -> int:
+    head = _align16(4 * (1 + n_images))
+    return _align16(head + 28 * total_keypoints) + 32 * total_keypoints
+
+
+def pack_host(results: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]]) -> np.ndarray:
+    """Host-side packing in the device layout (for CPU ranks and tests)."""
+    counts = np.array([len(k) for k, _ in results], np.int32)
+    total = int(counts.sum())
+    out = np.zeros(packed_bytes(len(results), total), np.uint8)
+    head = _align16(4 * (1 + len(results)))
+    out[:4] = np.frombuffer(np.int32(len(results)).tobytes(), np.uint8)
+    out[4:4 + 4 * len(results)] = np.frombuffer(counts.tobytes(), np.uint8)
+    kp = np.concatenate([np.ascontiguousarray(k, KEYPOINT_DTYPE) for k, _ in results]) if total else \
+        np.zeros(0, KEYPOINT_DTYPE)
+    out[head:head + 28 * total] = np.frombuffer(kp.tobytes(), np.uint8)
+    doff = _align16(head + 28 * total)
+    for (k, d) in results:
+        if len(k):
+            n = len(k)
+            out[doff:doff + 32 * n] = np.ascontiguousarray(d, np.uint8).reshape(-1)
+            doff += 32 * n
     return out
 
 
-def unpack(counts: np.ndarray, kps_bytes: np.ndarray, desc_bytes: np.ndarray,
-           cap: int) -> List[Tuple[np.ndarray, np.ndarray]]:
-    """Per-image (keypoints, descriptors) from fixed-capacity buffers."""
-    n_img = len(counts)
-    kp = np.frombuffer(np.ascontiguousarray(kps_bytes).tobytes(), KEYPOINT_DTYPE).reshape(n_img, cap)
-    de = np.ascontiguousarray(desc_bytes).reshape(n_img, cap, 32)
-    return [(kp[i, :counts[i]].copy(), de[i, :counts[i]].copy()) for i in range(n_img)]
+def unpack_packed(buf: np.ndarray) -> List[Tuple[np.ndarray, np.ndarray]]:
+    """Per-image (keypoints, descriptors) from a packed buffer."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    n_img = int(np.frombuffer(buf[:4].tobytes(), np.int32)[0])
+    counts = np.frombuffer(buf[4:4 + 4 * n_img].tobytes(), np.int32)
+    total = int(counts.sum())
+    head = _align16(4 * (1 + n_img))
+    kp = np.frombuffer(buf[head:head + 28 * total].tobytes(), KEYPOINT_DTYPE)
+    doff = _align16(head + 28 * total)
+    de = buf[doff:doff + 32 * total].reshape(total, 32)
+    out, o = [], 0
+    for c in counts:
+        out.append((kp[o:o + c].copy(), de[o:o + c].copy()))
+        o += int(c)
+    return out
 
 
-def pack(results: Sequence[Tuple[np.ndarray, Optional[np.ndarray]]], cap: int):
-    """Inverse of unpack: fixed-capacity (counts, keypoint bytes, descriptor bytes)."""
-    n_img = len(results)
-    counts = np.zeros(n_img, np.int32)
-    kp = np.zeros((n_img, cap), KEYPOINT_DTYPE)
-    de = np.zeros((n_img, cap, 32), np.uint8)
-    for i, (k, d) in enumerate(results):
-        n = len(k)
-        if n > cap:
-            raise ValueError("capacity exceeded")
-        counts[i] = n
-        kp[i, :n] = k
-        if n:
-            de[i, :n] = d
-    return counts, np.frombuffer(kp.tobytes(), np.uint8).copy(), de.reshape(-1).copy()
+def pack_keypoints_device(n_images: int, d_counts: int, d_kps: int, d_desc: int, cap: int,
+                          d_out: int, out_cap: int, d_total: int, stream: int = 0) -> None:
+    """orbfe_pack_keypoints_device: async on `stream`; the size lands in the int64 at d_total."""
+    L.check(L.lib().orbfe_pack_keypoints_device(int(n_images), c_void_p(d_counts), c_void_p(d_kps),
+                                                c_void_p(d_desc), int(cap), c_void_p(d_out),
+                                                c_size_t(out_cap), c_void_p(d_total), c_void_p(stream)),
+            "orbfe_pack_keypoints_device")
+
+
+def gather_packed(payload, size, dst: int = 0, recv: Optional[Sequence] = None):
+    """Gather every rank's packed payload to `dst`: sizes first (all_gather of one int64 per
+    rank), then one point-to-point transfer per peer of exactly its used bytes.
+
+    payload: uint8 tensor holding this rank's packed batch; size: int64 tensor [1] with its byte
+    count (on the payload's device: written by the pack kernel, or set by the host).
+    recv: on dst, per-rank uint8 receive buffers (allocated if None).
+    Returns (list of per-rank uint8 tensors of exact size on dst / None elsewhere, sizes).
+    Works on any backend: RCCL ("nccl") on GPUs, gloo on CPU tensors."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    sizes = [torch.empty(1, dtype=torch.int64, device=size.device) for _ in range(world)]
+    dist.all_gather(sizes, size.reshape(1))
+    sizes_h = [int(x) for x in torch.cat(sizes).cpu().tolist()]
+    ops = []
+    out = None
+    if rank == dst:
+        out = []
+        for r in range(world):
+            if r == dst:
+                out.append(payload[:sizes_h[r]])
+                continue
+            buf = recv[r] if recv is not None else torch.empty(sizes_h[r], dtype=torch.uint8,
+                                                               device=payload.device)
+            if buf.numel() < sizes_h[r]:
+                raise ValueError(f"receive buffer for rank {r} too small")
+            out.append(buf[:sizes_h[r]])
+            ops.append(dist.P2POp(dist.irecv, out[-1], r))
+    else:
+        ops.append(dist.P2POp(dist.isend, payload[:sizes_h[rank]], dst))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out, sizes_h
+
+
+def broadcast_arrays(arrays: Dict[str, np.ndarray], device, src: int = 0) -> Dict[str, object]:
+    """C5's replicated local map: the MapPoint SoA (names -> numpy arrays, meaningful on `src`;
+    the other ranks pass arrays of the same shapes and dtypes) broadcast from `src` into tensors on
+    every rank's `device`. Returns {name: tensor}."""
+    import torch
+    import torch.distributed as dist
+    out = {}
+    for name in sorted(arrays):
+        a = np.ascontiguousarray(arrays[name])
+        t = torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(device)
+        dist.broadcast(t, src=src)
+        out[name] = t
+    return out

@@ -1,0 +1,267 @@
+"""The C3 step on one GPU, device-resident (BASELINE.json configs[2]): B stereo frames ->
+
+  1. ORBextractor::operator() on all 2B images, lefts first   (ORBextractor.cc:1041-1103)
+  2. KeyFrame::ComputeBoW: TemplatedVocabulary::transform(desc, BowVector, FeatureVector, 4)
+                                                              (KeyFrame.cc:59-68)
+  3. ORBmatcher(0.6, false).SearchForTriangulation(left_i, right_i, F12, ..., false)
+                                                              (LocalMapping.cc:219-258, ORBmatcher.cc:671-839)
+  (+ Frame::ComputeStereoMatches after extraction with stereo=True, Frame.cc:125)
+
+bench.py times it and tests/test_gpu_c3.py checks it against the oracle, so both run this exact
+sequence. The KeyFrames' per-keypoint state the matcher reads (mvuRight, GetMapPoint) is given
+as device arrays `u_right` / `mp_state`, one `cap`-slot row per image.
+
+Two output sets (depth 2) let sub-batch i's vocabulary + matching overlap sub-batch i+1's
+extraction: extraction i -> matching i -> reuse of set i at sub-batch i + depth, ordered by
+events on two streams.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+def nodes_at_level_bound(tree, levelsup: int, cap: int) -> int:
+    """Upper bound on FeatureVector entries: the nodes the descent can report at
+    m_L - levelsup (nodes at that depth plus shallower leaves), capped by the feature count."""
+    nid_level = tree.levels - levelsup
+    if nid_level <= 0:
+        return 1
+    parent = tree.parent
+    depth = np.zeros(len(parent), np.int32)
+    par = np.maximum(parent, 0)
+    for _ in range(tree.levels + 1):  # converges after the tree's depth
+        depth[1:] = depth[par[1:]] + 1
+    has_child = np.zeros(len(parent), bool)
+    has_child[parent[1:]] = True
+    n = int(((depth == nid_level) | ((depth < nid_level) & ~has_child & (depth > 0))).sum())
+    return max(1, min(cap, n))
+
+
+class C3Pipeline:
+    def __init__(self, ext, voc, tree, B: int, H: int, W: int, cam: dict, F12: np.ndarray,
+                 epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
+                 depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
+                 nnratio: float = 0.6, check_ori: bool = False):
+        import torch
+        from .matcher import ORBmatcher
+        self.ext, self.voc = ext, voc
+        self.B, self.H, self.W = B, H, W
+        self.n_img = 2 * B
+        self.cap = cap = ext.max_keypoints(H, W)
+        self.levelsup = levelsup
+        self.stereo = stereo
+        self.bow = bow
+        self.mb = float(mb)
+        self.cam = cam
+        self.dev = dev = torch.device("cuda", device) if isinstance(device, int) else device
+        self.d_ur, self.d_mp = u_right, mp_state
+        self.d_scale = torch.from_numpy(ext.GetScaleFactors()).to(dev)
+        self.d_sigma2 = torch.from_numpy(ext.GetScaleSigmaSquares()).to(dev)
+        self.node_bound = nodes_at_level_bound(tree, levelsup, cap)
+        n_img = self.n_img
+        pipe = self
+
+        class OutSet:
+            def __init__(self):
+                self.kps = torch.empty(n_img * cap * 28, dtype=torch.uint8, device=dev)
+                self.desc = torch.empty(n_img * cap * 32, dtype=torch.uint8, device=dev)
+                self.cnt = torch.zeros(n_img, dtype=torch.int32, device=dev)
+                self.ids = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+                self.offs = torch.empty(n_img * (cap + 1), dtype=torch.int32, device=dev)
+                self.idx = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+                self.nodes = torch.zeros(n_img, dtype=torch.int32, device=dev)
+                self.bow_words = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
+                self.bow_weights = torch.empty(n_img * cap, dtype=torch.float64, device=dev)
+                self.bow_n = torch.zeros(n_img, dtype=torch.int32, device=dev)
+                self.m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
+                self.nm = torch.zeros(B, dtype=torch.int32, device=dev)
+                self.ur = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
+                self.dep = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
+                self.matcher = ORBmatcher(nnratio, check_ori, device=dev.index)
+                self.pairs = (L.sft_pair * B)()
+                for i in range(B):
+                    p = self.pairs[i]
+                    p.kf1, p.kf2 = self.view(i), self.view(B + i)
+                    p.fv1, p.fv2 = self.fvec(i), self.fvec(B + i)
+                    for k, x in enumerate(np.asarray(F12, np.float32).reshape(9)):
+                        p.f12[k] = float(x)
+                    p.ex, p.ey = epipole
+                    p.match12 = self.m12.data_ptr() + i * cap * 4
+                    p.nmatches = self.nm.data_ptr() + i * 4
+                    p.kf1_n_dev = self.cnt.data_ptr() + i * 4
+                    p.kf2_n_dev = self.cnt.data_ptr() + (B + i) * 4
+                    p.fv1_nodes_dev = self.nodes.data_ptr() + i * 4
+                    p.fv2_nodes_dev = self.nodes.data_ptr() + (B + i) * 4
+                self.extracted = torch.cuda.Event()
+                self.matched = torch.cuda.Event()
+
+            def view(self, i):
+                v = L.frame_view()
+                v.n = 0  # read on the device from cnt[i]
+                v.keys_un = self.kps.data_ptr() + i * cap * 28
+                # left keyframes take mvuRight from ComputeStereoMatches when it runs
+                v.u_right = (self.ur.data_ptr() + i * cap * 4 if stereo and i < B
+                             else pipe.d_ur.data_ptr() + i * cap * 4)
+                v.descriptors = self.desc.data_ptr() + i * cap * 32
+                v.mp_state = pipe.d_mp.data_ptr() + i * cap
+                v.nlevels = len(pipe.d_scale)
+                v.scale_factors = pipe.d_scale.data_ptr()
+                v.level_sigma2 = pipe.d_sigma2.data_ptr()
+                v.min_x, v.max_x, v.min_y, v.max_y = 0.0, float(W), 0.0, float(H)
+                v.grid_inv_w, v.grid_inv_h = float(grid_inv[0]), float(grid_inv[1])
+                v.fx, v.fy, v.cx, v.cy, v.bf = cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["bf"]
+                v.b = float(mb)
+                return v
+
+            def fvec(self, i):
+                f = L.feature_vector()
+                f.n_nodes = pipe.node_bound  # upper bound; the count is read on the device
+                f.node_ids = self.ids.data_ptr() + i * cap * 4
+                f.offsets = self.offs.data_ptr() + i * (cap + 1) * 4
+                f.indices = self.idx.data_ptr() + i * cap * 4
+                return f
+
+        self.sets = [OutSet() for _ in range(max(1, depth))]
+        self.lib = L.lib()
+        self.stream = torch.cuda.Stream(dev)   # extraction (+ ComputeStereoMatches)
+        self.mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
+        self.counter = 0
+        self.last = None
+        # optional HIP events around the vocabulary / matching / stereo launches
+        self.event_sel = set()
+        self.events = {"k_vocab": [], "k_sft": [], "k_stereo": []}
+
+    def _ev(self, name, stream, pair):
+        import torch
+        if name in self.event_sel:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            pair.append(e)
+
+    def run(self, d_img_ptr: int, after_match=None):
+        """One sub-batch: 2B images of H x W at d_img_ptr (lefts then rights, row pitch W).
+        `after_match(o)` runs on the matching stream after SearchForTriangulation (the C4 gather).
+        Returns the output set."""
+        o = self.sets[self.counter % len(self.sets)]
+        self.counter += 1
+        B, H, W, cap = self.B, self.H, self.W, self.cap
+        s = self.stream
+        s.wait_event(o.matched)  # the matching that last read this set is done
+        self.ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
+                                      o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
+        if self.stereo:  # Frame.cc:125, on the extraction stream while the pyramids are current
+            ev = []
+            self._ev("k_stereo", s, ev)
+            self.ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
+                                                         o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
+                                                         o.ur.data_ptr(), o.dep.data_ptr(),
+                                                         stream=s.cuda_stream)
+            self._ev("k_stereo", s, ev)
+            if ev:
+                self.events["k_stereo"].append(tuple(ev))
+        o.extracted.record(s)
+        m = self.mstream
+        m.wait_event(o.extracted)
+        ev = []
+        self._ev("k_vocab", m, ev)
+        bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
+                    d_bow_n=o.bow_n.data_ptr()) if self.bow else {})
+        self.voc.transform_batch_device(self.n_img, o.desc.data_ptr(), cap * 32, o.cnt.data_ptr(),
+                                        self.levelsup, o.ids.data_ptr(), o.offs.data_ptr(),
+                                        o.idx.data_ptr(), o.nodes.data_ptr(), cap,
+                                        stream=m.cuda_stream, **bow)
+        self._ev("k_vocab", m, ev)
+        if ev:
+            self.events["k_vocab"].append(tuple(ev))
+        ev = []
+        self._ev("k_sft", m, ev)
+        L.check(self.lib.orbfe_search_for_triangulation_batch_device(
+            o.matcher._h, B, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
+            "sft batch")
+        self._ev("k_sft", m, ev)
+        if ev:
+            self.events["k_sft"].append(tuple(ev))
+        if after_match is not None:
+            after_match(o)
+        o.matched.record(m)
+        self.last = o
+        return o
+
+    def event_times(self) -> dict:
+        """{kernel: (total ms, launches)} of the recorded vocabulary / matching / stereo events."""
+        return {k: (sum(a.elapsed_time(b) for a, b in v), len(v)) for k, v in self.events.items() if v}
+
+    def clear_events(self):
+        for v in self.events.values():
+            v.clear()
+
+    def to_host(self, o=None) -> dict:
+        """Every output of a sub-batch, per image / pair, as numpy (synchronises)."""
+        import torch
+        o = o or self.last
+        torch.cuda.synchronize()
+        cap, B = self.cap, self.B
+        K = o.kps.cpu().numpy().view(L.KEYPOINT_DTYPE).reshape(self.n_img, cap)
+        D = o.desc.cpu().numpy().reshape(self.n_img, cap, 32)
+        C = o.cnt.cpu().numpy()
+        I = o.ids.cpu().numpy().view(np.uint32).reshape(self.n_img, cap)
+        OF = o.offs.cpu().numpy().reshape(self.n_img, cap + 1)
+        X = o.idx.cpu().numpy().reshape(self.n_img, cap)
+        NN = o.nodes.cpu().numpy()
+        BW = o.bow_words.cpu().numpy().view(np.uint32).reshape(self.n_img, cap)
+        BT = o.bow_weights.cpu().numpy().reshape(self.n_img, cap)
+        BN = o.bow_n.cpu().numpy()
+        M = o.m12.cpu().numpy().reshape(B, cap)
+        NM = o.nm.cpu().numpy()
+        out = {"keypoints": [], "descriptors": [], "fv": [], "bow": [], "match12": [], "nmatches": NM.copy()}
+        for i in range(self.n_img):
+            n = int(C[i])
+            out["keypoints"].append(K[i, :n].copy())
+            out["descriptors"].append(D[i, :n].copy())
+            k = int(NN[i])
+            out["fv"].append((I[i, :k].copy(), OF[i, :k + 1].copy(), X[i, :OF[i, k]].copy()))
+            nb = int(BN[i]) if self.bow else 0
+            out["bow"].append((BW[i, :nb].copy(), BT[i, :nb].copy()))
+        for p in range(B):
+            out["match12"].append(M[p, :int(C[p])].copy())
+        if self.stereo:
+            UR = o.ur.cpu().numpy().reshape(B, cap)
+            out["u_right"] = [UR[p, :int(C[p])].copy() for p in range(B)]
+        return out
+
+
+def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
+             stereo: bool = False, levelsup: int = 4):
+    """The C3 scene of bench.py: KITTI intrinsics, the KeyFrame pair geometry of a stereo
+    baseline (t2 = -0.537 m, 0.05 m forward), F12 and epipole from LocalMapping::ComputeF12, and
+    seeded KeyFrame state per keypoint slot (half the keypoints stereo, 30 % with a MapPoint).
+    Returns (pipeline, state) with state holding the host copies the oracle check needs."""
+    import torch
+    from . import synthetic as S
+    from .frames import epipole as epipole_of
+    dev = torch.device("cuda", device) if isinstance(device, int) else device
+    n_img = 2 * B
+    cap = ext.max_keypoints(H, W)
+    rng = np.random.default_rng(seed)
+    ur = np.where(rng.random((n_img, cap)) < 0.5, rng.uniform(10, W - 41, (n_img, cap)), -1.0)
+    ur = ur.astype(np.float32)
+    mp = np.where(rng.random((n_img, cap)) < 0.3, L.ORBFE_MP_OBSERVED, L.ORBFE_MP_NONE).astype(np.uint8)
+    cam = S.KITTI_CAM
+    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    F12 = S.compute_f12(t1, t2, S.intrinsics(cam))
+    scale, sigma2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+    dummy = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t1)
+    dummy2 = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t2)
+    ex, ey = epipole_of(dummy, dummy2)
+    pipe = C3Pipeline(ext, voc, tree, B, H, W, cam, F12, (ex, ey),
+                      (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
+                      torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
+                      levelsup=levelsup, stereo=stereo)
+    state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
+                 epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo)
+    return pipe, state

@@ -19,12 +19,12 @@ GEO = np.hstack([GEO, np.zeros((8, 4), np.int64)])
 def test_roofline_object():
     counts = np.full(64, 2007, np.int32)
     kt = {"k_fast": (50 * 0.25, 100)}  # 50 steps, 2 launches per step, 0.25 ms per step
-    r = bench.roofline(kt, "k_fast", GEO, counts, 13_000 * 64, 64, 50)
+    r = bench.roofline(kt, "k_fast", GEO, counts, 13_000 * 64, 64, 50)  # 50 sub-batches
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
-    assert r["launches_per_step"] == 2
-    per_step = r["algorithmic_bytes_per_step"]
+    assert r["launches_per_subbatch"] == 2
+    per_step = r["algorithmic_bytes_per_subbatch"]
     assert abs(r["achieved"] - per_step / 0.25e-3 / 1e9) < 0.05
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-5
     px = sum(int(w) * int(h) for w, h in GEO[:, :2])
@@ -45,4 +45,6 @@ def test_cli_defaults():
     finally:
         sys.argv = saved
     assert a.gpus == 1 and 0 < a.steps <= 100 and 0 <= a.warmup <= 20 and a.batch == 32
-    assert a.pipeline == 2
+    assert a.pipeline == 2 and a.input_batches >= 4 and a.vocab_levels == 6 and a.levelsup == 4
+    # a step is long enough to be seen (>= 1024 sub-batches of 32 stereo frames)
+    assert a.batches_per_step * a.batch >= 32 * 1024

@@ -1,0 +1,57 @@
+"""The exact sequence bench.py times (orb_slam2_2021_amd.pipeline.C3Pipeline, config C3):
+extract_batch_device on 2B = 64 images -> vocabulary transform_batch_device (ORBvoc-shaped
+k=10/L=6 tree, levelsup 4, BowVector + FeatureVector) -> search_for_triangulation_batch_device
+with device-side counts (kf*_n_dev / fv*_nodes_dev), two output sets in flight -- every image's
+keypoints, descriptors, BowVector and FeatureVector and every pair's match12 against the oracle
+chain (oracle/c3_check.py)."""
+import numpy as np
+import pytest
+
+from orb_slam2_2021_amd import ORBextractor, synth_frame
+from orb_slam2_2021_amd import synthetic as S
+from orb_slam2_2021_amd.pipeline import build_c3
+from orb_slam2_2021_amd.vocabulary import ORBVocabulary
+from oracle.c3_check import check_c3
+from oracle.orbref import RefVocabulary
+
+pytestmark = pytest.mark.gpu
+
+H, W = 376, 1241
+
+
+@pytest.fixture(scope="module")
+def vocab():
+    tree = S.Vocabulary.synthetic_orbvoc()
+    ref = RefVocabulary.from_table(tree.k, tree.levels, tree.scoring, tree.weighting, tree.parent,
+                                   tree.is_leaf, tree.descriptors, tree.weights)
+    return tree, ORBVocabulary.from_tree(tree), ref
+
+
+def frames(B, base):
+    imgs = np.zeros((2 * B, H, W), np.uint8)
+    for i in range(B):
+        imgs[i], imgs[B + i] = synth_frame(base + i, H, W, right=True)
+    return imgs
+
+
+@pytest.mark.parametrize("stereo", [False, True])
+def test_c3_batch32_bit_exact(require_gpu, vocab, stereo):
+    import torch
+    tree, voc, ref = vocab
+    B = 32
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    pipe, st = build_c3(ext, tree, voc, B, H, W, 0, stereo=stereo)
+    batches = [frames(B, 0), frames(B, 1000)]
+    d = [torch.from_numpy(b).to("cuda") for b in batches]
+    # four sub-batches through both output sets; check the last one of each input batch
+    for j in range(4):
+        pipe.run(d[j % 2].data_ptr())
+    out_b = pipe.to_host(pipe.sets[1])  # sub-batch 3: batch 1
+    out_a = pipe.to_host(pipe.sets[0])  # sub-batch 2: batch 0
+    for imgs, out in ((batches[0], out_a), (batches[1], out_b)):
+        r = check_c3(imgs, out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"], st["cam"],
+                     st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"])
+        assert r["all"], r
+        assert min(len(k) for k in out["keypoints"]) >= 2000
+        assert int(np.sum(out["nmatches"])) > 32 * 50
+        assert all(len(b[0]) > 100 for b in out["bow"])

@@ -89,3 +89,27 @@ def test_empty_local_map(require_gpu):
     assert (nm, nv, len(best)) == (0, 0, 0)
     nv, _ = m.isInFrustum(F, G)
     assert nv == 0
+
+
+@pytest.mark.parametrize("idx", [100, 101, 102])
+def test_c5_50k_long_claim_chains_continue_rounds(require_gpu, idx):
+    """BASELINE config C5's size (640x480, 50k MapPoints) with the map built around another frame:
+    claim chains longer than the first launch's 12 rounds. The fixpoint continues in more rounds
+    (no serial walk) and stays bit-exact."""
+    ext = ORBextractor(2000, 1.2, 8, 12, 7)
+    sc, s2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+    k0, d0 = ext(synth_frame(7, 480, 640))
+    rng = np.random.default_rng(0x50C0DE)
+    F0 = S.make_frame(k0, d0, sc, s2, 480, 640, S.ARDUCAM_CAM, rng, mp_frac=0.0, tcw=S.pose(tx=0.1, yaw=0.02))
+    G = S.make_local_map(F0, 50000, rng)
+    k, d = ext(synth_frame(idx, 480, 640))
+    F = S.Frame(keys_un=k, descriptors=d, u_right=np.full(len(k), -1.0, np.float32),
+                mp_state=np.zeros(len(k), np.uint8), scale_factors=sc, level_sigma2=s2, min_x=0.0,
+                max_x=640.0, min_y=0.0, max_y=480.0, tcw=S.pose(tx=0.102, yaw=0.021), **S.ARDUCAM_CAM)
+    m = ORBmatcher(0.8, True)
+    nm, best, nv, lm = m.SearchLocalPoints(F, G, 3.0)
+    rounds, serial = m.last_stats()
+    wnm, wbest, wnv, want = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8)
+    assert (nm, nv) == (wnm, wnv)
+    assert np.array_equal(best, wbest)
+    assert serial == 0, f"serial walk after {rounds} rounds"

@@ -11,7 +11,7 @@ from conftest import gpu_available
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = ["orbfe.h", "orbfe_match_batch.h", "orbfe_debug.h", "orbfe_synth.h", "orbfe_vocab.h", "orbfe_frustum.h",
-           "orbfe_stereo.h"]
+           "orbfe_stereo.h", "orbfe_keyframe.h", "orbfe_pack.h"]
 
 
 def declared_functions():
