@@ -73,6 +73,9 @@ def parse(argv=None):
                         "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
     p.add_argument("--banded-pyramid", action="store_true",
                    help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
+    p.add_argument("--rehearse", action="store_true",
+                   help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
+                        "orchestration on a one-GPU box (not a measurement)")
     return p.parse_args(argv)
 
 
@@ -97,14 +100,15 @@ class Gatherer:
     payloads) happens after sub-batch i+1 is enqueued, so the host's wait on the sizes never
     starves the extraction stream."""
 
-    def __init__(self, pipe, world, rank, dev):
+    def __init__(self, pipe, world, rank, dev, comm_dev):
         import torch
         from orb_slam2_2021_amd.parallel import packed_bytes
         self.pipe, self.world, self.rank = pipe, world, rank
+        self.comm_dev = comm_dev  # the payload's device for the exchange (host only in --rehearse)
         self.cap_bytes = packed_bytes(pipe.n_img, pipe.n_img * pipe.cap)
         self.bufs = {id(o): torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for o in pipe.sets}
         self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
-        self.recv = ([torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+        self.recv = ([torch.empty(self.cap_bytes, dtype=torch.uint8, device=comm_dev) for _ in range(world)]
                      if rank == 0 else None)
         self.pending = None
         self.bytes_received = 0
@@ -128,7 +132,11 @@ class Gatherer:
         import torch
         from orb_slam2_2021_amd.parallel import gather_packed
         with torch.cuda.stream(self.pipe.mstream):
-            out, sizes = gather_packed(self.bufs[id(o)], self.sizes[id(o)], dst=0, recv=self.recv)
+            if self.comm_dev.type == "cpu":  # --rehearse: gloo, staged through the host
+                self.pipe.mstream.synchronize()
+                out, sizes = gather_packed(self.bufs[id(o)].cpu(), self.sizes[id(o)].cpu(), dst=0, recv=self.recv)
+            else:
+                out, sizes = gather_packed(self.bufs[id(o)], self.sizes[id(o)], dst=0, recv=self.recv)
         if self.rank == 0:
             self.bytes_received += sum(sizes[1:])
             self.transfers += len(sizes) - 1
@@ -154,13 +162,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
-    if world > 1:
+    if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        assert dist.get_world_size() == args.gpus
     else:
         torch.cuda.set_device(0)
+    if world > 1:
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", torch.cuda.current_device())
+    comm_dev = torch.device("cpu") if args.rehearse else dev  # tensors of the small collectives
 
     from orb_slam2_2021_amd import ORBextractor, synth_frame
     from orb_slam2_2021_amd import synthetic as S
@@ -186,7 +199,7 @@ def main():
     pipe, state = build_c3(ext, tree, voc, B, H, W, dev, seed=1234 + rank, depth=max(1, args.pipeline),
                            stereo=args.stereo, levelsup=args.levelsup)
     gather = world > 1 and not args.no_gather
-    g = Gatherer(pipe, world, rank, dev) if gather else None
+    g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
     counter = [0]
 
     def sub_batch():
@@ -260,7 +273,7 @@ def main():
     timed = {k: v for k, v in timed.items() if v[1] > 0}
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -334,7 +347,7 @@ def main():
                      stereo=args.stereo, mb=state["mb"])
         ok = bool(r["all"])
         if world > 1:
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             ok = bool(t.item())
         out["parity_bit_exact"] = ok
@@ -342,8 +355,10 @@ def main():
         out["parity"]["what"] = ("last timed sub-batch of every rank vs the oracle chain (extract, "
                                  "vocabulary transform, SearchForTriangulation): keypoints, descriptors, "
                                  "BowVector, FeatureVector, match12")
+    if args.rehearse:
+        out["rehearsal"] = "N ranks on one GPU over gloo, host-staged: not a measurement"
     if world > 1 and not args.no_legs:
-        out["legs"] = {"c5_search_local_points": c5_leg(args, world, rank, dev)}
+        out["legs"] = {"c5_search_local_points": c5_leg(args, world, rank, comm_dev)}
     if rank == 0 and world == 1:
         out["host_boundary"] = host_boundary_rate(ext, host[0])
         if not args.no_legs:
@@ -546,7 +561,7 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
     if world > 1:  # the replicated SoA: rank 0's map broadcast to every rank
         import torch.distributed as dist
         arrs = {f: np.ascontiguousarray(getattr(G, f)) for f in fields}
-        got = broadcast_arrays(arrs, dev, src=0)
+        got = broadcast_arrays(arrs, dev, src=0)  # dev: the rank's GPU (host in --rehearse)
         G = MapPointGeometry(**{f: got[f].cpu().numpy().view(arrs[f].dtype).reshape(arrs[f].shape)
                                 for f in fields})
     n_total = world * frames_per_rank
