@@ -31,6 +31,8 @@ int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
 /* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the
  * rest in one launch after the resize chain (k <= 0: the default, level 0 only). */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
+/* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
+int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe
  * computes them (a port of glibc's cosf / sinf), for the float degree values with bit patterns
  * deg_bits_begin .. deg_bits_begin + n - 1, into device buffers (NULL stream = default stream;

@@ -2863,6 +2863,12 @@ extern "C" int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k) {
   return ORBFE_OK;
 }
 
+extern "C" int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16) {
+  if (!h || !umax16) return ORBFE_ERR_ARG;
+  for (int v = 0; v < 16; v++) umax16[v] = h->umax[v];
+  return ORBFE_OK;
+}
+
 extern "C" int orbfe_debug_force_level_launches(orbfe_extractor* h, int on) {
   if (!h) return ORBFE_ERR_ARG;
   h->force_level_launches = on ? 1 : 0;

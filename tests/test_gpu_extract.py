@@ -155,3 +155,14 @@ def test_candidate_total_matches_per_level_lists(require_gpu):
     ext.extract_batch(imgs)
     want = sum(len(ext.debug_candidates(l, image=i)) for i in range(3) for l in range(8))
     assert ext.debug_candidate_total() == want > 0
+
+
+def test_library_umax_equals_oracle(require_gpu):
+    """liborbfe's IC_Angle circle table = the oracle's (pinned to ORBextractor.cc:457-472 by
+    tests/test_reference_pins.py)."""
+    from orb_slam2_2021_amd import _lib as L
+    from oracle.orbref import RefExtractor
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    u = np.zeros(16, np.int32)
+    L.check(L.lib().orbfe_debug_get_umax(ext._h, L.ptr(u)), "get_umax")
+    assert u.tolist() == RefExtractor(2000, 1.2, 8, 20, 7).tables()["umax"].tolist()

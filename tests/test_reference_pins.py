@@ -1,0 +1,116 @@
+"""Pins the tables and constants the oracle and liborbfe share to the reference's own source text
+(read as text from /root/reference; skipped where it is absent, e.g. on the GPU box):
+
+* bit_pattern_31_ (ORBextractor.cc:153-411) == orb_pattern31.inc, the table both the oracle and
+  the HIP kernels compile;
+* umax (ORBextractor.cc:457-472): the formula lines are the ones restated, evaluated here from the
+  reference's HALF_PATCH_SIZE, and equal to the oracle's table (the library's is compared with the
+  oracle's in test_gpu_extract.py);
+* PATCH_SIZE / HALF_PATCH_SIZE / EDGE_THRESHOLD (ORBextractor.cc:71-73) == the oracle's constants;
+* TH_HIGH / TH_LOW / HISTO_LENGTH (ORBmatcher.cc:37-39) == the oracle's, the HIP matchers' and
+  the Python mirror's.
+CPU only; nothing is compiled or run from the reference."""
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import orbref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference/src"
+
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference sources not present")
+
+
+def _strip_comments(s):
+    s = re.sub(r"/\*.*?\*/", " ", s, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", s)
+
+
+def _ref(name):
+    with open(os.path.join(REF, name)) as f:
+        return f.read()
+
+
+def _ints(body):
+    return [int(v) for v in re.findall(r"-?\d+", body)]
+
+
+def reference_pattern():
+    src = _strip_comments(_ref("ORBextractor.cc"))
+    m = re.search(r"bit_pattern_31_\s*\[\s*256\s*\*\s*4\s*\]\s*=\s*\{(.*?)\}\s*;", src, flags=re.S)
+    assert m, "bit_pattern_31_ not found"
+    return _ints(m.group(1))
+
+
+def repo_pattern():
+    src = open(os.path.join(ROOT, "orb_slam2_2021_amd", "csrc", "orb_pattern31.inc")).read()
+    body = _strip_comments(src).split("{", 1)[1].split("}", 1)[0]
+    return _ints(body)
+
+
+def test_pattern_equals_reference_text():
+    ref = reference_pattern()
+    assert len(ref) == 1024
+    assert repo_pattern() == ref
+
+
+def _ref_const(src, name):
+    m = re.search(r"const\s+int\s+(?:ORBmatcher::)?" + name + r"\s*=\s*(-?\d+)\s*;", src)
+    assert m, name
+    return int(m.group(1))
+
+
+def test_patch_constants_equal_reference_text():
+    src = _strip_comments(_ref("ORBextractor.cc"))
+    ref = {k: _ref_const(src, k) for k in ("PATCH_SIZE", "HALF_PATCH_SIZE", "EDGE_THRESHOLD")}
+    assert ref == {"PATCH_SIZE": 31, "HALF_PATCH_SIZE": 15, "EDGE_THRESHOLD": 19}
+    osrc = open(os.path.join(ROOT, "oracle", "orbref.cpp")).read()
+    mine = {k: int(re.search(r"const int " + k + r" = (\d+);", osrc).group(1))
+            for k in ("kPatchSize", "kHalfPatch", "kEdgeThreshold")}
+    assert (mine["kPatchSize"], mine["kHalfPatch"], mine["kEdgeThreshold"]) == \
+        (ref["PATCH_SIZE"], ref["HALF_PATCH_SIZE"], ref["EDGE_THRESHOLD"])
+
+
+def test_umax_formula_and_table_equal_reference():
+    src = _strip_comments(_ref("ORBextractor.cc"))
+    norm = re.sub(r"\s+", "", src)
+    # the lines restated by oracle/orbref.cpp and orbfe_extract.hip
+    for piece in ("vmax=cvFloor(HALF_PATCH_SIZE*sqrt(2.f)/2+1)",
+                  "intvmin=cvCeil(HALF_PATCH_SIZE*sqrt(2.f)/2)",
+                  "constdoublehp2=HALF_PATCH_SIZE*HALF_PATCH_SIZE",
+                  "for(v=0;v<=vmax;++v)umax[v]=cvRound(sqrt(hp2-v*v));",
+                  "for(v=HALF_PATCH_SIZE,v0=0;v>=vmin;--v){while(umax[v0]==umax[v0+1])++v0;umax[v]=v0;++v0;}"):
+        assert piece in norm, piece
+    hp = _ref_const(src, "HALF_PATCH_SIZE")
+    f = np.float32(hp) * np.float32(math.sqrt(2.0)) / np.float32(2)  # float arithmetic (sqrt(2.f))
+    vmax, vmin = math.floor(f + np.float32(1)), math.ceil(f)
+    umax = [0] * (hp + 1)
+    for v in range(vmax + 1):
+        umax[v] = int(np.rint(math.sqrt(hp * hp - v * v)))  # cvRound: half to even
+    v0 = 0
+    for v in range(hp, vmin - 1, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    t = orbref.RefExtractor(2000, 1.2, 8, 20, 7).tables()
+    assert t["umax"].tolist() == umax
+
+
+def test_matcher_thresholds_equal_reference_text():
+    src = _strip_comments(_ref("ORBmatcher.cc"))
+    ref = {k: _ref_const(src, k) for k in ("TH_HIGH", "TH_LOW", "HISTO_LENGTH")}
+    assert ref == {"TH_HIGH": 100, "TH_LOW": 50, "HISTO_LENGTH": 30}
+    o = open(os.path.join(ROOT, "oracle", "orbref_match.h")).read()
+    assert re.search(r"TH_HIGH = (\d+), TH_LOW = (\d+), HISTO_LENGTH = (\d+)", o).groups() == \
+        (str(ref["TH_HIGH"]), str(ref["TH_LOW"]), str(ref["HISTO_LENGTH"]))
+    h = open(os.path.join(ROOT, "orb_slam2_2021_amd", "csrc", "orbfe_match_internal.h")).read()
+    for k, v in ref.items():
+        assert re.search(r"#define " + k + r" (\d+)", h).group(1) == str(v), k
+    from orb_slam2_2021_amd import ORBmatcher
+    assert (ORBmatcher.TH_HIGH, ORBmatcher.TH_LOW, ORBmatcher.HISTO_LENGTH) == \
+        (ref["TH_HIGH"], ref["TH_LOW"], ref["HISTO_LENGTH"])
