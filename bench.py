@@ -71,8 +71,8 @@ def parse(argv=None):
     p.add_argument("--stereo", action="store_true",
                    help="run Frame::ComputeStereoMatches on every pair after extraction (the stereo "
                         "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
-    p.add_argument("--banded-pyramid", action="store_true",
-                   help="one banded k_pyramid launch instead of per-level k_resize (comparison)")
+    p.add_argument("--level-launches", action="store_true",
+                   help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
@@ -192,8 +192,8 @@ def main():
             host[j, i], host[j, B + i] = synth_frame(idx, H, W, right=True)
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
-    if args.banded_pyramid:
-        ext.debug_force_level_launches(False)
+    if args.level_launches:
+        ext.debug_force_level_launches(True)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
     pipe, state = build_c3(ext, tree, voc, B, H, W, dev, seed=1234 + rank, depth=max(1, args.pipeline),

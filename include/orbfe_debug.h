@@ -25,11 +25,12 @@ int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, 
 /* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
  * global-memory path for every level; < 0 restores the automatic size). */
 int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
-/* 1 (default): build the pyramid with one k_resize launch per level; 0: one banded k_pyramid
- * launch when its row bands fit in LDS (currently slower on MI355X; kept for comparison). */
+/* 0 (default): build the pyramid with the tiled k_pyramid launches (groups of levels, no
+ * k_copy0) when the geometry allows; 1: k_copy0 + one k_resize launch per level. */
 int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
-/* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the
- * rest in one launch after the resize chain (k <= 0: the default, level 0 only). */
+/* Per-level pyramid path only: FAST of levels 0..k-1 on the side stream, each launched as soon
+ * as its level is built, the rest in one launch after the resize chain (k <= 0: the default,
+ * level 0 only). The tiled path runs the first group's levels on the side stream. */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);

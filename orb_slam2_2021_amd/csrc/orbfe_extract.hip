@@ -27,9 +27,11 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/orbfe.h"
@@ -104,13 +106,16 @@ struct ExtractArgs {
   uint8_t* out_desc;
   int32_t* out_counts;
   int out_cap;
-  int ini_th, min_th, tlow;
+  int ini_th, min_th;
   int roi_w_max, roi_h_max;
   int node_cap, sort_cap, scan_cap, key_lds_cap;
-  const int4* band_rows;  // k_pyramid: per (band, level) {own0, own1, comp0, comp1}
+  const int4* pyr_xt;     // k_pyramid: per (tile column, level) {own0, own1, comp0, comp1}
+  const int4* pyr_yt;     // k_pyramid: per (tile row, level) {own0, own1, comp0, comp1}
+  const int2* pyr_blob;   // k_pyramid: per tile column / row {blob start, blob dwords}
+  const uint32_t* pyr_xblob;  // k_pyramid: resize tap records per tile column
+  const uint32_t* pyr_yblob;  // k_pyramid: ytab rows per tile row
   const uint4* rgrp;      // k_resize: per 4-column group {sel[4]}, {alpha[4]} (2 x uint4)
   const int* rgx0;        // k_resize: first source column of each group
-  int nbands, band_buf;   // bands per image, bytes per LDS row buffer
   int umax[16];
   AtanConsts atan;
   float factor_pi;
@@ -222,7 +227,7 @@ __device__ __forceinline__ void store_row4(uint8_t* row, int x, int w, uint32_t 
 
 // ---------------------------------------------------------------------------------------------
 // k_resize: level l from level l-1 (ComputePyramid, ORBextractor.cc:1105-1135), one launch per
-// level -- the fallback of k_pyramid for geometries whose row bands do not fit in LDS.
+// level -- the fallback of k_pyramid for scale factors whose taps do not fit an 8-byte window.
 #define RESIZE_ROWS 8  // output rows per thread (the column taps are loaded once)
 __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
   const LevelDesc ld = a.levels[l];
@@ -267,6 +272,57 @@ __device__ __forceinline__ int dot2_u16(uint32_t a, uint32_t b) {
   return (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), 0u, false);
 }
 
+// bits 32..47 of the 48-bit product of two 24-bit values (v_mul_hi_u32_u24, full rate)
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// One output row of the 4-column group at x of level ld from the 8-byte windows (W0, W1) of its
+// two source rows. Horizontal taps: one v_perm + one v_dot2_u32_u16 per pixel and source row with
+// the alphas premultiplied by 16 (a16 <= 32768 still fits a u16 half), so H = 16 h and
+// H & ~0xff = (h >> 4) << 8. OpenCV's SIMD128 vertical rounding (VResizeLinearVec_32s8u, whose
+// saturations never bind here) ((h >> 4) * b) >> 16 is then one full-rate v_mul_hi_u32_u24 of
+// (H & ~0xff) and b << 8 (both < 2^24; bits 32..47 of the product). Columns at or past simd_end
+// take FixedPtCast<int, uchar, 22> on h = H >> 4 (TAIL: groups reaching simd_end).
+template <bool TAIL>
+__device__ __forceinline__ uint32_t resize_win_row(const uint32_t W0r0, const uint32_t W1r0, const uint32_t W0r1,
+                                                   const uint32_t W1r1, const uint4 sel, const uint4 alp16,
+                                                   int x, const LevelDesc& ld, int2 yt) {
+  const uint32_t b0 = yt.y & 0xffffu, b1 = (uint32_t)yt.y >> 16;
+  const uint32_t sels[4] = {sel.x, sel.y, sel.z, sel.w}, alps[4] = {alp16.x, alp16.y, alp16.z, alp16.w};
+  uint32_t H0[4], H1[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    H0[k] = (uint32_t)dot2_u16(__builtin_amdgcn_perm(W1r0, W0r0, sels[k]), alps[k]);
+    H1[k] = (uint32_t)dot2_u16(__builtin_amdgcn_perm(W1r1, W0r1, sels[k]), alps[k]);
+  }
+  uint32_t packed = 0;
+  if constexpr (!TAIL) {  // every column below simd_end: the SIMD128 rounding only
+    const uint32_t B0 = b0 << 8, B1 = b1 << 8;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t m0 = mulhi_u24(H0[k] & 0xffff00u, B0);
+      const uint32_t m1 = mulhi_u24(H1[k] & 0xffff00u, B1);
+      packed |= ((m0 + m1 + 2u) >> 2) << (8 * k);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int h0 = (int)(H0[k] >> 4), h1 = (int)(H1[k] >> 4);
+      int v;
+      if (x + k < ld.simd_end) {
+        v = ((((h0 >> 4) * (int)b0) >> 16) + (((h1 >> 4) * (int)b1) >> 16) + 2) >> 2;
+      } else {
+        v = min(max((h0 * (int)b0 + h1 * (int)b1 + (1 << 21)) >> 22, 0), 255);
+      }
+      packed |= (uint32_t)v << (8 * k);
+    }
+  }
+  return packed;
+}
+
 __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
   const LevelDesc ld = a.levels[l];
   const int g = blockIdx.x * 64 + threadIdx.x, x = 4 * g;
@@ -277,7 +333,7 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
   const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ls.pyr_off;
   const int gi = ld.rgrp_begin + g;
   const int sx0 = a.rgx0[gi];
-  const uint4 sel = a.rgrp[2 * gi], alp = a.rgrp[2 * gi + 1];
+  const uint4 sel = a.rgrp[2 * gi], alp16 = a.rgrp[2 * gi + 1];
   const bool two = y0 + 1 < ld.h;
   const int2 ya = a.ytab[ld.tab_y + y0], yb = a.ytab[ld.tab_y + (two ? y0 + 1 : y0)];
   int rows[4] = {ya.x, ya.x + 1, yb.x, yb.x + 1};
@@ -285,7 +341,7 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(
-        src + (long long)min(max(rows[r], 0), ls.h - 1) * ls.pitch + (sx0 & ~3));
+        src + __umul24((uint32_t)min(max(rows[r], 0), ls.h - 1), (uint32_t)ls.pitch) + (sx0 & ~3));
 #pragma unroll
     for (int k = 0; k < 3; k++) wv[r][k] = p[k];
   }
@@ -296,32 +352,22 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
     W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
     W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
   }
-  const uint32_t sels[4] = {sel.x, sel.y, sel.z, sel.w}, alps[4] = {alp.x, alp.y, alp.z, alp.w};
-  uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-#pragma unroll
-  for (int o = 0; o < 2; o++) {
-    if (o == 1 && !two) break;
-    const int2 yt = o ? yb : ya;
-    const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int h0 = dot2_u16(__builtin_amdgcn_perm(W1[2 * o], W0[2 * o], sels[k]), alps[k]);
-      const int h1 = dot2_u16(__builtin_amdgcn_perm(W1[2 * o + 1], W0[2 * o + 1], sels[k]), alps[k]);
-      int v;
-      if (x + k < ld.simd_end) {  // VResizeLinearVec_32s8u; its saturations never bind here
-        v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
-      } else {  // FixedPtCast<int, uchar, 22>
-        v = min(max((h0 * b0 + h1 * b1 + (1 << 21)) >> 22, 0), 255);
-      }
-      packed |= (uint32_t)v << (8 * k);
-    }
-    store_row4(out + (long long)(y0 + o) * ld.pitch, x, ld.w, packed);
+  uint32_t pa, pb;
+  if (x + 4 <= ld.simd_end) {  // every column on the SIMD128 rounding (all but a row's tail)
+    pa = resize_win_row<false>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ya);
+    pb = resize_win_row<false>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, yb);
+  } else {
+    pa = resize_win_row<true>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ya);
+    pb = resize_win_row<true>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, yb);
   }
+  uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
+  store_row4(out + __umul24((uint32_t)y0, (uint32_t)ld.pitch), x, ld.w, pa);
+  if (two) store_row4(out + __umul24((uint32_t)(y0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
 }
 
+
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
-// padding columns) -- the fallback path's level 0; k_pyramid does this itself.
+// padding columns) -- the per-level path's level 0; k_pyramid's first group does this itself.
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
   // 16 columns per thread: 5 aligned dword loads + v_alignbyte (the caller's pitch need not be a
   // multiple of 4), one 16-byte store; byte loads only for the last columns of a row
@@ -355,72 +401,185 @@ __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_pyramid: the whole of ComputePyramid (ORBextractor.cc:1105-1135) plus the level-0 copy in one
-// launch. Workgroup (band, image) owns a horizontal band of rows at every level and computes the
-// rows it needs -- its own rows plus the halo rows the next level's bilinear taps reach, which
-// neighbouring bands also compute (identical bytes) -- level by level from the input image, with
-// the working rows of consecutive levels ping-ponged in LDS. Only own rows go to HBM. Host table
-// band_rows[band][level] = {own0, own1, comp0, comp1}.
-__global__ __launch_bounds__(256) void k_pyramid(ExtractArgs a) {
+// k_pyramid: ComputePyramid (ORBextractor.cc:1105-1135) as a few launches of 2-D tiles, each
+// building a group of consecutive levels src+1..top from level src (the caller's image for the
+// first group, whose tiles also write level 0 into the padded pyramid block: k_copy0's job).
+// A workgroup owns one tile of the group's top level and the matching (4-column aligned) piece
+// of every lower level; it loads the source region its cone of bilinear taps reaches into LDS
+// and computes each level's region -- its own piece plus the halo the next level reads, which
+// neighbouring tiles compute too (identical bytes) -- from the previous level's region in LDS,
+// writing only its own pieces to HBM. No dependency between workgroups; every level stays the
+// uint8 rounding of the level below, exactly the reference chain. Host tables per (tile column,
+// level) and (tile row, level): {own0, own1, comp0, comp1}, comp x bounds multiples of 4; per
+// tile column a blob of the resize taps of its 4-column groups (12 dwords: first source column,
+// 4 selectors, 4 alphas) level after level, per tile row a blob of its ytab rows. Every global
+// load of a workgroup (blobs, source region) is issued up front; the levels then run from LDS.
+struct PyrGroup {
+  int src, top;      // source level and top level of the group
+  int ntx, nty;      // tiles of the top level
+  int tx_off, ty_off;  // pyr_xt / pyr_yt index of tile (0, level src)
+  int bx_off, by_off;  // pyr_blob index of tile column 0 / tile row 0
+  int buf0, buf1;    // LDS bytes of the two ping-pong region buffers
+  int tab;           // LDS bytes of the staged blobs
+  int dbg;           // experiment switches (0 in production)
+};
+#define PYR_REC 12   // dwords per 4-column group record
+
+// LDS row pitch of a region with comp x bounds [c0, c1): the 12-byte window of the last
+// 4-column group may run 11 bytes past the region
+__host__ __device__ __forceinline__ int pyr_lds_pitch(int c0, int c1) { return c1 - c0 + 12; }
+
+
+typedef __attribute__((address_space(1))) const uint32_t global_u32;  // global_load, not flat_load
+// i / n as __umulhi(i, ceil(2^32 / n)), exact for i * n < 2^32; n == 1 has no 32-bit magic
+// (magic 0 marks it)
+__device__ __forceinline__ uint32_t magic_div(uint32_t n) { return n <= 1 ? 0u : (uint32_t)((0x100000000ull + n - 1) / n); }
+__device__ __forceinline__ int div_magic(int i, uint32_t m) { return m ? (int)__umulhi((uint32_t)i, m) : i; }
+
+// Own piece of level ld (rows oy.x..oy.y, columns ox.x..ox.y) from its LDS region (comp origin
+// (cx.z, cy.z), pitch P) to the padded pyramid block, one dword per item. Tiles on the image
+// edges also write the REFLECT_101 columns -3..-1 (dword -4..-1) and w..w+2 (in the dwords up to
+// column w+2) that k_blur reads; bytes past w+2 are never read.
+__device__ __forceinline__ void pyr_copy_own(const uint8_t* reg, int P, int4 ox, int4 oy, int cx0, int cy0,
+                                             const LevelDesc& ld, uint8_t* out, int t) {
+  const int w = ld.w;
+  const int d0 = ox.x == 0 ? -1 : ox.x >> 2;
+  const int d1 = ox.y == w ? ((w + 2) >> 2) + 1 : ox.y >> 2;
+  const int nd = d1 - d0, items = nd * (oy.y - oy.x);
+  const uint32_t m = magic_div((uint32_t)nd);
+  for (int i = t; i < items; i += 256) {
+    const int r = div_magic(i, m), x = 4 * (d0 + i - r * nd), y = oy.x + r;
+    const uint8_t* row = reg + __umul24((uint32_t)(y - cy0), (uint32_t)P);
+    uint32_t v;
+    if (x >= 0 && x + 4 <= w) {
+      v = *reinterpret_cast<const uint32_t*>(row + x - cx0);
+    } else {
+      v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int c = x + j, sc = c < 0 ? -c : (c >= w ? 2 * w - 2 - c : c);
+        if (c >= -3 && c <= w + 2) v |= (uint32_t)row[sc - cx0] << (8 * j);
+      }
+    }
+    *reinterpret_cast<uint32_t*>(out + (long long)y * ld.pitch + x) = v;
+  }
+}
+
+#define PYR_LOADS 8  // source-region dwords in flight per thread
+__global__ __launch_bounds__(256) void k_pyramid(ExtractArgs a, PyrGroup g) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int2 blk = xcd_block2d();
-  const int band = blk.x, img = blk.y, t = threadIdx.x;
-  uint8_t* bufs[2] = {smem, smem + a.band_buf};
-  int2* xt_lds = reinterpret_cast<int2*>(smem + 2 * a.band_buf);
-  const int4* br = a.band_rows + band * a.nlevels;
-  const uint8_t* in = a.img0 + (long long)img * a.img_stride;
-  // level 0: own rows of the caller's image -> the padded pyramid block (was k_copy0)
+  const int img = blk.y, tyi = blk.x / g.ntx, txi = blk.x - tyi * g.ntx;
+  const int t = threadIdx.x, NL = g.top - g.src + 1;
+  const int4* XT = a.pyr_xt + g.tx_off + txi * NL;
+  const int4* YT = a.pyr_yt + g.ty_off + tyi * NL;
+  uint32_t* const tabs = reinterpret_cast<uint32_t*>(smem + g.buf0 + g.buf1);
+  const int2 bx = a.pyr_blob[g.bx_off + txi], by = a.pyr_blob[g.by_off + tyi];
+  uint8_t* const pyr = a.pyr + (long long)img * a.pyr_stride;
+  // 1. blobs and the source level's region -> LDS; all loads of a thread in flight together
   {
-    const LevelDesc ld = a.levels[0];
-    const int4 r = br[0];
-    const int G = (ld.w + 3) >> 2;
-    const uint32_t gm = (uint32_t)((0x100000000ull + G - 1) / G);
-    const int items = (r.y - r.x) * G;
-    uint8_t* base = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-    for (int i = t; i < items; i += 256) {
-      const int ry = (int)__umulhi((uint32_t)i, gm), x = 4 * (i - ry * G), y = r.x + ry;
-      const uint8_t* src = in + (long long)y * a.img_pitch + x;
-      const int n = min(4, ld.w - x);
-      uint32_t v = 0;
-      for (int k = 0; k < n; k++) v |= (uint32_t)src[k] << (8 * k);
-      store_row4(base + (long long)y * ld.pitch, x, ld.w, v);
+    const int4 cx = XT[0], cy = YT[0];
+    const LevelDesc ls = a.levels[g.src];
+    const int nt = bx.y + by.y;
+    uint32_t tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = t + 256 * k;
+      tv[k] = i < bx.y ? a.pyr_xblob[bx.x + i] : (i < nt ? a.pyr_yblob[by.x + i - bx.y] : 0u);
     }
+    for (int i = t + 1024; i < nt; i += 256) tabs[i] = i < bx.y ? a.pyr_xblob[bx.x + i] : a.pyr_yblob[by.x + i - bx.y];
+    const int P = pyr_lds_pitch(cx.z, cx.w), G = (cx.w - cx.z) >> 2, items = G * (cy.w - cy.z);
+    const uint32_t gm = magic_div((uint32_t)G);
+    const uint8_t* in = g.src == 0 ? a.img0 + (long long)img * a.img_stride : pyr + ls.pyr_off;
+    const long long ipitch = g.src == 0 ? a.img_pitch : ls.pitch;
+    for (int i0 = 0; i0 < items; i0 += 256 * PYR_LOADS) {
+      uint32_t v[PYR_LOADS];
+#pragma unroll
+      for (int k = 0; k < PYR_LOADS; k++) {
+        const int i = min(i0 + t + 256 * k, items - 1);
+        const int r = div_magic(i, gm), x = cx.z + 4 * (i - r * G);
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(in + (long long)(cy.z + r) * ipitch + x);
+        // the aligned dwords holding bytes x..x+3 (any caller pitch); the second only when it
+        // holds a byte of the row, so nothing past the caller's buffer is touched
+        const global_u32* q = (const global_u32*)(pa & ~(uintptr_t)3);
+        const int sh = (int)(pa & 3);
+        if (g.dbg & 4) { v[k] = pa; continue; }
+        const uint32_t w0 = q[0], w1 = (sh != 0 && x - sh + 4 < ls.w) ? q[1] : 0u;
+        v[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+      }
+#pragma unroll
+      for (int k = 0; k < PYR_LOADS; k++) {
+        const int i = i0 + t + 256 * k;
+        if (i < items) {
+          const int r = div_magic(i, gm);
+          *reinterpret_cast<uint32_t*>(smem + __umul24((uint32_t)r, (uint32_t)P) + 4 * (i - r * G)) = v[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (t + 256 * k < nt) tabs[t + 256 * k] = tv[k];
+    __syncthreads();
+    if (g.src == 0 && !(g.dbg & 2)) pyr_copy_own(smem, P, cx, cy, cx.z, cy.z, ls, pyr + ls.pyr_off, t);
   }
-  for (int l = 1; l < a.nlevels; l++) {
-    const LevelDesc ld = a.levels[l], ls = a.levels[l - 1];
-    const int4 r = br[l];
-    for (int i = t; i < ld.w; i += 256) xt_lds[i] = a.xtab[ld.tab_x + i];
-    __syncthreads();
-    // source rows: the input image for level 1, else the previous level's band in LDS
-    const uint8_t* src;
-    long long spitch;
-    int sbase;
-    if (l == 1) {
-      src = in;
-      spitch = a.img_pitch;
-      sbase = 0;
-    } else {
-      src = bufs[(l - 1) & 1];
-      spitch = (ls.w + 3) & ~3;
-      sbase = br[l - 1].z;
+  if (g.dbg & 1) return;
+  // 2. levels src+1..top, each from the previous level's region in LDS into its own region
+  //    buffer, then (after the barrier) its own piece to HBM
+  int xo = 0, yo = bx.y;  // this level's records / ytab rows in the staged blobs (dwords)
+  for (int l = g.src + 1; l <= g.top; l++) {
+    const int j = l - g.src;
+    const int4 sx = XT[j - 1], sy = YT[j - 1], ox = XT[j], oy = YT[j];
+    // (offsets from smem itself, so that the compiler keeps these LDS accesses as ds_* ops)
+    const uint8_t* S = smem + (((j - 1) & 1) ? g.buf0 : 0);
+    uint8_t* D = smem + ((j & 1) ? g.buf0 : 0);
+    const int SP = pyr_lds_pitch(sx.z, sx.w), DP = pyr_lds_pitch(ox.z, ox.w);
+    const LevelDesc ld = a.levels[l];
+    const int sh_max = a.levels[l - 1].h - 1;
+    const int G = (ox.w - ox.z) >> 2, R = oy.w - oy.z, R2 = (R + 1) >> 1;
+    // groups [0, Gm) lie below simd_end (the SIMD128 rounding only); [Gm, G) reach it. Both rows
+    // of a pair are computed and stored (the region buffers hold one spare row for odd R).
+    const int Gm = min(G, max(0, ((ld.simd_end & ~3) - ox.z) >> 2));
+    auto item = [&](auto tail, int pr, int gx) {
+      const int x = ox.z + 4 * gx, r0 = 2 * pr;
+      const uint32_t* rec = tabs + xo + PYR_REC * gx;
+      const int lc = (int)rec[0] - sx.z, sh = lc & 3;
+      const uint4 sel = *reinterpret_cast<const uint4*>(rec + 4), alp = *reinterpret_cast<const uint4*>(rec + 8);
+      const int2 ya = *reinterpret_cast<const int2*>(tabs + yo + 2 * r0);
+      const int2 yb = *reinterpret_cast<const int2*>(tabs + yo + 2 * min(r0 + 1, R - 1));
+      const int rows[4] = {ya.x, ya.x + 1, yb.x, yb.x + 1};
+      uint32_t W0[4], W1[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(
+            S + __umul24((uint32_t)(min(max(rows[r], 0), sh_max) - sy.z), (uint32_t)SP) + (lc & ~3));
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
+        W0[r] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        W1[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+      }
+      uint32_t* d = reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)r0, (uint32_t)DP) + 4 * gx);
+      d[0] = resize_win_row<decltype(tail)::value>(W0[0], W1[0], W0[1], W1[1], sel, alp, x, ld, ya);
+      d[DP >> 2] = resize_win_row<decltype(tail)::value>(W0[2], W1[2], W0[3], W1[3], sel, alp, x, ld, yb);
+    };
+    {
+      const int items = Gm * R2;
+      const uint32_t gm = magic_div((uint32_t)Gm);
+      for (int i = t; i < items; i += 256) {
+        const int pr = div_magic(i, gm);
+        item(std::false_type{}, pr, i - pr * Gm);
+      }
     }
-    uint8_t* dst = bufs[l & 1];
-    const int dpitch = (ld.w + 3) & ~3;
-    const bool keep = l + 1 < a.nlevels;  // the top level is not read again
-    uint8_t* gbase = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-    const int G = (ld.w + 3) >> 2;
-    const uint32_t gm = (uint32_t)((0x100000000ull + G - 1) / G);
-    const int items = (r.w - r.z) * G;
-    for (int i = t; i < items; i += 256) {
-      const int ry = (int)__umulhi((uint32_t)i, gm), x = 4 * (i - ry * G), y = r.z + ry;
-      const int2 yt = a.ytab[ld.tab_y + y];
-      const int b0 = (int)(short)(yt.y & 0xffff), b1 = (int)(short)((unsigned)yt.y >> 16);
-      const int sy0 = min(max(yt.x, 0), ls.h - 1) - sbase, sy1 = min(max(yt.x + 1, 0), ls.h - 1) - sbase;
-      const uint32_t packed = resize4(src + sy0 * spitch, src + sy1 * spitch, xt_lds, x, ld, ls.w, b0, b1);
-      if (keep) *reinterpret_cast<uint32_t*>(dst + ry * dpitch + x) = packed;
-      if (y >= r.x && y < r.y) store_row4(gbase + (long long)y * ld.pitch, x, ld.w, packed);
+    if (Gm < G) {
+      const int Gt = G - Gm, items = Gt * R2;
+      const uint32_t gm = magic_div((uint32_t)Gt);
+      for (int i = t; i < items; i += 256) {
+        const int pr = div_magic(i, gm);
+        item(std::true_type{}, pr, Gm + i - pr * Gt);
+      }
     }
     __syncthreads();
+    if (!(g.dbg & 2)) pyr_copy_own(D, DP, ox, oy, ox.z, oy.z, ld, pyr + ld.pyr_off, t);
+    xo += PYR_REC * G;
+    yo += 2 * R;
   }
 }
 
@@ -777,83 +936,90 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
   for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
-  // 2a. OpenCV's first two antipodal pairs (ring 0/8 = dy +-3, ring 4/12 = dx +-3) at the lower
-  //     threshold in packed 16-bit halves (four pixels per lane on the constant-stride path, two
-  //     otherwise): dark <=> max(min(u,d), min(l,r)) < v - t, bright <=> min(max(u,d), max(l,r))
-  //     > v + t. Survivors (about 1 in 8 pixels) are compacted in row-major order.
-  const uint32_t T2 = (uint32_t)a.tlow * 0x10001u;
-  int nlist = 0;
-  if constexpr (RSC != 0) {
-    switch (xo) {
-      case 0: nlist = fast_prefilter4<RSC, 0>(roi, dw, dh, T2, list); break;
-      case 1: nlist = fast_prefilter4<RSC, 1>(roi, dw, dh, T2, list); break;
-      case 2: nlist = fast_prefilter4<RSC, 2>(roi, dw, dh, T2, list); break;
-      default: nlist = fast_prefilter4<RSC, 3>(roi, dw, dh, T2, list); break;
-    }
-  } else {
-    const int pw = (dw + 1) >> 1;
-    const uint32_t pmagic = ((1u << 20) + pw - 1) / pw;
-    for (int q0 = 0; q0 < pw * dh; q0 += 64) {
-      const int q = q0 + lane;
-      bool p0 = false, p1 = false;
-      int px = 0;
-      if (q < pw * dh) {
-        const int rr = RSC != 0 ? (int)(((uint32_t)q * pmagic) >> 20) : q / pw;
-        const int cc = 2 * (q - rr * pw);
-        px = rr * dw + cc;
-        const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
-        const uint32_t c = pack2(p[0], p[1]);
-        const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
-        const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
-        const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
-        const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
-        const uint32_t res = pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
-        p0 = (res & 0x8000u) != 0;
-        p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
-      }
-      const uint64_t b0 = wave_ballot(p0), b1 = wave_ballot(p1);
-      const int pos = nlist + prefix_in_wave(b0) + prefix_in_wave(b1);
-      if (p0) list[pos] = (uint16_t)px;
-      if (p1) list[pos + (p0 ? 1 : 0)] = (uint16_t)(px + 1);
-      nlist += __popcll(b0) + __popcll(b1);
-    }
-  }
-  wave_sync();
-  // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the full antipodal
-  //     quick test, then the arc strength (OpenCV cornerScore + 1) of the entries that pass; the
-  //     corners at the lower threshold go to m8 and, compacted in order, back into the list
-  int ncorner = 0;
-  for (int j0 = 0; j0 < nlist; j0 += 128) {
-    const int ja = j0 + 2 * lane, jb = ja + 1;
-    int qa = 0, qb = 0;
-    uint32_t m = 0;
-    if (ja < nlist) {
-      qa = list[ja];
-      qb = jb < nlist ? list[jb] : qa;
-      int ra, ca, rb, cb;
-      dec_rc(qa, ra, ca);
-      dec_rc(qb, rb, cb);
-      const uint8_t* pa = R + (ra + 3) * RS + (ca + 3);
-      const uint8_t* pb = R + (rb + 3) * RS + (cb + 3);
-      m = arc_strength_pk(pa, pb, RS, a.tlow);
-      const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
-      if (ma) m8[(ra + 1) * mw + (ca + 1)] = (uint8_t)min(ma, 255);
-      if (mb && jb < nlist) m8[(rb + 1) * mw + (cb + 1)] = (uint8_t)min(mb, 255);
-    }
-    const bool ka = ja < nlist && (m & 0xffffu) != 0, kb = jb < nlist && (m >> 16) != 0;
-    const uint64_t b0 = wave_ballot(ka), b1 = wave_ballot(kb);
-    wave_sync();  // every lane has read list[j0 .. j0+127] before it is overwritten
-    const int pos = ncorner + prefix_in_wave(b0) + prefix_in_wave(b1);
-    if (ka) list[pos] = (uint16_t)qa;
-    if (kb) list[pos + (ka ? 1 : 0)] = (uint16_t)qb;
-    ncorner += __popcll(b0) + __popcll(b1);
-  }
-  wave_sync();
-  // 4. NMS over the corners (out-of-region and non-corner neighbours score 0)
   uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
   int count = 0;
+  // ORBextractor.cc:812-819: FAST at iniThFAST; only a cell left empty runs again at minThFAST.
+  // Each pass filters, scores and suppresses at its own threshold, so the arc strengths of a
+  // textured cell are computed for the iniThFAST corners only. The arc strength M of a pixel does
+  // not depend on the threshold, so m8 entries of the first pass stay valid in the second.
   for (int pass = 0; pass < 2; pass++) {
     const int t = min(max(pass == 0 ? a.ini_th : a.min_th, 0), 255);
+    if (pass == 1) {
+      if (t == min(max(a.ini_th, 0), 255)) break;  // the same threshold finds the same nothing
+      wave_sync();  // every lane is done with pass 0's list
+    }
+    // 2a. OpenCV's first two antipodal pairs (ring 0/8 = dy +-3, ring 4/12 = dx +-3) at t in
+    //     packed 16-bit halves (four pixels per lane on the constant-stride path, two otherwise):
+    //     dark <=> max(min(u,d), min(l,r)) < v - t, bright <=> min(max(u,d), max(l,r)) > v + t.
+    //     Survivors are compacted in row-major order.
+    const uint32_t T2 = (uint32_t)t * 0x10001u;
+    int nlist = 0;
+    if constexpr (RSC != 0) {
+      switch (xo) {
+        case 0: nlist = fast_prefilter4<RSC, 0>(roi, dw, dh, T2, list); break;
+        case 1: nlist = fast_prefilter4<RSC, 1>(roi, dw, dh, T2, list); break;
+        case 2: nlist = fast_prefilter4<RSC, 2>(roi, dw, dh, T2, list); break;
+        default: nlist = fast_prefilter4<RSC, 3>(roi, dw, dh, T2, list); break;
+      }
+    } else {
+      const int pw = (dw + 1) >> 1;
+      for (int q0 = 0; q0 < pw * dh; q0 += 64) {
+        const int q = q0 + lane;
+        bool p0 = false, p1 = false;
+        int px = 0;
+        if (q < pw * dh) {
+          const int rr = q / pw;
+          const int cc = 2 * (q - rr * pw);
+          px = rr * dw + cc;
+          const uint8_t* p = R + (rr + 3) * RS + (cc + 3);
+          const uint32_t c = pack2(p[0], p[1]);
+          const uint32_t u = pack2(p[3 * RS], p[3 * RS + 1]), d = pack2(p[-3 * RS], p[-3 * RS + 1]);
+          const uint32_t r = pack2(p[3], p[4]), l = pack2(p[-3], p[-2]);
+          const uint32_t X = pk_max_u16(pk_min_u16(u, d), pk_min_u16(l, r));
+          const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
+          const uint32_t res = pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
+          p0 = (res & 0x8000u) != 0;
+          p1 = (res & 0x80000000u) != 0 && cc + 1 < dw;
+        }
+        const uint64_t b0 = wave_ballot(p0), b1 = wave_ballot(p1);
+        const int pos = nlist + prefix_in_wave(b0) + prefix_in_wave(b1);
+        if (p0) list[pos] = (uint16_t)px;
+        if (p1) list[pos + (p0 ? 1 : 0)] = (uint16_t)(px + 1);
+        nlist += __popcll(b0) + __popcll(b1);
+      }
+    }
+    wave_sync();
+    // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the arc strength
+    //     (OpenCV cornerScore + 1) of the corners at t goes to m8 and, compacted in order, back
+    //     into the list
+    int ncorner = 0;
+    for (int j0 = 0; j0 < nlist; j0 += 128) {
+      const int ja = j0 + 2 * lane, jb = ja + 1;
+      int qa = 0, qb = 0;
+      uint32_t m = 0;
+      if (ja < nlist) {
+        qa = list[ja];
+        qb = jb < nlist ? list[jb] : qa;
+        int ra, ca, rb, cb;
+        dec_rc(qa, ra, ca);
+        dec_rc(qb, rb, cb);
+        const uint8_t* pa = R + (ra + 3) * RS + (ca + 3);
+        const uint8_t* pb = R + (rb + 3) * RS + (cb + 3);
+        m = arc_strength_pk(pa, pb, RS, t);
+        const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
+        if (ma) m8[(ra + 1) * mw + (ca + 1)] = (uint8_t)min(ma, 255);
+        if (mb && jb < nlist) m8[(rb + 1) * mw + (cb + 1)] = (uint8_t)min(mb, 255);
+      }
+      const bool ka = ja < nlist && (m & 0xffffu) != 0, kb = jb < nlist && (m >> 16) != 0;
+      const uint64_t b0 = wave_ballot(ka), b1 = wave_ballot(kb);
+      wave_sync();  // every lane has read list[j0 .. j0+127] before it is overwritten
+      const int pos = ncorner + prefix_in_wave(b0) + prefix_in_wave(b1);
+      if (ka) list[pos] = (uint16_t)qa;
+      if (kb) list[pos + (ka ? 1 : 0)] = (uint16_t)qb;
+      ncorner += __popcll(b0) + __popcll(b1);
+    }
+    wave_sync();
+    // 4. NMS over the corners at t (out-of-region neighbours and non-corners score 0)
     for (int j0 = 0; j0 < ncorner; j0 += 64) {
       const int j = j0 + lane;
       bool keep = false;
@@ -864,7 +1030,8 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
         const uint8_t* mp = m8 + (rr + 1) * mw + (cc + 1);
         const int m = mp[0];
         // score m - 1 beats every neighbour's (mn >= t + 1 ? mn - 1 : 0) exactly when m > mn for
-        // all 8 neighbours and m >= 2: a neighbour below t + 1 is below m too, and scores 0
+        // all 8 neighbours and m >= 2: a neighbour below t + 1 (a corner of an earlier pass at a
+        // lower threshold or none) is below m too, and scores 0
         const int mn = max(max(max(max((int)mp[-mw - 1], (int)mp[-mw]), max((int)mp[-mw + 1], (int)mp[-1])),
                                max(max((int)mp[1], (int)mp[mw - 1]), (int)mp[mw])), (int)mp[mw + 1]);
         sc = m - 1;
@@ -1838,7 +2005,7 @@ struct orbfe_extractor {
   int umax[16];
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
-  int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level)
+  int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level launches)
   int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: level 0 only)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
@@ -1858,8 +2025,12 @@ struct orbfe_extractor {
   int2* d_ytab = nullptr;
   uint4* d_rgrp = nullptr;
   int* d_rgx0 = nullptr;
-  int4* d_band_rows = nullptr;
-  int nbands = 0, band_buf = 0;  // k_pyramid plan (nbands 0: per-level launches)
+  int4* d_pyr_xt = nullptr;          // k_pyramid tile tables
+  int4* d_pyr_yt = nullptr;
+  int2* d_pyr_blob = nullptr;
+  uint32_t* d_pyr_xblob = nullptr;
+  uint32_t* d_pyr_yblob = nullptr;
+  std::vector<PyrGroup> pyr_groups;  // k_pyramid plan (empty: per-level launches)
   size_t pyramid_lds = 0;
   // batch buffers
   int batch_cap = 0;
@@ -1910,6 +2081,165 @@ static hipEvent_t pool_event(orbfe_extractor* h) {
   hipEvent_t e;
   if (hipEventCreate(&e) != hipSuccess) return nullptr;
   return e;
+}
+
+// k_pyramid plan. Groups: levels 1..3 from the input image, then up to 4 levels per group from
+// the previous group's top. Own pieces: x boundaries at multiples of 4 (one writer per 4-column
+// group of store_row4), y boundaries by rows; the compute regions grow top-down by the bilinear
+// taps' reach (clamped rows, sx + 1 only below xmax). Tiles shrink until the two LDS region
+// buffers fit 48 KiB. False (per-level launches) when a level's taps need more than the
+// 8-byte window (rwin_ok) or with a single level.
+struct PyrPlan {
+  std::vector<PyrGroup> groups;
+  std::vector<int4> tx, ty;
+  std::vector<int2> blob;
+  std::vector<uint32_t> xblob, yblob;
+  size_t lds_max = 0;
+};
+static bool plan_pyramid(const std::vector<LevelDesc>& lv, const std::vector<int2>& xt, const std::vector<int2>& yt,
+                         const std::vector<uint4>& rgrp, const std::vector<int>& rgx0, PyrPlan& pp) {
+  std::vector<PyrGroup>& groups = pp.groups;
+  std::vector<int4>& tx = pp.tx;
+  std::vector<int4>& ty = pp.ty;
+  size_t& lds_max = pp.lds_max;
+  const int L = (int)lv.size();
+  if (L < 2) return false;
+  for (int l = 1; l < L; l++)
+    if (!lv[l].rwin_ok) return false;
+  auto a4 = [](int v) { return (v + 3) & ~3; };
+  int src = 0;
+  lds_max = 0;
+  while (src < L - 1) {
+    const int top = src == 0 ? std::min(3, L - 1) : std::min(src + 4, L - 1);
+    const int NL = top - src + 1;
+    int TW = src == 0 ? 64 : 32, TH = src == 0 ? 32 : 16;
+    if (const char* e = std::getenv(src == 0 ? "ORBFE_PYR_TILE_A" : "ORBFE_PYR_TILE_B")) std::sscanf(e, "%dx%d", &TW, &TH);
+    for (;;) {
+      const int ntx = std::max(1, std::min((lv[top].w + TW - 1) / TW, (lv[top].w + 3) / 4));
+      const int nty = std::max(1, std::min((lv[top].h + TH - 1) / TH, lv[top].h));
+      auto own_x = [&](int l, int k) {
+        if (k <= 0) return 0;
+        if (k >= ntx) return lv[l].w;
+        return std::min(lv[l].w, 4 * (int)((long long)k * ((lv[l].w + 3) / 4) / ntx));
+      };
+      auto own_y = [&](int l, int k) { return (int)((long long)k * lv[l].h / nty); };
+      std::vector<int4> gx((size_t)ntx * NL), gy((size_t)nty * NL);
+      for (int k = 0; k < ntx; k++) {
+        int4* e = &gx[(size_t)k * NL];
+        for (int l = src; l <= top; l++)
+          e[l - src] = (l == src && src > 0) ? make_int4(0, 0, 0, 0) : make_int4(own_x(l, k), own_x(l, k + 1), 0, 0);
+        e[NL - 1].z = e[NL - 1].x;
+        e[NL - 1].w = a4(e[NL - 1].y);
+        for (int l = top; l > src; l--) {
+          const LevelDesc& d = lv[l];
+          const int c0 = std::min(e[l - src].z, d.w - 1), c1 = std::min(e[l - src].w - 1, d.w - 1);
+          const int s0 = xt[d.tab_x + c0].x;
+          const int s1 = c1 < d.xmax ? xt[d.tab_x + c1].x + 1 : xt[d.tab_x + c1].x;
+          int4& p = e[l - 1 - src];
+          const bool has_own = p.y > p.x;
+          const int o0 = has_own ? std::min(s0, p.x) : s0, o1 = has_own ? std::max(s1 + 1, p.y) : s1 + 1;
+          p.z = o0 & ~3;
+          p.w = std::min(a4(o1), a4(lv[l - 1].w));
+        }
+      }
+      for (int k = 0; k < nty; k++) {
+        int4* e = &gy[(size_t)k * NL];
+        for (int l = src; l <= top; l++)
+          e[l - src] = (l == src && src > 0) ? make_int4(0, 0, 0, 0) : make_int4(own_y(l, k), own_y(l, k + 1), 0, 0);
+        e[NL - 1].z = e[NL - 1].x;
+        e[NL - 1].w = e[NL - 1].y;
+        for (int l = top; l > src; l--) {
+          const LevelDesc& d = lv[l];
+          const int hs = lv[l - 1].h;
+          const int s0 = std::min(std::max(yt[d.tab_y + e[l - src].z].x, 0), hs - 1);
+          const int s1 = std::min(std::max(yt[d.tab_y + e[l - src].w - 1].x + 1, 0), hs - 1);
+          int4& p = e[l - 1 - src];
+          const bool has_own = p.y > p.x;
+          p.z = has_own ? std::min(s0, p.x) : s0;
+          p.w = has_own ? std::max(s1 + 1, p.y) : s1 + 1;
+        }
+      }
+      // LDS: regions of levels src..top, even offsets in buffer 0, odd in buffer 1
+      size_t b[2] = {0, 0};
+      bool empty = false;
+      for (int kx = 0; kx < ntx; kx++)
+        for (int ky = 0; ky < nty; ky++)
+          for (int l = src; l <= top; l++) {
+            const int4 ex = gx[(size_t)kx * NL + l - src], ey = gy[(size_t)ky * NL + l - src];
+            if (ex.w <= ex.z || ey.w <= ey.z) empty = true;
+            // every level's region stays in LDS until its own piece is copied out; one spare
+            // row for the second row of an odd last pair
+            const size_t bytes = (size_t)pyr_lds_pitch(ex.z, ex.w) * (ey.w - ey.z + 1);
+            b[(l - src) & 1] = std::max(b[(l - src) & 1], bytes);
+          }
+      b[0] = align_up(b[0], 16);
+      b[1] = align_up(b[1], 16);
+      // staged blobs: per tile column the tap records of its 4-column groups, per tile row its
+      // ytab rows, levels src+1..top in order
+      size_t tab = 0, bxmax = 0, bymax = 0;
+      for (int k = 0; k < ntx; k++) {
+        size_t n = 0;
+        for (int l = src + 1; l <= top; l++) n += PYR_REC * (size_t)((gx[(size_t)k * NL + l - src].w - gx[(size_t)k * NL + l - src].z) >> 2);
+        bxmax = std::max(bxmax, n);
+      }
+      for (int k = 0; k < nty; k++) {
+        size_t n = 0;
+        for (int l = src + 1; l <= top; l++) n += 2 * (size_t)(gy[(size_t)k * NL + l - src].w - gy[(size_t)k * NL + l - src].z);
+        bymax = std::max(bymax, n);
+      }
+      tab = align_up(4 * (bxmax + bymax), 16);
+      if (!empty && b[0] + b[1] + tab <= 48 * 1024) {
+        PyrGroup pg;
+        pg.src = src;
+        pg.top = top;
+        pg.ntx = ntx;
+        pg.nty = nty;
+        pg.tx_off = (int)tx.size();
+        pg.ty_off = (int)ty.size();
+        pg.buf0 = (int)b[0];
+        pg.buf1 = (int)b[1];
+        pg.tab = (int)tab;
+        pg.dbg = std::getenv("ORBFE_PYR_DEBUG") ? std::atoi(std::getenv("ORBFE_PYR_DEBUG")) : 0;
+        pg.bx_off = (int)pp.blob.size();
+        for (int k = 0; k < ntx; k++) {
+          const int start = (int)pp.xblob.size();
+          for (int l = src + 1; l <= top; l++) {
+            const int4 e = gx[(size_t)k * NL + l - src];
+            for (int q = e.z >> 2; q < (e.w >> 2); q++) {
+              const int gi = lv[l].rgrp_begin + q;
+              const uint4 sl = rgrp[2 * gi], al = rgrp[2 * gi + 1];
+              const uint32_t rec[PYR_REC] = {(uint32_t)rgx0[gi], 0, 0, 0, sl.x, sl.y, sl.z, sl.w, al.x, al.y, al.z, al.w};
+              pp.xblob.insert(pp.xblob.end(), rec, rec + PYR_REC);
+            }
+          }
+          pp.blob.push_back(make_int2(start, (int)pp.xblob.size() - start));
+        }
+        pg.by_off = (int)pp.blob.size();
+        for (int k = 0; k < nty; k++) {
+          const int start = (int)pp.yblob.size();
+          for (int l = src + 1; l <= top; l++) {
+            const int4 e = gy[(size_t)k * NL + l - src];
+            for (int y = e.z; y < e.w; y++) {
+              const int2 v = yt[lv[l].tab_y + y];
+              pp.yblob.push_back((uint32_t)v.x);
+              pp.yblob.push_back((uint32_t)v.y);
+            }
+          }
+          pp.blob.push_back(make_int2(start, (int)pp.yblob.size() - start));
+        }
+        tx.insert(tx.end(), gx.begin(), gx.end());
+        ty.insert(ty.end(), gy.begin(), gy.end());
+        groups.push_back(pg);
+        lds_max = std::max(lds_max, b[0] + b[1] + tab);
+        break;
+      }
+      if (empty || (TW <= 8 && TH <= 4)) return false;
+      if (TW >= 2 * TH) TW /= 2;
+      else TH /= 2;
+    }
+    src = top;
+  }
+  return true;
 }
 
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
@@ -2037,10 +2367,10 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
           const int o = e.x - x0;
           if (col >= xmax) {
             sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)o << 16) | 0x0c000000u;
-            alp[k] = 2048u;
+            alp[k] = 16u * 2048u;
           } else {
             sel[k] = (uint32_t)o | 0x0c00u | ((uint32_t)(o + 1) << 16) | 0x0c000000u;
-            alp[k] = (uint32_t)e.y;
+            alp[k] = 16u * (uint32_t)e.y;  // x 16: see resize_win_row (each u16 half <= 32768)
           }
           if (o < 0 || o + 1 > 7) d.rwin_ok = 0;
         }
@@ -2056,51 +2386,19 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
       d.simd_end = se;
     }
   }
-  // k_pyramid row bands: own rows per band at every level, plus the halo rows the next level's
-  // taps reach (computed top-down); the largest working band of levels 1..L-2 sizes the LDS
-  std::vector<int4> bands;
-  int nb_sel = 0, buf_sel = 0;
-  size_t lds_sel = 0;
-  if (L >= 2) {
-    const int cands[] = {16, 24, 32, 48, 64, 12, 8, 4, 2, 1};
-    for (int nb : cands) {
-      if (nb > lv[L - 1].h) continue;
-      std::vector<int4> br((size_t)nb * L);
-      int buf = 0;
-      for (int k = 0; k < nb; k++) {
-        for (int l = 0; l < L; l++) {
-          const int o0 = (int)((long long)k * lv[l].h / nb), o1 = (int)((long long)(k + 1) * lv[l].h / nb);
-          br[(size_t)k * L + l] = make_int4(o0, o1, o0, o1);
-        }
-        for (int l = L - 1; l >= 2; l--) {
-          const int4 c = br[(size_t)k * L + l];
-          const int hs = lv[l - 1].h;
-          const int s0 = std::min(std::max(yt[lv[l].tab_y + c.z].x, 0), hs - 1);
-          const int s1 = std::min(std::max(yt[lv[l].tab_y + c.w - 1].x + 1, 0), hs - 1);
-          int4& p = br[(size_t)k * L + l - 1];
-          p.z = std::min(p.x, s0);
-          p.w = std::max(p.y, s1 + 1);
-        }
-        for (int l = 1; l + 1 < L; l++) {
-          const int4 c = br[(size_t)k * L + l];
-          buf = std::max(buf, (c.w - c.z) * ((lv[l].w + 3) & ~3));
-        }
-      }
-      buf = (buf + 15) & ~15;
-      const size_t lds = 2 * (size_t)buf + sizeof(int2) * lv[1].w;
-      if (lds <= 64 * 1024) {
-        bands = br;
-        nb_sel = nb;
-        buf_sel = buf;
-        lds_sel = lds;
-        break;
-      }
-    }
-  }
+  // k_pyramid tile plan (see the kernel): groups of levels, 2-D tiles of each group's top level
+  PyrPlan pp;
+  if (!plan_pyramid(lv, xt, yt, rgrp, rgx0, pp)) pp.groups.clear();
   // release old geometry buffers and upload new ones
   hipSetDevice(h->device);
-  hipFree(h->d_band_rows);
-  h->d_band_rows = nullptr;
+  hipFree(h->d_pyr_xt);
+  hipFree(h->d_pyr_yt);
+  hipFree(h->d_pyr_blob);
+  hipFree(h->d_pyr_xblob);
+  hipFree(h->d_pyr_yblob);
+  h->d_pyr_xt = h->d_pyr_yt = nullptr;
+  h->d_pyr_blob = nullptr;
+  h->d_pyr_xblob = h->d_pyr_yblob = nullptr;
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   h->d_rgrp = nullptr;
@@ -2111,13 +2409,19 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMemcpy(h->d_rgrp, rgrp.data(), sizeof(uint4) * rgrp.size(), hipMemcpyHostToDevice));
     ORBFE_HIP_CHECK(hipMemcpy(h->d_rgx0, rgx0.data(), sizeof(int) * rgx0.size(), hipMemcpyHostToDevice));
   }
-  if (!bands.empty()) {
-    ORBFE_HIP_CHECK(hipMalloc(&h->d_band_rows, sizeof(int4) * bands.size()));
-    ORBFE_HIP_CHECK(hipMemcpy(h->d_band_rows, bands.data(), sizeof(int4) * bands.size(), hipMemcpyHostToDevice));
+  if (!pp.groups.empty()) {
+    auto up = [](void** d, const void* src, size_t bytes) -> hipError_t {
+      hipError_t e = hipMalloc(d, std::max<size_t>(bytes, 4));
+      return e == hipSuccess ? hipMemcpy(*d, src, bytes, hipMemcpyHostToDevice) : e;
+    };
+    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_xt, pp.tx.data(), sizeof(int4) * pp.tx.size()));
+    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_yt, pp.ty.data(), sizeof(int4) * pp.ty.size()));
+    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_blob, pp.blob.data(), sizeof(int2) * pp.blob.size()));
+    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_xblob, pp.xblob.data(), sizeof(uint32_t) * pp.xblob.size()));
+    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_yblob, pp.yblob.data(), sizeof(uint32_t) * pp.yblob.size()));
   }
-  h->nbands = nb_sel;
-  h->band_buf = buf_sel;
-  h->pyramid_lds = lds_sel;
+  h->pyr_groups = pp.groups;
+  h->pyramid_lds = pp.lds_max;
   hipFree(h->d_levels);
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
@@ -2280,18 +2584,19 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.out_cap = cap;
   a.ini_th = h->ini_th;
   a.min_th = h->min_th;
-  a.tlow = std::min(std::min(std::max(h->ini_th, 0), 255), std::min(std::max(h->min_th, 0), 255));
   a.roi_w_max = h->roi_w_max;
   a.roi_h_max = h->roi_h_max;
   a.node_cap = h->node_cap;
   a.sort_cap = h->sort_cap;
   a.scan_cap = h->scan_cap;
   a.key_lds_cap = h->key_lds_cap;
-  a.band_rows = h->d_band_rows;
+  a.pyr_xt = h->d_pyr_xt;
+  a.pyr_yt = h->d_pyr_yt;
+  a.pyr_blob = h->d_pyr_blob;
+  a.pyr_xblob = h->d_pyr_xblob;
+  a.pyr_yblob = h->d_pyr_yblob;
   a.rgrp = h->d_rgrp;
   a.rgx0 = h->d_rgx0;
-  a.nbands = h->nbands;
-  a.band_buf = h->band_buf;
   for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
   a.atan.p1 = 0.9997878412794807f * (float)(180 / M_PI);
   a.atan.p3 = -0.3258083974640975f * (float)(180 / M_PI);
@@ -2309,10 +2614,24 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
     return ORBFE_OK;
   };
-  if (h->nbands > 0 && !h->force_level_launches) {
-    dim3 grid(h->nbands, n);
-    LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), h->pyramid_lds, st, a));
-    launch_fast(st, 0, a.ncells);
+  if (!h->pyr_groups.empty() && !h->force_level_launches) {
+    // the first group writes levels 0..top; their FAST cells run on the side stream beside the
+    // later groups, the rest after them on the main stream
+    const int top0 = h->pyr_groups[0].top;
+    for (size_t gi = 0; gi < h->pyr_groups.size(); gi++) {
+      const PyrGroup& pg = h->pyr_groups[gi];
+      dim3 grid(pg.ntx * pg.nty, n);
+      LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), pg.buf0 + pg.buf1 + pg.tab, st, a, pg));
+      if (gi == 0) {
+        ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
+        ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_l0, 0));
+        const int c1 = top0 + 1 < h->nlevels ? h->levels[top0 + 1].cell_begin : a.ncells;
+        launch_fast(h->side, 0, c1);
+      }
+    }
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
+    if (top0 + 1 < h->nlevels) launch_fast(st, h->levels[top0 + 1].cell_begin, a.ncells);
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   } else {
     {
       const LevelDesc& d = h->levels[0];
@@ -2497,7 +2816,11 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
-  hipFree(h->d_band_rows);
+  hipFree(h->d_pyr_blob);
+  hipFree(h->d_pyr_xblob);
+  hipFree(h->d_pyr_yblob);
+  hipFree(h->d_pyr_xt);
+  hipFree(h->d_pyr_yt);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   hipFree(h->d_in);

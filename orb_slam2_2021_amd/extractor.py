@@ -307,7 +307,8 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
     def debug_force_level_launches(self, on: bool = True) -> None:
-        """True (default): one k_resize launch per level; False: the banded k_pyramid launch."""
+        """True: k_copy0 + one k_resize launch per level; False (default): the tiled k_pyramid
+        launches."""
         L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),
                 "force_level_launches")
 

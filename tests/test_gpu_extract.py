@@ -84,14 +84,24 @@ def test_scalar_resize_mode(require_gpu, level_launches):
 
 @pytest.mark.parametrize("shape", [(376, 1241), (480, 640), (260, 1500), (900, 700)])
 def test_pyramid_paths_agree(require_gpu, shape):
-    """k_pyramid (banded, one launch) and the per-level k_resize launches give the reference
-    pyramid on wide, tall and KITTI/TUM shapes."""
+    """The tiled k_pyramid launches (groups of levels from LDS regions, level 0 copied by the first
+    group) and the per-level k_copy0 + k_resize launches give the reference pyramid on wide, tall
+    and KITTI/TUM shapes."""
     img = synth_frame(9, *shape)
     ref = RefExtractor(1000, 1.2, 8, 20, 7)
     for forced in (False, True):
         ext = ORBextractor(1000, 1.2, 8, 20, 7)
         ext.debug_force_level_launches(forced)
         assert_same_extraction(ext, ref, img)
+
+
+@pytest.mark.parametrize("params,shape", [((800, 1.1, 12, 20, 7), (480, 640)), ((300, 1.2, 1, 20, 7), (240, 333)),
+                                          ((500, 1.2, 2, 20, 7), (377, 643)), ((1500, 1.5, 5, 20, 7), (601, 1023))])
+def test_pyramid_group_splits(require_gpu, params, shape):
+    """k_pyramid's level groups (1..3 from the image, then up to 4 per group) for 1, 2, 5 and 12
+    levels on odd widths; every level's bytes, and the rest of the extraction, vs the oracle."""
+    img = synth_frame(17, *shape)
+    assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
 
 def test_flat_and_sparse_images(require_gpu):
