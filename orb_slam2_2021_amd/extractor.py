@@ -127,8 +127,8 @@ class ORBextractor:
             raise ValueError("extract_batch needs same-shaped images")
         cap = self.max_keypoints(rows, cols)
         B = len(imgs)
-        kps = np.zeros(B * cap, L.KEYPOINT_DTYPE)
-        desc = np.zeros((B * cap, 32), np.uint8)
+        kps = np.empty(B * cap, L.KEYPOINT_DTYPE)
+        desc = np.empty((B * cap, 32), np.uint8)
         counts = np.zeros(B, np.int32)
         arr = (c_void_p * B)(*[i.ctypes.data for i in imgs])
         L.check(self._lib.orbfe_extract_batch(self._h, B, ctypes.cast(arr, c_void_p), rows, cols,
