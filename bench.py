@@ -522,9 +522,30 @@ def c2_latency(args, left, right, reps=200):
         go[s].set()
     for t in th:
         t.join()
+    # the MI355X way to serve the stereo Frame: both images in one orbfe_extract_batch call (one
+    # launch sequence) on one handle
+    from ctypes import c_void_p
+    kb = np.empty(2 * cap, L.KEYPOINT_DTYPE)
+    db = np.empty((2 * cap, 32), np.uint8)
+    cb = np.zeros(2, np.int32)
+    arr = (c_void_p * 2)(imgs[0].ctypes.data, imgs[1].ctypes.data)
+
+    def call_pair():
+        L.check(lib.orbfe_extract_batch(exts[0]._h, 2, ctypes.cast(arr, c_void_p), rows, cols, c_size_t(cols),
+                                        L.ptr(kb), L.ptr(db), cap, L.ptr(cb)), "orbfe_extract_batch")
+
+    for _ in range(10):
+        call_pair()
+    one_call = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        call_pair()
+        one_call.append(time.perf_counter() - t0)
     out = {"single_image": percentiles(single), "stereo_two_threads": percentiles(pair[10:]),
-           "what": "orbfe_extract wall-clock per call (host buffers in and out), 1241x376, 1 GPU; stereo = "
-                   "two handles on two threads as Frame.cc:113-116"}
+           "stereo_pair_one_call": percentiles(one_call),
+           "what": "orbfe_extract wall-clock per call (host buffers in and out), 1241x376, 1 GPU; stereo_two_threads "
+                   "= two handles on two threads as Frame.cc:113-116; stereo_pair_one_call = both images in one "
+                   "orbfe_extract_batch call on one handle"}
     if not args.no_cpu:
         from oracle.orbref import RefExtractor
         k, d, n = bufs[0]
