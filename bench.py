@@ -71,6 +71,9 @@ def parse(argv=None):
     p.add_argument("--stereo", action="store_true",
                    help="run Frame::ComputeStereoMatches on every pair after extraction (the stereo "
                         "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
+    p.add_argument("--extractors", type=int, default=1,
+                   help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
+                        "own stream with its side-stream work inline (experiment)")
     p.add_argument("--level-launches", action="store_true",
                    help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
     p.add_argument("--rehearse", action="store_true",
@@ -196,7 +199,15 @@ def main():
         ext.debug_force_level_launches(True)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
-    pipe, state = build_c3(ext, tree, voc, B, H, W, dev, seed=1234 + rank, depth=max(1, args.pipeline),
+    exts = [ext]
+    if args.extractors > 1:
+        exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(args.extractors - 1)]
+        for e in exts:
+            e.debug_set_inline_side(True)
+            if args.level_launches:
+                e.debug_force_level_launches(True)
+    pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
+                           depth=max(1, args.pipeline),
                            stereo=args.stereo, levelsup=args.levelsup)
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
@@ -290,6 +301,9 @@ def main():
     roof["measured_in"] = (f"timed region (HIP events on every {ev_every}th sub-batch, "
                            f"{timed_events} sub-batches)" if use_timed else "probe pass")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B)
+    if roof["traffic"] is not None:  # per launch, like `achieved`: the sub-batch figure / its launches
+        roof["traffic_per_subbatch"] = roof["traffic"]
+        roof["traffic"] = int(roof["traffic"] / roof["launches_per_subbatch"])
     algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
     out = {
         "metric": METRIC,

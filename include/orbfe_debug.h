@@ -32,6 +32,10 @@ int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
  * as its level is built, the rest in one launch after the resize chain (k <= 0: the default,
  * level 0 only). The tiled path runs the first group's levels on the side stream. */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
+/* 1: run the side-stream work (k_blur, the early FAST levels) on the launch stream, for callers
+ * that overlap whole extractions on several streams of their own; 0 (default): the handle's
+ * high-priority side stream. */
+int orbfe_debug_set_inline_side(orbfe_extractor* h, int on);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

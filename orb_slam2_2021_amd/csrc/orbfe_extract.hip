@@ -2091,6 +2091,7 @@ struct orbfe_extractor {
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level launches)
   int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: level 0 only)
+  int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2643,6 +2644,10 @@ static int fast_side_split(const orbfe_extractor* h) {
 static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long long img_stride,
                           int pitch, orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
                           int32_t* d_counts, hipStream_t st, int i0 = 0) {
+  // the handle's high-priority side stream (k_blur and the early FAST levels beside the main chain),
+  // or the launch stream itself when the caller overlaps whole extractions instead
+  // (orbfe_debug_set_inline_side)
+  const hipStream_t side = h->inline_side ? st : h->side;
   ExtractArgs a;
   std::memset(&a, 0, sizeof(a));
   a.levels = h->d_levels;
@@ -2715,12 +2720,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), pg.buf0 + pg.buf1 + pg.tab, st, a, pg));
       if (gi == 0) {
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
-        ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_l0, 0));
+        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
         const int c1 = top0 + 1 < h->nlevels ? h->levels[top0 + 1].cell_begin : a.ncells;
-        launch_fast(h->side, 0, c1);
+        launch_fast(side, 0, c1);
       }
     }
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
     if (top0 + 1 < h->nlevels) launch_fast(st, h->levels[top0 + 1].cell_begin, a.ncells);
     ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   } else {
@@ -2743,9 +2748,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     auto side_fast = [&](int l) -> int {
       const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
       ORBFE_HIP_CHECK(hipEventRecord(e, st));
-      ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, e, 0));
+      ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
       const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
-      return launch_fast(h->side, h->levels[l].cell_begin, c1);
+      return launch_fast(side, h->levels[l].cell_begin, c1);
     };
     side_fast(0);
     for (int l = 1; l < h->nlevels; l++) {
@@ -2759,20 +2764,20 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       }
       if (l < k_side) side_fast(l);
     }
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, h->side));
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
     if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
     ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   }
   // fork: GaussianBlur needs only the pyramid, so it runs on the side stream beside k_octree (a
   // small, latency-bound grid that leaves most CUs idle); joined before k_describe
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
-  ORBFE_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+  ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
   {
-    hipStream_t sd = h->side;
+    hipStream_t sd = side;
     dim3 grid((h->blur_tiles + 3) / 4, n);
     LAUNCH_TIMED(h, 5, sd, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, sd, a));
   }
-  ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, h->side));
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   {
     dim3 grid(h->nlevels, n);
     if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
@@ -3360,6 +3365,12 @@ extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float
                        (float)(M_PI / 180.f), d_cos, d_sin);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_HIP_CHECK(hipStreamSynchronize(st));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->inline_side = on ? 1 : 0;
   return ORBFE_OK;
 }
 

@@ -306,6 +306,10 @@ class ORBextractor:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: level 0 only)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
+    def debug_set_inline_side(self, on: bool = True) -> None:
+        """Run the side-stream work (k_blur, early FAST levels) on the launch stream."""
+        L.check(self._lib.orbfe_debug_set_inline_side(self._h, 1 if on else 0), "set_inline_side")
+
     def debug_force_level_launches(self, on: bool = True) -> None:
         """True: k_copy0 + one k_resize launch per level; False (default): the tiled k_pyramid
         launches."""

@@ -49,6 +49,11 @@ class C3Pipeline:
                  nnratio: float = 0.6, check_ori: bool = False):
         import torch
         from .matcher import ORBmatcher
+        # one extractor, or several whose extractions of consecutive sub-batches overlap on their
+        # own streams (each keeps its own scratch)
+        self.exts = list(ext) if isinstance(ext, (list, tuple)) else [ext]
+        ext = self.exts[0]
+        depth = max(depth, len(self.exts) + 1)
         self.ext, self.voc = ext, voc
         self.B, self.H, self.W = B, H, W
         self.n_img = 2 * B
@@ -128,7 +133,8 @@ class C3Pipeline:
 
         self.sets = [OutSet() for _ in range(max(1, depth))]
         self.lib = L.lib()
-        self.stream = torch.cuda.Stream(dev)   # extraction (+ ComputeStereoMatches)
+        self.streams = [torch.cuda.Stream(dev) for _ in self.exts]  # extraction (+ ComputeStereoMatches)
+        self.stream = self.streams[0]
         self.mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
         self.counter = 0
         self.last = None
@@ -148,16 +154,17 @@ class C3Pipeline:
         `after_match(o)` runs on the matching stream after SearchForTriangulation (the C4 gather).
         Returns the output set."""
         o = self.sets[self.counter % len(self.sets)]
+        k = self.counter % len(self.exts)
         self.counter += 1
         B, H, W, cap = self.B, self.H, self.W, self.cap
-        s = self.stream
+        s, ext = self.streams[k], self.exts[k]
         s.wait_event(o.matched)  # the matching that last read this set is done
-        self.ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
+        ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
                                       o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
         if self.stereo:  # Frame.cc:125, on the extraction stream while the pyramids are current
             ev = []
             self._ev("k_stereo", s, ev)
-            self.ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
+            ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
                                                          o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
                                                          o.ur.data_ptr(), o.dep.data_ptr(),
                                                          stream=s.cuda_stream)
@@ -245,6 +252,8 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     from . import synthetic as S
     from .frames import epipole as epipole_of
     dev = torch.device("cuda", device) if isinstance(device, int) else device
+    exts = ext
+    ext = exts[0] if isinstance(exts, (list, tuple)) else exts
     n_img = 2 * B
     cap = ext.max_keypoints(H, W)
     rng = np.random.default_rng(seed)
@@ -258,7 +267,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     dummy = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t1)
     dummy2 = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t2)
     ex, ey = epipole_of(dummy, dummy2)
-    pipe = C3Pipeline(ext, voc, tree, B, H, W, cam, F12, (ex, ey),
+    pipe = C3Pipeline(exts, voc, tree, B, H, W, cam, F12, (ex, ey),
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo)

@@ -4,8 +4,9 @@ launch per kernel, with the gfx950 corrections of MI355X_MICROARCH.md ("HBM"): F
 counts half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE (KiB) is taken as is.
 
 usage: pmc_summary.py FETCH_CSV WRITE_CSV [OUT_JSON]
-Per step = mean per launch x launches per step (k_resize_win: one per pyramid level; k_fast: level
-0 beside the resize chain + levels 1..7; every other kernel once).
+Per sub-batch (one C3 batch of 64 images; bench.py's `traffic_bytes_per_step` key keeps its
+round-1 name) = mean per launch x launches per sub-batch (k_resize_win: one per pyramid level;
+k_fast: level 0 beside the resize chain + levels 1..7; every other kernel once).
 """
 import csv
 import json
@@ -48,7 +49,8 @@ def main():
                       "traffic_bytes_per_step": round((fb + wb) * per_step)}
     doc = {"workload": {"cols": 1241, "rows": 376, "batch": 32},
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "bench.py --no-cpu; FETCH_SIZE x 2 (gfx950 correction), KiB -> bytes",
+                     "bench.py --no-cpu --no-legs (profiles/scripts/refresh_profiles.sh); FETCH_SIZE x 2 "
+                     "(gfx950 correction), KiB -> bytes; per launch and per sub-batch of 64 images",
            "kernels": kernels}
     text = json.dumps(doc, indent=1)
     if len(sys.argv) > 3:

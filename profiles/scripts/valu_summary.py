@@ -4,13 +4,21 @@ import sys
 from collections import defaultdict
 
 path = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmcV/run_counter_collection.csv"
-sub = int(sys.argv[2]) if len(sys.argv) > 2 else 36  # warmup 16 + probe 4 + steps 16
 acc = defaultdict(lambda: defaultdict(float))
+disp = defaultdict(set)
 for row in csv.DictReader(open(path)):
-    acc[row["Kernel_Name"].split("(")[0][:30]][row["Counter_Name"]] += float(row["Counter_Value"])
+    k = row["Kernel_Name"].split("(")[0][:30]
+    acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+    disp[k].add(row["Dispatch_Id"])
+sub = len(disp["k_sft_init"])  # one per C3 sub-batch
+ext = len(disp["k_describe"])  # one per 64-image extraction (the bench's setup adds a few)
+EXTRACT = ("k_fast", "void k_fast", "k_resize", "k_blur", "k_describe", "k_octree", "k_copy0", "k_pyramid")
+print(f"{sub} sub-batches (k_sft_init dispatches), {ext} extractions (k_describe dispatches); extraction "
+      "kernels per extraction, the others per sub-batch")
 tot = defaultdict(float)
 for k, c in sorted(acc.items(), key=lambda kv: -kv[1]["SQ_INSTS_VALU"]):
-    print(f"{k:32s} VALU/sub {c['SQ_INSTS_VALU'] / sub / 1e6:7.2f}M  SALU/sub {c['SQ_INSTS_SALU'] / sub / 1e6:6.2f}M")
+    d = ext if k.startswith(EXTRACT) else sub
+    print(f"{k:32s} VALU {c['SQ_INSTS_VALU'] / d / 1e6:7.2f}M  SALU {c['SQ_INSTS_SALU'] / d / 1e6:6.2f}M")
     for x in c:
-        tot[x] += c[x]
-print(f"total VALU/sub {tot['SQ_INSTS_VALU'] / sub / 1e6:.1f}M  SALU/sub {tot['SQ_INSTS_SALU'] / sub / 1e6:.1f}M")
+        tot[x] += c[x] / d
+print(f"total per sub-batch: VALU {tot['SQ_INSTS_VALU'] / 1e6:.1f}M  SALU {tot['SQ_INSTS_SALU'] / 1e6:.1f}M")
