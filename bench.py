@@ -74,6 +74,9 @@ def parse(argv=None):
     p.add_argument("--extractors", type=int, default=1,
                    help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
                         "own stream with its side-stream work inline (experiment)")
+    p.add_argument("--fast-side", type=int, default=0,
+                   help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
+                        "(0: the library default, levels 0..2)")
     p.add_argument("--level-launches", action="store_true",
                    help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
     p.add_argument("--rehearse", action="store_true",
@@ -199,6 +202,8 @@ def main():
         ext.debug_force_level_launches(True)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
+    if args.fast_side > 0:
+        ext.debug_set_fast_side_levels(args.fast_side)
     exts = [ext]
     if args.extractors > 1:
         exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(args.extractors - 1)]

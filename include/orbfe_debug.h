@@ -30,7 +30,7 @@ int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
 int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
 /* Per-level pyramid path only: FAST of levels 0..k-1 on the side stream, each launched as soon
  * as its level is built, the rest in one launch after the resize chain (k <= 0: the default,
- * level 0 only). The tiled path runs the first group's levels on the side stream. */
+ * levels 0..2). The tiled path runs the first group's levels on the side stream. */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
 /* 1: run the side-stream work (k_blur, the early FAST levels) on the launch stream, for callers
  * that overlap whole extractions on several streams of their own; 0 (default): the handle's

@@ -1279,9 +1279,9 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
 }
 
 template <bool LDSK>
-__device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, int n, uint32_t* ka,
+__device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, int l, int n, uint32_t* ka,
                                            uint32_t* kb) {
-  const int l = blockIdx.x, img = blockIdx.y;
+  const int img = blockIdx.y;
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
   const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
   ONode* nodes0 = reinterpret_cast<ONode*>(smem);
@@ -1635,9 +1635,9 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
 }
 
 
-__global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
+__global__ __launch_bounds__(256) void k_octree(ExtractArgs a, int l0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int l = blockIdx.x, img = blockIdx.y, t = threadIdx.x;
+  const int l = l0 + blockIdx.x, img = blockIdx.y, t = threadIdx.x;  // levels l0 .. l0 + gridDim.x - 1
   const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
   int* sa = reinterpret_cast<int*>(smem + (sizeof(ONode) * 2 + sizeof(int4)) * NC);
   int* sx = sa + 2 * SA;
@@ -1656,9 +1656,9 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a) {
     return;
   }
   if (n <= a.key_lds_cap) {  // keys in LDS (two ping-pong halves)
-    octree_run<true>(a, smem, n, lds_keys, lds_keys + a.key_lds_cap);
+    octree_run<true>(a, smem, l, n, lds_keys, lds_keys + a.key_lds_cap);
   } else {  // very large levels: keys in the global scratch buffers
-    octree_run<false>(a, smem, n, a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin,
+    octree_run<false>(a, smem, l, n, a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin,
                       a.keys_b + (long long)img * a.keyscr_stride + ld.cand_begin);
   }
 }
@@ -2090,7 +2090,7 @@ struct orbfe_extractor {
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level launches)
-  int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: level 0 only)
+  int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: the default, 3 levels)
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
@@ -2631,12 +2631,12 @@ static size_t fast_lds(const orbfe_extractor* h) {
   } while (0)
 
 // How many levels, from level 0 up, get their FAST launch on the side stream as soon as the main
-// stream has built them; the rest run in one launch on the main stream after the resize chain.
-// Measured on MI355X (C3, 64 images): k = 4 shortens a lone extraction by ~3 % but in the
-// benchmark's pipelined steps the side-stream FAST launches only stretch the resize chain and
-// their own duration (no throughput change), so the default stays at level 0 alone.
+// stream has built them; the rest run in one launch after the resize chain. Measured on MI355X
+// (C3 bench, stereo frames/s): 1 level 67.6k, 2 levels 68.7k, 3 levels 69.1-69.4k, 4 levels
+// 69.0k, 5 66.6k, 8 60.3k -- the big levels' FAST fills the CUs the latency-bound resize chain
+// leaves idle, the small ones only stretch the chain.
 static int fast_side_split(const orbfe_extractor* h) {
-  return h->fast_side_levels > 0 ? std::min(h->fast_side_levels, h->nlevels) : 1;
+  return std::min(h->fast_side_levels > 0 ? h->fast_side_levels : 3, h->nlevels);
 }
 
 // Images i0..i0+n-1 of the handle's per-image scratch (pyramid, candidates, octree keys) hold
@@ -2710,10 +2710,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
     return ORBFE_OK;
   };
+  // k_side: the levels whose FAST cells run on the side stream, beside the rest of the pyramid
+  // launches
+  int k_side = 0;
   if (!h->pyr_groups.empty() && !h->force_level_launches) {
-    // the first group writes levels 0..top; their FAST cells run on the side stream beside the
-    // later groups, the rest after them on the main stream
-    const int top0 = h->pyr_groups[0].top;
+    // the first group writes levels 0..top
+    k_side = h->pyr_groups[0].top + 1;
     for (size_t gi = 0; gi < h->pyr_groups.size(); gi++) {
       const PyrGroup& pg = h->pyr_groups[gi];
       dim3 grid(pg.ntx * pg.nty, n);
@@ -2721,13 +2723,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       if (gi == 0) {
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
         ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
-        const int c1 = top0 + 1 < h->nlevels ? h->levels[top0 + 1].cell_begin : a.ncells;
-        launch_fast(side, 0, c1);
+        launch_fast(side, 0, k_side < h->nlevels ? h->levels[k_side].cell_begin : a.ncells);
       }
     }
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
-    if (top0 + 1 < h->nlevels) launch_fast(st, h->levels[top0 + 1].cell_begin, a.ncells);
-    ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   } else {
     {
       const LevelDesc& d = h->levels[0];
@@ -2737,7 +2735,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
     // stream has built it, beside the chain of small dependent resize launches that leaves most
     // CUs idle; levels k..L-1 follow the chain on the main stream
-    const int k_side = fast_side_split(h);
+    k_side = fast_side_split(h);
     if ((int)h->ev_lvl.size() < h->nlevels) {
       for (int l = (int)h->ev_lvl.size(); l < h->nlevels; l++) {
         hipEvent_t e = nullptr;
@@ -2764,12 +2762,23 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       }
       if (l < k_side) side_fast(l);
     }
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
-    if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
-    ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   }
-  // fork: GaussianBlur needs only the pyramid, so it runs on the side stream beside k_octree (a
-  // small, latency-bound grid that leaves most CUs idle); joined before k_describe
+  if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
+  ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)octree_lds(h)));
+  auto launch_octree = [&](hipStream_t s, int l0, int nl) {
+    if (nl <= 0) return;
+    dim3 grid(nl, n);
+    LAUNCH_TIMED(h, 2, s, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), s, a, l0));
+  };
+  // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
+  // only the pyramid, so it runs on the side stream beside k_octree (a small, latency-bound grid
+  // that leaves most CUs idle); joined before k_describe. (Measured on MI355X: DistributeOctTree
+  // of the side's levels on the side stream right after their FAST, beside the main stream's
+  // FAST, is slower -- bench 63.7k vs 67.0k stereo frames/s: it competes with that FAST.)
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
+  if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
+  ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
   ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
   {
@@ -2778,13 +2787,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     LAUNCH_TIMED(h, 5, sd, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, sd, a));
   }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
-  {
-    dim3 grid(h->nlevels, n);
-    if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
-    ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)octree_lds(h)));
-    LAUNCH_TIMED(h, 2, st, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), st, a));
-  }
+  launch_octree(st, 0, h->nlevels);
 
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {

@@ -303,7 +303,7 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_key_cap(self._h, int(cap)), "set_octree_key_cap")
 
     def debug_set_fast_side_levels(self, k: int) -> None:
-        """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: level 0 only)."""
+        """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
     def debug_set_inline_side(self, on: bool = True) -> None:
