@@ -2773,9 +2773,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   };
   // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
   // only the pyramid, so it runs on the side stream beside k_octree (a small, latency-bound grid
-  // that leaves most CUs idle); joined before k_describe. (Measured on MI355X: DistributeOctTree
-  // of the side's levels on the side stream right after their FAST, beside the main stream's
-  // FAST, is slower -- bench 63.7k vs 67.0k stereo frames/s: it competes with that FAST.)
+  // that leaves most CUs idle); joined before k_describe. (Measured on MI355X and not kept:
+  // DistributeOctTree of the side's levels on the side stream right after their FAST, beside the
+  // main stream's FAST -- bench 63.7k vs 67.0k stereo frames/s, it competes with that FAST; the
+  // blur on the side stream as soon as the pyramid is complete -- 65.1k vs 69.3-70.0k.)
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));

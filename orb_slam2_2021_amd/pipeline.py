@@ -133,7 +133,9 @@ class C3Pipeline:
 
         self.sets = [OutSet() for _ in range(max(1, depth))]
         self.lib = L.lib()
-        self.streams = [torch.cuda.Stream(dev) for _ in self.exts]  # extraction (+ ComputeStereoMatches)
+        # extraction (+ ComputeStereoMatches), default priority: giving it the side stream's high
+        # priority measured 64.3k vs 69.6k stereo frames/s (MI355X)
+        self.streams = [torch.cuda.Stream(dev) for _ in self.exts]
         self.stream = self.streams[0]
         self.mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
         self.counter = 0
