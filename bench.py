@@ -74,6 +74,9 @@ def parse(argv=None):
     p.add_argument("--extractors", type=int, default=1,
                    help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
                         "own stream with its side-stream work inline (experiment)")
+    p.add_argument("--defer-matching", action="store_true",
+                   help="enqueue sub-batch i's vocabulary + matching with sub-batch i+1's extraction, after its "
+                        "pyramid (overlapping the FAST / octree / blur / describe phase)")
     p.add_argument("--fast-side", type=int, default=0,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2)")
@@ -116,7 +119,8 @@ class Gatherer:
         self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
         self.recv = ([torch.empty(self.cap_bytes, dtype=torch.uint8, device=comm_dev) for _ in range(world)]
                      if rank == 0 else None)
-        self.pending = None
+        self.pending = None       # packed, exchanged after the next sub-batch is enqueued
+        self.pending_next = None  # packed during the current run
         self.bytes_received = 0
         self.transfers = 0
         self.last = None
@@ -131,6 +135,7 @@ class Gatherer:
 
     def after_run(self):
         prev, self.pending = self.pending, self.pending_next
+        self.pending_next = None
         if prev is not None:
             self.exchange(prev)
 
@@ -212,7 +217,7 @@ def main():
             if args.level_launches:
                 e.debug_force_level_launches(True)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
-                           depth=max(1, args.pipeline),
+                           depth=max(1, args.pipeline), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup)
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
@@ -225,6 +230,12 @@ def main():
         if g:
             g.after_run()
 
+    def drain():  # every enqueued sub-batch matched (and gathered)
+        pipe.flush(after_match=g.pack if g else None)
+        if g:
+            g.after_run()
+            g.flush()
+
     def barrier():
         if world > 1:
             dist.barrier()
@@ -233,8 +244,7 @@ def main():
     torch.cuda.set_stream(pipe.stream)
     for _ in range(args.warmup * S_sub):
         sub_batch()
-    if g:
-        g.flush()
+    drain()
     torch.cuda.synchronize()
     # probe pass (untimed): HIP events around every kernel -> per-kernel durations, dominant kernel
     ext.reset_kernel_times()
@@ -242,8 +252,7 @@ def main():
     pipe.event_sel.update(("k_vocab", "k_sft", "k_stereo"))
     for _ in range(args.probe_subbatches):
         sub_batch()
-    if g:
-        g.flush()
+    drain()
     torch.cuda.synchronize()
     probe = dict(ext.kernel_times())
     probe.update(pipe.event_times())
@@ -279,8 +288,7 @@ def main():
             sub_batch()
             if ev:
                 set_events(False)
-    if g:
-        g.flush()
+    drain()
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()

@@ -118,6 +118,15 @@ int orbfe_reset_kernel_times(orbfe_extractor* h);
 /* Stream the handle launches on (hipStream_t as void*). */
 void* orbfe_extractor_stream(orbfe_extractor* h);
 
+/* Event (hipEvent_t as void*) each launch sequence records on its stream as soon as the image
+ * pyramid is complete (before FAST of the late levels, DistributeOctTree, the blur and the
+ * descriptors). A caller that overlaps its own work with the extraction can order it after the
+ * latency-bound pyramid phase: orbfe_stream_wait_event(its_stream, event) right after the
+ * extract call, before the next one re-records the event. */
+void* orbfe_extractor_pyramid_event(orbfe_extractor* h);
+/* hipStreamWaitEvent(stream, event, 0) for callers without the HIP headers. */
+int orbfe_stream_wait_event(void* stream, void* event);
+
 /* ---- matcher data (packed struct-of-arrays views of Frame / KeyFrame / MapPoint) ---------- */
 
 /* MapPoint occupancy of a keypoint, from Frame::mvpMapPoints / KeyFrame::GetMapPoint:

@@ -115,6 +115,8 @@ _SIGNATURES = {
                                        POINTER(c_int)]),
     "orbfe_reset_kernel_times": (c_int, [c_void_p]),
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
+    "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
+    "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
     "orbfe_matcher_create": (c_int, [c_float, c_int, c_int, POINTER(c_void_p)]),
     "orbfe_matcher_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_stream": (c_void_p, [c_void_p]),

@@ -2095,6 +2095,7 @@ struct orbfe_extractor {
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
+  hipEvent_t ev_pyr = nullptr;              // pyramid complete (orbfe_extractor_pyramid_event)
   std::vector<hipEvent_t> ev_lvl;           // level l built (per-level FAST on the side stream)
   // geometry
   int rows = -1, cols = -1, geom_mode = -1;
@@ -2777,6 +2778,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // DistributeOctTree of the side's levels on the side stream right after their FAST, beside the
   // main stream's FAST -- bench 63.7k vs 67.0k stereo frames/s, it competes with that FAST; the
   // blur on the side stream as soon as the pyramid is complete -- 65.1k vs 69.3-70.0k.)
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));  // the pyramid is complete on st
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
@@ -2869,7 +2871,8 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
       hipEventCreateWithFlags(&h->ev_fork, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_l0, kForkJoinEvent) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_f0, kForkJoinEvent) != hipSuccess) {
+      hipEventCreateWithFlags(&h->ev_f0, kForkJoinEvent) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess) {
     delete h;
     return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_extractor_create: stream creation failed");
   }
@@ -2948,6 +2951,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->ev_l0) hipEventDestroy(h->ev_l0);
   if (h->ev_f0) hipEventDestroy(h->ev_f0);
+  if (h->ev_pyr) hipEventDestroy(h->ev_pyr);
   for (hipEvent_t e : h->ev_lvl) hipEventDestroy(e);
   delete h;
   return ORBFE_OK;
@@ -2981,6 +2985,12 @@ extern "C" int orbfe_max_keypoints(orbfe_extractor* h, int rows, int cols) {
 }
 
 extern "C" void* orbfe_extractor_stream(orbfe_extractor* h) { return h ? (void*)h->stream : nullptr; }
+extern "C" void* orbfe_extractor_pyramid_event(orbfe_extractor* h) { return h ? (void*)h->ev_pyr : nullptr; }
+extern "C" int orbfe_stream_wait_event(void* stream, void* event) {
+  if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stream_wait_event: null event");
+  ORBFE_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+  return ORBFE_OK;
+}
 
 extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8_t* d_imgs,
                                           size_t image_stride, int rows, int cols, size_t pitch,

@@ -222,6 +222,13 @@ class ORBextractor:
     def stream(self) -> int:
         return self._lib.orbfe_extractor_stream(self._h) or 0
 
+    def wait_pyramid(self, stream: int) -> None:
+        """Make `stream` wait for the pyramid of this handle's last extract call
+        (orbfe_extractor_pyramid_event): call right after the extract call."""
+        L.check(self._lib.orbfe_stream_wait_event(c_void_p(stream or 0),
+                                                  c_void_p(self._lib.orbfe_extractor_pyramid_event(self._h))),
+                "orbfe_stream_wait_event")
+
     # ---- mvImagePyramid (ORBextractor.h:100) --------------------------------------------
     def level(self, level: int, image: int = 0) -> np.ndarray:
         p = c_void_p()

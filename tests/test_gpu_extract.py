@@ -151,6 +151,45 @@ def test_batch_equals_single(require_gpu):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
+def test_host_batch_pipeline(require_gpu):
+    """orbfe_extract_batch with >= 8 host images takes the chunked staging / H2D / pieced D2H path:
+    every image equals its own single-image extraction, with a caller pitch wider than the rows,
+    and every image's pyramid stays readable afterwards (each chunk extracted into its own slots)."""
+    import ctypes
+    from orb_slam2_2021_amd import _lib as L
+    n, rows, cols, step = 19, 240, 333, 352
+    imgs = [synth_frame(40 + i, rows, cols) for i in range(n)]
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)
+    cap = ext.max_keypoints(rows, cols)
+    buf = np.zeros((n, rows, step), np.uint8)
+    for i in range(n):
+        buf[i, :, :cols] = imgs[i]
+        buf[i, :, cols:] = 255 - i  # padding bytes the extraction must never read
+    kps = np.empty(n * cap, L.KEYPOINT_DTYPE)
+    desc = np.empty((n * cap, 32), np.uint8)
+    counts = np.zeros(n, np.int32)
+    arr = (ctypes.c_void_p * n)(*[buf[i].ctypes.data for i in range(n)])
+    L.check(L.lib().orbfe_extract_batch(ext._h, n, ctypes.cast(arr, ctypes.c_void_p), rows, cols,
+                                        ctypes.c_size_t(step), L.ptr(kps), L.ptr(desc), cap, L.ptr(counts)),
+            "orbfe_extract_batch")
+    levels = [[ext.level(l, image=i).copy() for l in range(8)] for i in range(n)]
+    single = ORBextractor(1000, 1.2, 8, 20, 7)
+    for i in range(n):
+        k1, d1 = single(imgs[i])
+        c = int(counts[i])
+        assert c == len(k1), i
+        kb, db = kps[i * cap:i * cap + c], desc[i * cap:i * cap + c]
+        for f in ("x", "y", "size", "response", "octave", "angle"):
+            assert np.array_equal(kb[f], k1[f]), (i, f)
+        assert np.array_equal(db, d1), i
+        for l in range(8):
+            assert np.array_equal(levels[i][l], single.level(l)), (i, l)
+    # one image through the oracle as well
+    kr, dr = RefExtractor(1000, 1.2, 8, 20, 7)(imgs[7])
+    c = int(counts[7])
+    assert c == len(kr) and np.array_equal(desc[7 * cap:7 * cap + c], dr)
+
+
 def test_repeatable(require_gpu):
     img = synth_frame(9, 376, 1241)
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
