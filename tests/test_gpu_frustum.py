@@ -113,3 +113,30 @@ def test_c5_50k_long_claim_chains_continue_rounds(require_gpu, idx):
     assert (nm, nv) == (wnm, wnv)
     assert np.array_equal(best, wbest)
     assert serial == 0, f"serial walk after {rounds} rounds"
+
+
+def test_c5_shape_50k_mappoints(require_gpu):
+    """BASELINE config C5's shape: a 640x480 frame (arducam.yaml's 12/7 thresholds) against 50k
+    local MapPoints through orbfe_search_local_points, th = 3 (Tracking.cc:1186-1213), bit-exact
+    with the oracle (the pose and map of bench.py's C5 leg)."""
+    ext = ORBextractor(2000, 1.2, 8, 12, 7)
+    k0, d0 = ext(synth_frame(7, 480, 640))
+    rng = np.random.default_rng(0x50C0DE)
+    sc, s2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+    F0 = S.make_frame(k0, d0, sc, s2, 480, 640, S.ARDUCAM_CAM, rng, mp_frac=0.0, tcw=S.pose(tx=0.1, yaw=0.02))
+    G = S.make_local_map(F0, 50000, rng)
+    k, d = ext(synth_frame(103, 480, 640))
+    F = S.Frame(keys_un=k, descriptors=d, u_right=np.full(len(k), -1.0, np.float32),
+                mp_state=np.zeros(len(k), np.uint8), scale_factors=sc, level_sigma2=s2, min_x=0.0, max_x=640.0,
+                min_y=0.0, max_y=480.0, tcw=S.pose(tx=0.106, yaw=0.023), **S.ARDUCAM_CAM)
+    m = ORBmatcher(0.8, True)
+    nm, best, nv, lm = m.SearchLocalPoints(F, G, 3.0)
+    wnm, wbest, wnv, want = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8)
+    assert (nm, nv) == (wnm, wnv) and nv > 10000 and nm > 100
+    assert np.array_equal(best, wbest), f"best_idx differs at {np.flatnonzero(best != wbest)[:5]}"
+    assert_frustum_equal(lm.flags, lm, want["flags"], want)
+    # the same oracle source built with the reference's own flags (-O3 -march=native: GCC's default
+    # -ffp-contract=fast fuses multiply-adds) rounds some projections differently (DESIGN.md section 3)
+    # but makes the same matches here
+    nnm, nbest, nnv, _ = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8, kind="native")
+    assert (nnm, nnv) == (nm, nv) and np.array_equal(nbest, best)
