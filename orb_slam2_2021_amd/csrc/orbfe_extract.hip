@@ -332,12 +332,16 @@ __device__ __forceinline__ uint32_t resize_win_row(const uint32_t W0r0, const ui
   return packed;
 }
 
-__global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l) {
+// Items (4-column group, row pair) of the level are numbered row-major and dealt to the threads
+// linearly, so only the last wave of an image's grid has idle lanes (a 2-D grid of 256-column
+// blocks left up to a third of the lanes idle on the right edge of every row band).
+__global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G, uint32_t gmagic) {
   const LevelDesc ld = a.levels[l];
-  const int g = blockIdx.x * 64 + threadIdx.x, x = 4 * g;
-  const int y0 = (blockIdx.y * 4 + threadIdx.y) * 2;
-  const int img = blockIdx.z;
-  if (x >= ld.w || y0 >= ld.h) return;
+  const int item = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
+  const int pr = gmagic ? (int)__umulhi((uint32_t)item, gmagic) : item;  // item / G
+  const int g = item - pr * G, x = 4 * g;
+  const int y0 = 2 * pr;
+  if (y0 >= ld.h) return;
   const LevelDesc ls = a.levels[l - 1];
   const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ls.pyr_off;
   const int gi = ld.rgrp_begin + g;
@@ -2755,8 +2759,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     for (int l = 1; l < h->nlevels; l++) {
       const LevelDesc& d = h->levels[l];
       if (d.rwin_ok) {
-        dim3 grid((d.w + 255) / 256, (d.h + 7) / 8, n), block(64, 4);
-        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win, grid, block, 0, st, a, l));
+        const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
+        const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
+        dim3 grid((items + 255) / 256, n);
+        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win, grid, dim3(256), 0, st, a, l, G, gm));
       } else {
         dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
         LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
