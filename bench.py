@@ -65,21 +65,26 @@ def parse(argv=None):
     p.add_argument("--no-kernel-events", action="store_true")
     p.add_argument("--no-legs", action="store_true", help="skip the secondary measurements")
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last sub-batch")
-    p.add_argument("--pipeline", type=int, default=2,
-                   help="output sets in flight: 2 overlaps a sub-batch's matching with the next one's "
-                        "extraction (1: strictly one at a time)")
+    p.add_argument("--pipeline", type=int, default=0,
+                   help="output sets in flight (0: 2 per extractor handle; 1: strictly one at a time)")
     p.add_argument("--stereo", action="store_true",
                    help="run Frame::ComputeStereoMatches on every pair after extraction (the stereo "
                         "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
-    p.add_argument("--extractors", type=int, default=1,
+    p.add_argument("--extractors", type=int, default=2,
                    help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
-                        "own stream with its side-stream work inline (experiment)")
+                        "own stream, their side-stream work on one shared high-priority stream")
     p.add_argument("--defer-matching", action="store_true",
                    help="enqueue sub-batch i's vocabulary + matching with sub-batch i+1's extraction, after its "
                         "pyramid (overlapping the FAST / octree / blur / describe phase)")
     p.add_argument("--fast-side", type=int, default=0,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2)")
+    p.add_argument("--match-inline", action="store_true",
+                   help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
+    p.add_argument("--torch-streams", action="store_true",
+                   help="diagnostic: the pipeline's streams from torch's pool, created after the "
+                        "handles (hardware-queue assignment then depends on the stream count; with "
+                        "several extractors their side work runs inline)")
     p.add_argument("--level-launches", action="store_true",
                    help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
     p.add_argument("--rehearse", action="store_true",
@@ -130,7 +135,7 @@ class Gatherer:
         p = self.pipe
         pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
                               self.bufs[id(o)].data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
-                              p.mstream.cuda_stream)
+                              o.mstream.cuda_stream)
         self.pending_next = o
 
     def after_run(self):
@@ -142,9 +147,9 @@ class Gatherer:
     def exchange(self, o):
         import torch
         from orb_slam2_2021_amd.parallel import gather_packed
-        with torch.cuda.stream(self.pipe.mstream):
+        with torch.cuda.stream(o.mstream):
             if self.comm_dev.type == "cpu":  # --rehearse: gloo, staged through the host
-                self.pipe.mstream.synchronize()
+                o.mstream.synchronize()
                 out, sizes = gather_packed(self.bufs[id(o)].cpu(), self.sizes[id(o)].cpu(), dst=0, recv=self.recv)
             else:
                 out, sizes = gather_packed(self.bufs[id(o)], self.sizes[id(o)], dst=0, recv=self.recv)
@@ -153,7 +158,7 @@ class Gatherer:
             self.transfers += len(sizes) - 1
             self.last = out
         # the set may be reused only after its payload left: record after the transfers
-        o.matched.record(self.pipe.mstream)
+        o.matched.record(o.mstream)
 
     def flush(self):
         if self.pending is not None:
@@ -173,14 +178,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    gpu = 0 if (world == 1 or args.rehearse) else local
+    torch.cuda.set_device(gpu)
+    # the pipeline's busy streams first, before RCCL, torch's stream pool or any handle creates
+    # one, so that each opens its own hardware queue (PipelineStreams)
+    from orb_slam2_2021_amd.pipeline import PipelineStreams
+    n_ext = max(1, args.extractors)
+    pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
-        torch.cuda.set_device(0)
         dist.init_process_group("gloo")
     elif world > 1:
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
     if world > 1:
         assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -210,15 +218,20 @@ def main():
     if args.fast_side > 0:
         ext.debug_set_fast_side_levels(args.fast_side)
     exts = [ext]
-    if args.extractors > 1:
-        exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(args.extractors - 1)]
+    if n_ext > 1:
+        # several handles extract consecutive sub-batches concurrently; their side-stream work
+        # shares one high-priority stream (PipelineStreams.side)
+        exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_ext - 1)]
         for e in exts:
-            e.debug_set_inline_side(True)
+            if pstreams is None:
+                e.debug_set_inline_side(True)
+            if args.fast_side > 0:
+                e.debug_set_fast_side_levels(args.fast_side)
             if args.level_launches:
                 e.debug_force_level_launches(True)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
-                           depth=max(1, args.pipeline), defer=args.defer_matching,
-                           stereo=args.stereo, levelsup=args.levelsup)
+                           depth=pipe_depth(args), defer=args.defer_matching,
+                           stereo=args.stereo, levelsup=args.levelsup, streams=pstreams)
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
     counter = [0]
@@ -247,22 +260,25 @@ def main():
     drain()
     torch.cuda.synchronize()
     # probe pass (untimed): HIP events around every kernel -> per-kernel durations, dominant kernel
-    ext.reset_kernel_times()
-    ext.set_profiling(True)
+    for e in exts:
+        e.reset_kernel_times()
+        e.set_profiling(True)
     pipe.event_sel.update(("k_vocab", "k_sft", "k_stereo"))
     for _ in range(args.probe_subbatches):
         sub_batch()
     drain()
     torch.cuda.synchronize()
-    probe = dict(ext.kernel_times())
+    probe = merged_kernel_times(exts)
     probe.update(pipe.event_times())
     probe = {k: v for k, v in probe.items() if v[1] > 0}
-    ext.set_profiling(False)
+    for e in exts:
+        e.set_profiling(False)
     pipe.event_sel.clear()
     pipe.clear_events()
     dominant = max(probe, key=lambda k: probe[k][0])
     # timed region: events only around the dominant kernel's launches, on every n-th sub-batch
-    ext.reset_kernel_times()
+    for e in exts:
+        e.reset_kernel_times()
     ev_every = max(1, args.event_every)
     timed_events = 0
 
@@ -270,7 +286,8 @@ def main():
         if args.no_kernel_events:
             return
         if dominant in ext.KERNELS:
-            ext.set_profiling([dominant] if on else False)
+            for e in exts:
+                e.set_profiling([dominant] if on else False)
         elif on:
             pipe.event_sel.add(dominant)
         else:
@@ -281,7 +298,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         for k in range(S_sub):
-            ev = k % ev_every == 0
+            ev = (k // n_ext) % ev_every == 0  # n_ext consecutive sub-batches: every handle
             if ev:
                 set_events(True)
                 timed_events += 1
@@ -289,10 +306,11 @@ def main():
             if ev:
                 set_events(False)
     drain()
+    t_enq = time.perf_counter()  # every launch of the timed region enqueued
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
-    timed = dict(ext.kernel_times())
+    timed = merged_kernel_times(exts)
     timed.update(pipe.event_times())
     timed = {k: v for k, v in timed.items() if v[1] > 0}
     elapsed = t1 - t0
@@ -305,7 +323,7 @@ def main():
     value = frames / elapsed
     last = pipe.last
     counts = last.cnt.cpu().numpy()
-    cand = ext.debug_candidate_total()
+    cand = pipe.exts[(pipe.counter - 1) % len(pipe.exts)].debug_candidate_total()  # last sub-batch's handle
     nm = last.nm.cpu().numpy()
     geo = ext.geometry(H, W)
     use_timed = dominant in timed and not args.no_kernel_events
@@ -326,6 +344,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -343,8 +362,9 @@ def main():
             "stereo_frames_per_gpu_per_subbatch": B, "subbatches_per_step": S_sub,
             "stereo_frames_per_gpu_per_step": B * S_sub, "distinct_input_batches": NB,
             "parallelism": f"frame-sharded x{world}",
-            "pipeline": f"{pipe_depth(args)} output sets: sub-batch i's matching overlaps i+1's extraction"
-                        if args.pipeline > 1 else "one sub-batch at a time",
+            "pipeline": (f"{n_ext} extractor handles on their own streams (consecutive sub-batches' "
+                         f"extractions overlap), {'matching inline' if args.match_inline else 'matching on its own stream'}, "
+                         f"{pipe_depth(args)} output sets" if pipe_depth(args) > 1 else "one sub-batch at a time"),
         },
         "roofline": roof,
         "pipeline_hbm": {
@@ -404,7 +424,19 @@ def main():
 
 
 def pipe_depth(args):
-    return max(1, args.pipeline)
+    """Output sets in flight: --pipeline, or 2 per extractor handle (sub-batch i's set is reused
+    by i + depth, whose handle then finished i + depth - n_ext's extraction long before)."""
+    return args.pipeline if args.pipeline > 0 else 2 * max(1, args.extractors)
+
+
+def merged_kernel_times(exts):
+    """{kernel: (total ms, launches)} summed over the extractor handles."""
+    out = {}
+    for e in exts:
+        for k, (t, n) in e.kernel_times().items():
+            a = out.get(k, (0.0, 0))
+            out[k] = (a[0] + t, a[1] + n)
+    return out
 
 
 def level_pixels(geo):

@@ -126,6 +126,14 @@ void* orbfe_extractor_stream(orbfe_extractor* h);
 void* orbfe_extractor_pyramid_event(orbfe_extractor* h);
 /* hipStreamWaitEvent(stream, event, 0) for callers without the HIP headers. */
 int orbfe_stream_wait_event(void* stream, void* event);
+/* A non-blocking stream on `device` (high_priority: the device's greatest priority, as the
+ * extractor's side stream). The runtime maps streams onto a few hardware queues per priority
+ * (GPU_MAX_HW_QUEUES, 4 by default), choosing the least-shared queue at creation and the
+ * first queue on a tie; two busy streams that end up on one queue serialise. A caller that
+ * runs several streams concurrently (e.g. extraction, side and matching streams of a
+ * pipeline) creates them first, before any other stream, so that each takes its own queue. */
+int orbfe_stream_create(int device, int high_priority, void** out);
+int orbfe_stream_destroy(void* stream);
 
 /* ---- matcher data (packed struct-of-arrays views of Frame / KeyFrame / MapPoint) ---------- */
 

@@ -36,6 +36,9 @@ int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
  * that overlap whole extractions on several streams of their own; 0 (default): the handle's
  * high-priority side stream. */
 int orbfe_debug_set_inline_side(orbfe_extractor* h, int on);
+/* The side-stream work on a caller's stream (e.g. one high-priority stream shared by several
+ * handles whose extractions overlap); NULL restores the handle's own side stream. */
+int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

@@ -75,7 +75,8 @@ int orbfe_vocab_transform(orbfe_vocabulary* v, const uint8_t* desc, int n, int l
 /* Device batch: image i has d_counts[i] descriptors at d_desc + i*desc_stride. Its FeatureVector
  * goes to d_node_ids + i*cap, d_offsets + i*(cap+1), d_indices + i*cap, d_n_nodes[i]; its
  * BowVector to d_bow_words + i*cap, d_bow_weights + i*cap, d_bow_n[i] (all three NULL: the
- * FeatureVector only). cap <= 8192. */
+ * FeatureVector only). cap <= 8192. The handle keeps its launch scratch per stream: batches
+ * enqueued on different streams may run concurrently (the node table is read-only). */
 int orbfe_vocab_transform_batch_device(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc,
                                        size_t desc_stride, const int32_t* d_counts, int levelsup,
                                        uint32_t* d_bow_words, double* d_bow_weights,

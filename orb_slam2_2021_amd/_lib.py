@@ -117,6 +117,8 @@ _SIGNATURES = {
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
     "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
     "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
+    "orbfe_stream_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "orbfe_stream_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_create": (c_int, [c_float, c_int, c_int, POINTER(c_void_p)]),
     "orbfe_matcher_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_stream": (c_void_p, [c_void_p]),
@@ -145,6 +147,7 @@ _SIGNATURES = {
     "orbfe_debug_force_level_launches": (c_int, [c_void_p, c_int]),
     "orbfe_debug_set_fast_side_levels": (c_int, [c_void_p, c_int]),
     "orbfe_debug_set_inline_side": (c_int, [c_void_p, c_int]),
+    "orbfe_set_side_stream": (c_int, [c_void_p, c_void_p]),
     "orbfe_debug_get_umax": (c_int, [c_void_p, c_void_p]),
     "orbfe_debug_steer_trig": (c_int, [c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]),
     "orbfe_vocab_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

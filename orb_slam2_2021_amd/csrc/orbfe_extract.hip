@@ -2098,6 +2098,7 @@ struct orbfe_extractor {
   int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level launches)
   int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: the default, 3 levels)
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
+  hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2654,7 +2655,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // the handle's high-priority side stream (k_blur and the early FAST levels beside the main chain),
   // or the launch stream itself when the caller overlaps whole extractions instead
   // (orbfe_debug_set_inline_side)
-  const hipStream_t side = h->inline_side ? st : h->side;
+  const hipStream_t side = h->inline_side ? st : (h->side_ext ? h->side_ext : h->side);
   ExtractArgs a;
   std::memset(&a, 0, sizeof(a));
   a.levels = h->d_levels;
@@ -2994,6 +2995,27 @@ extern "C" int orbfe_max_keypoints(orbfe_extractor* h, int rows, int cols) {
 
 extern "C" void* orbfe_extractor_stream(orbfe_extractor* h) { return h ? (void*)h->stream : nullptr; }
 extern "C" void* orbfe_extractor_pyramid_event(orbfe_extractor* h) { return h ? (void*)h->ev_pyr : nullptr; }
+extern "C" int orbfe_stream_create(int device, int high_priority, void** out) {
+  if (!out) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stream_create: out is NULL");
+  *out = nullptr;
+  hipStream_t s = nullptr;
+  ORBFE_HIP_CHECK(hipSetDevice(device));
+  if (high_priority) {
+    ORBFE_HIP_CHECK(create_side_stream(&s));
+  } else {
+    ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  *out = (void*)s;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_stream_destroy(void* stream) {
+  if (!stream) return ORBFE_OK;
+  ORBFE_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  ORBFE_HIP_CHECK(hipStreamDestroy((hipStream_t)stream));
+  return ORBFE_OK;
+}
+
 extern "C" int orbfe_stream_wait_event(void* stream, void* event) {
   if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stream_wait_event: null event");
   ORBFE_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
@@ -3387,6 +3409,12 @@ extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float
                        (float)(M_PI / 180.f), d_cos, d_sin);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_HIP_CHECK(hipStreamSynchronize(st));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_set_side_stream(orbfe_extractor* h, void* stream) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->side_ext = (hipStream_t)stream;
   return ORBFE_OK;
 }
 

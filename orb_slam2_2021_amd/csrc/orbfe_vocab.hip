@@ -73,8 +73,14 @@ struct orbfe_vocabulary {
   // scratch
   uint8_t* d_scratch = nullptr;  // host-call staging
   size_t scratch_bytes = 0;
-  unsigned long long* d_keys = nullptr;  // FeatureVector keys, BowVector keys, leaf node per feature
-  size_t keys_bytes = 0;
+  // FeatureVector keys, BowVector keys, leaf node per feature: one buffer per launch stream, so
+  // that transforms enqueued on different streams may run concurrently
+  struct KeyScratch {
+    hipStream_t stream;
+    unsigned long long* d_keys;
+    size_t bytes;
+  };
+  std::vector<KeyScratch> keys;
 };
 
 struct VocabArgs {
@@ -565,7 +571,7 @@ extern "C" int orbfe_vocab_destroy(orbfe_vocabulary* v) {
   hipFree(v->d_rec);
   hipFree(v->d_weight);
   hipFree(v->d_scratch);
-  hipFree(v->d_keys);
+  for (auto& k : v->keys) hipFree(k.d_keys);
   if (v->stream) hipStreamDestroy(v->stream);
   delete v;
   return ORBFE_OK;
@@ -605,13 +611,21 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   while (P2 < cap) P2 <<= 1;
   const size_t slots = (size_t)cap * n_images;
   const size_t need = slots * (2 * sizeof(unsigned long long) + sizeof(int32_t));
-  if (need > v->keys_bytes) {
-    hipFree(v->d_keys);
-    v->d_keys = nullptr;
-    ORBFE_HIP_CHECK(hipMalloc(&v->d_keys, need));
-    v->keys_bytes = need;
+  orbfe_vocabulary::KeyScratch* ks = nullptr;
+  for (auto& k : v->keys)
+    if (k.stream == s) ks = &k;
+  if (!ks) {
+    v->keys.push_back({s, nullptr, 0});
+    ks = &v->keys.back();
   }
-  unsigned long long* fvk = v->d_keys;
+  if (need > ks->bytes) {
+    hipFree(ks->d_keys);  // synchronises the device: no launch still reads it
+    ks->d_keys = nullptr;
+    ks->bytes = 0;
+    ORBFE_HIP_CHECK(hipMalloc(&ks->d_keys, need));
+    ks->bytes = need;
+  }
+  unsigned long long* fvk = ks->d_keys;
   unsigned long long* bwk = fvk + slots;
   int32_t* leaves = reinterpret_cast<int32_t*>(bwk + slots);
   const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * P2 : 0);

@@ -313,6 +313,10 @@ class ORBextractor:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
+    def set_side_stream(self, stream: int) -> None:
+        """Run the side-stream work on `stream` (a hipStream_t address; 0 restores the handle's own)."""
+        L.check(self._lib.orbfe_set_side_stream(self._h, c_void_p(stream or 0)), "set_side_stream")
+
     def debug_set_inline_side(self, on: bool = True) -> None:
         """Run the side-stream work (k_blur, early FAST levels) on the launch stream."""
         L.check(self._lib.orbfe_debug_set_inline_side(self._h, 1 if on else 0), "set_inline_side")

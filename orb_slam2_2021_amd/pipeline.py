@@ -42,11 +42,48 @@ def nodes_at_level_bound(tree, levelsup: int, cap: int) -> int:
     return max(1, min(cap, n))
 
 
+class PipelineStreams:
+    """The pipeline's concurrently busy streams, created natively in one go: one extraction stream
+    per extractor, the matching stream, and (several extractors) one high-priority side stream
+    they share. The runtime spreads streams over GPU_MAX_HW_QUEUES hardware queues per priority
+    (4 by default), each new stream taking the least-shared queue and the first one on a tie, so
+    the queue a stream lands on depends on every stream the process created before it; two busy
+    streams on one queue serialise (measured on MI355X: 35.2k instead of 68.9k stereo frames/s
+    after two idle streams had been created in between). Created before any other stream of the
+    process, the busy streams each open a queue of their own."""
+
+    def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False):
+        import torch
+        self.device = device
+        self._ptrs = []
+
+        def make(high):
+            p = ctypes.c_void_p()
+            L.check(L.lib().orbfe_stream_create(device, 1 if high else 0, ctypes.byref(p)), "stream_create")
+            self._ptrs.append(p.value)
+            return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
+
+        self.extract = [make(False) for _ in range(max(1, n_extractors))]
+        # match_inline: each sub-batch's vocabulary + matching follow its extraction on the same
+        # stream (the other extractors' streams provide the overlap)
+        self.match = None if match_inline else make(False)
+        self.side = make(True)
+
+    def ordered(self):
+        """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
+        return self.extract + [self.match]
+
+    def close(self):
+        for p in self._ptrs:
+            L.lib().orbfe_stream_destroy(ctypes.c_void_p(p))
+        self._ptrs = []
+
+
 class C3Pipeline:
     def __init__(self, ext, voc, tree, B: int, H: int, W: int, cam: dict, F12: np.ndarray,
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
-                 nnratio: float = 0.6, check_ori: bool = False, defer: bool = False):
+                 nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -113,6 +150,7 @@ class C3Pipeline:
                     p.fv2_nodes_dev = self.nodes.data_ptr() + (B + i) * 4
                 self.extracted = torch.cuda.Event()
                 self.matched = torch.cuda.Event()
+                self.mstream = None  # the stream the last matching of this set ran on
 
             def view(self, i):
                 v = L.frame_view()
@@ -144,9 +182,21 @@ class C3Pipeline:
         self.lib = L.lib()
         # extraction (+ ComputeStereoMatches), default priority: giving it the side stream's high
         # priority measured 64.3k vs 69.6k stereo frames/s (MI355X)
-        self.streams = [torch.cuda.Stream(dev) for _ in self.exts]
+        # `streams` = (one extraction stream per extractor, the matching stream), or a
+        # PipelineStreams the caller created before anything else (hardware-queue assignment)
+        if isinstance(streams, PipelineStreams):
+            for e in self.exts:
+                e.set_side_stream(streams.side.cuda_stream)
+            streams = streams.ordered()
+        if streams is None:
+            streams = [torch.cuda.Stream(dev) for _ in range(len(self.exts) + 1)]
+        assert len(streams) == len(self.exts) + 1
+        self.streams = list(streams[:-1])
         self.stream = self.streams[0]
-        self.mstream = torch.cuda.Stream(dev)  # vocabulary + matching (+ gather)
+        # vocabulary + matching (+ gather); None: on each sub-batch's extraction stream
+        self.match_inline = streams[-1] is None
+        assert not (self.match_inline and defer), "deferred matching needs the matching stream"
+        self.mstream = self.stream if self.match_inline else streams[-1]
         self.counter = 0
         self.last = None
         # optional HIP events around the vocabulary / matching / stereo launches
@@ -184,6 +234,8 @@ class C3Pipeline:
                 self.events["k_stereo"].append(tuple(ev))
         o.extracted.record(s)
         self.last = o
+        if self.match_inline:
+            self.mstream = s
         if not self.defer:
             self._match(o, after_match)
             return o
@@ -201,8 +253,9 @@ class C3Pipeline:
 
     def _match(self, o, after_match):
         B, cap = self.B, self.cap
-        m = self.mstream
-        m.wait_event(o.extracted)
+        m = o.mstream = self.mstream
+        if not self.match_inline:
+            m.wait_event(o.extracted)
         ev = []
         self._ev("k_vocab", m, ev)
         bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
@@ -270,7 +323,7 @@ class C3Pipeline:
 
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
-             stereo: bool = False, levelsup: int = 4, defer: bool = False):
+             stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None):
     """The C3 scene of bench.py: KITTI intrinsics, the KeyFrame pair geometry of a stereo
     baseline (t2 = -0.537 m, 0.05 m forward), F12 and epipole from LocalMapping::ComputeF12, and
     seeded KeyFrame state per keypoint slot (half the keypoints stereo, 30 % with a MapPoint).
@@ -297,7 +350,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     pipe = C3Pipeline(exts, voc, tree, B, H, W, cam, F12, (ex, ey),
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
-                      levelsup=levelsup, stereo=stereo, defer=defer)
+                      levelsup=levelsup, stereo=stereo, defer=defer, streams=streams)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo)
     return pipe, state

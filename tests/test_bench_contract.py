@@ -45,6 +45,8 @@ def test_cli_defaults():
     finally:
         sys.argv = saved
     assert a.gpus == 1 and 0 < a.steps <= 100 and 0 <= a.warmup <= 20 and a.batch == 32
-    assert a.pipeline == 2 and a.input_batches >= 4 and a.vocab_levels == 6 and a.levelsup == 4
+    assert a.input_batches >= 4 and a.vocab_levels == 6 and a.levelsup == 4
+    # two extractor handles, two output sets each
+    assert a.extractors == 2 and bench.pipe_depth(a) == 4
     # a step is long enough to be seen (>= 1024 sub-batches of 32 stereo frames)
     assert a.batches_per_step * a.batch >= 32 * 1024

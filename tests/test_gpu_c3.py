@@ -55,3 +55,29 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, stereo):
         assert min(len(k) for k in out["keypoints"]) >= 2000
         assert int(np.sum(out["nmatches"])) > 32 * 50
         assert all(len(b[0]) > 100 for b in out["bow"])
+
+
+@pytest.mark.parametrize("match_inline,stereo", [(False, False), (True, False), (False, True)])
+def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo):
+    """bench.py's default schedule: two extractor handles extract consecutive sub-batches on their
+    own streams (side-stream work on one shared high-priority stream), matching on its own stream
+    or inline after each extraction (then two vocabulary transforms run concurrently on the one
+    handle: per-stream scratch), four output sets."""
+    import torch
+    from orb_slam2_2021_amd.pipeline import PipelineStreams
+    tree, voc, ref = vocab
+    B = 32
+    exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(2)]
+    streams = PipelineStreams(0, 2, match_inline=match_inline)
+    pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams)
+    batches = [frames(B, 0), frames(B, 1000), frames(B, 2000)]
+    d = [torch.from_numpy(b).to("cuda") for b in batches]
+    for j in range(7):  # sub-batch j: input j % 3, set j % 4, handle j % 2
+        pipe.run(d[j % 3].data_ptr())
+    torch.cuda.synchronize()
+    for j in (4, 5, 6):
+        out = pipe.to_host(pipe.sets[j % 4])
+        r = check_c3(batches[j % 3], out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"],
+                     st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"])
+        assert r["all"], (j, r)
+    streams.close()
