@@ -806,6 +806,59 @@ __device__ __forceinline__ int fast_prefilter4(const uint8_t* roi, int dw, int d
   return nlist;
 }
 
+// The same prefilter for cells whose detection rows fit 8 groups of 4 (dw <= 32: every full cell
+// of the 30-pixel grid, whose cells are 30-32 pixels wide): lane = (row of 8, group), so a lane's
+// group and its column mask are fixed for the whole cell and rows advance by a constant. The four
+// sign bits land in bytes 0..3 of one dword by a single v_perm (bits 7, 15, 23, 31), masked by
+// the precomputed column mask; a lane writes its survivors by a loop over its set bits.
+template <int RSC, int XO>
+__device__ __forceinline__ int fast_prefilter4_g8(const uint8_t* roi, int dw, int dh, uint32_t T2, uint16_t* list) {
+  static_assert(RSC % 4 == 0, "dword rows");
+  constexpr int RD = RSC / 4;
+  constexpr int OC = XO + 3, OR = XO + 6;
+  const int lane = lane_id(), g = lane & 7, rs = lane >> 3;
+  const int nv = dw - 4 * g;
+  const uint32_t vmask = nv >= 4 ? 0x80808080u : nv <= 0 ? 0u : (0x80808080u >> (8 * (4 - nv)));
+  const uint32_t* row = reinterpret_cast<const uint32_t*>(roi) + (rs + 3) * RD + g;
+  int nlist = 0;
+  for (int r0 = 0; r0 < dh; r0 += 8, row += 8 * RD) {
+    const int rr = r0 + rs;
+    const uint32_t* up = row - 3 * RD;
+    const uint32_t* dn = row + 3 * RD;
+    const uint32_t w0 = row[0], w1 = row[1], w2 = row[2];
+    const uint32_t w3 = XO == 3 ? row[3] : 0u;
+    const uint32_t l = XO == 0 ? w0 : __builtin_amdgcn_alignbyte(w1, w0, XO);
+    uint32_t c, r, u, d;
+    if constexpr (OC < 4) c = __builtin_amdgcn_alignbyte(w1, w0, OC);
+    else if constexpr (OC == 4) c = w1;
+    else c = __builtin_amdgcn_alignbyte(w2, w1, OC - 4);
+    if constexpr (OR < 8) r = __builtin_amdgcn_alignbyte(w2, w1, OR - 4);
+    else if constexpr (OR == 8) r = w2;
+    else r = __builtin_amdgcn_alignbyte(w3, w2, OR - 8);
+    if constexpr ((OC & 3) == 0) {
+      u = up[OC >> 2];
+      d = dn[OC >> 2];
+    } else {
+      u = __builtin_amdgcn_alignbyte(up[(OC >> 2) + 1], up[OC >> 2], OC & 3);
+      d = __builtin_amdgcn_alignbyte(dn[(OC >> 2) + 1], dn[OC >> 2], OC & 3);
+    }
+    const uint32_t re = quick2(pk_even(c), pk_even(u), pk_even(d), pk_even(l), pk_even(r), T2);
+    const uint32_t ro = quick2(pk_odd(c), pk_odd(u), pk_odd(d), pk_odd(l), pk_odd(r), T2);
+    // pixel k's sign bit at bit 8k + 7: bytes (re.1, ro.1, re.3, ro.3)
+    uint32_t m = __builtin_amdgcn_perm(ro, re, 0x07030501u) & (rr < dh ? vmask : 0u);
+    const int n = __popc(m);
+    const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
+    int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
+    const int px = (rr << 6) + 4 * g;  // list entry r << 6 | c
+    while (m) {
+      list[pos++] = (uint16_t)(px + (__builtin_ctz(m) >> 3));
+      m &= m - 1u;
+    }
+    nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  }
+  return nlist;
+}
+
 __device__ __forceinline__ uint32_t pack_key(int x, int y, int s) {
   return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
 }
@@ -970,11 +1023,20 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
     const uint32_t T2 = (uint32_t)t * 0x10001u;
     int nlist = 0;
     if constexpr (RSC != 0) {
-      switch (xo) {
-        case 0: nlist = fast_prefilter4<RSC, 0>(roi, dw, dh, T2, list); break;
-        case 1: nlist = fast_prefilter4<RSC, 1>(roi, dw, dh, T2, list); break;
-        case 2: nlist = fast_prefilter4<RSC, 2>(roi, dw, dh, T2, list); break;
-        default: nlist = fast_prefilter4<RSC, 3>(roi, dw, dh, T2, list); break;
+      if (dw <= 32) {
+        switch (xo) {
+          case 0: nlist = fast_prefilter4_g8<RSC, 0>(roi, dw, dh, T2, list); break;
+          case 1: nlist = fast_prefilter4_g8<RSC, 1>(roi, dw, dh, T2, list); break;
+          case 2: nlist = fast_prefilter4_g8<RSC, 2>(roi, dw, dh, T2, list); break;
+          default: nlist = fast_prefilter4_g8<RSC, 3>(roi, dw, dh, T2, list); break;
+        }
+      } else {
+        switch (xo) {
+          case 0: nlist = fast_prefilter4<RSC, 0>(roi, dw, dh, T2, list); break;
+          case 1: nlist = fast_prefilter4<RSC, 1>(roi, dw, dh, T2, list); break;
+          case 2: nlist = fast_prefilter4<RSC, 2>(roi, dw, dh, T2, list); break;
+          default: nlist = fast_prefilter4<RSC, 3>(roi, dw, dh, T2, list); break;
+        }
       }
     } else {
       const int pw = (dw + 1) >> 1;
