@@ -63,7 +63,7 @@ extern "C" const char* orbfe_version(void) { return "orbfe 0.1 gfx950"; }
 // geometry tables (host-computed, uploaded once per image shape)
 struct LevelDesc {
   int w, h, pitch;
-  int pad0;
+  int blur_h;                // k_blur: row bands per wavefront of the narrow last column strip (0: none)
   long long pyr_off;     // byte offset of column 0, row 0 of this level in one image's block
   int cell_begin, ncells;
   int cand_begin, cand_cap;  // candidate slots of this level inside one image's candidate block
@@ -76,7 +76,7 @@ struct LevelDesc {
   int size;                  // scaledPatchSize (:840)
   int tab_x, tab_y;          // resize table offsets (l >= 1)
   int xmax, simd_end;        // resize: first column using the clamped path / end of SIMD columns
-  int tile_begin, tiles_x;   // k_blur tiles of this level
+  int tile_begin, tiles_x;   // k_blur tiles of this level; full-width (BS_W) column strips
   int rgrp_begin, rwin_ok;   // k_resize 4-column group tables; 1 when every group's taps fit 8 bytes
   int ini_thr[8];            // smallest x with (int)(x / hx) >= b, b = 1..7 (initial node of key x)
 };
@@ -751,13 +751,17 @@ __device__ __forceinline__ uint32_t quick2(uint32_t c, uint32_t u, uint32_t d, u
   const uint32_t Y = pk_min_u16(pk_max_u16(u, d), pk_max_u16(l, r));
   return pk_sub16(X, pk_sub16(c, T2)) | pk_sub16(pk_add16(c, T2), Y);
 }
+// ceil(2^20 / g): q * kMagic20[g] >> 20 == q / g for the item counts of one cell (a table, so that
+// no division is hoisted into the kernel's prologue)
+__constant__ uint32_t kMagic20[16] = {0u, 1048576u, 524288u, 349526u, 262144u, 209716u, 174763u, 149797u,
+                                      131072u, 116509u, 104858u, 95326u, 87382u, 80660u, 74899u, 69906u};
 template <int RSC, int XO>
 __device__ __forceinline__ int fast_prefilter4(const uint8_t* roi, int dw, int dh, uint32_t T2, uint16_t* list) {
   static_assert(RSC % 4 == 0, "dword rows");
   constexpr int RD = RSC / 4;                         // row stride in dwords
   constexpr int OC = XO + 3, OR = XO + 6;             // centre / right byte offsets from 4g
-  const int gw = (dw + 3) >> 2;
-  const uint32_t gmagic = ((1u << 20) + gw - 1) / gw;
+  const int gw = (dw + 3) >> 2;  // <= 15 here (ROI <= 61 columns)
+  const uint32_t gmagic = kMagic20[gw];
   const int items = gw * dh;
   int nlist = 0;
   for (int q0 = 0; q0 < items; q0 += 64) {
@@ -1777,21 +1781,38 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   while (l + 1 < a.nlevels && strip >= a.levels[l + 1].tile_begin) l++;
   const LevelDesc ld = a.levels[l];
   strip -= ld.tile_begin;
-  const int sx = strip % ld.tiles_x, sy = strip / ld.tiles_x;
-  const int x = sx * BS_W - 4 + 4 * lane, y0 = sy * BS_H;  // this lane's 4 columns
+  // full strips: BS_W columns x BS_H rows. The level's last, narrower column strip (width
+  // w - tiles_x * BS_W) splits the wavefront into blur_h groups of 64 / blur_h lanes, each with
+  // its own halo lanes and its own band of BS_H rows (the wave shifts below cross a group edge
+  // only into halo lanes), so that few lanes idle beside a narrow remainder.
+  const int nfull = ld.tiles_x * ((ld.h + BS_H - 1) / BS_H);
+  int x, y0, gl, lg;
+  if (strip < nfull) {
+    const int sx = strip % ld.tiles_x, sy = strip / ld.tiles_x;
+    x = sx * BS_W - 4 + 4 * lane;  // this lane's 4 columns
+    y0 = sy * BS_H;
+    gl = lane;
+    lg = 64;
+  } else {
+    const int H = ld.blur_h;
+    lg = 64 / H;
+    gl = lane & (lg - 1);
+    x = ld.tiles_x * BS_W - 4 + 4 * gl;
+    y0 = ((strip - nfull) * H + lane / lg) * BS_H;
+  }
   const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
   uint8_t* dst = a.blur + (long long)img * a.pyr_stride + ld.pyr_off;
   const int w = ld.w, pitch = ld.pitch;
   // columns -4 .. w+7 exist in every row (padding; -3..-1 and w..w+2 hold the reflections)
   const bool cin = x < w + 8;
-  const bool out = lane >= 1 && lane <= 62 && x < w;
+  const bool out = gl >= 1 && gl <= lg - 2 && x < w;
   auto load_row = [&](int r) {
     return cin ? *reinterpret_cast<const uint32_t*>(src + (long long)reflect101(r, ld.h) * pitch + x) : 0u;
   };
   auto ev = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c020c00u); };  // columns 0, 2
   auto od = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c01u); };  // columns 1, 3
   const int yend = min(y0 + BS_H, ld.h);
-  const int nrows = yend - y0 + 6;  // input rows y0-3 .. yend+2 (<= BS_H + 6)
+  const int nrows = y0 < ld.h ? yend - y0 + 6 : 0;  // input rows y0-3 .. yend+2 (<= BS_H + 6)
   // every input row of the strip is loaded up front (fully unrolled: all loads in flight at once,
   // the window below is renamed, not moved)
   uint32_t rowv[BS_H + 6];
@@ -2478,9 +2499,13 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
-    d.tiles_x = (d.w + BS_W - 1) / BS_W;  // k_blur strips of BS_W x BS_H
-    d.tile_begin = tiles;
-    tiles += d.tiles_x * ((d.h + BS_H - 1) / BS_H);
+    {  // k_blur strips of BS_W x BS_H, the remainder columns in bands of blur_h x BS_H rows
+      d.tiles_x = d.w / BS_W;
+      const int rem = d.w - d.tiles_x * BS_W;
+      d.blur_h = rem == 0 ? 0 : rem <= 14 * 4 ? 4 : rem <= 30 * 4 ? 2 : 1;
+      d.tile_begin = tiles;
+      tiles += d.tiles_x * ((d.h + BS_H - 1) / BS_H) + (d.blur_h ? (d.h + BS_H * d.blur_h - 1) / (BS_H * d.blur_h) : 0);
+    }
     d.key_begin = keys;
     d.key_cap = std::max(d.budget + 3, 4 * d.nini);
     keys += d.key_cap;
