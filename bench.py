@@ -79,6 +79,15 @@ def parse(argv=None):
     p.add_argument("--fast-side", type=int, default=0,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2)")
+    p.add_argument("--blur-mode", type=int, default=-1,
+                   help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
+                        "side stream, 1 after it on the launch stream, 2 on the side stream once the pyramid is "
+                        "built (default: 0 with one handle, 1 with several)")
+    p.add_argument("--vocab-inline", action="store_true",
+                   help="ComputeBoW on the extraction streams, only SearchForTriangulation on the matching stream")
+    p.add_argument("--match-normal", action="store_true",
+                   help="the matching stream at normal priority (default: high, beside the shared side "
+                        "stream, so that the latency-bound vocabulary + SFT chain keeps up with two handles)")
     p.add_argument("--match-inline", action="store_true",
                    help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
     p.add_argument("--torch-streams", action="store_true",
@@ -184,7 +193,8 @@ def main():
     # one, so that each opens its own hardware queue (PipelineStreams)
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
-    pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline)
+    pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline,
+                                                                  match_high=not args.match_normal)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -217,6 +227,8 @@ def main():
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
     if args.fast_side > 0:
         ext.debug_set_fast_side_levels(args.fast_side)
+    if args.blur_mode >= 0:
+        ext.debug_set_blur_mode(args.blur_mode)
     exts = [ext]
     if n_ext > 1:
         # several handles extract consecutive sub-batches concurrently; their side-stream work
@@ -227,11 +239,16 @@ def main():
                 e.debug_set_inline_side(True)
             if args.fast_side > 0:
                 e.debug_set_fast_side_levels(args.fast_side)
+            # with two handles the other handle's kernels fill the CUs beside DistributeOctTree,
+            # and the shared side stream is better left to FAST alone: the blur follows the octree
+            # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
+            e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
             if args.level_launches:
                 e.debug_force_level_launches(True)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), defer=args.defer_matching,
-                           stereo=args.stereo, levelsup=args.levelsup, streams=pstreams)
+                           stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
+                           vocab_inline=args.vocab_inline)
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
     counter = [0]
@@ -257,6 +274,14 @@ def main():
     torch.cuda.set_stream(pipe.stream)
     for _ in range(args.warmup * S_sub):
         sub_batch()
+    drain()
+    torch.cuda.synchronize()
+    # host cost of enqueueing one sub-batch (untimed): 32 sub-batches right after a synchronize,
+    # while the device queues are still short enough that no launch blocks
+    th0 = time.perf_counter()
+    for _ in range(32):
+        sub_batch()
+    host_us = (time.perf_counter() - th0) / 32 * 1e6
     drain()
     torch.cuda.synchronize()
     # probe pass (untimed): HIP events around every kernel -> per-kernel durations, dominant kernel
@@ -345,6 +370,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / args.steps, 4),
+        "host_us_per_subbatch_unblocked": round(host_us, 1),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

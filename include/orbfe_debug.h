@@ -39,6 +39,9 @@ int orbfe_debug_set_inline_side(orbfe_extractor* h, int on);
 /* The side-stream work on a caller's stream (e.g. one high-priority stream shared by several
  * handles whose extractions overlap); NULL restores the handle's own side stream. */
 int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
+/* Where GaussianBlur runs: 0 (default) on the side stream beside DistributeOctTree, 1 on the
+ * launch stream after DistributeOctTree, 2 on the side stream as soon as the pyramid is built. */
+int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

@@ -9,7 +9,8 @@
 #define ORBFE_WAVE 64
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
-__device__ __forceinline__ int wave_id() { return (int)(threadIdx.x >> 6); }
+// wave-uniform, so that per-wave indices derived from it stay in SGPRs (scalar loads and address math)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 __device__ __forceinline__ uint64_t lanemask_lt() {
   return (1ull << (unsigned)lane_id()) - 1ull;
 }

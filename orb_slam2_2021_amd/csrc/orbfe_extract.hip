@@ -2182,6 +2182,7 @@ struct orbfe_extractor {
   int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: the default, 3 levels)
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
+  int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2875,20 +2876,24 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // main stream's FAST -- bench 63.7k vs 67.0k stereo frames/s, it competes with that FAST; the
   // blur on the side stream as soon as the pyramid is complete -- 65.1k vs 69.3-70.0k.)
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));  // the pyramid is complete on st
+  const dim3 blur_grid((h->blur_tiles + 3) / 4, n);
+  if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
+    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+  }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
-  ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
-  ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
-  {
-    hipStream_t sd = side;
-    dim3 grid((h->blur_tiles + 3) / 4, n);
-    LAUNCH_TIMED(h, 5, sd, hipLaunchKernelGGL(k_blur, grid, dim3(256), 0, sd, a));
+  if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
+    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+    ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
-  ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   launch_octree(st, 0, h->nlevels);
-
-  ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
+  if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
+    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, st, a));
+  if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
     dim3 grid((h->total_key_slots + 15) / 16, n);
     LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, a));
@@ -3496,6 +3501,12 @@ extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float
                        (float)(M_PI / 180.f), d_cos, d_sin);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_HIP_CHECK(hipStreamSynchronize(st));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode) {
+  if (!h || mode < 0 || mode > 2) return ORBFE_ERR_ARG;
+  h->blur_mode = mode;
   return ORBFE_OK;
 }
 

@@ -313,6 +313,11 @@ class ORBextractor:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
+    def debug_set_blur_mode(self, mode: int) -> None:
+        """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream
+        after it, 2 side stream as soon as the pyramid is built."""
+        L.check(self._lib.orbfe_debug_set_blur_mode(self._h, int(mode)), "set_blur_mode")
+
     def set_side_stream(self, stream: int) -> None:
         """Run the side-stream work on `stream` (a hipStream_t address; 0 restores the handle's own)."""
         L.check(self._lib.orbfe_set_side_stream(self._h, c_void_p(stream or 0)), "set_side_stream")

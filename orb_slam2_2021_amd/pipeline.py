@@ -52,7 +52,8 @@ class PipelineStreams:
     after two idle streams had been created in between). Created before any other stream of the
     process, the busy streams each open a queue of their own."""
 
-    def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False):
+    def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
+                 match_high: bool = False):
         import torch
         self.device = device
         self._ptrs = []
@@ -66,8 +67,10 @@ class PipelineStreams:
         self.extract = [make(False) for _ in range(max(1, n_extractors))]
         # match_inline: each sub-batch's vocabulary + matching follow its extraction on the same
         # stream (the other extractors' streams provide the overlap)
-        self.match = None if match_inline else make(False)
+        self.match = None if match_inline or match_high else make(False)
         self.side = make(True)
+        if match_high and not match_inline:  # the matching stream at the side stream's priority
+            self.match = make(True)
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
@@ -83,7 +86,8 @@ class C3Pipeline:
     def __init__(self, ext, voc, tree, B: int, H: int, W: int, cam: dict, F12: np.ndarray,
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
-                 nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None):
+                 nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
+                 vocab_inline: bool = False):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -97,6 +101,9 @@ class C3Pipeline:
         # stereo frames/s -- the matching then stretches DistributeOctTree 80 -> 142 us; off by
         # default)
         self.defer = defer
+        # vocab_inline: ComputeBoW runs on the extraction stream right after the descriptors, the
+        # matching stream only SearchForTriangulation (a shorter serial chain per sub-batch there)
+        self.vocab_inline = vocab_inline
         if defer:
             depth = max(depth, 3)
         self.pending = None
@@ -232,6 +239,8 @@ class C3Pipeline:
             self._ev("k_stereo", s, ev)
             if ev:
                 self.events["k_stereo"].append(tuple(ev))
+        if self.vocab_inline:
+            self._vocab(o, s)
         o.extracted.record(s)
         self.last = o
         if self.match_inline:
@@ -256,17 +265,8 @@ class C3Pipeline:
         m = o.mstream = self.mstream
         if not self.match_inline:
             m.wait_event(o.extracted)
-        ev = []
-        self._ev("k_vocab", m, ev)
-        bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
-                    d_bow_n=o.bow_n.data_ptr()) if self.bow else {})
-        self.voc.transform_batch_device(self.n_img, o.desc.data_ptr(), cap * 32, o.cnt.data_ptr(),
-                                        self.levelsup, o.ids.data_ptr(), o.offs.data_ptr(),
-                                        o.idx.data_ptr(), o.nodes.data_ptr(), cap,
-                                        stream=m.cuda_stream, **bow)
-        self._ev("k_vocab", m, ev)
-        if ev:
-            self.events["k_vocab"].append(tuple(ev))
+        if not self.vocab_inline:
+            self._vocab(o, m)
         ev = []
         self._ev("k_sft", m, ev)
         L.check(self.lib.orbfe_search_for_triangulation_batch_device(
@@ -278,6 +278,20 @@ class C3Pipeline:
         if after_match is not None:
             after_match(o)
         o.matched.record(m)
+
+    def _vocab(self, o, m):
+        """KeyFrame::ComputeBoW of the set's 2B images on stream m."""
+        ev = []
+        self._ev("k_vocab", m, ev)
+        bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
+                    d_bow_n=o.bow_n.data_ptr()) if self.bow else {})
+        self.voc.transform_batch_device(self.n_img, o.desc.data_ptr(), self.cap * 32, o.cnt.data_ptr(),
+                                        self.levelsup, o.ids.data_ptr(), o.offs.data_ptr(),
+                                        o.idx.data_ptr(), o.nodes.data_ptr(), self.cap,
+                                        stream=m.cuda_stream, **bow)
+        self._ev("k_vocab", m, ev)
+        if ev:
+            self.events["k_vocab"].append(tuple(ev))
 
     def event_times(self) -> dict:
         """{kernel: (total ms, launches)} of the recorded vocabulary / matching / stereo events."""
@@ -323,7 +337,8 @@ class C3Pipeline:
 
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
-             stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None):
+             stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
+             vocab_inline: bool = False):
     """The C3 scene of bench.py: KITTI intrinsics, the KeyFrame pair geometry of a stereo
     baseline (t2 = -0.537 m, 0.05 m forward), F12 and epipole from LocalMapping::ComputeF12, and
     seeded KeyFrame state per keypoint slot (half the keypoints stereo, 30 % with a MapPoint).
@@ -350,7 +365,8 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     pipe = C3Pipeline(exts, voc, tree, B, H, W, cam, F12, (ex, ey),
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
-                      levelsup=levelsup, stereo=stereo, defer=defer, streams=streams)
+                      levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
+                      vocab_inline=vocab_inline)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo)
     return pipe, state

@@ -57,8 +57,8 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, stereo):
         assert all(len(b[0]) > 100 for b in out["bow"])
 
 
-@pytest.mark.parametrize("match_inline,stereo", [(False, False), (True, False), (False, True)])
-def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo):
+@pytest.mark.parametrize("match_inline,stereo,blur_mode", [(False, False, 1), (True, False, 0), (False, True, 2)])
+def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode):
     """bench.py's default schedule: two extractor handles extract consecutive sub-batches on their
     own streams (side-stream work on one shared high-priority stream), matching on its own stream
     or inline after each extraction (then two vocabulary transforms run concurrently on the one
@@ -68,7 +68,9 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo):
     tree, voc, ref = vocab
     B = 32
     exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(2)]
-    streams = PipelineStreams(0, 2, match_inline=match_inline)
+    for e in exts:
+        e.debug_set_blur_mode(blur_mode)
+    streams = PipelineStreams(0, 2, match_inline=match_inline, match_high=not match_inline)
     pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams)
     batches = [frames(B, 0), frames(B, 1000), frames(B, 2000)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]

@@ -215,3 +215,16 @@ def test_library_umax_equals_oracle(require_gpu):
     u = np.zeros(16, np.int32)
     L.check(L.lib().orbfe_debug_get_umax(ext._h, L.ptr(u)), "get_umax")
     assert u.tolist() == RefExtractor(2000, 1.2, 8, 20, 7).tables()["umax"].tolist()
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_blur_placements(require_gpu, mode):
+    """GaussianBlur after DistributeOctTree on the launch stream (1) or on the side stream as soon as
+    the pyramid is built (2): the same blurred levels, keypoints and descriptors as the oracle."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_blur_mode(mode)
+    assert_same_extraction(ext, ref, synth_frame(4, 376, 1241))
+    imgs = [synth_frame(30 + i, 376, 1241) for i in range(3)]
+    outs = ext.extract_batch(imgs)
+    for i in reversed(range(3)):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
