@@ -83,6 +83,9 @@ def parse(argv=None):
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
                         "side stream, 1 after it on the launch stream, 2 on the side stream once the pyramid is "
                         "built (default: 0 with one handle, 1 with several)")
+    p.add_argument("--vocab-side", action="store_true",
+                   help="ComputeBoW on the shared side stream (deferred by one sub-batch), only "
+                        "SearchForTriangulation on the matching stream")
     p.add_argument("--vocab-inline", action="store_true",
                    help="ComputeBoW on the extraction streams, only SearchForTriangulation on the matching stream")
     p.add_argument("--match-normal", action="store_true",
@@ -248,7 +251,7 @@ def main():
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                           vocab_inline=args.vocab_inline)
+                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side)
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
     counter = [0]

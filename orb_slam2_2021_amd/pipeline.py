@@ -87,7 +87,7 @@ class C3Pipeline:
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
                  nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
-                 vocab_inline: bool = False):
+                 vocab_inline: bool = False, vocab_side: bool = False):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -104,7 +104,12 @@ class C3Pipeline:
         # vocab_inline: ComputeBoW runs on the extraction stream right after the descriptors, the
         # matching stream only SearchForTriangulation (a shorter serial chain per sub-batch there)
         self.vocab_inline = vocab_inline
-        if defer:
+        # vocab_side: sub-batch i's ComputeBoW is enqueued on the shared side stream during
+        # sub-batch i+1's call (behind i+1's side-stream FAST, ahead of i+2's, by which time i is
+        # extracted), the matching stream runs SearchForTriangulation only
+        self.vocab_side = vocab_side
+        self.side = None
+        if defer or vocab_side:
             depth = max(depth, 3)
         self.pending = None
         self.ext, self.voc = ext, voc
@@ -156,6 +161,7 @@ class C3Pipeline:
                     p.fv1_nodes_dev = self.nodes.data_ptr() + i * 4
                     p.fv2_nodes_dev = self.nodes.data_ptr() + (B + i) * 4
                 self.extracted = torch.cuda.Event()
+                self.vocabbed = torch.cuda.Event()
                 self.matched = torch.cuda.Event()
                 self.mstream = None  # the stream the last matching of this set ran on
 
@@ -194,7 +200,9 @@ class C3Pipeline:
         if isinstance(streams, PipelineStreams):
             for e in self.exts:
                 e.set_side_stream(streams.side.cuda_stream)
+            self.side = streams.side
             streams = streams.ordered()
+        assert not vocab_side or self.side is not None, "vocab_side needs PipelineStreams"
         if streams is None:
             streams = [torch.cuda.Stream(dev) for _ in range(len(self.exts) + 1)]
         assert len(streams) == len(self.exts) + 1
@@ -245,6 +253,12 @@ class C3Pipeline:
         self.last = o
         if self.match_inline:
             self.mstream = s
+        if self.vocab_side:
+            if self.pending is not None:
+                self._vocab_on_side(self.pending)
+                self._match(self.pending, after_match)
+            self.pending = o
+            return o
         if not self.defer:
             self._match(o, after_match)
             return o
@@ -255,17 +269,26 @@ class C3Pipeline:
         return o
 
     def flush(self, after_match=None):
-        """Deferred mode: enqueue the matching of the last sub-batch."""
+        """Deferred modes: enqueue the matching of the last sub-batch."""
         if self.pending is not None:
+            if self.vocab_side:
+                self._vocab_on_side(self.pending)
             self._match(self.pending, after_match)
             self.pending = None
+
+    def _vocab_on_side(self, o):
+        self.side.wait_event(o.extracted)
+        self._vocab(o, self.side)
+        o.vocabbed.record(self.side)
 
     def _match(self, o, after_match):
         B, cap = self.B, self.cap
         m = o.mstream = self.mstream
-        if not self.match_inline:
+        if self.vocab_side:
+            m.wait_event(o.vocabbed)
+        elif not self.match_inline:
             m.wait_event(o.extracted)
-        if not self.vocab_inline:
+        if not (self.vocab_inline or self.vocab_side):
             self._vocab(o, m)
         ev = []
         self._ev("k_sft", m, ev)
@@ -338,7 +361,7 @@ class C3Pipeline:
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
              stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
-             vocab_inline: bool = False):
+             vocab_inline: bool = False, vocab_side: bool = False):
     """The C3 scene of bench.py: KITTI intrinsics, the KeyFrame pair geometry of a stereo
     baseline (t2 = -0.537 m, 0.05 m forward), F12 and epipole from LocalMapping::ComputeF12, and
     seeded KeyFrame state per keypoint slot (half the keypoints stereo, 30 % with a MapPoint).
@@ -366,7 +389,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
-                      vocab_inline=vocab_inline)
+                      vocab_inline=vocab_inline, vocab_side=vocab_side)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo)
     return pipe, state
