@@ -79,6 +79,9 @@ def parse(argv=None):
     p.add_argument("--fast-side", type=int, default=0,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2)")
+    p.add_argument("--inline-side", action="store_true",
+                   help="diagnostic: every handle's side-stream work on its own launch stream (with "
+                        "--extractors 1 --pipeline 1 every kernel runs alone)")
     p.add_argument("--blur-mode", type=int, default=-1,
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
                         "side stream, 1 after it on the launch stream, 2 on the side stream once the pyramid is "
@@ -232,13 +235,15 @@ def main():
         ext.debug_set_fast_side_levels(args.fast_side)
     if args.blur_mode >= 0:
         ext.debug_set_blur_mode(args.blur_mode)
+    if args.inline_side:
+        ext.debug_set_inline_side(True)
     exts = [ext]
     if n_ext > 1:
         # several handles extract consecutive sub-batches concurrently; their side-stream work
         # shares one high-priority stream (PipelineStreams.side)
         exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_ext - 1)]
         for e in exts:
-            if pstreams is None:
+            if pstreams is None or args.inline_side:
                 e.debug_set_inline_side(True)
             if args.fast_side > 0:
                 e.debug_set_fast_side_levels(args.fast_side)

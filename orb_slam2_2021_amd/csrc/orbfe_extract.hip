@@ -382,37 +382,66 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
 // padding columns) -- the per-level path's level 0; k_pyramid's first group does this itself.
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
-  // 16 columns per thread: 5 aligned dword loads + v_alignbyte (the caller's pitch need not be a
-  // multiple of 4), one 16-byte store; byte loads only for the last columns of a row. (Dealing the
-  // (row, group) items to the threads linearly makes this kernel faster alone, 65 -> 57 us, but
-  // the C3 bench slower, 69.9k -> 66.2k stereo frames/s, measured interleaved on one MI355X.)
+  // One wavefront per row. The caller's row (any pitch, any byte alignment) comes in as coalesced
+  // aligned dwords into LDS (byte loads only for a last dword that would run past the row); the
+  // padded pyramid row goes out as 16-byte stores of its physical chunks, the REFLECT_101 columns
+  // -3..-1 and w..w+2 filled in the edge chunks, the other padding bytes zero. (The previous
+  // mapping, 16 columns per thread with 5 dword loads and per-dword stores, took 57-65 us per 64
+  // KITTI images alone, ~1 TB/s.)
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_rows[];
   const LevelDesc ld = a.levels[0];
-  const int x = (blockIdx.x * 64 + threadIdx.x) * 16;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  const int img = blockIdx.z;
-  if (x >= ld.w || y >= ld.h) return;
-  const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch + x;
-  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off + (long long)y * ld.pitch;
-  uint32_t v[4];
-  if (x + 20 <= ld.w) {  // the 5th dword ends at most 4 bytes past column x + 15: inside the row
-    const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(src - sh);
-    uint32_t w[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) w[k] = p[k];
-#pragma unroll
-    for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      v[k] = 0;
+  const int w = ld.w, lane = lane_id(), wv = wave_id();
+  const int y = blockIdx.x * 4 + wv, img = blockIdx.y;
+  if (y >= ld.h) return;
+  const int rd = (w + 11) >> 2;  // LDS dwords per wave: the row + alignment shift + one spare
+  uint32_t* s = s_rows + wv * rd;
+  const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch;
+  const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(src - sh);
+  const int nd = (sh + w + 3) >> 2;  // dwords holding columns 0..w-1 (and up to 3 bytes before)
+  for (int i = lane; i < nd; i += 64) {
+    uint32_t v;
+    if (4 * i + 4 <= sh + w) {
+      v = p[i];
+    } else {  // the row's last dword: only its bytes inside the row
+      v = 0;
       for (int j = 0; j < 4; j++)
-        if (x + 4 * k + j < ld.w) v[k] |= (uint32_t)src[4 * k + j] << (8 * j);
+        if (4 * i + j >= sh && 4 * i + j < sh + w) v |= (uint32_t)src[4 * i + j - sh] << (8 * j);
     }
+    s[i] = v;
   }
+  wave_sync();
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s) + sh;  // column c at sb[c]
+  uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off - 4 + (long long)y * ld.pitch;
+  const int nchunks = ld.pitch >> 4;  // physical bytes 0..pitch-1 = columns -4 .. pitch-5
+  for (int P = lane; P < nchunks; P += 64) {
+    const int c0 = 16 * P - 4;
+    uint32_t v[4];
+    if (c0 >= 0 && c0 + 16 <= w) {
+      const int b = sh + c0, r = b & 3;
+      const uint32_t* q = s + (b >> 2);
+      uint32_t w5[5];
 #pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (x + 4 * k < ld.w) store_row4(row, x + 4 * k, ld.w, v[k]);
+      for (int k = 0; k < 5; k++) w5[k] = q[k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w5[k + 1], w5[k], r);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        v[k] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int col = c0 + 4 * k + j;
+          int c = -1;
+          if (col >= 0 && col < w) c = col;
+          else if (col >= -3 && col < 0) c = min(-col, w - 1);
+          else if (col >= w && col <= w + 2) c = max(2 * w - 2 - col, 0);
+          if (c >= 0) v[k] |= (uint32_t)sb[c] << (8 * j);
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(row + 16 * P) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2825,8 +2854,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   } else {
     {
       const LevelDesc& d = h->levels[0];
-      dim3 grid((d.w + 1023) / 1024, (d.h + 3) / 4, n), block(64, 4);
-      LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, block, 0, st, a));
+      dim3 grid((d.h + 3) / 4, n);
+      const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.w + 11) >> 2);
+      LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
     }
     // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
     // stream has built it, beside the chain of small dependent resize launches that leaves most
