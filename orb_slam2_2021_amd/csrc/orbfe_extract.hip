@@ -384,17 +384,17 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
   // One wavefront per row. The caller's row (any pitch, any byte alignment) comes in as coalesced
   // aligned dwords into LDS (byte loads only for a last dword that would run past the row); the
-  // padded pyramid row goes out as 16-byte stores of its physical chunks, the REFLECT_101 columns
-  // -3..-1 and w..w+2 filled in the edge chunks, the other padding bytes zero. (The previous
-  // mapping, 16 columns per thread with 5 dword loads and per-dword stores, took 57-65 us per 64
-  // KITTI images alone, ~1 TB/s.)
+  // padded pyramid row goes out as 16-byte stores of its physical chunks (bytes past column w+2
+  // and column -4 are don't-care padding), then six lanes patch the REFLECT_101 columns -3..-1
+  // and w..w+2. (The previous mapping, 16 columns per thread with 5 dword loads and per-dword
+  // stores, took 57-65 us per 64 KITTI images alone.)
   extern __shared__ __attribute__((aligned(16))) uint32_t s_rows[];
   const LevelDesc ld = a.levels[0];
   const int w = ld.w, lane = lane_id(), wv = wave_id();
   const int y = blockIdx.x * 4 + wv, img = blockIdx.y;
   if (y >= ld.h) return;
-  const int rd = (w + 11) >> 2;  // LDS dwords per wave: the row + alignment shift + one spare
-  uint32_t* s = s_rows + wv * rd;
+  const int rd = (ld.pitch >> 2) + 4;  // LDS dwords per wave: one before the row, the row, slack
+  uint32_t* s = s_rows + wv * rd + 1;
   const uint8_t* src = a.img0 + (long long)img * a.img_stride + (long long)y * a.img_pitch;
   const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
   const uint32_t* p = reinterpret_cast<const uint32_t*>(src - sh);
@@ -411,36 +411,29 @@ __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
     s[i] = v;
   }
   wave_sync();
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s) + sh;  // column c at sb[c]
   uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off - 4 + (long long)y * ld.pitch;
   const int nchunks = ld.pitch >> 4;  // physical bytes 0..pitch-1 = columns -4 .. pitch-5
   for (int P = lane; P < nchunks; P += 64) {
-    const int c0 = 16 * P - 4;
-    uint32_t v[4];
-    if (c0 >= 0 && c0 + 16 <= w) {
-      const int b = sh + c0, r = b & 3;
-      const uint32_t* q = s + (b >> 2);
-      uint32_t w5[5];
+    const int b = sh + 16 * P - 4;  // LDS byte of the chunk's first column (>= -4)
+    const int r = b & 3;
+    const uint32_t* q = s + (b >> 2);  // arithmetic shift: b = -4..-1 -> s[-1]
+    uint32_t w5[5];
 #pragma unroll
-      for (int k = 0; k < 5; k++) w5[k] = q[k];
-#pragma unroll
-      for (int k = 0; k < 4; k++) v[k] = __builtin_amdgcn_alignbyte(w5[k + 1], w5[k], r);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        v[k] = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int col = c0 + 4 * k + j;
-          int c = -1;
-          if (col >= 0 && col < w) c = col;
-          else if (col >= -3 && col < 0) c = min(-col, w - 1);
-          else if (col >= w && col <= w + 2) c = max(2 * w - 2 - col, 0);
-          if (c >= 0) v[k] |= (uint32_t)sb[c] << (8 * j);
-        }
-      }
-    }
-    *reinterpret_cast<uint4*>(row + 16 * P) = make_uint4(v[0], v[1], v[2], v[3]);
+    for (int k = 0; k < 5; k++) w5[k] = q[k];
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(w5[1], w5[0], r);
+    o.y = __builtin_amdgcn_alignbyte(w5[2], w5[1], r);
+    o.z = __builtin_amdgcn_alignbyte(w5[3], w5[2], r);
+    o.w = __builtin_amdgcn_alignbyte(w5[4], w5[3], r);
+    *reinterpret_cast<uint4*>(row + 16 * P) = o;
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the chunk stores before the patches of their padding bytes
+  if (lane < 6) {
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(s) + sh;  // column c at sb[c]
+    const int k = lane < 3 ? lane : lane - 3;
+    const int col = lane < 3 ? -1 - k : w + k;                        // -1..-3, w..w+2
+    const int from = lane < 3 ? min(1 + k, w - 1) : max(w - 2 - k, 0);  // REFLECT_101
+    row[4 + col] = sb[from];
   }
 }
 
@@ -2855,7 +2848,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     {
       const LevelDesc& d = h->levels[0];
       dim3 grid((d.h + 3) / 4, n);
-      const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.w + 11) >> 2);
+      const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
       LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
     }
     // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
