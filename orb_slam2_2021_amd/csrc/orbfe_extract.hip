@@ -91,6 +91,7 @@ struct ExtractArgs {
   const CellDesc* cells;
   const int2* xtab;
   const int2* ytab;
+  const int4* ywin;  // k_resize_win: per output row the clamped source rows as dword offsets, betas
   int nlevels, ncells, n_images, total_key_slots, blur_strips;
   const uint8_t* img0;
   long long img_stride;
@@ -343,35 +344,39 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
   const int y0 = 2 * pr;
   if (y0 >= ld.h) return;
   const LevelDesc ls = a.levels[l - 1];
-  const uint8_t* src = a.pyr + (long long)img * a.pyr_stride + ls.pyr_off;
-  const int gi = ld.rgrp_begin + g;
-  const int sx0 = a.rgx0[gi];
+  // the source level as dwords from a wave-uniform base; per-lane offsets are 32-bit unsigned
+  // (row offsets precomputed and clamped on the host: LevelDesc rows are 4-byte aligned)
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(a.pyr + (long long)img * a.pyr_stride + ls.pyr_off);
+  const uint32_t gi = (uint32_t)(ld.rgrp_begin + g);
+  const uint32_t sx0 = (uint32_t)a.rgx0[gi];
   const uint4 sel = a.rgrp[2 * gi], alp16 = a.rgrp[2 * gi + 1];
   const bool two = y0 + 1 < ld.h;
-  const int2 ya = a.ytab[ld.tab_y + y0], yb = a.ytab[ld.tab_y + (two ? y0 + 1 : y0)];
-  int rows[4] = {ya.x, ya.x + 1, yb.x, yb.x + 1};
+  const int4 ya = a.ywin[(uint32_t)(ld.tab_y + y0)], yb = a.ywin[(uint32_t)(ld.tab_y + (two ? y0 + 1 : y0))];
+  const uint32_t cx = sx0 >> 2;
+  const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
+  // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
   uint32_t wv[4][3];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(
-        src + __umul24((uint32_t)min(max(rows[r], 0), ls.h - 1), (uint32_t)ls.pitch) + (sx0 & ~3));
 #pragma unroll
-    for (int k = 0; k < 3; k++) wv[r][k] = p[k];
+    for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
   }
-  const int sh = sx0 & 3;
+  const int sh = (int)(sx0 & 3u);
   uint32_t W0[4], W1[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
     W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
   }
+  const int2 ba = make_int2(0, ya.z), bb = make_int2(0, yb.z);
   uint32_t pa, pb;
   if (x + 4 <= ld.simd_end) {  // every column on the SIMD128 rounding (all but a row's tail)
-    pa = resize_win_row<false>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ya);
-    pb = resize_win_row<false>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, yb);
+    pa = resize_win_row<false>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
+    pb = resize_win_row<false>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
   } else {
-    pa = resize_win_row<true>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ya);
-    pb = resize_win_row<true>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, yb);
+    pa = resize_win_row<true>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
+    pb = resize_win_row<true>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
   }
   uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
   store_row4(out + __umul24((uint32_t)y0, (uint32_t)ld.pitch), x, ld.w, pa);
@@ -2222,6 +2227,7 @@ struct orbfe_extractor {
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
   int2* d_ytab = nullptr;
+  int4* d_ywin = nullptr;
   uint4* d_rgrp = nullptr;
   int* d_rgx0 = nullptr;
   int4* d_pyr_xt = nullptr;          // k_pyramid tile tables
@@ -2452,6 +2458,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   std::vector<LevelDesc> lv(L);
   std::vector<CellDesc> cells;
   std::vector<int2> xt, yt;
+  std::vector<int4> yw;  // k_resize_win row table, indexed like yt
   std::vector<uint4> rgrp;
   std::vector<int> rgx0;
   long long pyr = 0;
@@ -2559,6 +2566,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
         fy -= sy;
         const short b0 = h_sat_short((1.f - fy) * 2048.f), b1 = h_sat_short(fy * 2048.f);
         yt.push_back(make_int2(sy, (int)(((unsigned)(unsigned short)b1 << 16) | (unsigned short)b0)));
+        const int r0 = std::min(std::max(sy, 0), s.h - 1), r1 = std::min(std::max(sy + 1, 0), s.h - 1);
+        yw.push_back(make_int4(r0 * (s.pitch / 4), r1 * (s.pitch / 4), yt.back().y, 0));
       }
       d.xmax = xmax;
       // 4-column groups: the taps of output columns 4g..4g+3 as byte selectors into the 8-byte
@@ -2634,13 +2643,16 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
+  hipFree(h->d_ywin);
   h->d_levels = nullptr;
   h->d_cells = nullptr;
   h->d_xtab = h->d_ytab = nullptr;
+  h->d_ywin = nullptr;
   ORBFE_HIP_CHECK(hipMalloc(&h->d_levels, sizeof(LevelDesc) * L));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_cells, sizeof(CellDesc) * std::max<size_t>(cells.size(), 1)));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_xtab, sizeof(int2) * std::max<size_t>(xt.size(), 1)));
   ORBFE_HIP_CHECK(hipMalloc(&h->d_ytab, sizeof(int2) * std::max<size_t>(yt.size(), 1)));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_ywin, sizeof(int4) * std::max<size_t>(yw.size(), 1)));
   ORBFE_HIP_CHECK(hipMemcpy(h->d_levels, lv.data(), sizeof(LevelDesc) * L, hipMemcpyHostToDevice));
   if (!cells.empty())
     ORBFE_HIP_CHECK(hipMemcpy(h->d_cells, cells.data(), sizeof(CellDesc) * cells.size(), hipMemcpyHostToDevice));
@@ -2648,6 +2660,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMemcpy(h->d_xtab, xt.data(), sizeof(int2) * xt.size(), hipMemcpyHostToDevice));
   if (!yt.empty())
     ORBFE_HIP_CHECK(hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice));
+  if (!yw.empty())
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_ywin, yw.data(), sizeof(int4) * yw.size(), hipMemcpyHostToDevice));
   h->levels = lv;
   h->cells = cells;
   h->xtab = xt;
@@ -2772,6 +2786,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.cells = h->d_cells;
   a.xtab = h->d_xtab;
   a.ytab = h->d_ytab;
+  a.ywin = h->d_ywin;
   a.nlevels = h->nlevels;
   a.ncells = (int)h->cells.size();
   a.n_images = n;
@@ -3043,6 +3058,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
+  hipFree(h->d_ywin);
   hipFree(h->d_pyr_blob);
   hipFree(h->d_pyr_xblob);
   hipFree(h->d_pyr_yblob);
