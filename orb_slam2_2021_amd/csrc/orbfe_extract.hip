@@ -1770,11 +1770,13 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 }
 
 // whole-wavefront lane shifts (DPP wave_shr:1 / wave_shl:1, gfx9): lane i <- lane i-1 / i+1
+// (bound_ctrl: the lane without a source, 0 or 63, reads 0 -- a halo lane whose output is
+// unused -- and no old value has to be kept in the destination register)
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
 }
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
 }
 __device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2v, a) * __builtin_bit_cast(u16x2v, b) +
@@ -1833,6 +1835,9 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   // columns -4 .. w+7 exist in every row (padding; -3..-1 and w..w+2 hold the reflections)
   const bool cin = x < w + 8;
   const bool out = gl >= 1 && gl <= lg - 2 && x < w;
+  // stores through a buffer resource on the level's column -4: 32-bit offsets
+  const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(dst - 4, 0, 0x7fffffff, 0x00020000);
+  const int wo = y0 * ld.pitch + x + 4;  // this lane's first output row, column x
   auto load_row = [&](int r) {
     return cin ? *reinterpret_cast<const uint32_t*>(src + (long long)reflect101(r, ld.h) * pitch + x) : 0u;
   };
@@ -1845,6 +1850,10 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   uint32_t rowv[BS_H + 6];
 #pragma unroll
   for (int i = 0; i < BS_H + 6; i++) rowv[i] = i < nrows ? load_row(y0 - 3 + i) : 0u;
+  // the rounding constant 2^15 in one VGPR for the whole strip (not an inline constant; left to
+  // the compiler it is rematerialised per row)
+  uint32_t seed;
+  asm volatile("v_mov_b32 %0, 0x8000" : "=v"(seed));
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;  // window, even columns
   uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;  // window, odd columns
 #pragma unroll
@@ -1869,8 +1878,8 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
     const uint32_t P6 = __builtin_amdgcn_perm(RO, RE, 0x07060302u);   // (V6, V7)
     // the sum of one pixel on the v_dot2 accumulator chain, the rounding constant as its seed:
     // s = 2^15 + sum k V < 2^24, so the result (s >> 16) is byte 2 of s
-    auto hz = [](uint32_t pa, uint32_t pb, uint32_t pc, uint32_t pd) {
-      uint32_t s = dot2_acc(pd, 0x00000012u, 32768u);  // 18 V(j+3)
+    auto hz = [seed](uint32_t pa, uint32_t pb, uint32_t pc, uint32_t pd) {
+      uint32_t s = dot2_acc(pd, 0x00000012u, seed);  // 18 V(j+3) + 2^15
       s = dot2_acc(pc, 0x00220031u, s);                // 49 V(j+1) + 34 V(j+2)
       s = dot2_acc(pb, 0x00360031u, s);                // 49 V(j-1) + 54 V(j)
       return dot2_acc(pa, 0x00220012u, s);             // 18 V(j-3) + 34 V(j-2)
@@ -1880,7 +1889,7 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
     // bytes 2 of s0..s3 -> bytes 0..3 of r
     const uint32_t r = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0c0c0602u),
                                              __builtin_amdgcn_perm(s1, s0, 0x0c0c0602u), 0x05040100u);
-    if (out) *reinterpret_cast<uint32_t*>(dst + (long long)(y0 + i - 6) * pitch + x) = r;
+    if (out) __builtin_amdgcn_raw_buffer_store_b32(r, ws, wo, (i - 6) * pitch, 0);  // row offset in an SGPR
   }
 }
 
