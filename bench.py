@@ -79,6 +79,8 @@ def parse(argv=None):
     p.add_argument("--fast-side", type=int, default=0,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2)")
+    p.add_argument("--diag-skip-matching", action="store_true",
+                   help="diagnostic, not the metric: skip ComputeBoW + SearchForTriangulation (extraction-only rate)")
     p.add_argument("--inline-side", action="store_true",
                    help="diagnostic: every handle's side-stream work on its own launch stream (with "
                         "--extractors 1 --pipeline 1 every kernel runs alone)")
@@ -257,6 +259,12 @@ def main():
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            vocab_inline=args.vocab_inline, vocab_side=args.vocab_side)
+    if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
+        def extract_only(o, after_match):
+            m = o.mstream = pipe.mstream
+            m.wait_event(o.extracted)
+            o.matched.record(m)
+        pipe._match = extract_only
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
     counter = [0]
@@ -379,6 +387,7 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / args.steps, 4),
         "host_us_per_subbatch_unblocked": round(host_us, 1),
+        **({"diagnostic": "matching skipped: extraction only, not the C3 metric"} if args.diag_skip_matching else {}),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
