@@ -2083,8 +2083,11 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
     const f32x2 sc = {sb, ca}, cs = {ca, -sb}, magic = {12582912.0f, 12582912.0f};
     const f32x2 q0 = (f32x2){P.x, P.x} * sc + (f32x2){P.y, P.y} * cs + magic;
     const f32x2 q1 = (f32x2){P.z, P.z} * sc + (f32x2){P.w, P.w} * cs + magic;
-    const int i0 = (int)((uint32_t)__float_as_int(q0.x) * 40u + (uint32_t)__float_as_int(q0.y) - 0x4B400000u * 41u);
-    const int i1 = (int)((uint32_t)__float_as_int(q1.x) * 40u + (uint32_t)__float_as_int(q1.y) - 0x4B400000u * 41u);
+    // the bits of q are 0x4B400000 + v (|v| < 2^22): their low 24 bits 0x400000 + v feed a
+    // full-rate v_mad_u32_u24 (a plain 32-bit multiply-add here compiles to quarter-rate
+    // v_mad_u64_u32); (0x400000 + vr) * 40 + 0x4B400000 + vc - 0x55400000 = 40 vr + vc
+    const int i0 = (int)(__umul24((uint32_t)__float_as_int(q0.x), 40u) + (uint32_t)__float_as_int(q0.y) - 0x55400000u);
+    const int i1 = (int)(__umul24((uint32_t)__float_as_int(q1.x), 40u) + (uint32_t)__float_as_int(q1.y) - 0x55400000u);
     const int t0 = wb[i0];
     const int t1 = wb[i1];
     const uint32_t hv = (uint32_t)(wave_ballot(t0 < t1) >> (16 * grp)) & 0xffffu;
