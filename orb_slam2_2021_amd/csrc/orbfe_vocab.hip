@@ -196,6 +196,28 @@ __device__ __forceinline__ void bitonic_lds(unsigned long long* skeys, int P2) {
   }
 }
 
+// Two ascending bitonic sorts of P2 keys each at once, the workgroup's first half on ka, the
+// second on kb: the same stage sequence, so one barrier per stage serves both (half the barriers
+// and stage latencies of two sorts in a row)
+__device__ __forceinline__ void bitonic_lds2(unsigned long long* ka, unsigned long long* kb, int P2) {
+  constexpr int HALF = VOCAB_THREADS / 2;
+  const int t = threadIdx.x & (HALF - 1);
+  unsigned long long* sk = threadIdx.x < HALF ? ka : kb;
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int pidx = t; pidx < (P2 >> 1); pidx += HALF) {
+        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;
+        const unsigned long long x = sk[i], y = sk[ixj];
+        if ((i & k) == 0 ? (x > y) : (x < y)) {
+          sk[i] = y;
+          sk[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // Starts of the runs of equal key>>32 among the nv sorted valid keys: every thread owns a
 // contiguous chunk; returns this thread's first output position and the total run count.
 __device__ __forceinline__ int2 run_starts(const unsigned long long* skeys, int nv, int beg, int end,
@@ -232,11 +254,20 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   int P2 = 1;
   while (P2 < n) P2 <<= 1;
   const long long kbase = (long long)img * a.cap;
-  // ---- FeatureVector: (node, feature) keys, stable by construction ----
+  // ---- FeatureVector: (node, feature) keys, stable by construction; with the BowVector the
+  //      (word, feature) keys are sorted beside them in bkeys (after the P2 doubles) ----
+  const bool bow = a.bow_words != nullptr;
+  const bool dual = bow && P2 <= 4096;  // the LDS holds 3 P2 entries (launch_vocab)
+  unsigned long long* bkeys = skeys + 2 * P2;
   for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? fvkeys[kbase + i] : ~0ull;
+  if (dual)
+    for (int i = t; i < P2; i += VOCAB_THREADS) bkeys[i] = i < n ? bowkeys[kbase + i] : ~0ull;
   if (t == 0) s_n = 0;
   __syncthreads();
-  bitonic_lds(skeys, P2);
+  if (dual)
+    bitonic_lds2(skeys, bkeys, P2);
+  else
+    bitonic_lds(skeys, P2);
   int nvalid = 0;
   for (int i = t; i < n; i += VOCAB_THREADS) nvalid += skeys[i] != ~0ull;
   nvalid = wave_sum(nvalid);
@@ -264,12 +295,17 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
       a.n_nodes[img] = pr.y;
     }
   }
-  if (!a.bow_words) return;
-  // ---- BowVector: (word, feature) keys ----
+  if (!bow) return;
+  // ---- BowVector: (word, feature) keys (sorted above beside the node keys, or now) ----
   __syncthreads();
-  for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? bowkeys[kbase + i] : ~0ull;
-  __syncthreads();
-  bitonic_lds(skeys, P2);
+  if (dual) {
+    for (int i = t; i < nv; i += VOCAB_THREADS) skeys[i] = bkeys[i];
+    __syncthreads();
+  } else {
+    for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? bowkeys[kbase + i] : ~0ull;
+    __syncthreads();
+    bitonic_lds(skeys, P2);
+  }
   double* sval = reinterpret_cast<double*>(skeys + P2);
   uint32_t* words = a.bow_words + kbase;
   double* wout = a.bow_weights + kbase;
@@ -628,7 +664,9 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   unsigned long long* fvk = ks->d_keys;
   unsigned long long* bwk = fvk + slots;
   int32_t* leaves = reinterpret_cast<int32_t*>(bwk + slots);
-  const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * P2 : 0);
+  // keys, then (BowVector) P2 doubles and the P2 word keys sorted beside the node keys
+  const size_t lds = sizeof(unsigned long long) * P2 +
+                     (d_bow_words ? (P2 <= 4096 ? 2 : 1) * sizeof(double) * P2 : 0);
   hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
   hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(VOCAB_THREADS), lds, s, a, (const unsigned long long*)fvk,
                      (const unsigned long long*)bwk, (const int32_t*)leaves);
