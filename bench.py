@@ -202,7 +202,8 @@ def main():
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
     pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline,
-                                                                  match_high=not args.match_normal)
+                                                                  match_high=not args.match_normal,
+                                                                  side_last=args.inline_side)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:

@@ -53,7 +53,7 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 match_high: bool = False):
+                 match_high: bool = False, side_last: bool = False):
         import torch
         self.device = device
         self._ptrs = []
@@ -68,8 +68,10 @@ class PipelineStreams:
         # match_inline: each sub-batch's vocabulary + matching follow its extraction on the same
         # stream (the other extractors' streams provide the overlap)
         self.match = None if match_inline or match_high else make(False)
+        if match_high and not match_inline and side_last:
+            self.match = make(True)
         self.side = make(True)
-        if match_high and not match_inline:  # the matching stream at the side stream's priority
+        if match_high and not match_inline and not side_last:  # at the side stream's priority
             self.match = make(True)
 
     def ordered(self):
