@@ -81,6 +81,9 @@ def parse(argv=None):
                         "(0: the library default, levels 0..2)")
     p.add_argument("--diag-skip-matching", action="store_true",
                    help="diagnostic, not the metric: skip ComputeBoW + SearchForTriangulation (extraction-only rate)")
+    p.add_argument("--copy0-side", action="store_true",
+                   help="level 1 from the caller's image, the level-0 copy on the side stream "
+                        "(orbfe_debug_set_copy0_side; measured slower)")
     p.add_argument("--inline-side", action="store_true",
                    help="diagnostic: every handle's side-stream work on its own launch stream (with "
                         "--extractors 1 --pipeline 1 every kernel runs alone)")
@@ -240,6 +243,8 @@ def main():
         ext.debug_set_blur_mode(args.blur_mode)
     if args.inline_side:
         ext.debug_set_inline_side(True)
+    if args.copy0_side:
+        ext.debug_set_copy0_side(True)
     exts = [ext]
     if n_ext > 1:
         # several handles extract consecutive sub-batches concurrently; their side-stream work
@@ -254,6 +259,8 @@ def main():
             # and the shared side stream is better left to FAST alone: the blur follows the octree
             # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
+            if args.copy0_side:
+                e.debug_set_copy0_side(True)
             if args.level_launches:
                 e.debug_force_level_launches(True)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,

@@ -42,6 +42,10 @@ int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
 /* Where GaussianBlur runs: 0 (default) on the side stream beside DistributeOctTree, 1 on the
  * launch stream after DistributeOctTree, 2 on the side stream as soon as the pyramid is built. */
 int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode);
+/* 1: with a side stream and the window resize, level 1 is resized from the caller's image and
+ * the copy into pyramid level 0 runs on the side stream beside the resize chain; 0 (default,
+ * measured faster): the copy first on the launch stream, level 1 from the copied level 0. */
+int orbfe_debug_set_copy0_side(orbfe_extractor* h, int on);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

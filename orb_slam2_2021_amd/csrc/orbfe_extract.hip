@@ -336,6 +336,12 @@ __device__ __forceinline__ uint32_t resize_win_row(const uint32_t W0r0, const ui
 // Items (4-column group, row pair) of the level are numbered row-major and dealt to the threads
 // linearly, so only the last wave of an image's grid has idle lanes (a 2-D grid of 256-column
 // blocks left up to a third of the lanes idle on the right edge of every row band).
+// SRC_IN (level 1 only): the source is the caller's image itself (any pitch and alignment) rather
+// than level 0 of the pyramid, so that k_copy0 can run beside the resize chain on the side
+// stream: per-row byte offsets from the row indices in ywin.w, dword-aligned loads from the
+// aligned image base and a per-row v_alignbyte shift; the buffer's extent ends at the last
+// input byte, so the window of a row's last group past the image end reads zeros (unused taps).
+template <bool SRC_IN>
 __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G, uint32_t gmagic) {
   const LevelDesc ld = a.levels[l];
   const int item = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
@@ -354,20 +360,48 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
   const int4 ya = a.ywin[(uint32_t)(ld.tab_y + y0)], yb = a.ywin[(uint32_t)(ld.tab_y + (two ? y0 + 1 : y0))];
   const uint32_t cx = sx0 >> 2;
   const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
-  // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
   uint32_t wv[4][3];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
-  }
-  const int sh = (int)(sx0 & 3u);
   uint32_t W0[4], W1[4];
+  if constexpr (!SRC_IN) {
+    // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-  for (int r = 0; r < 4; r++) {
-    W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
-    W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
+    for (int r = 0; r < 4; r++) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
+    }
+    const int sh = (int)(sx0 & 3u);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
+      W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
+    }
+  } else {
+    const uint8_t* ib = a.img0 + (long long)img * a.img_stride;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(ib) & 3u);
+    const LevelDesc l0 = a.levels[0];
+    const long long extent = (long long)(a.n_images - 1 - img) * a.img_stride + (long long)(l0.h - 1) * a.img_pitch + l0.w + mis;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ib - mis), 0, (int)min(extent, 0x7fffffffll), 0x00020000);
+    const uint32_t ri[4] = {(uint32_t)ya.w & 0xffffu, (uint32_t)ya.w >> 16, (uint32_t)yb.w & 0xffffu, (uint32_t)yb.w >> 16};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t b = ri[r] * (uint32_t)a.img_pitch + sx0 + mis;
+      if ((long long)(b & ~3u) + 12 <= extent) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b & ~3u) + 4 * k, 0, 0);
+      } else {  // the image block's last bytes: a dword past the extent would read as all zeros
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(b & ~3u) + 4 * k + j, 0, 0) << (8 * j);
+          wv[r][k] = v;
+        }
+      }
+      W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], b & 3u);
+      W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], b & 3u);
+    }
   }
   const int2 ba = make_int2(0, ya.z), bb = make_int2(0, yb.z);
   uint32_t pa, pb;
@@ -2224,7 +2258,8 @@ struct orbfe_extractor {
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr, ev_c0 = nullptr;
+  int copy0_side = 0;  // orbfe_debug_set_copy0_side (measured slower, off)
   hipEvent_t ev_pyr = nullptr;              // pyramid complete (orbfe_extractor_pyramid_event)
   std::vector<hipEvent_t> ev_lvl;           // level l built (per-level FAST on the side stream)
   // geometry
@@ -2579,7 +2614,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
         const short b0 = h_sat_short((1.f - fy) * 2048.f), b1 = h_sat_short(fy * 2048.f);
         yt.push_back(make_int2(sy, (int)(((unsigned)(unsigned short)b1 << 16) | (unsigned short)b0)));
         const int r0 = std::min(std::max(sy, 0), s.h - 1), r1 = std::min(std::max(sy + 1, 0), s.h - 1);
-        yw.push_back(make_int4(r0 * (s.pitch / 4), r1 * (s.pitch / 4), yt.back().y, 0));
+        yw.push_back(make_int4(r0 * (s.pitch / 4), r1 * (s.pitch / 4), yt.back().y, r0 | (r1 << 16)));
       }
       d.xmax = xmax;
       // 4-column groups: the taps of output columns 4g..4g+3 as byte selectors into the 8-byte
@@ -2858,6 +2893,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // k_side: the levels whose FAST cells run on the side stream, beside the rest of the pyramid
   // launches
   int k_side = 0;
+  bool c0side = false;
   if (!h->pyr_groups.empty() && !h->force_level_launches) {
     // the first group writes levels 0..top
     k_side = h->pyr_groups[0].top + 1;
@@ -2872,11 +2908,25 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       }
     }
   } else {
+    // c0side (debug option, off): level 1 is resized from the caller's image, so k_copy0 runs on
+    // the side stream beside the resize chain (followed there by FAST of level 0); the main
+    // stream joins it before the pyramid counts as complete. Measured on MI355X: 66.3k vs 72.3k
+    // stereo frames/s with one handle, 79.4-82.8k vs 84.6k with two (the side stream's FAST of
+    // level 0 then waits for the copy, and with two handles the other handle's side work too).
+    c0side = h->copy0_side && side != st && h->nlevels > 1 && h->levels[1].rwin_ok &&
+             h->levels[0].h < 65536;
     {
       const LevelDesc& d = h->levels[0];
       dim3 grid((d.h + 3) / 4, n);
       const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
-      LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
+      if (c0side) {
+        ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));  // the input is ready on st
+        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
+        LAUNCH_TIMED(h, 4, side, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, side, a));
+        ORBFE_HIP_CHECK(hipEventRecord(h->ev_c0, side));
+      } else {
+        LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
+      }
     }
     // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
     // stream has built it, beside the chain of small dependent resize launches that leaves most
@@ -2890,9 +2940,11 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       }
     }
     auto side_fast = [&](int l) -> int {
-      const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
-      ORBFE_HIP_CHECK(hipEventRecord(e, st));
-      ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
+      if (!(l == 0 && c0side)) {  // with c0side level 0 is the side stream's own k_copy0
+        const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
+        ORBFE_HIP_CHECK(hipEventRecord(e, st));
+        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
+      }
       const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
       return launch_fast(side, h->levels[l].cell_begin, c1);
     };
@@ -2903,13 +2955,17 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
         const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
         const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
         dim3 grid((items + 255) / 256, n);
-        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win, grid, dim3(256), 0, st, a, l, G, gm));
+        if (l == 1 && c0side)
+          LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win<true>, grid, dim3(256), 0, st, a, l, G, gm));
+        else
+          LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win<false>, grid, dim3(256), 0, st, a, l, G, gm));
       } else {
         dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
         LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
       }
       if (l < k_side) side_fast(l);
     }
+    if (c0side) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_c0, 0));  // level 0 is in the pyramid
   }
   if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
   ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3022,6 +3078,7 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
       hipEventCreateWithFlags(&h->ev_fork, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_l0, kForkJoinEvent) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_c0, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_f0, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess) {
     delete h;
@@ -3102,6 +3159,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->ev_l0) hipEventDestroy(h->ev_l0);
+  if (h->ev_c0) hipEventDestroy(h->ev_c0);
   if (h->ev_f0) hipEventDestroy(h->ev_f0);
   if (h->ev_pyr) hipEventDestroy(h->ev_pyr);
   for (hipEvent_t e : h->ev_lvl) hipEventDestroy(e);
@@ -3552,6 +3610,12 @@ extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float
                        (float)(M_PI / 180.f), d_cos, d_sin);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_HIP_CHECK(hipStreamSynchronize(st));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_copy0_side(orbfe_extractor* h, int on) {
+  if (!h) return ORBFE_ERR_ARG;
+  h->copy0_side = on ? 1 : 0;
   return ORBFE_OK;
 }
 

@@ -313,6 +313,10 @@ class ORBextractor:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
+    def debug_set_copy0_side(self, on: bool = True) -> None:
+        """Level 1 resized from the caller's image, the level-0 copy on the side stream (default off)."""
+        L.check(self._lib.orbfe_debug_set_copy0_side(self._h, 1 if on else 0), "set_copy0_side")
+
     def debug_set_blur_mode(self, mode: int) -> None:
         """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream
         after it, 2 side stream as soon as the pyramid is built."""

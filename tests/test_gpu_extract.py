@@ -228,3 +228,35 @@ def test_blur_placements(require_gpu, mode):
     outs = ext.extract_batch(imgs)
     for i in reversed(range(3)):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
+@pytest.mark.parametrize("copy0_side", [True, False])
+def test_device_input_odd_pitch_and_alignment(require_gpu, copy0_side):
+    """extract_batch_device on images at an odd byte offset with an odd row pitch: level 1 is then
+    resized straight from the unaligned caller rows (the level-0 copy beside it on the side
+    stream) or from the copied level 0; both equal the oracle, image by image."""
+    import torch
+    from orb_slam2_2021_amd import _lib as L
+    n, rows, cols, pitch = 3, 376, 1241, 1247
+    imgs = [synth_frame(60 + i, rows, cols) for i in range(n)]
+    buf = np.full(n * rows * pitch + 8, 77, np.uint8)
+    for i in range(n):
+        v = buf[1 + i * rows * pitch:1 + (i + 1) * rows * pitch].reshape(rows, pitch)
+        v[:, :cols] = imgs[i]
+    d = torch.from_numpy(buf).to("cuda")
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_copy0_side(copy0_side)
+    cap = ext.max_keypoints(rows, cols)
+    kps = torch.empty(n * cap * 28, dtype=torch.uint8, device="cuda")
+    desc = torch.empty(n * cap * 32, dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ext.extract_batch_device(n, d.data_ptr() + 1, rows * pitch, rows, cols, pitch, kps.data_ptr(),
+                             desc.data_ptr(), cap, cnt.data_ptr())
+    torch.cuda.synchronize()
+    K = kps.cpu().numpy().view(L.KEYPOINT_DTYPE).reshape(n, cap)
+    D = desc.cpu().numpy().reshape(n, cap, 32)
+    C = cnt.cpu().numpy()
+    ref = RefExtractor(2000, 1.2, 8, 20, 7)
+    for i in reversed(range(n)):
+        c = int(C[i])
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=(K[i, :c], D[i, :c]))
