@@ -81,6 +81,8 @@ def parse(argv=None):
                         "(0: the library default, levels 0..2)")
     p.add_argument("--diag-skip-matching", action="store_true",
                    help="diagnostic, not the metric: skip ComputeBoW + SearchForTriangulation (extraction-only rate)")
+    p.add_argument("--side-normal", action="store_true",
+                   help="the shared side stream at normal priority (default: high)")
     p.add_argument("--copy0-side", action="store_true",
                    help="level 1 from the caller's image, the level-0 copy on the side stream "
                         "(orbfe_debug_set_copy0_side; measured slower)")
@@ -206,7 +208,8 @@ def main():
     n_ext = max(1, args.extractors)
     pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline,
                                                                   match_high=not args.match_normal,
-                                                                  side_last=args.inline_side)
+                                                                  side_last=args.inline_side,
+                                                                  side_high=not args.side_normal)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:

@@ -53,7 +53,7 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 match_high: bool = False, side_last: bool = False):
+                 match_high: bool = False, side_last: bool = False, side_high: bool = True):
         import torch
         self.device = device
         self._ptrs = []
@@ -70,7 +70,7 @@ class PipelineStreams:
         self.match = None if match_inline or match_high else make(False)
         if match_high and not match_inline and side_last:
             self.match = make(True)
-        self.side = make(True)
+        self.side = make(side_high)
         if match_high and not match_inline and not side_last:  # at the side stream's priority
             self.match = make(True)
 
