@@ -109,6 +109,9 @@ def parse(argv=None):
                         "several extractors their side work runs inline)")
     p.add_argument("--level-launches", action="store_true",
                    help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
+    p.add_argument("--dump-gather", default="",
+                   help="test hook: write each rank's last sub-batch (own keypoints + descriptors) and "
+                        "rank 0's gathered payloads to this directory")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
@@ -132,9 +135,11 @@ def spawn_ranks(args) -> int:
 
 class Gatherer:
     """C4: each sub-batch's used keypoints + descriptors to rank 0. The pack kernel runs on the
-    matching stream right after SearchForTriangulation; the exchange of sub-batch i (sizes, then
-    payloads) happens after sub-batch i+1 is enqueued, so the host's wait on the sizes never
-    starves the extraction stream."""
+    matching stream right after SearchForTriangulation, and the point-to-point transfers of a
+    fixed byte count (the packed worst case; the packed header carries the per-image counts) are
+    enqueued right behind it on the same stream: no size exchange, so the host never waits for
+    the device inside the timed loop (parallel.gather_fixed). The output set is reused only after
+    its payload left (o.matched is recorded behind the transfers)."""
 
     def __init__(self, pipe, world, rank, dev, comm_dev):
         import torch
@@ -146,46 +151,28 @@ class Gatherer:
         self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
         self.recv = ([torch.empty(self.cap_bytes, dtype=torch.uint8, device=comm_dev) for _ in range(world)]
                      if rank == 0 else None)
-        self.pending = None       # packed, exchanged after the next sub-batch is enqueued
-        self.pending_next = None  # packed during the current run
-        self.bytes_received = 0
         self.transfers = 0
-        self.last = None
+        self.last = None  # rank 0: the last exchange's per-rank views (alias the receive buffers)
+        self.last_set = None
 
     def pack(self, o):
-        from orb_slam2_2021_amd.parallel import pack_keypoints_device
-        p = self.pipe
-        pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
-                              self.bufs[id(o)].data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
-                              o.mstream.cuda_stream)
-        self.pending_next = o
-
-    def after_run(self):
-        prev, self.pending = self.pending, self.pending_next
-        self.pending_next = None
-        if prev is not None:
-            self.exchange(prev)
-
-    def exchange(self, o):
         import torch
-        from orb_slam2_2021_amd.parallel import gather_packed
+        from orb_slam2_2021_amd.parallel import gather_fixed, pack_keypoints_device
+        p = self.pipe
+        buf = self.bufs[id(o)]
+        pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                              buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
+                              o.mstream.cuda_stream)
         with torch.cuda.stream(o.mstream):
             if self.comm_dev.type == "cpu":  # --rehearse: gloo, staged through the host
                 o.mstream.synchronize()
-                out, sizes = gather_packed(self.bufs[id(o)].cpu(), self.sizes[id(o)].cpu(), dst=0, recv=self.recv)
+                out = gather_fixed(buf.cpu(), self.cap_bytes, dst=0, recv=self.recv)
             else:
-                out, sizes = gather_packed(self.bufs[id(o)], self.sizes[id(o)], dst=0, recv=self.recv)
+                out = gather_fixed(buf, self.cap_bytes, dst=0, recv=self.recv)
+        self.transfers += 1
+        self.last_set = o
         if self.rank == 0:
-            self.bytes_received += sum(sizes[1:])
-            self.transfers += len(sizes) - 1
             self.last = out
-        # the set may be reused only after its payload left: record after the transfers
-        o.matched.record(o.mstream)
-
-    def flush(self):
-        if self.pending is not None:
-            self.exchange(self.pending)
-            self.pending = None
 
 
 def main():
@@ -284,14 +271,9 @@ def main():
         j = counter[0] % NB
         counter[0] += 1
         pipe.run(d_img[j].data_ptr(), after_match=g.pack if g else None)
-        if g:
-            g.after_run()
 
     def drain():  # every enqueued sub-batch matched (and gathered)
         pipe.flush(after_match=g.pack if g else None)
-        if g:
-            g.after_run()
-            g.flush()
 
     def barrier():
         if world > 1:
@@ -433,9 +415,15 @@ def main():
         "cpu_baseline": None,
     }
     if g is not None and rank == 0:
-        out["gather"] = {"payload_bytes_received_per_subbatch": round(g.bytes_received / max(g.transfers, 1)
-                                                                      * (world - 1), 1),
-                         "what": "packed used keypoints + descriptors of ranks 1..N-1 (sizes all-gathered first)"}
+        from orb_slam2_2021_amd.parallel import packed_size
+        used = [packed_size(v) for v in g.last]
+        out["gather"] = {"bytes_sent_per_rank_per_subbatch": g.cap_bytes,
+                         "used_bytes_last_subbatch": used,
+                         "bytes_received_per_subbatch": g.cap_bytes * (world - 1),
+                         "what": "packed keypoints + descriptors of ranks 1..N-1 to rank 0, point-to-point, "
+                                 "fixed worst-case byte count (no size exchange, no host sync per sub-batch)"}
+    if g is not None and args.dump_gather:
+        dump_gather(args.dump_gather, g, pipe, rank, world)
     # ---- parity of the last timed sub-batch (every rank checks its own) ----
     if not args.no_parity:
         from oracle.c3_check import check_c3
@@ -481,6 +469,22 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dump_gather(d, g, pipe, rank, world):
+    """--dump-gather: rank r writes its last gathered sub-batch as extracted (r_own.npz); rank 0
+    writes every rank's payload as received (r_gathered.bin). tests/test_gpu_gather.py compares
+    them byte for byte."""
+    import torch
+    torch.cuda.synchronize()
+    os.makedirs(d, exist_ok=True)
+    h = pipe.to_host(g.last_set)
+    np.savez(os.path.join(d, f"{rank}_own.npz"),
+             kps=np.concatenate(h["keypoints"]).view(np.uint8) if h["keypoints"] else np.zeros(0, np.uint8),
+             desc=np.concatenate(h["descriptors"]).reshape(-1), counts=np.array([len(k) for k in h["keypoints"]]))
+    if rank == 0:
+        for r, v in enumerate(g.last):
+            v.cpu().numpy().tofile(os.path.join(d, f"{r}_gathered.bin"))
 
 
 def pipe_depth(args):

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void k_pack(int n_images, const int32_t* __res
     all += c;
     if (j < img) before += c;
   }
-  // workgroup sums of (before, all): pack both into one 64-bit lane sum (each < 2^31)
+  // workgroup sums of (before, all): pack both into one 64-bit lane sum; the host check keeps
+  // n_images * cap < 2^31, so neither 32-bit half can carry into the other
   unsigned long long v = ((unsigned long long)before << 32) | (unsigned long long)all;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -63,6 +64,8 @@ extern "C" int orbfe_pack_keypoints_device(int n_images, const int32_t* d_counts
   if (n_images <= 0 || cap <= 0 || !d_counts || !d_kps || !d_desc || !d_out || !d_total_bytes ||
       n_images > (1 << 20))
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_pack_keypoints_device: bad argument");
+  if ((long long)n_images * cap >= (1ll << 31))  // k_pack sums keypoint counts in 32-bit halves
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_pack_keypoints_device: n_images * cap must stay below 2^31");
   if (out_cap < orbfe_packed_bytes(n_images, (long long)n_images * cap))
     return orbfe_set_error(ORBFE_ERR_CAPACITY, "orbfe_pack_keypoints_device: out_cap below the worst case");
   hipLaunchKernelGGL(k_pack, dim3(n_images), dim3(256), 0, (hipStream_t)stream, n_images, d_counts, d_kps,

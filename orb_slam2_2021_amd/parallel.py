@@ -4,10 +4,13 @@ Extraction is independent per image (ORBextractor::operator(), ORBextractor.cc:1
 SearchForTriangulation per KeyFrame pair, so frames shard embarrassingly: rank r owns a block of
 frames and no collective touches the data path. The exchange steps BASELINE.json names:
 
-* C4: every rank's keypoints and descriptors gathered to rank 0. Each rank packs only its used
-  slots on the device (orbfe_pack_keypoints_device, include/orbfe_pack.h), the packed sizes are
-  all-gathered (8 bytes per rank), then rank 0 receives each payload point-to-point over RCCL
-  (xGMI: one link per peer) -- no fixed-capacity buffers cross the links.
+* C4: every rank's keypoints and descriptors gathered to rank 0. Each rank packs its used slots
+  on the device (orbfe_pack_keypoints_device, include/orbfe_pack.h: a header of per-image counts,
+  then the keypoints and descriptors back to back), and rank 0 receives each payload
+  point-to-point over RCCL (xGMI: one link per peer). gather_fixed moves a fixed byte count
+  (the packed worst case, about 1 % above a full batch's used bytes), so no size crosses to the
+  host and the exchange never synchronises it; gather_packed exchanges the sizes first and moves
+  exactly the used bytes (one host sync per call).
 * C5: the local map (the MapPoint SoA Tracking::SearchLocalPoints projects, Tracking.cc:1164-1216)
   is replicated: broadcast once from rank 0, then every rank matches its own frames against it.
 """
@@ -123,6 +126,48 @@ def gather_packed(payload, size, dst: int = 0, recv: Optional[Sequence] = None):
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     return out, sizes_h
+
+
+def gather_fixed(payload, nbytes: int, dst: int = 0, recv: Optional[Sequence] = None):
+    """Gather the first `nbytes` of every rank's payload to `dst` with point-to-point transfers
+    and no size exchange: the packed header (n_images, counts) tells the receiver what is used.
+    Enqueued on the caller's current stream; the host never waits for the device (the returned
+    requests are already waited on the stream, which is what torch's NCCL work.wait() does).
+
+    recv: on dst, per-rank uint8 buffers of at least nbytes (allocated if None). Returns the list
+    of per-rank views on dst (dst's own entry is payload[:nbytes]) and None elsewhere. The views
+    alias `payload` / `recv`: valid until the caller reuses them."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if payload.numel() < nbytes:
+        raise ValueError("payload smaller than nbytes")
+    ops, out = [], None
+    if rank == dst:
+        out = []
+        for r in range(world):
+            if r == dst:
+                out.append(payload[:nbytes])
+                continue
+            buf = recv[r] if recv is not None else torch.empty(nbytes, dtype=torch.uint8, device=payload.device)
+            if buf.numel() < nbytes:
+                raise ValueError(f"receive buffer for rank {r} too small")
+            out.append(buf[:nbytes])
+            ops.append(dist.P2POp(dist.irecv, out[-1], r))
+    else:
+        ops.append(dist.P2POp(dist.isend, payload[:nbytes], dst))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    return out
+
+
+def packed_size(buf) -> int:
+    """Used bytes of a packed buffer (numpy or a uint8 tensor), from its header."""
+    a = np.ascontiguousarray(buf[:4].cpu().numpy() if hasattr(buf, "cpu") else buf[:4], np.uint8)
+    n_img = int(a.view(np.int32)[0])
+    h = buf[4:4 + 4 * n_img]
+    c = np.ascontiguousarray(h.cpu().numpy() if hasattr(h, "cpu") else h, np.uint8).view(np.int32)
+    return packed_bytes(n_img, int(c.astype(np.int64).sum()))
 
 
 def broadcast_arrays(arrays: Dict[str, np.ndarray], device, src: int = 0) -> Dict[str, object]:

@@ -60,6 +60,35 @@ def _c4_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _c4_fixed_worker(rank, world, port, q):
+    """bench.py's exchange: fixed byte count (the packed worst case), no size collective."""
+    import torch
+    import torch.distributed as dist
+    _init(rank, world, port)
+    from orb_slam2_2021_amd import synth_frame
+    from orb_slam2_2021_amd.parallel import gather_fixed, packed_size
+    from oracle.orbref import RefExtractor
+    ref = RefExtractor(500, 1.2, 4, 20, 7)
+    mine = shard_frames(N_FRAMES, world, rank)
+    results = [ref(synth_frame(i, ROWS, COLS)) for i in mine]
+    buf = pack_host(results)
+    nbytes = packed_bytes(3, 3 * 600)  # every rank: the same worst case for 3 images of <= 600 kps
+    payload = torch.full((nbytes,), 0xEE, dtype=torch.uint8)
+    payload[:len(buf)] = torch.from_numpy(buf)
+    out = gather_fixed(payload, nbytes, dst=0)
+    if rank == 0:
+        frames = []
+        for r in range(world):
+            assert out[r].numel() == nbytes
+            v = out[r].numpy()
+            frames.extend(unpack_packed(v[:packed_size(v)]))
+        q.put(("c4f", [(f[0].tobytes(), f[1].tobytes()) for f in frames], None))
+    else:
+        assert out is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _c5_worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
@@ -155,6 +184,17 @@ def test_gloo_two_rank_c4_gather_matches_single_process():
         n = [len(RefExtractor(500, 1.2, 4, 20, 7)(synth_frame(i, ROWS, COLS))[0])
              for i in shard_frames(N_FRAMES, 2, r)]
         assert sizes[r] == packed_bytes(len(n), sum(n))
+
+
+def test_gloo_two_rank_c4_fixed_count_gather():
+    tag, got, _ = _run(_c4_fixed_worker)
+    from orb_slam2_2021_amd import synth_frame
+    from oracle.orbref import RefExtractor
+    ref = RefExtractor(500, 1.2, 4, 20, 7)
+    assert len(got) == N_FRAMES
+    for i, (kb, db) in enumerate(got):
+        k, d = ref(synth_frame(i, ROWS, COLS))
+        assert kb == k.tobytes() and db == d.tobytes()
 
 
 def test_gloo_two_rank_c5_replicated_map_sharded_frames():

@@ -89,6 +89,12 @@ def test_bad_arguments_rejected_without_device():
     assert lib.orbfe_extractor_create(2000, 1.0, 8, 20, 7, 0, byref(h)) == L.ORBFE_ERR_ARG
     assert lib.orbfe_extract(None, None, 10, 10, 10, None, 0, None, None) == L.ORBFE_ERR_ARG
     assert lib.orbfe_descriptor_distance(None, None) == L.ORBFE_ERR_ARG
+    # k_pack sums counts in 32-bit halves: n_images * cap >= 2^31 is refused before any launch
+    from ctypes import c_size_t, c_void_p
+    one = c_void_p(16)
+    assert lib.orbfe_pack_keypoints_device(1 << 16, one, one, one, 1 << 15, one, c_size_t(1 << 62), one,
+                                           None) == L.ORBFE_ERR_ARG
+    assert b"2^31" in lib.orbfe_last_error()
 
 
 def test_product_never_imports_the_oracle():
