@@ -4,14 +4,18 @@
 A step is one pass of the hot path over one batch of synthetic input resident in HBM: S
 sub-batches (default 1024) of B = 32 stereo frames per GPU (BASELINE.json configs[2], "C3"), each
 sub-batch (orb_slam2_2021_amd.pipeline.C3Pipeline):
-  1. ORBextractor::operator() on its 2B images  (k_copy0, k_resize x7, k_fast, k_octree, k_blur, k_describe)
-  2. KeyFrame::ComputeBoW: vocabulary transform, ORBvoc-shaped k=10/L=6 tree, levelsup 4
-     (BowVector + FeatureVector; k_vocab_descend + k_vocab)
-  3. ORBmatcher::SearchForTriangulation(left_i, right_i) for the B pairs  (k_sft_*)
+  1. the stereo Frame constructor (Frame.cc:113-125): ORBextractor::operator() on its 2B images
+     (k_copy0, k_resize x7, k_fast, k_octree, k_blur, k_describe), then Frame::ComputeStereoMatches
+     (k_stereo_*) for the left KeyFrames' mvuRight
+  2. KeyFrame::ComputeBoW of the B left KeyFrames: vocabulary transform, ORBvoc-shaped k=10/L=6
+     tree, levelsup 4 (BowVector + FeatureVector; k_vocab_descend + k_vocab)
+  3. ORBmatcher::SearchForTriangulation(KF t, KF t+1) for the B-1 consecutive KeyFrame pairs of the
+     driving sequence, 1 m apart along z (k_sft_*)
   4. with N > 1 GPUs: the used keypoints + descriptors of every rank gathered to rank 0 over RCCL
-     (config C4: packed on the device, sizes first, then point-to-point payloads)
-The sub-batches cycle over --input-batches (default 8) distinct resident batches, so no
-sub-batch re-reads the previous one's input.
+     (config C4: packed on the device, fixed-count point-to-point payloads, no host sync)
+--pairs stereo runs rounds 1-2's workload instead (ComputeBoW on all 2B images,
+SearchForTriangulation(left_i, right_i) of one frame). The sub-batches cycle over --input-batches
+(default 8) distinct resident batches, so no sub-batch re-reads the previous one's input.
 value = stereo frames processed by all ranks / max-over-ranks wall time of the K timed steps.
 
 Launch: python bench.py [--gpus N] [--steps K] [--warmup W]. With N > 1 and no torch.distributed
@@ -37,7 +41,6 @@ sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec (ORB extract+match) on 1241×376, 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-BOX_CPU_SHARE = 16     # host cores a one-GPU box grants a job (OMP_NUM_THREADS there)
 
 
 def parse(argv=None):
@@ -56,7 +59,8 @@ def parse(argv=None):
     p.add_argument("--vocab-levels", type=int, default=6, help="synthetic ORBvoc depth (k = 10)")
     p.add_argument("--levelsup", type=int, default=4, help="KeyFrame::ComputeBoW's levelsup")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per mode")
-    p.add_argument("--cpu-threads", type=int, default=BOX_CPU_SHARE)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the all-core CPU baseline (0: the affinity mask, capped by OMP_NUM_THREADS)")
     p.add_argument("--event-every", type=int, default=4,
                    help="HIP events around the dominant kernel on every n-th timed sub-batch")
     p.add_argument("--probe-subbatches", type=int, default=24)
@@ -67,9 +71,12 @@ def parse(argv=None):
     p.add_argument("--no-parity", action="store_true", help="skip the oracle check of the last sub-batch")
     p.add_argument("--pipeline", type=int, default=0,
                    help="output sets in flight (0: 2 per extractor handle; 1: strictly one at a time)")
-    p.add_argument("--stereo", action="store_true",
-                   help="run Frame::ComputeStereoMatches on every pair after extraction (the stereo "
-                        "Frame constructor's full path); its mvuRight feeds SearchForTriangulation")
+    p.add_argument("--pairs", choices=("kf", "stereo"), default="kf",
+                   help="SearchForTriangulation pairs: kf = KeyFrame t vs t+1 of a driving sequence (SURVEY 8(d); "
+                        "ComputeBoW on the lefts), stereo = left vs right image of one frame (rounds 1-2)")
+    p.add_argument("--no-stereo", dest="stereo", action="store_false",
+                   help="skip Frame::ComputeStereoMatches (the stereo Frame constructor's matching, Frame.cc:125, "
+                        "whose mvuRight feeds SearchForTriangulation; on by default)")
     p.add_argument("--extractors", type=int, default=2,
                    help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
                         "own stream, their side-stream work on one shared high-priority stream")
@@ -116,6 +123,35 @@ def parse(argv=None):
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
     return p.parse_args(argv)
+
+
+SEQ_SEED = 0x0C3  # the C3 driving sequence (orbfe_synth_sequence_frame)
+
+
+def make_inputs(args, world, rank):
+    """NB distinct batches of B stereo frames of this rank (frames sharded contiguously over the
+    ranks, shard_frames): frames of the seeded driving sequence for --pairs kf (batch j holds
+    consecutive frames, so KeyFrame t and t+1 are neighbours), independent seeded frames
+    (orbfe_synth_frame) for --pairs stereo. Rendered on a thread pool (the C renderer releases the
+    GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from orb_slam2_2021_amd import synth_frame, synth_sequence_frame
+    from orb_slam2_2021_amd.parallel import shard_frames
+    B, H, W, NB = args.batch, args.rows, args.cols, max(1, args.input_batches)
+    host = np.zeros((NB, 2 * B, H, W), np.uint8)
+    mine = shard_frames(world * NB * B, world, rank)
+
+    def one(ji):
+        j, i = ji
+        idx = mine[j * B + i]
+        if args.pairs == "kf":
+            host[j, i], host[j, B + i] = synth_sequence_frame(SEQ_SEED, idx, H, W, right=True)
+        else:
+            host[j, i], host[j, B + i] = synth_frame(idx, H, W, right=True)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as pool:
+        list(pool.map(one, [(j, i) for j in range(NB) for i in range(B)]))
+    return host
 
 
 def spawn_ranks(args) -> int:
@@ -217,10 +253,7 @@ def main():
     NB = max(1, args.input_batches)
     S_sub = max(1, args.batches_per_step)
     # ---- inputs: NB distinct batches of B stereo frames of this rank, resident in HBM ----
-    host = np.zeros((NB, n_img, H, W), np.uint8)
-    for j in range(NB):
-        for i, idx in enumerate(shard_frames(world * NB * B, world, rank)[j * B:(j + 1) * B]):
-            host[j, i], host[j, B + i] = synth_frame(idx, H, W, right=True)
+    host = make_inputs(args, world, rank)
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     if args.level_launches:
@@ -256,7 +289,7 @@ def main():
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side)
+                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs)
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream
@@ -362,14 +395,14 @@ def main():
     geo = ext.geometry(H, W)
     use_timed = dominant in timed and not args.no_kernel_events
     roof = roofline(timed if use_timed else probe, dominant, geo, counts, cand, n_img,
-                    timed_events if use_timed else args.probe_subbatches)
+                    timed_events if use_timed else args.probe_subbatches, pipe)
     roof["measured_in"] = (f"timed region (HIP events on every {ev_every}th sub-batch, "
                            f"{timed_events} sub-batches)" if use_timed else "probe pass")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B)
     if roof["traffic"] is not None:  # per launch, like `achieved`: the sub-batch figure / its launches
         roof["traffic_per_subbatch"] = roof["traffic"]
         roof["traffic"] = int(roof["traffic"] / roof["launches_per_subbatch"])
-    algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B)
+    algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B, pipe.n_pairs)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -385,12 +418,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded KITTI-shaped stereo frames, orbfe_synth_frame; synthetic ORBvoc-shaped "
+        "data": ("synthetic (seeded KITTI-shaped driving sequence, orbfe_synth_sequence_frame, 1 m per frame along z"
+                 if args.pairs == "kf" else "synthetic (seeded KITTI-shaped stereo frames, orbfe_synth_frame")
+                + "; synthetic ORBvoc-shaped "
                 f"vocabulary k=10 L={args.vocab_levels})",
         "config": {
             "workload": "C3: stereo extract + ComputeBoW + "
                         + ("ComputeStereoMatches + " if args.stereo else "")
-                        + f"SearchForTriangulation, {W}x{H}, batch {B} stereo frames/GPU"
+                        + (f"SearchForTriangulation(KF t, KF t+1) x{pipe.n_pairs}" if args.pairs == "kf"
+                           else f"SearchForTriangulation(left, right) x{pipe.n_pairs}")
+                        + f", {W}x{H}, batch {B} stereo frames/GPU"
                         + (" + RCCL gather to rank 0 (C4)" if gather else ""),
             "nfeatures": args.nfeatures, "scale_factor": 1.2, "nlevels": 8, "ini_th_fast": 20,
             "min_th_fast": 7, "vocabulary": f"k=10 L={args.vocab_levels} ({tree.n_nodes} nodes), "
@@ -410,7 +447,8 @@ def main():
         },
         "kernels_ms_per_subbatch": {k: round(v[0] / args.probe_subbatches, 4) for k, v in probe.items()},
         "keypoints_per_image": round(float(counts.mean()), 1),
-        "sft_matches_per_pair": round(float(nm.mean()), 1),
+        "sft_matches_per_pair": round(float(nm[:pipe.n_pairs].mean()), 1),
+        "sft_pairs_per_subbatch": pipe.n_pairs,
         "stereo_matches_per_pair": (round(float((last.ur >= 0).sum().item()) / B, 1) if args.stereo else None),
         "cpu_baseline": None,
     }
@@ -433,7 +471,7 @@ def main():
         j = (counter[0] - 1) % NB
         r = check_c3(host[j], pipe.to_host(last), ref_voc, state["u_right"], state["mp_state"], state["scale"],
                      state["sigma2"], state["cam"], state["F12"], state["epipole"], levelsup=args.levelsup,
-                     stereo=args.stereo, mb=state["mb"])
+                     stereo=args.stereo, mb=state["mb"], pairs=args.pairs)
         ok = bool(r["all"])
         if world > 1:
             t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=comm_dev)
@@ -462,7 +500,8 @@ def main():
                            "keyframe_searches": keyframe_leg(args),
                            "compute_stereo_matches": stereo_leg(args, ext, d_img[0], host[0], B, H, W,
                                                                 pipe.cap, state["cam"]["bf"], state["mb"]),
-                           "vocabulary_transform": vocab_leg(args, voc, tree, pipe)}
+                           "vocabulary_transform": vocab_leg(args, voc, tree, pipe),
+                           "c3_other_pairing": pairing_leg(args, exts, tree, voc, d_img, pstreams, dev)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(host[0], B, H, W, args, tree, state)
     if rank == 0:
@@ -507,7 +546,7 @@ def level_pixels(geo):
     return [int(w) * int(h) for w, h in geo[:, :2]]
 
 
-def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches):
+def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches, pipe):
     """Roofline of the dominant kernel: ALGORITHMIC bytes per sub-batch / its HIP-event time per
     sub-batch (a kernel may run as several launches per sub-batch, e.g. k_resize once per level and
     k_fast as level 0 beside the resize chain + levels 1..7; per launch = per sub-batch / launches).
@@ -521,7 +560,8 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches):
       k_describe 4 B in + 60 B out per keypoint (+ 749 + 512 gathered bytes per keypoint, not
                  counted: they overlap between keypoints and come from L2)
       k_vocab    32 B in + 6 x 48 B child records + 32 B out (FeatureVector + BowVector) per descriptor
-      k_sft      per pair 2 N (32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out
+                 of the KeyFrame images (the B lefts with --pairs kf)
+      k_sft      per pair (N1 + N2)(32 + 28 + 4) B (descriptors, keypoints, flags/uRight) + 4 N1 out
       k_stereo   per pair 2 N (28 + 32) B + 2 x 16 B per right keypoint (buckets) + 12 B per left
                  keypoint (the 11x11 windows and candidate descriptors come from L2)"""
     px = level_pixels(geo)
@@ -535,8 +575,8 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches):
         "k_blur": n_img * 2 * sum(px),
         "k_copy0": n_img * 2 * px[0],
         "k_pyramid": n_img * (2 * px[0] + sum(px[1:])),
-        "k_vocab": (32 + 6 * 48 + 32) * nkp,
-        "k_sft": 64 * nkp + 4 * nkp // 2,
+        "k_vocab": (32 + 6 * 48 + 32) * int(counts[:pipe.n_vocab].sum()),
+        "k_sft": sum(64 * int(counts[a] + counts[b]) + 4 * int(counts[a]) for a, b in pipe.pair_idx),
         "k_stereo": 60 * nkp + 32 * nkp // 2 + 12 * nkp // 2,
     }
     total_ms, launches = kt[dom]
@@ -571,14 +611,14 @@ def pmc_traffic(kernel, W, H, B):
     return int(k["traffic_bytes_per_step"]), doc.get("source")
 
 
-def pipeline_bytes_per_stereo_frame(geo, counts, B):
+def pipeline_bytes_per_stereo_frame(geo, counts, B, n_pairs):
     """SURVEY 8(d): per image sum_l px (read once) + sum_l>=1 px (write) + 60 B per keypoint;
-    SearchForTriangulation per pair 2 N (32 + 28 + 4) + N/4 + 8 N."""
+    SearchForTriangulation per pair 2 N (32 + 28 + 4) + N/4 + 8 N, n_pairs pairs per B frames."""
     px = level_pixels(geo)
     n_per_img = float(counts.mean())
     extract = sum(px) + sum(px[1:]) + 60 * n_per_img
     sft = 2 * n_per_img * 64 + 2 * n_per_img / 8 + 4 * 2 * n_per_img
-    return 2 * extract + sft
+    return 2 * extract + sft * n_pairs / B
 
 
 def percentiles(xs):
@@ -747,6 +787,35 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
         out["cpu_oracle_ms_per_search"] = round(1e3 * (time.perf_counter() - t0), 3)
         out["cpu_bit_exact"] = bool(nr == nm and nvr == nv and np.array_equal(br, best))
     return out
+
+
+def pairing_leg(args, exts, tree, voc, d_img, pstreams, dev, subbatches=256):
+    """The C3 step with the other SearchForTriangulation pairing on the same resident frames and
+    handles (--pairs kf runs: left_i vs right_i of each frame with ComputeBoW on all 2B images, the
+    rounds 1-2 workload; --pairs stereo runs: KeyFrame t vs t+1): `subbatches` sub-batches timed
+    wall-clock after a warm-up, and its SearchForTriangulation matches per pair. Reported beside
+    `value`, which is the default pairing's."""
+    import torch
+    from orb_slam2_2021_amd.pipeline import build_c3
+    other = "stereo" if args.pairs == "kf" else "kf"
+    B, H, W = args.batch, args.rows, args.cols
+    pipe, _ = build_c3(exts if len(exts) > 1 else exts[0], tree, voc, B, H, W, dev, seed=1234,
+                       depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
+                       pairs=other)
+    torch.cuda.set_stream(pipe.stream)
+    nb = d_img.shape[0]
+    for j in range(16):
+        pipe.run(d_img[j % nb].data_ptr())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(subbatches):
+        pipe.run(d_img[j % nb].data_ptr())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    nm = pipe.last.nm.cpu().numpy()[:pipe.n_pairs]
+    return {"pairs": other, "value": round(B * subbatches / dt, 1), "unit": "stereo frames/s",
+            "sft_pairs_per_subbatch": pipe.n_pairs, "sft_matches_per_pair": round(float(nm.mean()), 1),
+            "what": f"{subbatches} sub-batches of the C3 step with pairs={other} on the same frames and handles"}
 
 
 def keyframe_leg(args, reps=20):
@@ -1010,14 +1079,29 @@ def _cpu_name():
     return cpu
 
 
+def cpu_threads(args):
+    """Threads for the all-core CPU baseline: --cpu-threads, else the CPUs this process may run on
+    (os.sched_getaffinity), capped by OMP_NUM_THREADS when the environment sets it (a GPU box
+    grants a job a share of a larger machine and says so there: 16 for one GPU)."""
+    if args.cpu_threads > 0:
+        return args.cpu_threads, "--cpu-threads"
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"OMP_NUM_THREADS={omp} (affinity mask: {aff} CPUs)"
+    return aff, f"affinity mask ({aff} CPUs)"
+
+
 def cpu_baseline(host, B, H, W, args, tree, state):
     """The oracle built with the reference's flags (-O3 -march=native, CMakeLists.txt:10-11) on the
-    host's cores, three ways, each per stereo frame = extract left + right,
-    ComputeBoW of both (L=6 vocabulary), SearchForTriangulation(left, right):
+    host's cores, three ways. Per stereo frame, the same work as the GPU step: the
+    stereo Frame (extract left + right, Frame::ComputeStereoMatches on their pyramids), ComputeBoW
+    of the KeyFrame, and SearchForTriangulation against the previous KeyFrame of the sequence
+    (--pairs kf; with --pairs stereo: ComputeBoW of both images, SearchForTriangulation(left, right)):
       1 thread        -- the latency of one frame on one core;
       2 threads       -- the stereo Frame pattern (Frame.cc:113-116): left and right extracted on
-                         two threads, then ComputeBoW + matching;
-      all cores       -- --cpu-threads independent streams of frames (the box's CPU share).
+                         two threads, then the rest;
+      all cores       -- cpu_threads() independent streams of frames.
     `value` is the all-core rate. The oracle is a scalar restatement, not OpenCV's SIMD FAST /
     resize / GaussianBlur, so it understates the real reference's speed. Plus C1: 100 distinct
     synthetic stereo frames through the 2-thread extraction (the CPU-only config)."""
@@ -1029,27 +1113,44 @@ def cpu_baseline(host, B, H, W, args, tree, state):
                                               tree.is_leaf, tree.descriptors, tree.weights)
     cam, F12, (ex, ey) = state["cam"], state["F12"], state["epipole"]
     ur, mp = state["u_right"], state["mp_state"]
+    kf_pairs = args.pairs == "kf"
 
     def new_extractors():
         return [orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native") for _ in range(2)]
 
-    def match(p, k1, d1, k2, d2):
-        res = []
-        for i, (k, d) in ((p, (k1, d1)), (B + p, (k2, d2))):
-            d = d if d is not None else np.zeros((0, 32), np.uint8)
+    def keyframe(i, k, d, with_bow):
+        d = d if d is not None else np.zeros((0, 32), np.uint8)
+        F = S.Frame(keys_un=k, descriptors=d, u_right=ur[i, :len(k)], mp_state=mp[i, :len(k)],
+                    scale_factors=state["scale"], level_sigma2=state["sigma2"], min_x=0.0, max_x=float(W),
+                    min_y=0.0, max_y=float(H), **cam)
+        if with_bow:
             _, _, fv = ref_voc.transform(d, args.levelsup)
-            F = S.Frame(keys_un=k, descriptors=d, u_right=ur[i, :len(k)], mp_state=mp[i, :len(k)],
-                        scale_factors=state["scale"], level_sigma2=state["sigma2"], min_x=0.0, max_x=float(W),
-                        min_y=0.0, max_y=float(H), **cam)
             F.feat_vec = FeatureVector(*fv)
-            res.append(F)
-        orbref.search_for_triangulation(res[0], res[1], F12, ex, ey, False, False)
+        return F
+
+    def frame_work(ext, p, k1, d1, k2, d2, prev):
+        """Everything after the two extractions; returns this frame's left KeyFrame."""
+        F1 = keyframe(p, k1, d1, True)
+        F2 = keyframe(B + p, k2, d2, not kf_pairs)
+        if args.stereo:
+            lv = [ext[0].level(i) for i in range(8)]
+            rv = [ext[1].level(i) for i in range(8)]
+            F1.u_right, _ = orbref.compute_stereo_matches(F1.keys_un, F1.descriptors, F2.keys_un, F2.descriptors,
+                                                          lv, rv, state["scale"], ext[0].tables()["inv_scale"], state["mb"],
+                                                          cam["bf"], kind="native")
+        if not kf_pairs:
+            orbref.search_for_triangulation(F1, F2, F12, ex, ey, False, False)
+        elif prev is not None:
+            orbref.search_for_triangulation(prev, F1, F12, ex, ey, False, False)
+        return F1
 
     def stream(n_threads_inner, budget, first, stats, lock):
         ext = new_extractors()
-        frames, t_total = 0, 0.0
+        frames, t_total, prev = 0, 0.0, None
         while t_total < budget or frames < 2:
             p = (first + frames) % B
+            if p == 0:
+                prev = None  # the batch wraps: frame 0 does not follow frame B-1
             t0 = time.perf_counter()
             if n_threads_inner == 2:
                 out = [None, None]
@@ -1061,7 +1162,7 @@ def cpu_baseline(host, B, H, W, args, tree, state):
             else:
                 k1, d1 = ext[0](host[p])
                 k2, d2 = ext[1](host[B + p])
-            match(p, k1, d1, k2, d2)
+            prev = frame_work(ext, p, k1, d1, k2, d2, prev)
             t_total += time.perf_counter() - t0
             frames += 1
         with lock:
@@ -1075,9 +1176,9 @@ def cpu_baseline(host, B, H, W, args, tree, state):
         f, t = st[0]
         modes[name] = {"stereo_frames_per_s": round(f / t, 3), "ms_per_frame": round(1e3 * t / f, 2),
                        "frames": f, "threads": inner}
-    T = max(1, args.cpu_threads)
+    T, why = cpu_threads(args)
     st = []
-    th = [threading.Thread(target=stream, args=(1, args.cpu_seconds, i, st, lock)) for i in range(T)]
+    th = [threading.Thread(target=stream, args=(1, args.cpu_seconds, (i * 7) % B, st, lock)) for i in range(T)]
     t0 = time.perf_counter()
     for t in th:
         t.start()
@@ -1086,7 +1187,7 @@ def cpu_baseline(host, B, H, W, args, tree, state):
     wall = time.perf_counter() - t0
     all_frames = sum(f for f, _ in st)
     modes["all_cores"] = {"stereo_frames_per_s": round(all_frames / wall, 3), "frames": all_frames,
-                          "threads": T, "wall_s": round(wall, 2)}
+                          "threads": T, "threads_from": why, "wall_s": round(wall, 2)}
     # C1: 100 distinct stereo frames, extraction only, the stereo Frame's two threads
     ext = new_extractors()
     t0 = time.perf_counter()
@@ -1097,12 +1198,14 @@ def cpu_baseline(host, B, H, W, args, tree, state):
         ext[0](l)
         t.join()
     c1 = time.perf_counter() - t0
+    work = ("2 x ORBextractor" + (" + ComputeStereoMatches" if args.stereo else "")
+            + (f" + ComputeBoW (k=10 L={tree.levels}) + SearchForTriangulation(previous KF, KF)" if kf_pairs
+               else f" + 2 x ComputeBoW (k=10 L={tree.levels}) + SearchForTriangulation(left, right)"))
     return {"value": modes["all_cores"]["stereo_frames_per_s"], "unit": "stereo frames/s", "cores": T,
             "kind": "port",
             "sample": f"{all_frames} stereo frames over {T} threads (each cycling this rank's {B} frames) "
-                      f"{W}x{H}: 2 x ORBextractor + 2 x ComputeBoW (k=10 L={tree.levels}) + SearchForTriangulation "
-                      f"per frame, on {_cpu_name()}; oracle built -O3 -march=native -- a scalar restatement, "
-                      "not OpenCV's SIMD FAST/resize/GaussianBlur, so it understates the reference",
+                      f"{W}x{H}: {work} per frame, on {_cpu_name()}; oracle built -O3 -march=native -- a scalar "
+                      "restatement, not OpenCV's SIMD FAST/resize/GaussianBlur, so it understates the reference",
             "modes": modes,
             "c1_100_frames": {"seconds": round(c1, 2), "ms_per_stereo_frame": round(10 * c1, 2),
                               "what": "100 distinct synthetic KITTI-shaped stereo frames, ORBextractor on "

@@ -19,6 +19,15 @@ extern "C" {
 int orbfe_synth_frame(uint64_t index, int rows, int cols, int n_rects, uint8_t* left,
                       uint8_t* right, size_t step);
 
+/* Frame t of a seeded driving sequence (SURVEY 8(d), C3 KeyFrame pairs): a world of textured
+ * billboards seen by a pinhole camera (fx, fy, cx, cy) at (0, 0, t * step_z) looking down +z, the
+ * right camera `baseline` metres to the right (true stereo disparity fx * baseline / depth). Pose of
+ * left frame t: Rcw = I, tcw = (0, 0, -t * step_z). Consecutive frames share most billboards, and
+ * their epipole is (cx, cy). left and/or right (either may be NULL), rows `step` bytes apart. */
+int orbfe_synth_sequence_frame(uint64_t seq_seed, long long t, int rows, int cols, float fx, float fy,
+                               float cx, float cy, float baseline, float step_z, uint8_t* left,
+                               uint8_t* right, size_t step);
+
 #ifdef __cplusplus
 }
 #endif

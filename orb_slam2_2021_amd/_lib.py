@@ -185,6 +185,8 @@ _SIGNATURES = {
                                           c_float, c_void_p, POINTER(c_int), POINTER(frustum_out),
                                           POINTER(c_int)]),
     "orbfe_synth_frame": (c_int, [c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t]),
+    "orbfe_synth_sequence_frame": (c_int, [c_uint64, ctypes.c_longlong, c_int, c_int, c_float, c_float, c_float,
+                                           c_float, c_float, c_float, c_void_p, c_void_p, c_size_t]),
     # orbfe_keyframe.h
     "orbfe_search_by_bow_kf_frame": (c_int, [c_void_p, POINTER(frame_view), POINTER(feature_vector),
                                              POINTER(frame_view), POINTER(feature_vector), c_void_p,

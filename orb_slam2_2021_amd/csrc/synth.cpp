@@ -6,6 +6,7 @@
 // a layer of random rectangles composited in order (the corner-rich part FAST responds to), and
 // sum-of-4-uniforms noise (sigma ~= 3). The right image of a stereo pair sees the same scene
 // shifted left by d(y) = 8 + 32*y/H pixels, with independent noise.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -105,5 +106,98 @@ extern "C" int orbfe_synth_frame(uint64_t index, int rows, int cols, int n_rects
   Scene sc(seed, rows, cols, n_rects > 0 ? n_rects : ORBFE_SYNTH_DEFAULT_RECTS);
   if (left) render(sc, seed ^ 0x1111111111111111ull, 0, left, step);
   if (right) render(sc, seed ^ 0x2222222222222222ull, 1, right, step);
+  return 0;
+}
+
+// ---- driving sequence (SURVEY 8(d) C3 KeyFrame pairs: frame t and t+1, poses step_z apart along z)
+//
+// A world of fronto-parallel textured billboards. Depth slab k (world z in [k, k+1) m) holds
+// kSeqPerSlab billboards drawn from seed (seq_seed, k): centre x in +-70 m, y in +-21 m, width and
+// height 0.3-2.5 m, an intensity, and for half of them an inner panel (inset by a quarter) of a
+// second intensity. Frame t's left camera sits at (0, 0, t * step_z) looking down +z (pinhole fx,
+// fy, cx, cy); the right camera of the pair is `baseline` metres to the right. Billboards between
+// kSeqNear and kSeqFar metres ahead are painted far to near over the sinusoidal background at
+// infinity (the same field as orbfe_synth_frame, zero disparity), then sum-of-4-uniforms noise
+// (sigma ~= 3) seeded per (frame, side). The epipole of two consecutive left frames is (cx, cy):
+// inside the image, so SearchForTriangulation's epipole gate (ORBmatcher.cc:757-763) is live.
+namespace {
+constexpr int kSeqPerSlab = 160;
+constexpr float kSeqNear = 6.0f, kSeqFar = 80.0f;
+
+struct Billboard {
+  float z, x, y, hw, hh;
+  int v, v_in;  // v_in < 0: no inner panel
+};
+
+void slab_billboards(uint64_t seq_seed, int64_t k, std::vector<Billboard>& out) {
+  Xoshiro128ss g(seq_seed * 0x9E3779B97F4A7C15ull ^ (uint64_t)(k + 0x5EEDull) * 0xD1B54A32D192ED03ull);
+  for (int i = 0; i < kSeqPerSlab; i++) {
+    Billboard b;
+    b.z = (float)k + g.uniform();
+    b.x = -70.f + 140.f * g.uniform();
+    b.y = -21.f + 42.f * g.uniform();
+    b.hw = 0.5f * (0.3f + 2.2f * g.uniform());
+    b.hh = 0.5f * (0.3f + 2.2f * g.uniform());
+    b.v = g.range(0, 255);
+    b.v_in = (g.next() & 1u) ? g.range(0, 255) : -1;
+    out.push_back(b);
+  }
+}
+
+// pixel columns [a, b) whose centres lie in [u0, u1)
+inline void span(float u0, float u1, int n, int& a, int& b) {
+  a = (int)std::ceil(u0 - 0.5f);
+  b = (int)std::ceil(u1 - 0.5f);
+  a = std::max(a, 0);
+  b = std::min(b, n);
+}
+
+void render_sequence(const std::vector<Billboard>& bbs, float cam_x, float cam_z, int rows, int cols,
+                     float fx, float fy, float cx, float cy, uint64_t noise_seed, uint8_t* out, size_t step) {
+  Scene bg(0x0B5EED00ull, rows, cols, 0);  // the background field only (no rectangles)
+  std::vector<float> img((size_t)rows * cols);
+  for (int y = 0; y < rows; y++) bg.row(y, 0, img.data() + (size_t)y * cols);
+  for (const Billboard& b : bbs) {  // far to near
+    const float d = b.z - cam_z;
+    if (d < kSeqNear || d >= kSeqFar) continue;
+    const float sx = fx / d, sy = fy / d, u = cx + (b.x - cam_x) * sx, v = cy + b.y * sy;
+    int x0, x1, y0, y1;
+    span(u - b.hw * sx, u + b.hw * sx, cols, x0, x1);
+    span(v - b.hh * sy, v + b.hh * sy, rows, y0, y1);
+    for (int y = y0; y < y1; y++)
+      for (int x = x0; x < x1; x++) img[(size_t)y * cols + x] = (float)b.v;
+    if (b.v_in >= 0) {
+      span(u - 0.5f * b.hw * sx, u + 0.5f * b.hw * sx, cols, x0, x1);
+      span(v - 0.5f * b.hh * sy, v + 0.5f * b.hh * sy, rows, y0, y1);
+      for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++) img[(size_t)y * cols + x] = (float)b.v_in;
+    }
+  }
+  Xoshiro128ss g(noise_seed);
+  const float k = 3.0f * 1.7320508f;
+  for (int y = 0; y < rows; y++)
+    for (int x = 0; x < cols; x++) {
+      float n = g.uniform() + g.uniform() + g.uniform() + g.uniform() - 2.0f;
+      float v = std::nearbyint(img[(size_t)y * cols + x] + k * n);
+      out[(size_t)y * step + x] = (uint8_t)(v < 0.f ? 0.f : (v > 255.f ? 255.f : v));
+    }
+}
+}  // namespace
+
+extern "C" int orbfe_synth_sequence_frame(uint64_t seq_seed, long long t, int rows, int cols, float fx, float fy,
+                                          float cx, float cy, float baseline, float step_z, uint8_t* left,
+                                          uint8_t* right, size_t step) {
+  if (rows <= 0 || cols <= 0 || step < (size_t)cols || (!left && !right) || t < 0 || !(fx > 0.f) ||
+      !(fy > 0.f) || !(step_z >= 0.f))
+    return -1;
+  const float cam_z = (float)((double)t * step_z);
+  std::vector<Billboard> bbs;
+  for (int64_t k = (int64_t)std::floor(cam_z + kSeqNear); k <= (int64_t)std::ceil(cam_z + kSeqFar); k++)
+    slab_billboards(seq_seed, k, bbs);
+  std::stable_sort(bbs.begin(), bbs.end(), [](const Billboard& a, const Billboard& b) { return a.z > b.z; });
+  const uint64_t ns = (seq_seed ^ 0x5E0F5E0F5E0F5E0Full) + (uint64_t)t * 0x9E3779B97F4A7C15ull;
+  if (left) render_sequence(bbs, 0.f, cam_z, rows, cols, fx, fy, cx, cy, ns ^ 0x1111111111111111ull, left, step);
+  if (right)
+    render_sequence(bbs, baseline, cam_z, rows, cols, fx, fy, cx, cy, ns ^ 0x2222222222222222ull, right, step);
   return 0;
 }

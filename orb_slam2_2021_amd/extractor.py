@@ -352,3 +352,20 @@ def synth_frame(index: int, rows: int = 376, cols: int = 1241, n_rects: int = 0,
     L.check(lib.orbfe_synth_frame(int(index), rows, cols, int(n_rects), L.ptr(left),
                                   L.ptr(r) if right else None, c_size_t(cols)), "orbfe_synth_frame")
     return (left, r) if right else left
+
+
+def synth_sequence_frame(seq: int, t: int, rows: int = 376, cols: int = 1241, cam: dict = None,
+                         step_z: float = 1.0, right: bool = False):
+    """Frame t of a seeded driving sequence (orbfe_synth_sequence_frame): the camera moves step_z m
+    along +z per frame, so frames t and t+1 are the C3 KeyFrame pair of SURVEY 8(d). `cam` holds
+    fx, fy, cx, cy and bf (baseline = bf / fx); KITTI-like by default. Returns left or (left, right)."""
+    from .synthetic import KITTI_CAM
+    cam = cam or KITTI_CAM
+    lib = L.lib()
+    left = np.zeros((rows, cols), np.uint8)
+    r = np.zeros((rows, cols), np.uint8) if right else None
+    L.check(lib.orbfe_synth_sequence_frame(int(seq), int(t), rows, cols, cam["fx"], cam["fy"], cam["cx"], cam["cy"],
+                                           cam["bf"] / cam["fx"], float(step_z), L.ptr(left),
+                                           L.ptr(r) if right else None, c_size_t(cols)),
+            "orbfe_synth_sequence_frame")
+    return (left, r) if right else left

@@ -1,11 +1,22 @@
 """The C3 step on one GPU, device-resident (BASELINE.json configs[2]): B stereo frames ->
 
   1. ORBextractor::operator() on all 2B images, lefts first   (ORBextractor.cc:1041-1103)
+  (+ Frame::ComputeStereoMatches after extraction with stereo=True, Frame.cc:125)
   2. KeyFrame::ComputeBoW: TemplatedVocabulary::transform(desc, BowVector, FeatureVector, 4)
                                                               (KeyFrame.cc:59-68)
-  3. ORBmatcher(0.6, false).SearchForTriangulation(left_i, right_i, F12, ..., false)
+  3. ORBmatcher(0.6, false).SearchForTriangulation(KF1, KF2, F12, ..., false)
                                                               (LocalMapping.cc:219-258, ORBmatcher.cc:671-839)
-  (+ Frame::ComputeStereoMatches after extraction with stereo=True, Frame.cc:125)
+
+Two pairings (`pairs`):
+  "kf"      SURVEY 8(d)'s KeyFrame pairs: the B frames are consecutive frames of a driving sequence
+            (orbfe_synth_sequence_frame, poses step_z apart along z), each a stereo KeyFrame whose
+            keypoints and descriptors are the left image's (the stereo Frame's mvKeys,
+            Frame.cc:113-130); ComputeBoW runs on the B lefts and SearchForTriangulation on
+            (KF t, KF t+1) for t = 0..B-2 -- what LocalMapping::CreateNewMapPoints does for the new
+            KeyFrame and its covisible predecessor (LocalMapping.cc:211-272). The epipole is the
+            principal point, inside the image, so the epipole gate is live.
+  "stereo"  the round-1/2 workload: ComputeBoW on all 2B images and SearchForTriangulation on
+            (left_i, right_i) of one stereo frame (an x baseline: the epipole lies far outside).
 
 bench.py times it and tests/test_gpu_c3.py checks it against the oracle, so both run this exact
 sequence. The KeyFrames' per-keypoint state the matcher reads (mvuRight, GetMapPoint) is given
@@ -57,6 +68,7 @@ class PipelineStreams:
         import torch
         self.device = device
         self._ptrs = []
+        self._attached = []
 
         def make(high):
             p = ctypes.c_void_p()
@@ -78,7 +90,20 @@ class PipelineStreams:
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
         return self.extract + [self.match]
 
+    def attach(self, ext) -> None:
+        """Route `ext`'s side-stream work to the shared side stream (detached again by close())."""
+        ext.set_side_stream(self.side.cuda_stream)
+        self._attached.append(ext)
+
     def close(self):
+        """Wait for the streams, point every attached extractor back at its own side stream, then
+        destroy the streams (no handle is left holding a destroyed hipStream_t)."""
+        for s in self.extract + [self.match, self.side]:
+            if s is not None:
+                s.synchronize()
+        for e in self._attached:
+            e.set_side_stream(0)
+        self._attached = []
         for p in self._ptrs:
             L.lib().orbfe_stream_destroy(ctypes.c_void_p(p))
         self._ptrs = []
@@ -89,7 +114,7 @@ class C3Pipeline:
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
                  nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
-                 vocab_inline: bool = False, vocab_side: bool = False):
+                 vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo"):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -117,6 +142,13 @@ class C3Pipeline:
         self.ext, self.voc = ext, voc
         self.B, self.H, self.W = B, H, W
         self.n_img = 2 * B
+        assert pairs in ("kf", "stereo")
+        self.pairs_mode = pairs
+        # images with a BowVector / FeatureVector, SearchForTriangulation pairs (kf1, kf2) per sub-batch
+        self.n_vocab = B if pairs == "kf" else 2 * B
+        self.pair_idx = [(i, i + 1) for i in range(B - 1)] if pairs == "kf" else [(i, B + i) for i in range(B)]
+        self.n_pairs = len(self.pair_idx)
+        n_pairs = self.n_pairs
         self.cap = cap = ext.max_keypoints(H, W)
         self.levelsup = levelsup
         self.stereo = stereo
@@ -143,25 +175,25 @@ class C3Pipeline:
                 self.bow_words = torch.empty(n_img * cap, dtype=torch.int32, device=dev)
                 self.bow_weights = torch.empty(n_img * cap, dtype=torch.float64, device=dev)
                 self.bow_n = torch.zeros(n_img, dtype=torch.int32, device=dev)
-                self.m12 = torch.empty(B * cap, dtype=torch.int32, device=dev)
-                self.nm = torch.zeros(B, dtype=torch.int32, device=dev)
+                self.m12 = torch.empty(max(n_pairs, 1) * cap, dtype=torch.int32, device=dev)
+                self.nm = torch.zeros(max(n_pairs, 1), dtype=torch.int32, device=dev)
                 self.ur = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
                 self.dep = torch.full((B * cap,), -1.0, dtype=torch.float32, device=dev)
                 self.matcher = ORBmatcher(nnratio, check_ori, device=dev.index)
-                self.pairs = (L.sft_pair * B)()
-                for i in range(B):
+                self.pairs = (L.sft_pair * max(n_pairs, 1))()
+                for i, (a, b) in enumerate(pipe.pair_idx):
                     p = self.pairs[i]
-                    p.kf1, p.kf2 = self.view(i), self.view(B + i)
-                    p.fv1, p.fv2 = self.fvec(i), self.fvec(B + i)
+                    p.kf1, p.kf2 = self.view(a), self.view(b)
+                    p.fv1, p.fv2 = self.fvec(a), self.fvec(b)
                     for k, x in enumerate(np.asarray(F12, np.float32).reshape(9)):
                         p.f12[k] = float(x)
                     p.ex, p.ey = epipole
                     p.match12 = self.m12.data_ptr() + i * cap * 4
                     p.nmatches = self.nm.data_ptr() + i * 4
-                    p.kf1_n_dev = self.cnt.data_ptr() + i * 4
-                    p.kf2_n_dev = self.cnt.data_ptr() + (B + i) * 4
-                    p.fv1_nodes_dev = self.nodes.data_ptr() + i * 4
-                    p.fv2_nodes_dev = self.nodes.data_ptr() + (B + i) * 4
+                    p.kf1_n_dev = self.cnt.data_ptr() + a * 4
+                    p.kf2_n_dev = self.cnt.data_ptr() + b * 4
+                    p.fv1_nodes_dev = self.nodes.data_ptr() + a * 4
+                    p.fv2_nodes_dev = self.nodes.data_ptr() + b * 4
                 self.extracted = torch.cuda.Event()
                 self.vocabbed = torch.cuda.Event()
                 self.matched = torch.cuda.Event()
@@ -201,7 +233,7 @@ class C3Pipeline:
         # PipelineStreams the caller created before anything else (hardware-queue assignment)
         if isinstance(streams, PipelineStreams):
             for e in self.exts:
-                e.set_side_stream(streams.side.cuda_stream)
+                streams.attach(e)
             self.side = streams.side
             streams = streams.ordered()
         assert not vocab_side or self.side is not None, "vocab_side needs PipelineStreams"
@@ -294,9 +326,10 @@ class C3Pipeline:
             self._vocab(o, m)
         ev = []
         self._ev("k_sft", m, ev)
-        L.check(self.lib.orbfe_search_for_triangulation_batch_device(
-            o.matcher._h, B, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
-            "sft batch")
+        if self.n_pairs:
+            L.check(self.lib.orbfe_search_for_triangulation_batch_device(
+                o.matcher._h, self.n_pairs, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
+                "sft batch")
         self._ev("k_sft", m, ev)
         if ev:
             self.events["k_sft"].append(tuple(ev))
@@ -305,12 +338,13 @@ class C3Pipeline:
         o.matched.record(m)
 
     def _vocab(self, o, m):
-        """KeyFrame::ComputeBoW of the set's 2B images on stream m."""
+        """KeyFrame::ComputeBoW of the set's KeyFrame images (n_vocab: the B lefts, or all 2B) on
+        stream m."""
         ev = []
         self._ev("k_vocab", m, ev)
         bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
                     d_bow_n=o.bow_n.data_ptr()) if self.bow else {})
-        self.voc.transform_batch_device(self.n_img, o.desc.data_ptr(), self.cap * 32, o.cnt.data_ptr(),
+        self.voc.transform_batch_device(self.n_vocab, o.desc.data_ptr(), self.cap * 32, o.cnt.data_ptr(),
                                         self.levelsup, o.ids.data_ptr(), o.offs.data_ptr(),
                                         o.idx.data_ptr(), o.nodes.data_ptr(), self.cap,
                                         stream=m.cuda_stream, **bow)
@@ -342,32 +376,40 @@ class C3Pipeline:
         BW = o.bow_words.cpu().numpy().view(np.uint32).reshape(self.n_img, cap)
         BT = o.bow_weights.cpu().numpy().reshape(self.n_img, cap)
         BN = o.bow_n.cpu().numpy()
-        M = o.m12.cpu().numpy().reshape(B, cap)
-        NM = o.nm.cpu().numpy()
+        M = o.m12.cpu().numpy().reshape(-1, cap)
+        NM = o.nm.cpu().numpy()[:self.n_pairs]
         out = {"keypoints": [], "descriptors": [], "fv": [], "bow": [], "match12": [], "nmatches": NM.copy()}
         for i in range(self.n_img):
             n = int(C[i])
             out["keypoints"].append(K[i, :n].copy())
             out["descriptors"].append(D[i, :n].copy())
+            if i >= self.n_vocab:
+                continue
             k = int(NN[i])
             out["fv"].append((I[i, :k].copy(), OF[i, :k + 1].copy(), X[i, :OF[i, k]].copy()))
             nb = int(BN[i]) if self.bow else 0
             out["bow"].append((BW[i, :nb].copy(), BT[i, :nb].copy()))
-        for p in range(B):
-            out["match12"].append(M[p, :int(C[p])].copy())
+        for p, (a, _) in enumerate(self.pair_idx):
+            out["match12"].append(M[p, :int(C[a])].copy())
         if self.stereo:
             UR = o.ur.cpu().numpy().reshape(B, cap)
             out["u_right"] = [UR[p, :int(C[p])].copy() for p in range(B)]
         return out
 
 
+STEP_Z = 1.0  # metres between consecutive frames of the C3 driving sequence
+
+
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
              stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
-             vocab_inline: bool = False, vocab_side: bool = False):
-    """The C3 scene of bench.py: KITTI intrinsics, the KeyFrame pair geometry of a stereo
-    baseline (t2 = -0.537 m, 0.05 m forward), F12 and epipole from LocalMapping::ComputeF12, and
-    seeded KeyFrame state per keypoint slot (half the keypoints stereo, 30 % with a MapPoint).
-    Returns (pipeline, state) with state holding the host copies the oracle check needs."""
+             vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo"):
+    """The C3 scene of bench.py: KITTI intrinsics, seeded KeyFrame state per keypoint slot (half
+    the keypoints stereo unless ComputeStereoMatches provides mvuRight, 30 % with a MapPoint), and
+    the KeyFrame pair geometry with F12 and epipole from LocalMapping::ComputeF12
+    (LocalMapping.cc:545-561): pairs="kf" -- frame t and t+1 of the driving sequence, STEP_Z
+    apart along z (epipole = principal point); pairs="stereo" -- the two cameras of one frame
+    (t2 = -0.537 m, 0.05 m forward). Returns (pipeline, state) with state holding the host copies
+    the oracle check needs."""
     import torch
     from . import synthetic as S
     from .frames import epipole as epipole_of
@@ -381,7 +423,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     ur = ur.astype(np.float32)
     mp = np.where(rng.random((n_img, cap)) < 0.3, L.ORBFE_MP_OBSERVED, L.ORBFE_MP_NONE).astype(np.uint8)
     cam = S.KITTI_CAM
-    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    t1, t2 = (S.pose(), S.pose(tz=-STEP_Z)) if pairs == "kf" else (S.pose(), S.pose(tx=-0.537, tz=0.05))
     F12 = S.compute_f12(t1, t2, S.intrinsics(cam))
     scale, sigma2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
     dummy = S.make_frame(np.zeros(0, L.KEYPOINT_DTYPE), None, scale, sigma2, H, W, cam, rng, tcw=t1)
@@ -391,7 +433,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
-                      vocab_inline=vocab_inline, vocab_side=vocab_side)
+                      vocab_inline=vocab_inline, vocab_side=vocab_side, pairs=pairs)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
-                 epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo)
+                 epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo, pairs=pairs)
     return pipe, state

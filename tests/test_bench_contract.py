@@ -4,6 +4,8 @@ CLI defaults are N=1 with a short run."""
 import os
 import sys
 
+from types import SimpleNamespace
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -19,7 +21,8 @@ GEO = np.hstack([GEO, np.zeros((8, 4), np.int64)])
 def test_roofline_object():
     counts = np.full(64, 2007, np.int32)
     kt = {"k_fast": (50 * 0.25, 100)}  # 50 steps, 2 launches per step, 0.25 ms per step
-    r = bench.roofline(kt, "k_fast", GEO, counts, 13_000 * 64, 64, 50)  # 50 sub-batches
+    pipe = SimpleNamespace(n_vocab=32, pair_idx=[(i, i + 1) for i in range(31)], n_pairs=31)
+    r = bench.roofline(kt, "k_fast", GEO, counts, 13_000 * 64, 64, 50, pipe)  # 50 sub-batches
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
@@ -29,6 +32,10 @@ def test_roofline_object():
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-5
     px = sum(int(w) * int(h) for w, h in GEO[:, :2])
     assert per_step == 64 * (px + 4 * int(GEO[:, 2].sum())) + 4 * 13_000 * 64
+    # SearchForTriangulation bytes follow the pairing: 31 KeyFrame pairs (t, t+1) of 2007 keypoints
+    kt = {"k_sft": (50 * 0.1, 50)}
+    r = bench.roofline(kt, "k_sft", GEO, counts, 0, 64, 50, pipe)
+    assert r["algorithmic_bytes_per_subbatch"] == 31 * (64 * 2 * 2007 + 4 * 2007)
 
 
 def test_committed_pmc_traffic_matches_workload():
@@ -48,5 +55,7 @@ def test_cli_defaults():
     assert a.input_batches >= 4 and a.vocab_levels == 6 and a.levelsup == 4
     # two extractor handles, two output sets each
     assert a.extractors == 2 and bench.pipe_depth(a) == 4
+    # SURVEY 8(d)'s KeyFrame pairs with the stereo Frame's ComputeStereoMatches
+    assert a.pairs == "kf" and a.stereo
     # a step is long enough to be seen (>= 1024 sub-batches of 32 stereo frames)
     assert a.batches_per_step * a.batch >= 32 * 1024

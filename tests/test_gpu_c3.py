@@ -1,13 +1,15 @@
 """The exact sequence bench.py times (orb_slam2_2021_amd.pipeline.C3Pipeline, config C3):
-extract_batch_device on 2B = 64 images -> vocabulary transform_batch_device (ORBvoc-shaped
-k=10/L=6 tree, levelsup 4, BowVector + FeatureVector) -> search_for_triangulation_batch_device
-with device-side counts (kf*_n_dev / fv*_nodes_dev), two output sets in flight -- every image's
-keypoints, descriptors, BowVector and FeatureVector and every pair's match12 against the oracle
-chain (oracle/c3_check.py)."""
+extract_batch_device on 2B = 64 images [-> ComputeStereoMatches] -> vocabulary
+transform_batch_device (ORBvoc-shaped k=10/L=6 tree, levelsup 4, BowVector + FeatureVector) ->
+search_for_triangulation_batch_device with device-side counts (kf*_n_dev / fv*_nodes_dev), output
+sets in flight -- every image's keypoints, descriptors, BowVector and FeatureVector, mvuRight and
+every pair's match12 against the oracle chain (oracle/c3_check.py). Both pairings: "kf" (the
+bench default: KeyFrame t vs t+1 of the driving sequence, SURVEY 8(d), LocalMapping.cc:211-272)
+and "stereo" (left vs right of one frame)."""
 import numpy as np
 import pytest
 
-from orb_slam2_2021_amd import ORBextractor, synth_frame
+from orb_slam2_2021_amd import ORBextractor, synth_frame, synth_sequence_frame
 from orb_slam2_2021_amd import synthetic as S
 from orb_slam2_2021_amd.pipeline import build_c3
 from orb_slam2_2021_amd.vocabulary import ORBVocabulary
@@ -27,21 +29,24 @@ def vocab():
     return tree, ORBVocabulary.from_tree(tree), ref
 
 
-def frames(B, base):
+def frames(B, base, pairs="stereo"):
     imgs = np.zeros((2 * B, H, W), np.uint8)
     for i in range(B):
-        imgs[i], imgs[B + i] = synth_frame(base + i, H, W, right=True)
+        if pairs == "kf":  # consecutive frames of the bench's driving sequence
+            imgs[i], imgs[B + i] = synth_sequence_frame(0x0C3, base + i, H, W, right=True)
+        else:
+            imgs[i], imgs[B + i] = synth_frame(base + i, H, W, right=True)
     return imgs
 
 
-@pytest.mark.parametrize("stereo", [False, True])
-def test_c3_batch32_bit_exact(require_gpu, vocab, stereo):
+@pytest.mark.parametrize("pairs,stereo", [("stereo", False), ("stereo", True), ("kf", True), ("kf", False)])
+def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
     import torch
     tree, voc, ref = vocab
     B = 32
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
-    pipe, st = build_c3(ext, tree, voc, B, H, W, 0, stereo=stereo)
-    batches = [frames(B, 0), frames(B, 1000)]
+    pipe, st = build_c3(ext, tree, voc, B, H, W, 0, stereo=stereo, pairs=pairs)
+    batches = [frames(B, 0, pairs), frames(B, 1000, pairs)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]
     # four sub-batches through both output sets; check the last one of each input batch
     for j in range(4):
@@ -50,15 +55,20 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, stereo):
     out_a = pipe.to_host(pipe.sets[0])  # sub-batch 2: batch 0
     for imgs, out in ((batches[0], out_a), (batches[1], out_b)):
         r = check_c3(imgs, out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"], st["cam"],
-                     st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"])
+                     st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"], pairs=pairs)
         assert r["all"], r
         assert min(len(k) for k in out["keypoints"]) >= 2000
-        assert int(np.sum(out["nmatches"])) > 32 * 50
+        assert len(out["nmatches"]) == (31 if pairs == "kf" else 32)
+        assert int(np.sum(out["nmatches"])) > len(out["nmatches"]) * (40 if pairs == "kf" else 50)
+        assert len(out["bow"]) == (32 if pairs == "kf" else 64)
         assert all(len(b[0]) > 100 for b in out["bow"])
+        if pairs == "kf":  # the epipole is the principal point (forward motion)
+            assert abs(st["epipole"][0] - st["cam"]["cx"]) < 1e-3 and abs(st["epipole"][1] - st["cam"]["cy"]) < 1e-3
 
 
-@pytest.mark.parametrize("match_inline,stereo,blur_mode", [(False, False, 1), (True, False, 0), (False, True, 2)])
-def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode):
+@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs", [(False, False, 1, "stereo"), (True, False, 0, "stereo"),
+                                                                (False, True, 2, "stereo"), (False, True, 1, "kf")])
+def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs):
     """bench.py's default schedule: two extractor handles extract consecutive sub-batches on their
     own streams (side-stream work on one shared high-priority stream), matching on its own stream
     or inline after each extraction (then two vocabulary transforms run concurrently on the one
@@ -71,8 +81,8 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
     for e in exts:
         e.debug_set_blur_mode(blur_mode)
     streams = PipelineStreams(0, 2, match_inline=match_inline, match_high=not match_inline)
-    pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams)
-    batches = [frames(B, 0), frames(B, 1000), frames(B, 2000)]
+    pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs)
+    batches = [frames(B, 0, pairs), frames(B, 1000, pairs), frames(B, 2000, pairs)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]
     for j in range(7):  # sub-batch j: input j % 3, set j % 4, handle j % 2
         pipe.run(d[j % 3].data_ptr())
@@ -80,6 +90,6 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
     for j in (4, 5, 6):
         out = pipe.to_host(pipe.sets[j % 4])
         r = check_c3(batches[j % 3], out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"],
-                     st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"])
+                     st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"], pairs=pairs)
         assert r["all"], (j, r)
     streams.close()
