@@ -114,8 +114,9 @@ def parse(argv=None):
                    help="diagnostic: the pipeline's streams from torch's pool, created after the "
                         "handles (hardware-queue assignment then depends on the stream count; with "
                         "several extractors their side work runs inline)")
-    p.add_argument("--level-launches", action="store_true",
-                   help="k_copy0 + one k_resize launch per level instead of the tiled k_pyramid (comparison)")
+    p.add_argument("--tiled-pyramid", action="store_true",
+                   help="the tiled k_pyramid launches instead of the default k_copy0 + one k_resize launch per "
+                        "level (comparison; measured slower)")
     p.add_argument("--dump-gather", default="",
                    help="test hook: write each rank's last sub-batch (own keypoints + descriptors) and "
                         "rank 0's gathered payloads to this directory")
@@ -256,8 +257,8 @@ def main():
     host = make_inputs(args, world, rank)
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
-    if args.level_launches:
-        ext.debug_force_level_launches(True)
+    if args.tiled_pyramid:
+        ext.debug_force_level_launches(False)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
     if args.fast_side > 0:
@@ -284,8 +285,8 @@ def main():
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
             if args.copy0_side:
                 e.debug_set_copy0_side(True)
-            if args.level_launches:
-                e.debug_force_level_launches(True)
+            if args.tiled_pyramid:
+                e.debug_force_level_launches(False)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,

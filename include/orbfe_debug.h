@@ -25,8 +25,9 @@ int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, 
 /* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
  * global-memory path for every level; < 0 restores the automatic size). */
 int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
-/* 0 (default): build the pyramid with the tiled k_pyramid launches (groups of levels, no
- * k_copy0) when the geometry allows; 1: k_copy0 + one k_resize launch per level. */
+/* 1 (default): k_copy0 + one k_resize launch per level; 0: build the pyramid with the tiled
+ * k_pyramid launches (groups of levels, no k_copy0) when the geometry allows (measured slower,
+ * DESIGN.md section 5). */
 int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
 /* Per-level pyramid path only: FAST of levels 0..k-1 on the side stream, each launched as soon
  * as its level is built, the rest in one launch after the resize chain (k <= 0: the default,

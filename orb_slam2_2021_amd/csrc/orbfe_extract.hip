@@ -933,6 +933,12 @@ __device__ __forceinline__ int key_s(uint32_t k) { return (int)(k >> 24); }
 
 // k_fast: one wavefront per cell (4 cells per 256-thread workgroup). No workgroup barriers: waves
 // are independent and synchronise their own LDS with wave_sync().
+// Round 3, measured and rejected: each wavefront running 2-8 consecutive
+// cells with the next cell's ROI in flight during the current one -- through a second VGPR set
+// (68 -> 109 VGPRs, 7 -> 4 waves per SIMD: 176 -> 198-229 us per 64-image extraction) or by
+// LDS-DMA into a second LDS buffer (global_load_lds_dword, 17 dwords per 68-byte row: 206 us at
+// one cell per wavefront, 228-275 us at 4-8); LDS sized per launch instead of per pyramid (no
+// change). The kernel wants many short wavefronts.
 //   1. the cell ROI (<= roi_w_max x roi_h_max) lands in LDS with aligned dword loads;
 //   2. OpenCV's antipodal quick test at the lower threshold runs on every detection pixel and the
 //      survivors are compacted (ballot + popcount, row-major order kept);
@@ -1067,6 +1073,13 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
     }
   };
   for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
+#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 1
+  // phase-cost diagnostic builds only (profiles/scripts/r3_fast_phases.sh; -DORBFE_FAST_DIAG=1..3
+  // stop after the ROI load, the prefilter, the arc strength): no corners, the work kept alive
+  wave_sync();
+  if (lane == 0) *cnt_out = (int)m8[lane] + roi[lane] == 1000 ? 1 : 0;
+  return;
+#endif
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
   uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
@@ -1131,6 +1144,10 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
       }
     }
     wave_sync();
+#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 2
+    if (lane == 0) *cnt_out = nlist == 100000 ? 1 : 0;
+    return;
+#endif
     // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the arc strength
     //     (OpenCV cornerScore + 1) of the corners at t goes to m8 and, compacted in order, back
     //     into the list
@@ -1161,6 +1178,10 @@ __global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell
       ncorner += __popcll(b0) + __popcll(b1);
     }
     wave_sync();
+#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 3
+    if (lane == 0) *cnt_out = ncorner == 100000 ? 1 : 0;
+    return;
+#endif
     // 4. NMS over the corners at t (out-of-region neighbours and non-corners score 0)
     for (int j0 = 0; j0 < ncorner; j0 += 64) {
       const int j = j0 + lane;

@@ -331,8 +331,8 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_inline_side(self._h, 1 if on else 0), "set_inline_side")
 
     def debug_force_level_launches(self, on: bool = True) -> None:
-        """True: k_copy0 + one k_resize launch per level; False (default): the tiled k_pyramid
-        launches."""
+        """True (the library default): k_copy0 + one k_resize launch per level; False: the tiled
+        k_pyramid launches (measured slower, kept for comparison)."""
         L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),
                 "force_level_launches")
 

@@ -1,5 +1,6 @@
 """Extraction only, C3 shape (64 images of 1241x376 per call), for PMC passes on the extractor
-kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel] [--side=K] [--levels]"""
+kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel] [--side=K] [--tiled]
+[--seq] (--seq: the bench's driving-sequence frames instead of orbfe_synth_frame)"""
 import os
 import sys
 import time
@@ -8,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import numpy as np
 import torch
 
-from orb_slam2_2021_amd import ORBextractor, synth_frame
+from orb_slam2_2021_amd import ORBextractor, synth_frame, synth_sequence_frame
 
 
 def main():
@@ -16,7 +17,10 @@ def main():
     B, H, W = 32, 376, 1241
     host = np.zeros((2 * B, H, W), np.uint8)
     for i in range(B):
-        l, r = synth_frame(i, H, W, right=True)
+        if "--seq" in sys.argv:
+            l, r = synth_sequence_frame(0x0C3, i, H, W, right=True)
+        else:
+            l, r = synth_frame(i, H, W, right=True)
         host[i], host[B + i] = l, r
     dev = torch.device("cuda", 0)
     d_img = torch.from_numpy(host).to(dev)
@@ -24,8 +28,8 @@ def main():
     for a in sys.argv:
         if a.startswith("--side="):
             ext.debug_set_fast_side_levels(int(a.split("=")[1]))
-        if a == "--levels":
-            ext.debug_force_level_launches(True)
+        if a == "--tiled":
+            ext.debug_force_level_launches(False)
     cap = ext.max_keypoints(H, W)
     kps = torch.empty(2 * B * cap * 28, dtype=torch.uint8, device=dev)
     desc = torch.empty(2 * B * cap * 32, dtype=torch.uint8, device=dev)
