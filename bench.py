@@ -114,6 +114,9 @@ def parse(argv=None):
                    help="diagnostic: the pipeline's streams from torch's pool, created after the "
                         "handles (hardware-queue assignment then depends on the stream count; with "
                         "several extractors their side work runs inline)")
+    p.add_argument("--stereo-on-match", action="store_true",
+                   help="ComputeStereoMatches on the matching stream, the handle's next extraction waiting for it "
+                        "(default: on the extraction stream right after each extraction; measured: no gain)")
     p.add_argument("--tiled-pyramid", action="store_true",
                    help="the tiled k_pyramid launches instead of the default k_copy0 + one k_resize launch per "
                         "level (comparison; measured slower)")
@@ -290,7 +293,8 @@ def main():
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs)
+                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs,
+                           stereo_on_match=args.stereo_on_match)
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream
@@ -1036,12 +1040,16 @@ def vocab_leg(args, voc, tree, pipe, reps=20):
 
 def host_boundary_rate(ext, host, reps=20):
     """PCIe-inclusive extraction rate through the host-buffer C ABI entry orbfe_extract_batch on
-    the step's 64 host images (pinned staging by the handle's worker threads, chunked H2D /
-    extraction / D2H on overlapping streams, used slots unpacked into the caller's buffers), with
-    preallocated output buffers as a C++ caller keeps them. Reported beside `value`, never as it
-    (DESIGN.md section 6). Wall clock per call."""
+    the step's 64 host images, with preallocated output buffers as a C++ caller keeps them.
+    Reported beside `value`, never as it. Wall clock per call, two ways:
+      staged      -- plain caller memory: pinned staging by the handle's worker threads, chunked
+                     H2D / extraction / D2H on overlapping streams, used slots unpacked;
+      registered  -- the caller's image and output buffers page-locked once (orbfe_host_register):
+                     images DMA'd straight from them, results DMA'd straight into them.
+    pcie_GBps = (image bytes in + keypoint/descriptor slot bytes out) / wall time."""
     from ctypes import c_size_t, c_void_p
     from orb_slam2_2021_amd import _lib as L
+    from orb_slam2_2021_amd import register_host, unregister_host
     lib = L.lib()
     n, rows, cols = host.shape
     cap = ext.max_keypoints(rows, cols)
@@ -1054,17 +1062,40 @@ def host_boundary_rate(ext, host, reps=20):
         L.check(lib.orbfe_extract_batch(ext._h, n, ctypes.cast(arr, c_void_p), rows, cols, c_size_t(cols),
                                         L.ptr(kps), L.ptr(desc), cap, L.ptr(counts)), "orbfe_extract_batch")
 
-    for _ in range(3):
-        call()
-    times = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        call()
-        times.append(time.perf_counter() - t0)
-    dt = float(np.median(times))
-    return {"value": round(n / 2 / dt, 2), "unit": "stereo frames/s", "ms_per_call_p50": round(1e3 * dt, 3),
-            "what": f"orbfe_extract_batch on {n} host images {cols}x{rows} (extract only, staging + H2D + "
-                    "kernels + D2H + unpacking; median of {reps} calls)".replace("{reps}", str(reps))}
+    def timed():
+        for _ in range(3):
+            call()
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            times.append(time.perf_counter() - t0)
+        return float(np.median(times))
+
+    moved = host.nbytes + n * cap * (28 + 32)
+    dt_staged = timed()
+    staged = (kps[:counts[0]].copy(), desc[:counts[0]].copy(), counts.copy())
+    hostc = np.ascontiguousarray(host)
+    register_host(hostc)
+    register_host(kps)
+    register_host(desc)
+    try:
+        arr = (c_void_p * n)(*[hostc[i].ctypes.data for i in range(n)])
+        dt_reg = timed()
+        same = bool(np.array_equal(counts, staged[2]) and kps[:counts[0]].tobytes() == staged[0].tobytes()
+                    and np.array_equal(desc[:counts[0]], staged[1]))
+    finally:
+        unregister_host(hostc)
+        unregister_host(kps)
+        unregister_host(desc)
+    return {"value": round(n / 2 / dt_reg, 2), "unit": "stereo frames/s", "ms_per_call_p50": round(1e3 * dt_reg, 3),
+            "pcie_GBps": round(moved / dt_reg / 1e9, 2),
+            "staged": {"value": round(n / 2 / dt_staged, 2), "ms_per_call_p50": round(1e3 * dt_staged, 3),
+                       "pcie_GBps": round(moved / dt_staged / 1e9, 2)},
+            "registered_equals_staged": same,
+            "what": f"orbfe_extract_batch on {n} host images {cols}x{rows} (extract only; H2D + kernels + D2H; "
+                    f"median of {reps} calls): value = caller buffers registered (orbfe_host_register, direct DMA), "
+                    "staged = plain caller memory through the handle's pinned staging"}
 
 
 def _cpu_name():

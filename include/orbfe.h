@@ -88,6 +88,17 @@ int orbfe_extract_batch(orbfe_extractor* h, int n_images, const uint8_t* const* 
                         int cols, size_t step, orbfe_keypoint* kps, uint8_t* desc, int cap,
                         int32_t* counts);
 
+/* Page-lock a caller buffer (hipHostRegister) that the host-buffer entry points then copy from /
+ * to directly: images wholly inside registered ranges skip the pinned staging copy (runs of
+ * images adjacent in memory go up in one DMA), and kps / desc inside registered ranges with
+ * cap == orbfe_max_keypoints receive the results by DMA with no unpacking. Process-wide (any
+ * handle, any device); a caller that reuses its image and keypoint buffers registers them once
+ * (the reference's Frame keeps its cv::Mat images per frame; the adapter registers its ring of
+ * frame buffers). Unregister before freeing the memory. Returns ORBFE_ERR_HIP if the runtime
+ * refuses the range. */
+int orbfe_host_register(const void* p, size_t bytes);
+int orbfe_host_unregister(const void* p);
+
 /* Device-resident batch: d_imgs holds n_images images, image i at d_imgs + i*image_stride, rows
  * `pitch` bytes apart. Outputs are device buffers laid out as in orbfe_extract_batch. Async on
  * `stream`. cap must be >= orbfe_max_keypoints(h). */

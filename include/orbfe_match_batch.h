@@ -30,8 +30,8 @@ typedef struct orbfe_sft_pair {
   const int32_t* fv2_nodes_dev;
 } orbfe_sft_pair;
 
-/* n_pairs independent SearchForTriangulation calls, one workgroup each, async on `stream`
- * (NULL = the matcher's stream). */
+/* n_pairs independent SearchForTriangulation calls, async on `stream` (NULL = the matcher's
+ * stream). */
 int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int n_pairs,
                                                 const orbfe_sft_pair* pairs, int only_stereo,
                                                 void* stream);

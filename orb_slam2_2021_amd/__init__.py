@@ -7,11 +7,11 @@ from ._lib import (KEYPOINT_DTYPE, LIB_PATH, LibraryMissing, OrbfeError, ORBFE_M
                    ORBFE_MP_OBSERVED, ORBFE_MP_PRESENT, ORBFE_RESIZE_SCALAR, ORBFE_RESIZE_SIMD128,
                    MPF_BAD, MPF_OBSERVED, MPF_OUTLIER, MPF_PRESENT, MPF_SEEN, MPF_SKIP,
                    MPF_TRACK_IN_VIEW)
-from .extractor import ORBextractor, synth_frame, synth_sequence_frame
+from .extractor import ORBextractor, register_host, synth_frame, synth_sequence_frame, unregister_host
 from .frames import (FeatureVector, Frame, KeyFrame, KeyFrameMapPoints, LastFrameMapPoints,
                      LocalMapPoints, MapPointGeometry)
 from .matcher import ORBmatcher
 
 __all__ = ["ORBextractor", "ORBmatcher", "Frame", "KeyFrame", "FeatureVector", "LocalMapPoints",
            "LastFrameMapPoints", "MapPointGeometry", "KeyFrameMapPoints", "KEYPOINT_DTYPE",
-           "synth_frame", "synth_sequence_frame", "OrbfeError", "LibraryMissing"]
+           "synth_frame", "synth_sequence_frame", "register_host", "unregister_host", "OrbfeError", "LibraryMissing"]

@@ -2865,6 +2865,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.img_pitch = pitch;
   a.pyr = h->d_pyr + (long long)i0 * h->pyr_stride;
   a.blur = h->d_blur + (long long)i0 * h->pyr_stride;
+#if defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1  // ablation build: no GaussianBlur (wrong output)
+  a.blur = a.pyr;
+#endif
   a.pyr_stride = h->pyr_stride;
   a.cand = h->d_cand + (long long)i0 * h->cand_stride;
   a.cand_stride = h->cand_stride;
@@ -2943,10 +2946,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       if (c0side) {
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));  // the input is ready on st
         ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
         LAUNCH_TIMED(h, 4, side, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, side, a));
+#endif
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_c0, side));
       } else {
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
         LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
+#endif
       }
     }
     // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
@@ -3006,7 +3013,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   const dim3 blur_grid((h->blur_tiles + 3) / 4, n);
   if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
     LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+#endif
   }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
@@ -3014,12 +3023,16 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
     LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+#endif
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   launch_octree(st, 0, h->nlevels);
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
     LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, st, a));
+#endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
     dim3 grid((h->total_key_slots + 15) / 16, n);
@@ -3300,6 +3313,42 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
   return ORBFE_OK;
 }
 
+// ---- registered host buffers (orbfe_host_register): copied from / to directly, no staging
+namespace {
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, size_t>> g_reg;  // registered [begin, begin + bytes)
+
+bool host_registered(const void* p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  for (const auto& r : g_reg)
+    if (a >= r.first && a + bytes <= r.first + r.second) return true;
+  return false;
+}
+}  // namespace
+
+extern "C" int orbfe_host_register(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_host_register: bad argument");
+  if (host_registered(p, bytes)) return ORBFE_OK;
+  ORBFE_HIP_CHECK(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault));
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  g_reg.emplace_back((uintptr_t)p, bytes);
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_host_unregister(const void* p) {
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = std::find_if(g_reg.begin(), g_reg.end(), [&](const std::pair<uintptr_t, size_t>& r) {
+      return r.first == (uintptr_t)p;
+    });
+    if (it == g_reg.end()) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_host_unregister: not registered");
+    g_reg.erase(it);
+  }
+  ORBFE_HIP_CHECK(hipHostUnregister(const_cast<void*>(p)));
+  return ORBFE_OK;
+}
+
 // Host-buffer batch (what the reference's ORBextractor::operator() costs a caller). The images go
 // through pinned staging in chunks: chunk c's H2D copy (copy stream) overlaps chunk c+1's staging
 // (row bands spread over the handle's host worker pool). One extraction of all images follows
@@ -3350,7 +3399,15 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
   // One group: 2 groups of 32 measured slower on MI355X (1.98 vs 1.60 ms p50 for 64 KITTI
   // images; a 32-image extraction costs far more than half of a 64-image one), and so did
   // splitting the H2D chunks over both copy streams (1.71 ms).
-  const int ngroups = 1;
+  static const int env_groups = std::getenv("ORBFE_HOST_GROUPS") ? std::atoi(std::getenv("ORBFE_HOST_GROUPS")) : 0;
+  // registered caller memory (orbfe_host_register): images DMA'd straight from the caller's rows
+  // (step == cols), results DMA'd straight into the caller's buffers (cap == slots per image)
+  bool direct_in = step == (size_t)cols;
+  for (int i = 0; i < n && direct_in; i++) direct_in = host_registered(imgs[i], (size_t)rows * cols);
+  const int K0 = h->total_key_slots;
+  const bool direct_out = cap == K0 && kps && desc && host_registered(kps, (size_t)n * cap * sizeof(orbfe_keypoint)) &&
+                          host_registered(desc, (size_t)n * cap * 32);
+  const int ngroups = env_groups > 0 ? std::min(env_groups, std::max(1, n / 8)) : 1;
   const int cpg = std::max(1, std::min(4, n / (8 * ngroups)));  // H2D chunks per group
   // small batches (a single image: orbfe_extract) stay on the handle's stream, in one piece:
   // the cross-stream event hops cost more latency than the overlap saves
@@ -3373,6 +3430,16 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
   for (int g = 0; g < ngroups; g++) {
     for (int c = g * cpg; c < (g + 1) * cpg; c++) {
       const int i0 = part(c, nchunks), nc = part(c + 1, nchunks) - i0;
+      if (direct_in) {  // one DMA per run of images adjacent in the caller's memory
+        for (int i = i0; i < i0 + nc;) {
+          int j = i + 1;
+          while (j < i0 + nc && imgs[j] == imgs[j - 1] + img_bytes) j++;
+          ORBFE_HIP_CHECK(hipMemcpyAsync(h->d_in + (size_t)i * img_bytes, imgs[i], (size_t)(j - i) * img_bytes,
+                                         hipMemcpyHostToDevice, s_in));
+          i = j;
+        }
+        continue;
+      }
       auto stage = [&](int task) {
         const int i = i0 + task / bands, r0 = (task % bands) * band, r1 = std::min(rows, r0 + band);
         uint8_t* dst = h->h_in + (size_t)i * img_bytes;
@@ -3406,9 +3473,11 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
     const int ppg = npieces / ngroups;
     for (int p = ppg * g; p < ppg * (g + 1); p++) {
       const int i0 = part(p, npieces), np = part(p + 1, npieces) - i0;
-      ORBFE_HIP_CHECK(hipMemcpyAsync(hk + (size_t)i0 * K, h->d_kps + (size_t)i0 * K, (size_t)np * K * sizeof(orbfe_keypoint),
+      orbfe_keypoint* kd = direct_out ? kps : hk;  // cap == K on the direct path
+      uint8_t* dd = direct_out ? desc : hd;
+      ORBFE_HIP_CHECK(hipMemcpyAsync(kd + (size_t)i0 * K, h->d_kps + (size_t)i0 * K, (size_t)np * K * sizeof(orbfe_keypoint),
                                      hipMemcpyDeviceToHost, s_out));
-      ORBFE_HIP_CHECK(hipMemcpyAsync(hd + (size_t)i0 * K * 32, h->d_desc + (size_t)i0 * K * 32, (size_t)np * K * 32,
+      ORBFE_HIP_CHECK(hipMemcpyAsync(dd + (size_t)i0 * K * 32, h->d_desc + (size_t)i0 * K * 32, (size_t)np * K * 32,
                                      hipMemcpyDeviceToHost, s_out));
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_out[p], s_out));
     }
@@ -3424,6 +3493,7 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
       need = std::max(need, (int)hc[i]);
     }
     if (need > cap || (need > 0 && (!kps || !desc))) break;  // reported below
+    if (direct_out) continue;  // the slots landed in the caller's buffers
     h->pool->parallel_for(np, [&](int k) {
       const int i = i0 + k;
       if (hc[i] == 0) return;

@@ -36,19 +36,15 @@
 using namespace orbfe_mi;
 
 // ---------------------------------------------------------------------------------------------
-// SearchForTriangulation: k_sft_init (match12 = -1), k_sft_nodes (one wavefront per common
-// vocabulary node, many workgroups per pair), k_sft_finish (rotation filter + count per pair).
+// SearchForTriangulation: k_sft_nodes (one wavefront per KF1 vocabulary node, many workgroups
+// per pair; each wavefront writes the final match12 of every KF1 feature of its node, -1 included,
+// and one more workgroup per pair writes -1 for the features no node lists, so no initialisation
+// pass runs first), k_sft_finish (rotation filter + count per pair).
 __device__ __forceinline__ void sft_resolve_sizes(orbfe_sft_pair& P) {
   if (P.kf1_n_dev) P.kf1.n = *P.kf1_n_dev;
   if (P.kf2_n_dev) P.kf2.n = *P.kf2_n_dev;
   if (P.fv1_nodes_dev) P.fv1.n_nodes = *P.fv1_nodes_dev;
   if (P.fv2_nodes_dev) P.fv2.n_nodes = *P.fv2_nodes_dev;
-}
-
-__global__ __launch_bounds__(256) void k_sft_init(const orbfe_sft_pair* pairs) {
-  orbfe_sft_pair P = pairs[blockIdx.x];
-  sft_resolve_sizes(P);
-  for (int i = threadIdx.x; i < P.kf1.n; i += 256) P.match12[i] = -1;
 }
 
 #define SFT_REG_CHUNKS 4  // node-2 candidates held in registers: 4 x 64 per wavefront
@@ -231,8 +227,9 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     if (wave_ballot(changed) == 0) break;
     wave_sync();  // claim[] is rewritten by the next round
   }
-  if (chA >= 0) P.match12[idx1[0]] = P.fv2.indices[o2 + chA];
-  if (chB >= 0) P.match12[idx1[1]] = P.fv2.indices[o2 + chB];
+  // every feature of the node gets its final value (-1: no match), written once
+  if (lane < n1) P.match12[idx1[0]] = chA >= 0 ? P.fv2.indices[o2 + chA] : -1;
+  if (64 + lane < n1) P.match12[idx1[1]] = chB >= 0 ? P.fv2.indices[o2 + chB] : -1;
 }
 
 __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
@@ -241,6 +238,27 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
   orbfe_sft_pair P = pairs[blockIdx.y];
   sft_resolve_sizes(P);
+  if (blockIdx.x == gridDim.x - 1) {
+    // the last workgroup of a pair: KF1 features that no FeatureVector node lists -- a stopped
+    // word (weight 0) is not added (TemplatedVocabulary.h:1198-1201) -- never match: -1. Disjoint
+    // from the features the node wavefronts write, so no ordering is needed between them.
+    uint32_t* bits = &s_fp_desc[0][0];  // 16 KiB = 131072 feature bits per round
+    const int t = threadIdx.x;
+    const int nidx = P.fv1.n_nodes > 0 ? P.fv1.offsets[P.fv1.n_nodes] : 0;
+    for (int c0 = 0; c0 < P.kf1.n; c0 += 131072) {
+      for (int i = t; i < 4096; i += 256) bits[i] = 0u;
+      __syncthreads();
+      for (int i = t; i < nidx; i += 256) {
+        const int f = P.fv1.indices[i] - c0;
+        if (f >= 0 && f < 131072) atomicOr(&bits[f >> 5], 1u << (f & 31));
+      }
+      __syncthreads();
+      for (int f = c0 + t; f < min(P.kf1.n, c0 + 131072); f += 256)
+        if (!((bits[(f - c0) >> 5] >> ((f - c0) & 31)) & 1u)) P.match12[f] = -1;
+      __syncthreads();
+    }
+    return;
+  }
   const int w = wave_id(), lane = lane_id();
   const int a = blockIdx.x * 4 + w;
   if (a >= P.fv1.n_nodes || P.kf2.n > SFT_MAX_KF2) return;
@@ -257,12 +275,19 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
     if (m0) lo = b + __builtin_ctzll(m0);
     else if (m1) lo = b + 64 + __builtin_ctzll(m1);
   }
-  if (lo < 0) return;
+  if (lo < 0) {  // no common node (the merge-join skips it): no matches for these features
+    for (int i = o1 + lane; i < e1; i += 64) P.match12[P.fv1.indices[i]] = -1;
+    return;
+  }
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
   if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
     sft_node_fixpoint(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
+  // large nodes: -1 first, stored before the walk's matches overwrite some of them (the wait
+  // orders the two stores to one address from different lanes)
+  for (int i = o1 + lane; i < e1; i += 64) P.match12[P.fv1.indices[i]] = -1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint32_t* far = s_claim_far[w];
   if (n2 > SFT_REG_CHUNKS * 64)
     for (int i = lane; i < (n2 + 31) / 32; i += 64) far[i] = 0;
@@ -1256,8 +1281,8 @@ extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int
   // fv1.n_nodes bounds the node grid (with fv1_nodes_dev set it must be an upper bound)
   int max_nodes = 1;
   for (int p = 0; p < n_pairs; p++) max_nodes = std::max(max_nodes, pairs[p].fv1.n_nodes);
-  hipLaunchKernelGGL(k_sft_init, dim3(n_pairs), dim3(256), 0, s, m->d_pairs);
-  hipLaunchKernelGGL(k_sft_nodes, dim3((max_nodes + 3) / 4, n_pairs), dim3(256), 0, s, m->d_pairs,
+  // (max_nodes + 3) / 4 workgroups of node wavefronts + one for the features no node lists
+  hipLaunchKernelGGL(k_sft_nodes, dim3((max_nodes + 3) / 4 + 1, n_pairs), dim3(256), 0, s, m->d_pairs,
                      only_stereo ? 1 : 0);
   hipLaunchKernelGGL(k_sft_finish, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, m->check_ori);
   ORBFE_HIP_CHECK(hipGetLastError());

@@ -343,6 +343,19 @@ class ORBextractor:
         return info.reshape(self.nlevels, 7)
 
 
+def register_host(a: np.ndarray) -> None:
+    """orbfe_host_register: page-lock a (C-contiguous) numpy buffer the host-buffer entry points
+    then DMA from / to directly (images; keypoint and descriptor outputs with cap equal to
+    max_keypoints). Keep the array alive and call unregister_host before dropping it."""
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("register_host needs a C-contiguous array")
+    L.check(L.lib().orbfe_host_register(c_void_p(a.ctypes.data), c_size_t(a.nbytes)), "orbfe_host_register")
+
+
+def unregister_host(a: np.ndarray) -> None:
+    L.check(L.lib().orbfe_host_unregister(c_void_p(a.ctypes.data)), "orbfe_host_unregister")
+
+
 def synth_frame(index: int, rows: int = 376, cols: int = 1241, n_rects: int = 0,
                 right: bool = False):
     """Seeded synthetic KITTI-shaped frame (orbfe_synth.h). Returns left or (left, right)."""

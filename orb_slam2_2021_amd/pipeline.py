@@ -114,7 +114,8 @@ class C3Pipeline:
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
                  nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
-                 vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo"):
+                 vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
+                 stereo_on_match: bool = False):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -248,6 +249,14 @@ class C3Pipeline:
         self.mstream = self.stream if self.match_inline else streams[-1]
         self.counter = 0
         self.last = None
+        self._torch = torch
+        # stereo_on_match: ComputeStereoMatches on the matching stream (it needs only the extracted
+        # pyramids and keypoints) instead of right after the extraction. Measured on MI355X: no
+        # gain (73.6-73.8k vs 74.2-76.5k stereo frames/s, interleaved) -- the stereo kernels cost
+        # their run time wherever they sit; off by default
+        self.stereo_on_match = stereo and stereo_on_match and not (self.match_inline or defer or vocab_side
+                                                                   or vocab_inline)
+        self.stereo_done = [None] * len(self.exts)
         # optional HIP events around the vocabulary / matching / stereo launches
         self.event_sel = set()
         self.events = {"k_vocab": [], "k_sft": [], "k_stereo": []}
@@ -269,18 +278,16 @@ class C3Pipeline:
         B, H, W, cap = self.B, self.H, self.W, self.cap
         s, ext = self.streams[k], self.exts[k]
         s.wait_event(o.matched)  # the matching that last read this set is done
+        if self.stereo_on_match and self.stereo_done[k] is not None:
+            # ComputeStereoMatches of this handle's previous sub-batch (matching stream) read the
+            # pyramids this extraction overwrites
+            s.wait_event(self.stereo_done[k])
         ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
                                       o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
-        if self.stereo:  # Frame.cc:125, on the extraction stream while the pyramids are current
-            ev = []
-            self._ev("k_stereo", s, ev)
-            ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
-                                                         o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
-                                                         o.ur.data_ptr(), o.dep.data_ptr(),
-                                                         stream=s.cuda_stream)
-            self._ev("k_stereo", s, ev)
-            if ev:
-                self.events["k_stereo"].append(tuple(ev))
+        o.ext = ext
+        o.k = k
+        if self.stereo and not self.stereo_on_match:  # Frame.cc:125, on the extraction stream
+            self._stereo(o, ext, s)
         if self.vocab_inline:
             self._vocab(o, s)
         o.extracted.record(s)
@@ -310,6 +317,19 @@ class C3Pipeline:
             self._match(self.pending, after_match)
             self.pending = None
 
+    def _stereo(self, o, ext, stream):
+        """Frame::ComputeStereoMatches (Frame.cc:125) of the set's B pairs on `stream`, from the
+        pyramids handle `ext` built for it."""
+        B, cap = self.B, self.cap
+        ev = []
+        self._ev("k_stereo", stream, ev)
+        ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
+                                                o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
+                                                o.ur.data_ptr(), o.dep.data_ptr(), stream=stream.cuda_stream)
+        self._ev("k_stereo", stream, ev)
+        if ev:
+            self.events["k_stereo"].append(tuple(ev))
+
     def _vocab_on_side(self, o):
         self.side.wait_event(o.extracted)
         self._vocab(o, self.side)
@@ -322,6 +342,11 @@ class C3Pipeline:
             m.wait_event(o.vocabbed)
         elif not self.match_inline:
             m.wait_event(o.extracted)
+        if self.stereo and self.stereo_on_match:
+            # off the extraction chain: the handle's next extraction waits for it (run())
+            self._stereo(o, o.ext, m)
+            ev = self.stereo_done[o.k] = self._torch.cuda.Event()
+            ev.record(m)
         if not (self.vocab_inline or self.vocab_side):
             self._vocab(o, m)
         ev = []
@@ -402,7 +427,8 @@ STEP_Z = 1.0  # metres between consecutive frames of the C3 driving sequence (SU
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
              stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
-             vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo"):
+             vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
+             stereo_on_match: bool = False):
     """The C3 scene of bench.py: KITTI intrinsics, seeded KeyFrame state per keypoint slot (half
     the keypoints stereo unless ComputeStereoMatches provides mvuRight, 30 % with a MapPoint), and
     the KeyFrame pair geometry with F12 and epipole from LocalMapping::ComputeF12
@@ -433,7 +459,8 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
-                      vocab_inline=vocab_inline, vocab_side=vocab_side, pairs=pairs)
+                      vocab_inline=vocab_inline, vocab_side=vocab_side, pairs=pairs,
+                      stereo_on_match=stereo_on_match)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo, pairs=pairs)
     return pipe, state

@@ -66,13 +66,16 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
             assert abs(st["epipole"][0] - st["cam"]["cx"]) < 1e-3 and abs(st["epipole"][1] - st["cam"]["cy"]) < 1e-3
 
 
-@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs", [(False, False, 1, "stereo"), (True, False, 0, "stereo"),
-                                                                (False, True, 2, "stereo"), (False, True, 1, "kf")])
-def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs):
+@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match",
+                         [(False, False, 1, "stereo", True), (True, False, 0, "stereo", True),
+                          (False, True, 2, "stereo", False), (False, True, 1, "kf", True),
+                          (True, True, 1, "kf", True), (False, True, 1, "kf", False)])
+def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match):
     """bench.py's default schedule: two extractor handles extract consecutive sub-batches on their
     own streams (side-stream work on one shared high-priority stream), matching on its own stream
     or inline after each extraction (then two vocabulary transforms run concurrently on the one
-    handle: per-stream scratch), four output sets."""
+    handle: per-stream scratch), four output sets; ComputeStereoMatches on the matching stream
+    (the handle's next extraction waits for it) or right after the extraction."""
     import torch
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     tree, voc, ref = vocab
@@ -81,7 +84,8 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
     for e in exts:
         e.debug_set_blur_mode(blur_mode)
     streams = PipelineStreams(0, 2, match_inline=match_inline, match_high=not match_inline)
-    pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs)
+    pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs,
+                        stereo_on_match=stereo_on_match)
     batches = [frames(B, 0, pairs), frames(B, 1000, pairs), frames(B, 2000, pairs)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]
     for j in range(7):  # sub-batch j: input j % 3, set j % 4, handle j % 2

@@ -87,6 +87,43 @@ def test_search_for_triangulation_node_sizes(require_gpu, kitti_pair, k, levels,
     assert nm > 0
 
 
+def test_search_for_triangulation_unlisted_features(require_gpu, kitti_pair):
+    """Features a FeatureVector does not list -- DBoW2 leaves out stopped words (weight 0,
+    TemplatedVocabulary.h:1198-1201) -- are never matched: match12 = -1 for them even when the
+    matcher's buffers hold an earlier call's matches."""
+    from orb_slam2_2021_amd.frames import FeatureVector
+    k1, d1, k2, d2, scale, sigma2 = kitti_pair
+    rng = np.random.default_rng(9)
+    voc = S.Vocabulary.synthetic()
+    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    F1 = S.make_frame(k1, d1, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.5, tcw=t1)
+    F2 = S.make_frame(k2, d2, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.5, tcw=t2)
+    F12 = S.compute_f12(t1, t2, S.intrinsics(S.KITTI_CAM))
+    ex, ey = -1.0e7, 185.0
+    m = ORBmatcher(0.6, False)
+    full1, full2 = voc.feature_vector(d1, 0), voc.feature_vector(d2, 0)
+    F1.feat_vec, F2.feat_vec = full1, full2
+    nm0, _, _ = m.SearchForTriangulation(F1, F2, F12, False, epipole_xy=(ex, ey))
+    assert nm0 > 0
+
+    def drop(fv, every):  # the same nodes without every `every`-th feature
+        d = {}
+        for a in range(len(fv.node_ids)):
+            kept = [int(i) for i in fv.indices[fv.offsets[a]:fv.offsets[a + 1]] if i % every != 0]
+            if kept:
+                d[int(fv.node_ids[a])] = kept
+        return FeatureVector.from_dict(d)
+
+    for every in (3, 7):
+        F1.feat_vec, F2.feat_vec = drop(full1, every), drop(full2, every + 2)
+        assert int(F1.feat_vec.offsets[-1]) < len(k1)
+        nm, _, m12 = m.SearchForTriangulation(F1, F2, F12, False, epipole_xy=(ex, ey))
+        nr, r12 = orbref.search_for_triangulation(F1, F2, F12, ex, ey, False, False)
+        assert nm == nr and np.array_equal(m12, r12)
+        assert np.all(m12[np.arange(len(k1)) % every == 0] == -1)
+        assert nm > 0
+
+
 def test_search_for_triangulation_epipole_from_poses(require_gpu, kitti_pair):
     k1, d1, k2, d2, scale, sigma2 = kitti_pair
     rng = np.random.default_rng(8)
