@@ -117,6 +117,9 @@ def parse(argv=None):
     p.add_argument("--stereo-on-match", action="store_true",
                    help="ComputeStereoMatches on the matching stream, the handle's next extraction waiting for it "
                         "(default: on the extraction stream right after each extraction; measured: no gain)")
+    p.add_argument("--cu-split", type=int, default=0,
+                   help="each extractor handle's stream on its own share of the CUs (hipExtStreamCreateWithCUMask; "
+                        "1: contiguous CU ranges, 2: interleaved), side work inline on it")
     p.add_argument("--tiled-pyramid", action="store_true",
                    help="the tiled k_pyramid launches instead of the default k_copy0 + one k_resize launch per "
                         "level (comparison; measured slower)")
@@ -236,7 +239,8 @@ def main():
     pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline,
                                                                   match_high=not args.match_normal,
                                                                   side_last=args.inline_side,
-                                                                  side_high=not args.side_normal)
+                                                                  side_high=not args.side_normal,
+                                                                  cu_split=args.cu_split)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -268,7 +272,7 @@ def main():
         ext.debug_set_fast_side_levels(args.fast_side)
     if args.blur_mode >= 0:
         ext.debug_set_blur_mode(args.blur_mode)
-    if args.inline_side:
+    if args.inline_side or args.cu_split:
         ext.debug_set_inline_side(True)
     if args.copy0_side:
         ext.debug_set_copy0_side(True)
@@ -278,7 +282,7 @@ def main():
         # shares one high-priority stream (PipelineStreams.side)
         exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_ext - 1)]
         for e in exts:
-            if pstreams is None or args.inline_side:
+            if pstreams is None or args.inline_side or args.cu_split:
                 e.debug_set_inline_side(True)
             if args.fast_side > 0:
                 e.debug_set_fast_side_levels(args.fast_side)
@@ -403,7 +407,7 @@ def main():
                     timed_events if use_timed else args.probe_subbatches, pipe)
     roof["measured_in"] = (f"timed region (HIP events on every {ev_every}th sub-batch, "
                            f"{timed_events} sub-batches)" if use_timed else "probe pass")
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B)
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(dominant, W, H, B, args)
     if roof["traffic"] is not None:  # per launch, like `achieved`: the sub-batch figure / its launches
         roof["traffic_per_subbatch"] = roof["traffic"]
         roof["traffic"] = int(roof["traffic"] / roof["launches_per_subbatch"])
@@ -597,7 +601,11 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches, pipe):
             "launches_per_subbatch": per_launch}
 
 
-def pmc_traffic(kernel, W, H, B):
+def pmc_workload(W, H, B, args):
+    return {"cols": W, "rows": H, "batch": B, "pairs": args.pairs, "stereo": bool(args.stereo)}
+
+
+def pmc_traffic(kernel, W, H, B, args):
     """HBM bytes per sub-batch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (profiles/pmc_traffic.json, written by profiles/pmc_summary.py from separate FETCH_SIZE and
     WRITE_SIZE passes of bench.py; FETCH_SIZE doubled per MI355X_MICROARCH.md), or None when no
@@ -608,7 +616,7 @@ def pmc_traffic(kernel, W, H, B):
             doc = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if doc.get("workload") != {"cols": W, "rows": H, "batch": B}:
+    if doc.get("workload") != pmc_workload(W, H, B, args):
         return None, None
     k = doc.get("kernels", {}).get(kernel)
     if not k:
@@ -726,21 +734,15 @@ def c2_latency(args, left, right, reps=200):
     return out
 
 
-def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
-    """BASELINE config C5: a 640x480 stream through Tracking::SearchLocalPoints' hot part --
-    Frame::isInFrustum(pMP, 0.5) for every MapPoint of the local map, then
-    ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th=3) (Tracking.cc:1186-1213) -- with
-    frames sharded over the ranks and the 50k-MapPoint local map replicated (built on rank 0,
-    broadcast over RCCL when N > 1). Per frame: extraction (ORBextractor 12/7, arducam.yaml) and
-    orbfe_search_local_points (host-buffer call: frame + map uploaded, PCIe included). frames/s =
-    all ranks' frames / max-over-ranks wall time. Rank 0 checks its first frame bit-exact against
-    the oracle."""
-    import torch
-    from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame
+def c5_scene(nfeatures, world, rank, dev, m_points=50000, frames_per_rank=16):
+    """BASELINE config C5's inputs: 640x480 frames of this rank (frame sharding) with their poses,
+    and the 50k-MapPoint local map (seed 0x50C0DE) built identically on every rank,
+    replicated from rank 0 over the process group when N > 1."""
+    from orb_slam2_2021_amd import ORBextractor, synth_frame
     from orb_slam2_2021_amd import synthetic as S
-    from orb_slam2_2021_amd.frames import MapPointGeometry, log_scale_factor
+    from orb_slam2_2021_amd.frames import MapPointGeometry
     from orb_slam2_2021_amd.parallel import broadcast_arrays, shard_frames
-    ext = ORBextractor(args.nfeatures, 1.2, 8, 12, 7)  # arducam.yaml:126-127
+    ext = ORBextractor(nfeatures, 1.2, 8, 12, 7)  # arducam.yaml:126-127
     sc, s2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
     k0, d0 = ext(synth_frame(7, 480, 640))
     rng = np.random.default_rng(0x50C0DE)
@@ -748,7 +750,6 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
     G = S.make_local_map(F0, m_points, rng)  # identical on every rank (same seed)
     fields = ("flags", "world_pos", "normal", "min_distance", "max_distance", "descriptors")
     if world > 1:  # the replicated SoA: rank 0's map broadcast to every rank
-        import torch.distributed as dist
         arrs = {f: np.ascontiguousarray(getattr(G, f)) for f in fields}
         got = broadcast_arrays(arrs, dev, src=0)  # dev: the rank's GPU (host in --rehearse)
         G = MapPointGeometry(**{f: got[f].cpu().numpy().view(arrs[f].dtype).reshape(arrs[f].shape)
@@ -757,21 +758,47 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
     mine = shard_frames(n_total, world, rank)
     imgs = [synth_frame(100 + i, 480, 640) for i in mine]
     poses = [S.pose(tx=0.1 + 0.002 * (i % 8), yaw=0.02 + 0.001 * (i % 5)) for i in mine]
+    return ext, F0, G, imgs, poses, n_total
+
+
+def c5_frame(ext, img, tcw):
+    from orb_slam2_2021_amd import synthetic as S
+    k, d = ext(img)
+    return S.Frame(keys_un=k, descriptors=d if d is not None else np.zeros((0, 32), np.uint8),
+                   u_right=np.full(len(k), -1.0, np.float32), mp_state=np.zeros(len(k), np.uint8),
+                   scale_factors=ext.GetScaleFactors(), level_sigma2=ext.GetScaleSigmaSquares(), min_x=0.0,
+                   max_x=640.0, min_y=0.0, max_y=480.0, tcw=tcw, **S.ARDUCAM_CAM)
+
+
+def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
+    """BASELINE config C5: a 640x480 stream through Tracking::SearchLocalPoints' hot part --
+    Frame::isInFrustum(pMP, 0.5) for every MapPoint of the local map, then
+    ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th=3) (Tracking.cc:1186-1213) -- with
+    frames sharded over the ranks and the 50k-MapPoint local map replicated (built on rank 0,
+    broadcast over RCCL when N > 1). Per frame: extraction (ORBextractor 12/7, arducam.yaml) and
+    orbfe_search_local_points (host-buffer call: frame + map uploaded, PCIe included). frames/s =
+    all ranks' frames / max-over-ranks wall time. Then the device part alone: HIP events around
+    k_frustum .. the last SearchByProjection kernel of each search (orbfe_matcher_set_profiling),
+    and its roofline against SURVEY 8(d)'s bytes: isInFrustum 49 B in + 21 B out per MapPoint,
+    SearchByProjection M (32 + 20) + N (32 + 16 + 4) + 3072 x 8 per frame (2.73 MB at 50k), the
+    PMC traffic of the same kernels from profiles/pmc_traffic_c5.json. Rank 0 checks its first
+    frame bit-exact against the oracle."""
+    import torch
+    from orb_slam2_2021_amd import ORBmatcher
+    from orb_slam2_2021_amd.frames import log_scale_factor
+    ext, F0, G, imgs, poses, n_total = c5_scene(args.nfeatures, world, rank, dev, m_points, frames_per_rank)
     m = ORBmatcher(0.8, True)  # Tracking.cc:1206
     ext(imgs[0])
     m.SearchLocalPoints(F0, G, 3.0)
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    nm_total, first = 0, None
+    nm_total, first, frames = 0, None, []
     for img, tcw in zip(imgs, poses):
-        k, d = ext(img)
-        F = S.Frame(keys_un=k, descriptors=d if d is not None else np.zeros((0, 32), np.uint8),
-                    u_right=np.full(len(k), -1.0, np.float32), mp_state=np.zeros(len(k), np.uint8),
-                    scale_factors=sc, level_sigma2=s2, min_x=0.0, max_x=640.0, min_y=0.0, max_y=480.0,
-                    tcw=tcw, **S.ARDUCAM_CAM)
+        F = c5_frame(ext, img, tcw)
         nm, best, nv, _ = m.SearchLocalPoints(F, G, 3.0)
         nm_total += nm
+        frames.append(F)
         if first is None:
             first = (F, nm, best, nv)
     dt = time.perf_counter() - t0
@@ -779,9 +806,31 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    out = {"frames_per_s": round(n_total / dt, 1), "ms_per_frame_per_rank": round(1e3 * dt / len(mine), 3),
-           "frames": n_total, "ranks": world, "map_points": m_points,
-           "matches_per_frame_rank0": round(nm_total / len(mine), 1),
+    # the device part alone (no extraction, no PCIe)
+    m.set_profiling(True)
+    dev_ms, rounds = [], []
+    for _ in range(3):
+        for F in frames:
+            m.SearchLocalPoints(F, G, 3.0)
+            dev_ms.append(m.last_device_ms())
+            rounds.append(m.last_stats()[0])
+    m.set_profiling(False)
+    M = len(G.flags)
+    N = float(np.mean([F.N for F in frames]))
+    algo = M * (49 + 21) + M * (32 + 20) + N * (32 + 16 + 4) + 3072 * 8
+    us = 1e3 * float(np.median(dev_ms))
+    achieved = algo / (us * 1e-6) / 1e9
+    traffic = c5_pmc_traffic(M)
+    out = {"frames_per_s": round(n_total / dt, 1), "ms_per_frame_per_rank": round(1e3 * dt / len(imgs), 3),
+           "frames": n_total, "ranks": world, "map_points": M,
+           "matches_per_frame_rank0": round(nm_total / len(imgs), 1),
+           "device_us_per_search": round(us, 2),
+           "claim_rounds_per_search": round(float(np.mean(rounds)), 1),
+           "roofline": {"kernel": "k_frustum + k_sbp_* (isInFrustum + SearchByProjection, one frame)",
+                        "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                        "algorithmic_bytes_per_frame": int(algo),
+                        "measured_in": "HIP events around the device part of each search (orbfe_matcher_set_profiling)"},
            "what": "640x480 frames sharded over ranks, local map replicated (broadcast from rank 0 when N > 1); "
                    "per frame ORBextractor + orbfe_search_local_points (host buffers, PCIe included)"}
     if rank == 0 and not args.no_cpu:
@@ -792,6 +841,20 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
         out["cpu_oracle_ms_per_search"] = round(1e3 * (time.perf_counter() - t0), 3)
         out["cpu_bit_exact"] = bool(nr == nm and nvr == nv and np.array_equal(br, best))
     return out
+
+
+def c5_pmc_traffic(m_points):
+    """HBM bytes of one SearchLocalPoints call's kernels (isInFrustum + SearchByProjection) from the
+    committed rocprofv3 PMC summary (profiles/pmc_traffic_c5.json, profiles/scripts/c5_only.py), or
+    None when none is committed for this map size."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic_c5.json")) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if doc.get("workload", {}).get("map_points") != m_points:
+        return None
+    return int(doc["traffic_bytes_per_search"])
 
 
 def pairing_leg(args, exts, tree, voc, d_img, pstreams, dev, subbatches=256):
@@ -983,7 +1046,9 @@ def stereo_leg(args, ext, d_img, host, B, H, W, cap, mbf, mb, reps=30):
         "parity_all_pairs_bit_exact": same,
         "roofline": {"kernel": "k_stereo_rows + k_stereo_match + k_stereo_median", "bound": "hbm",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": stereo_traffic(args, W, H, B),
+                     "traffic_what": "PMC HBM bytes of the three stereo kernels per launch sequence (B pairs), "
+                                     "profiles/pmc_traffic.json",
                      "algorithmic_bytes_per_launch_sequence": algo},
         "cpu_baseline": {"value": round(B / cpu_s, 1), "unit": "pairs/s", "cores": 1, "kind": "port",
                          "sample": f"ComputeStereoMatches oracle (-O3 -march=native) on the same {B} "
@@ -992,9 +1057,22 @@ def stereo_leg(args, ext, d_img, host, B, H, W, cap, mbf, mb, reps=30):
     }
 
 
+def stereo_traffic(args, W, H, B):
+    """PMC HBM bytes of one ComputeStereoMatches launch sequence (k_stereo_rows + k_stereo_match +
+    k_stereo_median over B pairs), from the bench workload's committed summary, or None."""
+    tot = 0
+    for k in ("k_stereo_rows", "k_stereo_match", "k_stereo_median"):
+        t, _ = pmc_traffic(k, W, H, B, args)
+        if t is None:
+            return None
+        tot += t
+    return tot
+
+
 def vocab_leg(args, voc, tree, pipe, reps=20):
     """KeyFrame::ComputeBoW alone (SURVEY 8(f) row 3): the vocabulary transform of the last
-    sub-batch's 64 descriptor sets (BowVector + FeatureVector, L=6 tree, levelsup 4), HIP events
+    sub-batch's KeyFrame descriptor sets (the B lefts with --pairs kf; BowVector + FeatureVector,
+    L=6 tree, levelsup 4), HIP events
     around `reps` device launches; the oracle (std::map containers, one core) on the same sets."""
     import torch
     o = pipe.last
@@ -1002,7 +1080,7 @@ def vocab_leg(args, voc, tree, pipe, reps=20):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run():
-        voc.transform_batch_device(pipe.n_img, o.desc.data_ptr(), pipe.cap * 32, o.cnt.data_ptr(),
+        voc.transform_batch_device(pipe.n_vocab, o.desc.data_ptr(), pipe.cap * 32, o.cnt.data_ptr(),
                                    pipe.levelsup, o.ids.data_ptr(), o.offs.data_ptr(), o.idx.data_ptr(),
                                    o.nodes.data_ptr(), pipe.cap, stream=s.cuda_stream,
                                    d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
@@ -1016,8 +1094,8 @@ def vocab_leg(args, voc, tree, pipe, reps=20):
     e1.record(s)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    nkp = int(o.cnt.sum().item())
-    out = {"us_per_subbatch": round(us, 2), "descriptor_sets": pipe.n_img, "descriptors": nkp,
+    nkp = int(o.cnt[:pipe.n_vocab].sum().item())
+    out = {"us_per_subbatch": round(us, 2), "descriptor_sets": pipe.n_vocab, "descriptors": nkp,
            "tree_nodes": tree.n_nodes, "descriptors_per_s": round(nkp / (us * 1e-6), 1)}
     if not args.no_cpu:
         from oracle.orbref import RefVocabulary
@@ -1026,7 +1104,7 @@ def vocab_leg(args, voc, tree, pipe, reps=20):
         host = pipe.to_host(o)
         t0 = time.perf_counter()
         same = True
-        for i in range(pipe.n_img):
+        for i in range(pipe.n_vocab):
             w, wt, fv = ref.transform(host["descriptors"][i], pipe.levelsup)
             gw, gt = host["bow"][i]
             gi, go, gx = host["fv"][i]

@@ -145,6 +145,9 @@ int orbfe_stream_wait_event(void* stream, void* event);
  * pipeline) creates them first, before any other stream, so that each takes its own queue. */
 int orbfe_stream_create(int device, int high_priority, void** out);
 int orbfe_stream_destroy(void* stream);
+/* A stream whose kernels run only on the CUs set in cu_mask (n_words 32-bit words, bit i = CU i;
+ * hipExtStreamCreateWithCUMask), normal priority: e.g. one half of the CUs per extractor handle. */
+int orbfe_stream_create_masked(int device, const uint32_t* cu_mask, int n_words, void** out);
 
 /* ---- matcher data (packed struct-of-arrays views of Frame / KeyFrame / MapPoint) ---------- */
 

@@ -38,6 +38,11 @@ int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int n_pairs,
 
 /* hipStream_t of the matcher (as void*). */
 void* orbfe_matcher_stream(orbfe_matcher* m);
+/* Profiling of the host-buffer searches (SearchByProjection family, isInFrustum + SearchLocalPoints):
+ * with it on, each call records HIP events around its device part (first kernel to last kernel,
+ * H2D / D2H excluded); orbfe_matcher_last_device_ms returns the last call's device milliseconds. */
+int orbfe_matcher_set_profiling(orbfe_matcher* m, int on);
+int orbfe_matcher_last_device_ms(orbfe_matcher* m, float* ms);
 
 /* Statistics of the last SearchByProjection call: fixpoint rounds run and whether the serial
  * fallback kernel had to finish the claim order. */

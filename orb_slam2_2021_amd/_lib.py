@@ -117,9 +117,12 @@ _SIGNATURES = {
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
     "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
     "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
+    "orbfe_matcher_set_profiling": (c_int, [c_void_p, c_int]),
+    "orbfe_matcher_last_device_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "orbfe_host_register": (c_int, [c_void_p, c_size_t]),
     "orbfe_host_unregister": (c_int, [c_void_p]),
     "orbfe_stream_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "orbfe_stream_create_masked": (c_int, [c_int, c_void_p, c_int, POINTER(c_void_p)]),
     "orbfe_stream_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_create": (c_int, [c_float, c_int, c_int, POINTER(c_void_p)]),
     "orbfe_matcher_destroy": (c_int, [c_void_p]),

@@ -2091,6 +2091,17 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
     bw[k] = make_uint2(0u, 0u);
     if (l16 + 16 * k < 185) __builtin_memcpy(&bw[k], bsrc + (k / 5) * step16 + br[k % 5] * pitch + 8 * bc[k % 5], 8);
   }
+#if defined(ORBFE_DESC_DIAG) && ORBFE_DESC_DIAG == 1  // phase-cost diagnostic builds only (wrong output)
+  {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) acc ^= mu[k].x ^ mu[k].y ^ mu[k].z;
+#pragma unroll
+    for (int k = 0; k < 12; k++) acc ^= bw[k].x ^ bw[k].y;
+    if (acc == 0x12345678u && valid) a.out_desc[0] = 1;  // keeps the loads
+    return;
+  }
+#endif
   // 2. IC_Angle moments (:75-102) over the 749-pixel circle: bytes with |u| <= umax[|v|] (masks in
   //    LDS), sums of I and col * I by byte dot products
   const uint32_t* mt = s_mom + ((cx - 15) & 3) * 279;
@@ -2123,6 +2134,10 @@ __global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
   float ca, sb;
   steer_cos_sin(angle, a.factor_pi, ca, sb);
   wave_sync();
+#if defined(ORBFE_DESC_DIAG) && ORBFE_DESC_DIAG == 2
+  if (__float_as_uint(ca + sb) == 0x12345678u && valid) a.out_desc[0] = 1;  // keeps the angle work
+  return;
+#endif
   // 3. the 256 steered tests (:105-151) on the LDS window, pixel (dy, dx) at byte
   //    (dy + 18) * 40 + (dx + cx - xb); test p = 16 j + l16 lands in bit l16 of the group's
   //    16-bit slice of ballot j = descriptor bytes 2j, 2j+1
@@ -3240,6 +3255,16 @@ extern "C" int orbfe_stream_create(int device, int high_priority, void** out) {
   } else {
     ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   }
+  *out = (void*)s;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_stream_create_masked(int device, const uint32_t* cu_mask, int n_words, void** out) {
+  if (!out || !cu_mask || n_words <= 0) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stream_create_masked: bad argument");
+  *out = nullptr;
+  hipStream_t s = nullptr;
+  ORBFE_HIP_CHECK(hipSetDevice(device));
+  ORBFE_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, cu_mask));
   *out = (void*)s;
   return ORBFE_OK;
 }

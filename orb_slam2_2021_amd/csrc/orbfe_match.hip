@@ -1222,11 +1222,33 @@ extern "C" int orbfe_matcher_destroy(orbfe_matcher* m) {
   hipFree(m->d_pairs);
   hipFree(m->d_serial);
   if (m->stream) hipStreamDestroy(m->stream);
+  if (m->prof_ev0) hipEventDestroy(m->prof_ev0);
+  if (m->prof_ev1) hipEventDestroy(m->prof_ev1);
   delete m;
   return ORBFE_OK;
 }
 
 extern "C" void* orbfe_matcher_stream(orbfe_matcher* m) { return m ? (void*)m->stream : nullptr; }
+
+extern "C" int orbfe_matcher_set_profiling(orbfe_matcher* m, int on) {
+  if (!m) return ORBFE_ERR_ARG;
+  hipSetDevice(m->device);
+  if (on && !m->prof_ev0) {
+    ORBFE_HIP_CHECK(hipEventCreate(&m->prof_ev0));
+    ORBFE_HIP_CHECK(hipEventCreate(&m->prof_ev1));
+  }
+  m->profile = on ? 1 : 0;
+  m->prof_started = m->prof_done = false;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_matcher_last_device_ms(orbfe_matcher* m, float* ms) {
+  if (!m || !ms) return ORBFE_ERR_ARG;
+  if (!m->profile || !m->prof_done) return orbfe_set_error(ORBFE_ERR_STATE, "no profiled call yet");
+  ORBFE_HIP_CHECK(hipEventSynchronize(m->prof_ev1));
+  ORBFE_HIP_CHECK(hipEventElapsedTime(ms, m->prof_ev0, m->prof_ev1));
+  return ORBFE_OK;
+}
 
 extern "C" int orbfe_descriptor_distance(const uint8_t* a, const uint8_t* b) {
   if (!a || !b) return ORBFE_ERR_ARG;
@@ -1556,6 +1578,8 @@ int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatch
       ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
     }
   }
+  // the device part ends after the last round (continuations included, with their host syncs)
+  prof_end(m);
   if (p.nq > 0) {
     if (best_idx)
       ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, A + p.obest, 4 * (size_t)p.nq, hipMemcpyDeviceToHost, m->stream));
@@ -1620,11 +1644,13 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, const Sb
   if (st) return st;
   uint8_t* A = m->arena;
   orbfe_frame_view dF;
+  m->prof_started = m->prof_done = false;
   if ((st = sbp_stage(m, p, F, h_qdesc, h_qangle, &dF))) return st;
   if (nq > 0 && (st = make_q(A, dF, (SbpQuery*)(A + p.oq)))) return st;  // stages, flushes, builds queries
   if ((st = flush_h2d(m))) return st;
+  prof_begin(m);  // (no-op when make_q's k_frustum already opened the window)
   if ((st = sbp_launch(m, p, F, dF, md, true))) return st;
-  return sbp_fetch(m, p, best_idx, nmatches, F, &dF, &md);
+  return sbp_fetch(m, p, best_idx, nmatches, F, &dF, &md);  // (closes the profiling window)
 }
 
 extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_frame_view* F,
@@ -1822,6 +1848,7 @@ static int launch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, co
   stage_h2d(m, A + p.maxd, G->max_distance, 4 * M);
   int st = flush_h2d(m);
   if (st) return st;
+  prof_begin(m);
   ORBFE_HIP_CHECK(hipMemsetAsync(A + p.counter, 0, 4, m->stream));
   fa.m = G->m;
   fa.flags_in = A + p.flags_in;

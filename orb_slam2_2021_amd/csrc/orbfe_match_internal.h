@@ -47,7 +47,26 @@ struct orbfe_matcher {
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
+  // orbfe_matcher_set_profiling: HIP events around the device part (first kernel .. last kernel,
+  // no H2D / D2H) of each SearchByProjection-family call
+  int profile = 0;
+  bool prof_started = false, prof_done = false;
+  hipEvent_t prof_ev0 = nullptr, prof_ev1 = nullptr;
 };
+
+// device-time window of one call (orbfe_matcher_set_profiling)
+inline void prof_begin(orbfe_matcher* m) {
+  if (m->profile && !m->prof_started) {
+    hipEventRecord(m->prof_ev0, m->stream);
+    m->prof_started = true;
+  }
+}
+inline void prof_end(orbfe_matcher* m) {
+  if (m->profile && m->prof_started && !m->prof_done) {
+    hipEventRecord(m->prof_ev1, m->stream);
+    m->prof_done = true;
+  }
+}
 
 // ---- device helpers shared by the matcher kernels ---------------------------------------------
 __device__ __forceinline__ int rot_bin_dev(float a1, float a2) {

@@ -54,6 +54,16 @@ class ORBmatcher:
         except Exception:
             pass
 
+    def set_profiling(self, on: bool = True) -> None:
+        """HIP events around the device part of each host-buffer search (orbfe_matcher_set_profiling)."""
+        L.check(self._lib.orbfe_matcher_set_profiling(self._h, 1 if on else 0), "set_profiling")
+
+    def last_device_ms(self) -> float:
+        """Device milliseconds of the last profiled search (first to last kernel, no PCIe)."""
+        ms = ctypes.c_float()
+        L.check(self._lib.orbfe_matcher_last_device_ms(self._h, byref(ms)), "last_device_ms")
+        return float(ms.value)
+
     @staticmethod
     def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
         a = np.ascontiguousarray(a, np.uint8).reshape(32)

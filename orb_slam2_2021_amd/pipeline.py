@@ -64,19 +64,38 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 match_high: bool = False, side_last: bool = False, side_high: bool = True):
+                 match_high: bool = False, side_last: bool = False, side_high: bool = True,
+                 cu_split: int = 0):
         import torch
         self.device = device
         self._ptrs = []
         self._attached = []
+        self.cu_split = cu_split
+
+        def wrap(p):
+            self._ptrs.append(p.value)
+            return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
 
         def make(high):
             p = ctypes.c_void_p()
             L.check(L.lib().orbfe_stream_create(device, 1 if high else 0, ctypes.byref(p)), "stream_create")
-            self._ptrs.append(p.value)
-            return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
+            return wrap(p)
 
-        self.extract = [make(False) for _ in range(max(1, n_extractors))]
+        def make_masked(k, n):
+            # cu_split 1: contiguous CU ranges; 2: CU i to extractor i mod n (every XCD's CUs shared)
+            ncu = torch.cuda.get_device_properties(device).multi_processor_count
+            bits = [(i * n // ncu == k) if cu_split == 1 else (i % n == k) for i in range(ncu)]
+            words = np.zeros((ncu + 31) // 32, np.uint32)
+            for i, b in enumerate(bits):
+                if b:
+                    words[i // 32] |= np.uint32(1 << (i % 32))
+            p = ctypes.c_void_p()
+            L.check(L.lib().orbfe_stream_create_masked(device, words.ctypes.data, len(words), ctypes.byref(p)),
+                    "stream_create_masked")
+            return wrap(p)
+
+        n = max(1, n_extractors)
+        self.extract = [make_masked(k, n) if cu_split else make(False) for k in range(n)]
         # match_inline: each sub-batch's vocabulary + matching follow its extraction on the same
         # stream (the other extractors' streams provide the overlap)
         self.match = None if match_inline or match_high else make(False)

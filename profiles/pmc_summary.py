@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def kname(raw):
-    name = raw.split("(")[0]
+    name = raw.replace("(anonymous namespace)::", "").split("(")[0]
     if name.startswith("void "):
         name = name[5:]
     return name.split("<")[0]
@@ -47,10 +47,11 @@ def main():
         kernels[k] = {"fetch_bytes_corrected_per_launch": round(fb), "write_bytes_per_launch": round(wb),
                       "traffic_bytes_per_launch": round(fb + wb), "launches_per_step": per_step,
                       "traffic_bytes_per_step": round((fb + wb) * per_step)}
-    doc = {"workload": {"cols": 1241, "rows": 376, "batch": 32},
+    doc = {"workload": {"cols": 1241, "rows": 376, "batch": 32, "pairs": "kf", "stereo": True},
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "bench.py --no-cpu --no-legs (profiles/scripts/refresh_profiles.sh); FETCH_SIZE x 2 "
-                     "(gfx950 correction), KiB -> bytes; per launch and per sub-batch of 64 images",
+                     "bench.py --no-cpu --no-legs (profiles/scripts/refresh_profiles.sh; default workload: KeyFrame "
+                     "pairs, ComputeStereoMatches on); FETCH_SIZE x 2 (gfx950 correction), KiB -> bytes; per launch "
+                     "and per sub-batch of 64 images",
            "kernels": kernels}
     text = json.dumps(doc, indent=1)
     if len(sys.argv) > 3:

@@ -17,7 +17,7 @@ from collections import defaultdict
 acc = defaultdict(lambda: defaultdict(lambda: [0.0, 0]))
 with open(sys.argv[1]) as f:
     for row in csv.DictReader(f):
-        k = row["Kernel_Name"].split("(")[0]
+        k = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         c = acc[k][row["Counter_Name"]]
         c[0] += float(row["Counter_Value"])
         c[1] += 1

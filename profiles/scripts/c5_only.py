@@ -1,0 +1,32 @@
+"""BASELINE config C5's device part alone, for rocprofv3 passes: SearchLocalPoints (isInFrustum +
+SearchByProjection th=3, Tracking.cc:1186-1213) of the bench's 16 frames against its 50k-MapPoint
+local map, repeated. python profiles/scripts/c5_only.py [reps]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from orb_slam2_2021_amd import ORBmatcher  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    ext, F0, G, imgs, poses, _ = bench.c5_scene(2000, 1, 0, None)
+    frames = [bench.c5_frame(ext, img, tcw) for img, tcw in zip(imgs, poses)]
+    m = ORBmatcher(0.8, True)
+    m.SearchLocalPoints(frames[0], G, 3.0)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for F in frames:
+            m.SearchLocalPoints(F, G, 3.0)
+    dt = (time.perf_counter() - t0) / (reps * len(frames))
+    print(f"c5: {len(G.flags)} MapPoints, {np.mean([F.N for F in frames]):.0f} keypoints per frame, "
+          f"{1e3 * dt:.3f} ms per search (host buffers), {reps * len(frames)} searches")
+
+
+if __name__ == "__main__":
+    main()

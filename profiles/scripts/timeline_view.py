@@ -6,7 +6,7 @@ import sys
 
 f = glob.glob(f"{sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out/tl'}/**/*kernel_trace.csv", recursive=True)[0]
 r = list(csv.DictReader(open(f)))
-ev = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]), x["Kernel_Name"].split("(")[0].replace("void ", "")[:16],
+ev = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"]), x["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:16],
              x.get("Queue_Id", "")) for x in r)
 sft = [e for e in ev if e[2].startswith("k_sft_nodes")]
 mid = len(sft) // 2
