@@ -39,9 +39,15 @@ def test_roofline_object():
 
 
 def test_committed_pmc_traffic_matches_workload():
-    t, src = bench.pmc_traffic("k_fast", 1241, 376, 32)
+    a = SimpleNamespace(pairs="kf", stereo=True)  # the bench default
+    t, src = bench.pmc_traffic("k_fast", 1241, 376, 32, a)
     assert t is not None and t > 0 and "FETCH_SIZE" in src
-    assert bench.pmc_traffic("k_fast", 640, 480, 32) == (None, None)  # other workload: not reported
+    assert bench.pmc_traffic("k_fast", 640, 480, 32, a) == (None, None)  # other workload: not reported
+    assert bench.pmc_traffic("k_fast", 1241, 376, 32, SimpleNamespace(pairs="stereo", stereo=False)) == (None, None)
+    # the stereo leg's traffic: all three ComputeStereoMatches kernels are in the summary
+    assert bench.stereo_traffic(a, 1241, 376, 32) > 0
+    # C5: the search's kernels for the 50k-MapPoint map
+    assert bench.c5_pmc_traffic(50000) > 0 and bench.c5_pmc_traffic(1000) is None
 
 
 def test_cli_defaults():
