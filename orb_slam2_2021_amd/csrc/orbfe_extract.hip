@@ -978,11 +978,11 @@ __host__ __device__ inline FastLds fast_lds_layout(int rw_max, int rh_max, int r
 // with shifts and the row/column split of a detection index is a multiply-shift.
 // RSC == 0: any geometry, runtime stride.
 template <int RSC>
-__global__ __launch_bounds__(256) void k_fast(ExtractArgs a, int cell0, int cell1) {
+__global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell1) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int w = wave_id(), lane = lane_id();
   const int2 blk = xcd_block2d();
-  const int cell = cell0 + blk.x * 4 + w;  // cells [cell0, cell1) of this launch
+  const int cell = cell0 + blk.x * (int)(blockDim.x >> 6) + w;  // cells [cell0, cell1) of this launch
   const int img = blk.y;
   if (cell >= cell1) return;
   const FastLds lay = fast_lds_layout(a.roi_w_max, a.roi_h_max, RSC);
@@ -2920,13 +2920,20 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
 
-  auto launch_fast = [&](hipStream_t s, int c0, int c1) -> int {
+  auto launch_fast = [&](hipStream_t s, int c0, int c1, bool main_launch = false) -> int {
     if (c1 <= c0) return ORBFE_OK;
-    dim3 grid((c1 - c0 + 3) / 4, n);
+    // wavefronts (cells) per workgroup: 4 for the side-stream launches of levels 0-2, which run
+    // beside the resize chain (smaller workgroups there take CUs from it: 1 per workgroup made
+    // k_fast 176 -> 161 us alone but k_resize 146 -> 177 us); 1 for the levels-3..7 launch after
+    // the chain (bench 77.4 / 77.6k vs 76.5 / 76.8k stereo frames/s, interleaved; 8 per workgroup
+    // everywhere: 71.3k). profiles/scripts/r3_fast_wpb.sh
+    const int wpb = main_launch ? 1 : 4;
+    dim3 grid((c1 - c0 + wpb - 1) / wpb, n);
+    const size_t lds = fast_lds(h) / 4 * wpb;
     if (fast_rs(h) == 68)
-      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<68>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
+      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<68>, grid, dim3(64 * wpb), lds, s, a, c0, c1));
     else
-      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(256), fast_lds(h), s, a, c0, c1));
+      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(64 * wpb), lds, s, a, c0, c1));
     return ORBFE_OK;
   };
   // k_side: the levels whose FAST cells run on the side stream, beside the rest of the pyramid
@@ -3033,7 +3040,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
 #endif
   }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
-  if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells);
+  if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
