@@ -1860,7 +1860,7 @@ __device__ __forceinline__ uint32_t vtap7(uint32_t r0, uint32_t r1, uint32_t r2,
 __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
   const int2 blk = xcd_block2d();
   const int img = blk.y, lane = lane_id();
-  int strip = blk.x * 4 + wave_id(), l = 0;
+  int strip = blk.x * (int)(blockDim.x >> 6) + wave_id(), l = 0;
   if (strip >= a.blur_strips) return;
   while (l + 1 < a.nlevels && strip >= a.levels[l + 1].tile_begin) l++;
   const LevelDesc ld = a.levels[l];
@@ -3032,11 +3032,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // main stream's FAST -- bench 63.7k vs 67.0k stereo frames/s, it competes with that FAST; the
   // blur on the side stream as soon as the pyramid is complete -- 65.1k vs 69.3-70.0k.)
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));  // the pyramid is complete on st
-  const dim3 blur_grid((h->blur_tiles + 3) / 4, n);
+  const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
+  const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
-    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
 #endif
   }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
@@ -3046,14 +3047,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
-    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, side, a));
+    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
 #endif
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   launch_octree(st, 0, h->nlevels);
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
-    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(256), 0, st, a));
+    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a));
 #endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
