@@ -80,6 +80,12 @@ def parse(argv=None):
     p.add_argument("--extractors", type=int, default=2,
                    help="extractor handles whose extractions of consecutive sub-batches overlap, each on its "
                         "own stream, their side-stream work on one shared high-priority stream")
+    p.add_argument("--handles-per-stream", type=int, default=2,
+                   help="extractor handles per extraction stream (handle k on stream k mod --extractors): "
+                        "a handle's pyramids are rebuilt every extractors x this sub-batches")
+    p.add_argument("--hw-queues", type=int, default=0,
+                   help="GPU_MAX_HW_QUEUES for this process (set before the HIP runtime starts; 0: the "
+                        "environment's, 4 by default): hardware queues the busy streams spread over")
     p.add_argument("--defer-matching", action="store_true",
                    help="enqueue sub-batch i's vocabulary + matching with sub-batch i+1's extraction, after its "
                         "pyramid (overlapping the FAST / octree / blur / describe phase)")
@@ -114,9 +120,10 @@ def parse(argv=None):
                    help="diagnostic: the pipeline's streams from torch's pool, created after the "
                         "handles (hardware-queue assignment then depends on the stream count; with "
                         "several extractors their side work runs inline)")
-    p.add_argument("--stereo-on-match", action="store_true",
-                   help="ComputeStereoMatches on the matching stream, the handle's next extraction waiting for it "
-                        "(default: on the extraction stream right after each extraction; measured: no gain)")
+    p.add_argument("--stereo-on-extract", action="store_true",
+                   help="ComputeStereoMatches on the extraction stream right after each extraction (rounds 1-3's "
+                        "placement; default: on the matching stream ahead of the vocabulary, with two handles per "
+                        "extraction stream so no extraction waits for it: 78.4-78.5k vs 77.1-77.5k)")
     p.add_argument("--cu-split", type=int, default=0,
                    help="each extractor handle's stream on its own share of the CUs (hipExtStreamCreateWithCUMask; "
                         "1: contiguous CU ranges, 2: interleaved), side work inline on it")
@@ -220,6 +227,8 @@ class Gatherer:
 
 def main():
     args = parse()
+    if args.hw_queues > 0:  # read once by the HIP runtime at its start (no HIP call before this)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
     import torch
@@ -277,10 +286,11 @@ def main():
     if args.copy0_side:
         ext.debug_set_copy0_side(True)
     exts = [ext]
-    if n_ext > 1:
+    n_handles = n_ext * max(1, args.handles_per_stream)
+    if n_handles > 1:
         # several handles extract consecutive sub-batches concurrently; their side-stream work
         # shares one high-priority stream (PipelineStreams.side)
-        exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_ext - 1)]
+        exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_handles - 1)]
         for e in exts:
             if pstreams is None or args.inline_side or args.cu_split:
                 e.debug_set_inline_side(True)
@@ -298,7 +308,7 @@ def main():
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs,
-                           stereo_on_match=args.stereo_on_match)
+                           stereo_on_match=not args.stereo_on_extract)
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream
@@ -374,7 +384,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         for k in range(S_sub):
-            ev = (k // n_ext) % ev_every == 0  # n_ext consecutive sub-batches: every handle
+            ev = (k // len(exts)) % ev_every == 0  # len(exts) consecutive sub-batches: every handle
             if ev:
                 set_events(True)
                 timed_events += 1
@@ -444,8 +454,8 @@ def main():
             "stereo_frames_per_gpu_per_subbatch": B, "subbatches_per_step": S_sub,
             "stereo_frames_per_gpu_per_step": B * S_sub, "distinct_input_batches": NB,
             "parallelism": f"frame-sharded x{world}",
-            "pipeline": (f"{n_ext} extractor handles on their own streams (consecutive sub-batches' "
-                         f"extractions overlap), {'matching inline' if args.match_inline else 'matching on its own stream'}, "
+            "pipeline": (f"{len(exts)} extractor handles on {n_ext} streams (consecutive sub-batches' "
+                         f"extractions overlap), {'matching inline' if args.match_inline else ('' if args.stereo_on_extract else 'ComputeStereoMatches + ') + 'vocabulary + matching on its own stream'}, "
                          f"{pipe_depth(args)} output sets" if pipe_depth(args) > 1 else "one sub-batch at a time"),
         },
         "roofline": roof,
@@ -502,7 +512,7 @@ def main():
         # on the pipeline's)
         torch.cuda.synchronize()
         ext.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 0)
-        out["host_boundary"] = host_boundary_rate(ext, host[0])
+        out["host_boundary"] = host_boundary_rate(ext, host[0], others=exts[1:])
         if not args.no_legs:
             out["c2_latency"] = c2_latency(args, host[0][0], host[0][B])
             out["legs"] = {"c5_search_local_points": c5_leg(args, 1, 0, dev),
@@ -538,7 +548,7 @@ def dump_gather(d, g, pipe, rank, world):
 def pipe_depth(args):
     """Output sets in flight: --pipeline, or 2 per extractor handle (sub-batch i's set is reused
     by i + depth, whose handle then finished i + depth - n_ext's extraction long before)."""
-    return args.pipeline if args.pipeline > 0 else 2 * max(1, args.extractors)
+    return args.pipeline if args.pipeline > 0 else 2 * max(1, args.extractors) * max(1, args.handles_per_stream)
 
 
 def merged_kernel_times(exts):
@@ -869,7 +879,7 @@ def pairing_leg(args, exts, tree, voc, d_img, pstreams, dev, subbatches=256):
     B, H, W = args.batch, args.rows, args.cols
     pipe, _ = build_c3(exts if len(exts) > 1 else exts[0], tree, voc, B, H, W, dev, seed=1234,
                        depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                       pairs=other)
+                       pairs=other, stereo_on_match=not args.stereo_on_extract)
     torch.cuda.set_stream(pipe.stream)
     nb = d_img.shape[0]
     for j in range(16):
@@ -1116,7 +1126,7 @@ def vocab_leg(args, voc, tree, pipe, reps=20):
     return out
 
 
-def host_boundary_rate(ext, host, reps=20):
+def host_boundary_rate(ext, host, reps=20, others=()):
     """PCIe-inclusive extraction rate through the host-buffer C ABI entry orbfe_extract_batch on
     the step's 64 host images, with preallocated output buffers as a C++ caller keeps them.
     Reported beside `value`, never as it. Wall clock per call, two ways:
@@ -1166,14 +1176,99 @@ def host_boundary_rate(ext, host, reps=20):
         unregister_host(hostc)
         unregister_host(kps)
         unregister_host(desc)
-    return {"value": round(n / 2 / dt_reg, 2), "unit": "stereo frames/s", "ms_per_call_p50": round(1e3 * dt_reg, 3),
-            "pcie_GBps": round(moved / dt_reg / 1e9, 2),
-            "staged": {"value": round(n / 2 / dt_staged, 2), "ms_per_call_p50": round(1e3 * dt_staged, 3),
-                       "pcie_GBps": round(moved / dt_staged / 1e9, 2)},
-            "registered_equals_staged": same,
-            "what": f"orbfe_extract_batch on {n} host images {cols}x{rows} (extract only; H2D + kernels + D2H; "
-                    f"median of {reps} calls): value = caller buffers registered (orbfe_host_register, direct DMA), "
-                    "staged = plain caller memory through the handle's pinned staging"}
+    out = {"value": round(n / 2 / dt_reg, 2), "unit": "stereo frames/s", "ms_per_call_p50": round(1e3 * dt_reg, 3),
+           "pcie_GBps": round(moved / dt_reg / 1e9, 2),
+           "staged": {"value": round(n / 2 / dt_staged, 2), "ms_per_call_p50": round(1e3 * dt_staged, 3),
+                      "pcie_GBps": round(moved / dt_staged / 1e9, 2)},
+           "registered_equals_staged": same,
+           "what": f"orbfe_extract_batch on {n} host images {cols}x{rows} (extract only; H2D + kernels + D2H; "
+                   f"median of {reps} calls): value = caller buffers registered (orbfe_host_register, direct DMA), "
+                   "staged = plain caller memory through the handle's pinned staging"}
+    if others:
+        out["threads"] = host_threads([ext] + list(others), hostc, cap, reps)
+    return out
+
+
+def host_threads(exts, host, cap, reps):
+    """The host boundary with several extractor handles on as many threads, registered buffers:
+      left_right  -- Frame.cc:113-116's own threading: per call pair, one thread extracts the B left
+                     images and another the B right images (orbfe_extract_batch each), joined;
+      streamed_N  -- N callers (2, and every handle), each extracting all 2B images per call back to
+                     back into its own output buffers, so one caller's H2D overlaps another's kernels.
+    Both in stereo frames/s over wall time (median per joined pair / total over the run)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from ctypes import c_size_t, c_void_p
+    from orb_slam2_2021_amd import _lib as L
+    from orb_slam2_2021_amd import register_host, unregister_host
+    lib = L.lib()
+    n, rows, cols = host.shape
+    B = n // 2
+
+    class Caller:
+        def __init__(self, h, imgs):
+            self.h, self.m = h, len(imgs)
+            self.kps = np.empty(self.m * cap, L.KEYPOINT_DTYPE)
+            self.desc = np.empty((self.m * cap, 32), np.uint8)
+            self.counts = np.zeros(self.m, np.int32)
+            self.arr = (c_void_p * self.m)(*[im.ctypes.data for im in imgs])
+            register_host(self.kps)
+            register_host(self.desc)
+
+        def __call__(self, k=1):
+            for _ in range(k):
+                L.check(lib.orbfe_extract_batch(self.h, self.m, ctypes.cast(self.arr, c_void_p), rows, cols,
+                                                c_size_t(cols), L.ptr(self.kps), L.ptr(self.desc), cap,
+                                                L.ptr(self.counts)), "orbfe_extract_batch")
+
+        def close(self):
+            unregister_host(self.kps)
+            unregister_host(self.desc)
+
+    register_host(host)
+    pool = ThreadPoolExecutor(max_workers=len(exts))
+    callers = []
+    ext0 = exts[0]
+    ext0.debug_set_blur_mode(1)  # the several-handle placement (the blur after DistributeOctTree)
+    out = {}
+    try:
+        lr = [Caller(exts[0]._h, [host[i] for i in range(B)]), Caller(exts[1]._h, [host[B + i] for i in range(B)])]
+        st = [Caller(e._h, list(host)) for e in exts]
+        callers = lr + st
+
+        def run_all(group, k=1):
+            fs = [pool.submit(c, k) for c in group]
+            for f in fs:
+                f.result()
+
+        for _ in range(3):
+            run_all(lr)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            run_all(lr)
+            times.append(time.perf_counter() - t0)
+        dt_lr = float(np.median(times))
+        out["left_right"] = {"value": round(B / dt_lr, 2), "ms_per_frame_batch_p50": round(1e3 * dt_lr, 3)}
+        for m in sorted({2, len(exts)}):
+            run_all(st[:m], 2)
+            t0 = time.perf_counter()
+            run_all(st[:m], reps)
+            dt = time.perf_counter() - t0
+            out[f"streamed_{m}"] = {"value": round(m * reps * B / dt, 2), "ms_per_call": round(1e3 * dt / reps, 3),
+                                    "pcie_GBps": round(m * reps * (host.nbytes + n * cap * 60) / dt / 1e9, 2)}
+        out["counts_equal"] = bool(all(np.array_equal(c.counts, st[0].counts) for c in st)
+                                   and np.array_equal(np.concatenate([lr[0].counts, lr[1].counts]), st[0].counts))
+    finally:
+        pool.shutdown()
+        for c in callers:
+            c.close()
+        unregister_host(host)
+        ext0.debug_set_blur_mode(0)
+    out["what"] = (f"handles on threads, registered buffers: left_right = {B} lefts and {B} rights extracted "
+                   "concurrently by two handles (Frame.cc:113-116), median of the joined pairs; streamed_N = N "
+                   f"callers each extracting all {n} images per call back to back ({reps} calls each), total over "
+                   "wall time; one 30 MB H2D copy runs at ~53 GB/s on this link (profiles/scripts/h2d_bw.py)")
+    return out
 
 
 def _cpu_name():

@@ -259,7 +259,10 @@ class C3Pipeline:
         assert not vocab_side or self.side is not None, "vocab_side needs PipelineStreams"
         if streams is None:
             streams = [torch.cuda.Stream(dev) for _ in range(len(self.exts) + 1)]
-        assert len(streams) == len(self.exts) + 1
+        # several handles may share an extraction stream (handle k on stream k mod S): a handle's
+        # pyramids are then rebuilt only every len(exts) sub-batches
+        assert len(streams) >= 2 and len(self.exts) % (len(streams) - 1) == 0, \
+            "the extractor count must be a multiple of the extraction streams"
         self.streams = list(streams[:-1])
         self.stream = self.streams[0]
         # vocabulary + matching (+ gather); None: on each sub-batch's extraction stream
@@ -295,7 +298,7 @@ class C3Pipeline:
         k = self.counter % len(self.exts)
         self.counter += 1
         B, H, W, cap = self.B, self.H, self.W, self.cap
-        s, ext = self.streams[k], self.exts[k]
+        s, ext = self.streams[k % len(self.streams)], self.exts[k]
         s.wait_event(o.matched)  # the matching that last read this set is done
         if self.stereo_on_match and self.stereo_done[k] is not None:
             # ComputeStereoMatches of this handle's previous sub-batch (matching stream) read the

@@ -60,7 +60,7 @@ def test_cli_defaults():
     assert a.gpus == 1 and 0 < a.steps <= 100 and 0 <= a.warmup <= 20 and a.batch == 32
     assert a.input_batches >= 4 and a.vocab_levels == 6 and a.levelsup == 4
     # two extractor handles, two output sets each
-    assert a.extractors == 2 and bench.pipe_depth(a) == 4
+    assert a.extractors == 2 and a.handles_per_stream == 2 and bench.pipe_depth(a) == 8 and not a.stereo_on_extract
     # SURVEY 8(d)'s KeyFrame pairs with the stereo Frame's ComputeStereoMatches
     assert a.pairs == "kf" and a.stereo
     # a step is long enough to be seen (>= 1024 sub-batches of 32 stereo frames)

@@ -66,21 +66,24 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
             assert abs(st["epipole"][0] - st["cam"]["cx"]) < 1e-3 and abs(st["epipole"][1] - st["cam"]["cy"]) < 1e-3
 
 
-@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match",
-                         [(False, False, 1, "stereo", True), (True, False, 0, "stereo", True),
-                          (False, True, 2, "stereo", False), (False, True, 1, "kf", True),
-                          (True, True, 1, "kf", True), (False, True, 1, "kf", False)])
-def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match):
-    """bench.py's default schedule: two extractor handles extract consecutive sub-batches on their
-    own streams (side-stream work on one shared high-priority stream), matching on its own stream
-    or inline after each extraction (then two vocabulary transforms run concurrently on the one
-    handle: per-stream scratch), four output sets; ComputeStereoMatches on the matching stream
-    (the handle's next extraction waits for it) or right after the extraction."""
+@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match,handles",
+                         [(False, False, 1, "stereo", True, 2), (True, False, 0, "stereo", True, 2),
+                          (False, True, 2, "stereo", False, 2), (False, True, 1, "kf", True, 2),
+                          (True, True, 1, "kf", True, 2), (False, True, 1, "kf", False, 2),
+                          (False, True, 1, "kf", True, 4)])
+def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match,
+                                     handles):
+    """bench.py's schedules: extractor handles extract consecutive sub-batches on two extraction
+    streams (handle k on stream k mod 2; side-stream work on one shared high-priority stream),
+    matching on its own stream or inline after each extraction (then two vocabulary transforms run
+    concurrently on the one handle: per-stream scratch), 4+ output sets; ComputeStereoMatches on the
+    matching stream (with 2 handles the handle's next extraction waits for it; with 4 -- bench.py's
+    default -- nothing waits) or right after the extraction."""
     import torch
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     tree, voc, ref = vocab
     B = 32
-    exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(2)]
+    exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(handles)]
     for e in exts:
         e.debug_set_blur_mode(blur_mode)
     streams = PipelineStreams(0, 2, match_inline=match_inline, match_high=not match_inline)
@@ -88,11 +91,12 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
                         stereo_on_match=stereo_on_match)
     batches = [frames(B, 0, pairs), frames(B, 1000, pairs), frames(B, 2000, pairs)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]
-    for j in range(7):  # sub-batch j: input j % 3, set j % 4, handle j % 2
+    nsets = len(pipe.sets)
+    for j in range(7):  # sub-batch j: input j % 3, set j % nsets, handle j % handles
         pipe.run(d[j % 3].data_ptr())
     torch.cuda.synchronize()
     for j in (4, 5, 6):
-        out = pipe.to_host(pipe.sets[j % 4])
+        out = pipe.to_host(pipe.sets[j % nsets])
         r = check_c3(batches[j % 3], out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"],
                      st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"], pairs=pairs)
         assert r["all"], (j, r)
