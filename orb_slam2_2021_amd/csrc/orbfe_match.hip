@@ -143,6 +143,11 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     }
   }
   wave_sync();
+#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 1  // phase-cost build: loads only (no matches)
+  if (lane < n1) P.match12[idx1[0]] = -1;
+  if (64 + lane < n1) P.match12[idx1[1]] = -1;
+  return;
+#endif
   const float* F = P.f12;
   const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
               f7 = F[7], f8 = F[8];
@@ -213,6 +218,11 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
   };
   int chA = ch[0], chB = ch[1];
   const uint4 qa0 = a0[0], qa1 = a1[0], qb0 = a0[1], qb1 = a1[1];
+#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 2  // + passing sets (round-0 choices, unresolved)
+  if (lane < n1) P.match12[idx1[0]] = chA >= 0 ? P.fv2.indices[o2 + chA] : -1;
+  if (64 + lane < n1) P.match12[idx1[1]] = chB >= 0 ? P.fv2.indices[o2 + chB] : -1;
+  return;
+#endif
   for (int round = 0; round <= n1; round++) {
     for (int p = lane; p < n2; p += 64) claim[p] = 0x7fffffff;
     wave_sync();
@@ -238,6 +248,12 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
   orbfe_sft_pair P = pairs[blockIdx.y];
   sft_resolve_sizes(P);
+#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 3  // phase-cost builds (match12 left unwritten):
+  return;                                             // an empty k_sft_nodes
+#endif
+#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 4  // the coverage workgroups only
+  if (blockIdx.x != gridDim.x - 1) return;
+#endif
   if (blockIdx.x == gridDim.x - 1) {
     // the last workgroup of a pair: KF1 features that no FeatureVector node lists -- a stopped
     // word (weight 0) is not added (TemplatedVocabulary.h:1198-1201) -- never match: -1. Disjoint
@@ -280,6 +296,9 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
     return;
   }
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
+#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 5  // + node lookup (match12 of the node's features unwritten)
+  if (n2 >= 0) return;
+#endif
   if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
     sft_node_fixpoint(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;

@@ -22,11 +22,11 @@
 // k=10), popcount the xor, and a 16-lane min of (distance << 23 | sibling) picks the first best
 // child together with everything the next level needs.
 //
-// k_vocab (one 1024-thread workgroup per image) sorts the (node, feature) keys stably in LDS into
-// the FeatureVector CSR (std::map<NodeId, vector<unsigned>> iteration order), then the
+// k_vocab (two 1024-thread workgroups per image) sorts, in one, the (node, feature) keys into the
+// FeatureVector CSR (std::map<NodeId, vector<unsigned>> iteration order) and, in the other, the
 // (word, feature) keys into the BowVector: per word the weights are added in feature order
-// (addWeight) or the first kept (addIfNotExist); one thread sums the norm in word order, the
-// workgroup divides.
+// (addWeight) or the first kept (addIfNotExist); wave 0 sums the norm in word order, the
+// workgroup divides. The sorts are bitonic in registers (bitonic_reg).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -178,44 +178,101 @@ __global__ __launch_bounds__(256) void k_vocab_descend(VocabArgs a, unsigned lon
   }
 }
 
-// ascending bitonic sort of P2 keys in LDS by the whole workgroup
-__device__ __forceinline__ void bitonic_lds(unsigned long long* skeys, int P2) {
-  const int t = threadIdx.x;
-  for (int k = 2; k <= P2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int pidx = t; pidx < (P2 >> 1); pidx += VOCAB_THREADS) {
-        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
-        const unsigned long long x = skeys[i], y = skeys[ixj];
-        if ((i & k) == 0 ? (x > y) : (x < y)) {
-          skeys[i] = y;
-          skeys[ixj] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
+// Ascending bitonic sort of P2 = 1024 E keys (one or two arrays) held in registers: element
+// e = (wave * E + r) * 64 + lane is register r of that lane, so a wave owns 64 E consecutive keys.
+// Stages with j < 64 swap across lanes (ds_bpermute), 64 <= j < 64 E across a lane's registers,
+// and only j >= 64 E (10 of the 55-78 stages) go through LDS with barriers. The keys come from and
+// return to ka / kb (the LDS arrays the rest of k_vocab reads).
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ unsigned long long cx_keep(unsigned long long me, unsigned long long other, int e, int j,
+                                                      int k) {
+  const bool lower = (e & j) == 0, asc = (e & k) == 0;
+  return (lower == asc) ? (other < me ? other : me) : (other > me ? other : me);
+}
+__device__ __forceinline__ void cx_pair(unsigned long long& lo, unsigned long long& hi, bool asc) {
+  const unsigned long long a = lo, b = hi;
+  const bool sw = asc ? (a > b) : (a < b);
+  lo = sw ? b : a;
+  hi = sw ? a : b;
 }
 
-// Two ascending bitonic sorts of P2 keys each at once, the workgroup's first half on ka, the
-// second on kb: the same stage sequence, so one barrier per stage serves both (half the barriers
-// and stage latencies of two sorts in a row)
-__device__ __forceinline__ void bitonic_lds2(unsigned long long* ka, unsigned long long* kb, int P2) {
-  constexpr int HALF = VOCAB_THREADS / 2;
-  const int t = threadIdx.x & (HALF - 1);
-  unsigned long long* sk = threadIdx.x < HALF ? ka : kb;
+template <int E>
+__device__ __forceinline__ void bitonic_reg(unsigned long long* ka, unsigned long long* kb) {
+  constexpr int P2 = 1024 * E;
+  const int l = lane_id(), w = wave_id();
+  const bool two = kb != nullptr;
+  unsigned long long va[E], vb[E];
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const int e = (w * E + r) * 64 + l;
+    va[r] = ka[e];
+    vb[r] = two ? kb[e] : 0ull;
+  }
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int pidx = t; pidx < (P2 >> 1); pidx += HALF) {
-        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;
-        const unsigned long long x = sk[i], y = sk[ixj];
-        if ((i & k) == 0 ? (x > y) : (x < y)) {
-          sk[i] = y;
-          sk[ixj] = x;
+      if (j >= 64 * E) {  // across waves
+        __syncthreads();  // the previous such stage's partner reads are done
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const int e = (w * E + r) * 64 + l;
+          ka[e] = va[r];
+          if (two) kb[e] = vb[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const int e = (w * E + r) * 64 + l;
+          va[r] = cx_keep(va[r], ka[e ^ j], e, j, k);
+          if (two) vb[r] = cx_keep(vb[r], kb[e ^ j], e, j, k);
+        }
+      } else if (j >= 64) {  // across this lane's registers (static indices per q)
+        const int jr = j >> 6;
+#pragma unroll
+        for (int q = 1; q < E; q <<= 1) {
+          if (jr == q) {
+#pragma unroll
+            for (int r = 0; r < E; r++) {
+              if ((r & q) == 0) {
+                const bool asc = ((((w * E + r) * 64 + l) & k) == 0);
+                cx_pair(va[r], va[r | q], asc);
+                if (two) cx_pair(vb[r], vb[r | q], asc);
+              }
+            }
+          }
+        }
+      } else {  // across lanes
+#pragma unroll
+        for (int r = 0; r < E; r++) {
+          const int e = (w * E + r) * 64 + l;
+          va[r] = cx_keep(va[r], shfl_xor_u64(va[r], j), e, j, k);
+          if (two) vb[r] = cx_keep(vb[r], shfl_xor_u64(vb[r], j), e, j, k);
         }
       }
-      __syncthreads();
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < E; r++) {
+    const int e = (w * E + r) * 64 + l;
+    ka[e] = va[r];
+    if (two) kb[e] = vb[r];
+  }
+  __syncthreads();
+}
+
+// P2 in {1024, 2048, 4096, 8192} (k_vocab pads to at least 1024 keys)
+__device__ __forceinline__ void sort_keys(unsigned long long* ka, unsigned long long* kb, int P2) {
+  if (P2 <= 1024)
+    bitonic_reg<1>(ka, kb);
+  else if (P2 == 2048)
+    bitonic_reg<2>(ka, kb);
+  else if (P2 == 4096)
+    bitonic_reg<4>(ka, kb);
+  else
+    bitonic_reg<8>(ka, kb);
 }
 
 // Starts of the runs of equal key>>32 among the nv sorted valid keys: every thread owns a
@@ -242,6 +299,27 @@ __device__ __forceinline__ int2 run_starts(const unsigned long long* skeys, int 
   return make_int2(pos, runs);
 }
 
+// ((0 + f(v[0])) + f(v[1])) + ... over v[0..nw), f = |x| or x*x, one thread; v is readable and
+// zero from nw to nw + 3H (k_vocab zeroes 128 slots)
+template <bool L2>
+__device__ __forceinline__ double ordered_sum(const double* v, int nw) {
+  constexpr int H = 24;  // words per register set (2 x 24 doubles)
+  double A[H], B[H], s = 0.0;
+#pragma unroll
+  for (int i = 0; i < H; i++) A[i] = v[i];
+  for (int j0 = 0; j0 < nw; j0 += 2 * H) {
+#pragma unroll
+    for (int i = 0; i < H; i++) B[i] = v[j0 + H + i];
+#pragma unroll
+    for (int i = 0; i < H; i++) s += L2 ? A[i] * A[i] : fabs(A[i]);
+#pragma unroll
+    for (int i = 0; i < H; i++) A[i] = v[j0 + 2 * H + i];
+#pragma unroll
+    for (int i = 0; i < H; i++) s += L2 ? B[i] * B[i] : fabs(B[i]);
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsigned long long* fvkeys,
                                                          const unsigned long long* bowkeys,
                                                          const int32_t* leaves) {
@@ -250,37 +328,40 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   __shared__ int s_wsum[VOCAB_THREADS / 64];
   __shared__ double s_norm;
   const int img = blockIdx.x, t = threadIdx.x;
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 5  // phase-cost build: an empty k_vocab
+  return;
+#endif
   const int n = a.empty ? 0 : min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
-  int P2 = 1;
+  int P2 = 1024;  // sort_keys' smallest size: one key per thread
   while (P2 < n) P2 <<= 1;
   const long long kbase = (long long)img * a.cap;
-  // ---- FeatureVector: (node, feature) keys, stable by construction; with the BowVector the
-  //      (word, feature) keys are sorted beside them in bkeys (after the P2 doubles) ----
-  const bool bow = a.bow_words != nullptr;
-  const bool dual = bow && P2 <= 4096;  // the LDS holds 3 P2 entries (launch_vocab)
-  unsigned long long* bkeys = skeys + 2 * P2;
-  for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? fvkeys[kbase + i] : ~0ull;
-  if (dual)
-    for (int i = t; i < P2; i += VOCAB_THREADS) bkeys[i] = i < n ? bowkeys[kbase + i] : ~0ull;
+  // blockIdx.y 0: the FeatureVector from the (node, feature) keys; 1: the BowVector from the
+  // (word, feature) keys -- two workgroups per image, each sorting one key set
+  const bool fv = blockIdx.y == 0;
+  const unsigned long long* src = fv ? fvkeys : bowkeys;
+  for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? src[kbase + i] : ~0ull;
   if (t == 0) s_n = 0;
   __syncthreads();
-  if (dual)
-    bitonic_lds2(skeys, bkeys, P2);
-  else
-    bitonic_lds(skeys, P2);
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 4  // phase-cost build: key loads only
+  return;
+#endif
+  sort_keys(skeys, nullptr, P2);  // stable: the feature index is the low half of every key
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 1  // phase-cost build: loads + sorts only
+  return;
+#endif
   int nvalid = 0;
   for (int i = t; i < n; i += VOCAB_THREADS) nvalid += skeys[i] != ~0ull;
   nvalid = wave_sum(nvalid);
   if (lane_id() == 0) atomicAdd(&s_n, nvalid);
   __syncthreads();
   const int nv = s_n;  // valid keys sort first; the stopped set is the same for both vectors
-  uint32_t* ids = a.node_ids + kbase;
-  int32_t* offs = a.offsets + (long long)img * (a.cap + 1);
-  int32_t* idx = a.indices + kbase;
-  for (int i = t; i < nv; i += VOCAB_THREADS) idx[i] = (int32_t)(skeys[i] & 0xffffffffull);
   const int per = (nv + VOCAB_THREADS - 1) / VOCAB_THREADS;
   const int beg = min(t * per, nv), end = min(beg + per, nv);
-  {
+  if (fv) {
+    uint32_t* ids = a.node_ids + kbase;
+    int32_t* offs = a.offsets + (long long)img * (a.cap + 1);
+    int32_t* idx = a.indices + kbase;
+    for (int i = t; i < nv; i += VOCAB_THREADS) idx[i] = (int32_t)(skeys[i] & 0xffffffffull);
     const int2 pr = run_starts(skeys, nv, beg, end, s_wsum);
     int pos = pr.x;
     for (int i = beg; i < end; i++) {
@@ -294,18 +375,11 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
       offs[pr.y] = nv;
       a.n_nodes[img] = pr.y;
     }
+    return;
   }
-  if (!bow) return;
-  // ---- BowVector: (word, feature) keys (sorted above beside the node keys, or now) ----
-  __syncthreads();
-  if (dual) {
-    for (int i = t; i < nv; i += VOCAB_THREADS) skeys[i] = bkeys[i];
-    __syncthreads();
-  } else {
-    for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? bowkeys[kbase + i] : ~0ull;
-    __syncthreads();
-    bitonic_lds(skeys, P2);
-  }
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 2  // + FeatureVector CSR
+  return;
+#endif
   double* sval = reinterpret_cast<double*>(skeys + P2);
   uint32_t* words = a.bow_words + kbase;
   double* wout = a.bow_weights + kbase;
@@ -326,14 +400,25 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
     pos++;
   }
   __syncthreads();
+  // zero the slots the norm loop reads past nw (up to 128 beyond; the LDS holds P2 + 128 doubles)
+  for (int j = nw + t; j < nw + 128; j += VOCAB_THREADS) sval[j] = 0.0;
+  __syncthreads();
   if (t == 0) {
-    // BowVector::normalize (BowVector.cpp:63-85): the norm accumulates in word order
+    // BowVector::normalize (BowVector.cpp:63-85): the norm accumulates in word order -- one
+    // dependent add per word. Thread 0 reads 32 words ahead from LDS into registers (two
+    // alternating sets), so the chain is one v_add_f64 per word (|w| as a source modifier); the
+    // zero slots past nw add nothing (norm + 0 == norm, norm >= 0).
     double norm = 0.0;
-    if (a.norm_kind == NORM_L1) {
-      for (int j = 0; j < nw; j++) norm += fabs(sval[j]);
-    } else if (a.norm_kind == NORM_L2) {
-      for (int j = 0; j < nw; j++) norm += sval[j] * sval[j];
-      norm = sqrt(norm);
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 3  // everything but the serial norm
+    const bool sum = false;
+#else
+    const bool sum = a.norm_kind == NORM_L1 || a.norm_kind == NORM_L2;
+#endif
+    if (sum) {
+      if (a.norm_kind == NORM_L2)
+        norm = sqrt(ordered_sum<true>(sval, nw));
+      else
+        norm = ordered_sum<false>(sval, nw);
     } else if (a.norm_kind == NORM_DIV_SIZE) {
       norm = (double)nw;  // transform :1176-1182, "unnecessary when normalizing"
     }
@@ -390,9 +475,9 @@ static int vocab_build(orbfe_vocabulary* v, int device) {
   ORBFE_HIP_CHECK(hipMemcpy(v->d_rec, rec.data(), sizeof(VocRec) * rec.size(), hipMemcpyHostToDevice));
   ORBFE_HIP_CHECK(hipMemcpy(v->d_weight, v->weight.data(), sizeof(double) * (size_t)N, hipMemcpyHostToDevice));
   ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
-  // k_vocab holds up to 8192 keys + 8192 weights in LDS (128 KiB of the CU's 160 KiB)
+  // k_vocab holds up to 8192 keys + 8192 + 128 weights in LDS (129 KiB of the CU's 160 KiB)
   ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_vocab, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      2 * sizeof(unsigned long long) * VOCAB_MAX_FEATURES));
+                                      2 * sizeof(unsigned long long) * VOCAB_MAX_FEATURES + 128 * sizeof(double)));
   return ORBFE_OK;
 }
 
@@ -664,11 +749,12 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   unsigned long long* fvk = ks->d_keys;
   unsigned long long* bwk = fvk + slots;
   int32_t* leaves = reinterpret_cast<int32_t*>(bwk + slots);
-  // keys, then (BowVector) P2 doubles and the P2 word keys sorted beside the node keys
-  const size_t lds = sizeof(unsigned long long) * P2 +
-                     (d_bow_words ? (P2 <= 4096 ? 2 : 1) * sizeof(double) * P2 : 0);
+  // P2 keys, then (BowVector workgroups) P2 doubles
+  P2 = P2 < 1024 ? 1024 : P2;  // k_vocab sorts at least 1024 keys
+  const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * (P2 + 128) : 0);
   hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
-  hipLaunchKernelGGL(k_vocab, dim3(n_images), dim3(VOCAB_THREADS), lds, s, a, (const unsigned long long*)fvk,
+  hipLaunchKernelGGL(k_vocab, dim3(n_images, d_bow_words ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
+                     (const unsigned long long*)fvk,
                      (const unsigned long long*)bwk, (const int32_t*)leaves);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;

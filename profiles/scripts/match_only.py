@@ -47,6 +47,24 @@ def main():
     nm = o.nm.cpu().numpy()[:pipe.n_pairs]
     print(f"matching chain ({pairs}): {1e6 * dt:.1f} us per sub-batch, {pipe.n_pairs} pairs, "
           f"{nm.mean():.1f} matches per pair")
+    # SearchForTriangulation alone (k_sft_nodes + k_sft_finish), HIP events per call
+    import ctypes
+    from orb_slam2_2021_amd import _lib as L
+    lib = L.lib()
+    ts = []
+    for r in range(reps + 3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(m)
+        L.check(lib.orbfe_search_for_triangulation_batch_device(
+            o.matcher._h, pipe.n_pairs, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
+            "sft batch")
+        b.record(m)
+        if r >= 3:
+            ts.append((a, b))
+    torch.cuda.synchronize()
+    us = [1e3 * a.elapsed_time(b) for a, b in ts]
+    print(f"SearchForTriangulation x{pipe.n_pairs}: {np.median(us):.1f} us per call (median of {reps}), "
+          f"min {min(us):.1f}")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 # Ablation (timing only, outputs wrong): the bench line with k_blur skipped (abl1), k_copy0 skipped
 # (abl2), matching skipped (--diag-skip-matching), against the full pipeline, interleaved.
+# builds: bash profiles/scripts/build_variant.sh abl1 -DORBFE_DIAG_SKIP=1; ... abl2 -DORBFE_DIAG_SKIP=2
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 B="timeout -k 10 200 python bench.py --no-cpu --no-legs --no-parity --steps 3 --warmup 1"

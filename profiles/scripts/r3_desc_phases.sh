@@ -1,5 +1,6 @@
 # k_describe phase costs (diagnostic builds -DORBFE_DESC_DIAG=1: window loads only, 2: + IC_Angle,
 # fastAtan2, cos/sin; wrong descriptors) against the full kernel, extraction alone.
+# builds: bash profiles/scripts/build_variant.sh dd1 -DORBFE_DESC_DIAG=1; ... dd2 -DORBFE_DESC_DIAG=2
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 X="timeout -k 10 120 python profiles/scripts/extract_only.py 20 --per-kernel --seq"

@@ -1,3 +1,4 @@
+# builds: bash profiles/scripts/build_variant.sh d1 -DORBFE_FAST_DIAG=1 (and d2, d3)
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 X="timeout -k 10 120 python profiles/scripts/extract_only.py 20 --per-kernel --seq"

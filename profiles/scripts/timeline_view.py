@@ -15,3 +15,20 @@ print("sub-batch periods (k_sft_nodes starts, us):", [round((sft[i + 1][0] - sft
 for s, e, n, q in ev:
     if t0 <= s <= t1:
         print(f"{(s - t0) / 1e3:8.1f} {(e - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  q{q:>3s}  {n}")
+# busy fraction of each queue over the window (union of its kernels' intervals)
+busy = {}
+for s, e, n, q in ev:
+    if t0 <= s <= t1:
+        busy.setdefault(q, []).append((s, min(e, t1)))
+for q, iv in sorted(busy.items()):
+    iv.sort()
+    tot, cs, ce = 0, None, None
+    for s, e in iv:
+        if cs is None or s > ce:
+            if cs is not None:
+                tot += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    tot += ce - cs
+    print(f"queue {q}: busy {100 * tot / (t1 - t0):.0f} % of the {(t1 - t0) / 1e3:.0f} us window")
