@@ -59,23 +59,46 @@ struct SftCand {
   bool usable, stereo;   // usable: in range, no MapPoint, stereo if bOnlyStereo
 };
 
+// Per-octave thresholds of KF2, lane l holding octave l (read with a lane shuffle, no dependent
+// global load per candidate)
+struct SftOctTab {
+  float epi;   // 100 * mvScaleFactors[o] (:761)
+  double sig;  // 3.84 * mvLevelSigma2[o] (:162)
+};
+__device__ __forceinline__ SftOctTab sft_oct_tab(const orbfe_sft_pair& P) {
+  const int lane = lane_id();
+  SftOctTab t;
+  t.epi = lane < P.kf2.nlevels ? 100 * P.kf2.scale_factors[lane] : 0.f;
+  t.sig = lane < P.kf2.nlevels ? 3.84 * (double)P.kf2.level_sigma2[lane] : 0.0;
+  return t;
+}
+
+// All of a candidate's loads are issued together (index, then MapPoint state, uRight, keypoint
+// and descriptor at once): two dependent rounds.
 __device__ __forceinline__ void sft_load_cand(const orbfe_sft_pair& P, int o2, int n2, int p,
-                                              int only_stereo, SftCand& c) {
+                                              int only_stereo, const SftOctTab& tab, SftCand& c) {
   c.usable = false;
+  c.stereo = false;
   c.idx2 = -1;
-  if (p >= n2) return;
-  const int idx2 = P.fv2.indices[o2 + p];
-  c.idx2 = idx2;
-  if (P.kf2.mp_state[idx2] != ORBFE_MP_NONE) return;
-  c.stereo = P.kf2.u_right[idx2] >= 0;
-  if (only_stereo && !c.stereo) return;
-  const orbfe_keypoint kp2 = P.kf2.keys_un[idx2];
-  load_desc(P.kf2.descriptors + (size_t)idx2 * 32, c.d0, c.d1);
-  c.x = kp2.x;
-  c.y = kp2.y;
-  c.epi_thr = 100 * P.kf2.scale_factors[kp2.octave];
-  c.sig_thr = 3.84 * (double)P.kf2.level_sigma2[kp2.octave];
-  c.usable = true;
+  c.x = c.y = c.epi_thr = 0.f;
+  c.sig_thr = 0.0;
+  c.d0 = c.d1 = make_uint4(0, 0, 0, 0);
+  int oct = 0;
+  if (p < n2) {
+    const int idx2 = P.fv2.indices[o2 + p];
+    const uint8_t mp = P.kf2.mp_state[idx2];
+    const float ur = P.kf2.u_right[idx2];
+    const orbfe_keypoint kp2 = P.kf2.keys_un[idx2];
+    load_desc(P.kf2.descriptors + (size_t)idx2 * 32, c.d0, c.d1);
+    c.idx2 = idx2;
+    c.stereo = ur >= 0;
+    c.usable = mp == ORBFE_MP_NONE && !(only_stereo && !c.stereo);
+    c.x = kp2.x;
+    c.y = kp2.y;
+    oct = kp2.octave;
+  }
+  c.epi_thr = __shfl(tab.epi, oct, 64);
+  c.sig_thr = __shfl(tab.sig, oct, 64);
 }
 
 // Key of a passing candidate: smallest distance, then the LAST position (ties replace, :752).
@@ -97,35 +120,36 @@ __device__ __forceinline__ unsigned long long sft_key(const SftCand& c, bool cla
   return ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
 }
 
-// Nodes with at most SFT_FP_MAX features on each side: lanes take KF1 features (two per lane),
-// every lane finds its passing KF2 candidates once (dist <= TH_LOW, the epipole and epipolar
-// checks: the candidate set S_i of the reference loop), then the claim order of :772-777 is
-// solved as a fixpoint -- choice(i) = best of S_i minus the choices of features before i in the
-// node -- iterated from "no claims" until a round reproduces the previous one. That fixpoint is
-// unique and equals the sequential result (feature i's choice is final once those before it are).
-#define SFT_FP_MAX 128
+// Nodes with at most 64 K features on each side (K = 2, or 4 up to SFT_FP_MAX): lanes take KF1
+// features (K per lane), every lane finds its passing KF2 candidates once (dist <= TH_LOW, the
+// epipole and epipolar checks: the candidate set S_i of the reference loop), then the claim order
+// of :772-777 is solved as a fixpoint -- choice(i) = best of S_i minus the choices of features
+// before i in the node -- iterated from "no claims" until a round reproduces the previous one.
+// That fixpoint is unique and equals the sequential result (feature i's choice is final once
+// those before it are).
+#define SFT_FP_MAX 256
+template <int K>
 __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o1, int n1, int o2, int n2,
                                                   int only_stereo, uint32_t* cdesc, int* claim) {
   const int lane = lane_id();
-  // candidates: lane p (and 64 + p) loads KF2 feature p of the node; descriptors go to LDS
-  SftCand c0, c1;
-  sft_load_cand(P, o2, n2, lane, only_stereo, c0);
-  sft_load_cand(P, o2, n2, 64 + lane, only_stereo, c1);
-  if (lane < n2) {
-    *reinterpret_cast<uint4*>(cdesc + 8 * lane) = c0.d0;
-    *reinterpret_cast<uint4*>(cdesc + 8 * lane + 4) = c0.d1;
-  }
-  if (64 + lane < n2) {
-    *reinterpret_cast<uint4*>(cdesc + 8 * (64 + lane)) = c1.d0;
-    *reinterpret_cast<uint4*>(cdesc + 8 * (64 + lane) + 4) = c1.d1;
-  }
-  // KF1 features i = lane and 64 + lane
-  int idx1[2];
-  bool ok1[2], st1[2];
-  float x1[2], y1[2];
-  uint4 a0[2], a1[2];
+  // candidates: lane p (and 64 h + p) loads KF2 feature p of the node; descriptors go to LDS
+  const SftOctTab tab = sft_oct_tab(P);
+  SftCand c[K];
 #pragma unroll
-  for (int k = 0; k < 2; k++) {
+  for (int h = 0; h < K; h++) {
+    sft_load_cand(P, o2, n2, 64 * h + lane, only_stereo, tab, c[h]);
+    if (64 * h + lane < n2) {
+      *reinterpret_cast<uint4*>(cdesc + 8 * (64 * h + lane)) = c[h].d0;
+      *reinterpret_cast<uint4*>(cdesc + 8 * (64 * h + lane) + 4) = c[h].d1;
+    }
+  }
+  // KF1 features i = 64 k + lane
+  int idx1[K];
+  bool ok1[K], st1[K];
+  float x1[K], y1[K];
+  uint4 a0[K], a1[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
     const int i = 64 * k + lane;
     idx1[k] = -1;
     ok1[k] = false;
@@ -144,105 +168,119 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
   }
   wave_sync();
 #if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 1  // phase-cost build: loads only (no matches)
-  if (lane < n1) P.match12[idx1[0]] = -1;
-  if (64 + lane < n1) P.match12[idx1[1]] = -1;
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    if (64 * k + lane < n1) P.match12[idx1[k]] = -1;
   return;
 #endif
   const float* F = P.f12;
   const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
               f7 = F[7], f8 = F[8];
-  float la[2], lb[2], lc[2], den[2];
+  float la[K], lb[K], lc[K], den[K];
 #pragma unroll
-  for (int k = 0; k < 2; k++) {  // epipolar line l = x1' F12 (CheckDistEpipolarLine :149-151)
+  for (int k = 0; k < K; k++) {  // epipolar line l = x1' F12 (CheckDistEpipolarLine :149-151)
     la[k] = x1[k] * f0 + y1[k] * f3 + f6;
     lb[k] = x1[k] * f1 + y1[k] * f4 + f7;
     lc[k] = x1[k] * f2 + y1[k] * f5 + f8;
     den[k] = la[k] * la[k] + lb[k] * lb[k];
   }
-  // 1. passing sets (bit p of pm[k][p >> 6]) and the round-0 choice (no claims)
-  uint64_t pm00 = 0, pm01 = 0, pm10 = 0, pm11 = 0;  // pm<k><h>: bit p - 64 h of feature 64 k + lane
-  unsigned long long best0 = ~0ull, best1 = ~0ull;
-  for (int p = 0; p < n2; p++) {
-    const int src = p & 63;
-    const bool hi = p >= 64;
-    SftCand c;  // candidate p broadcast from its lane (scalar registers)
-    c.usable = __builtin_amdgcn_readlane((int)(hi ? c1.usable : c0.usable), src) != 0;
-    if (!c.usable) continue;  // uniform
-    c.stereo = __builtin_amdgcn_readlane((int)(hi ? c1.stereo : c0.stereo), src) != 0;
-    c.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.x : c0.x), src));
-    c.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.y : c0.y), src));
-    c.epi_thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi ? c1.epi_thr : c0.epi_thr), src));
-    const long long sb = __double_as_longlong(hi ? c1.sig_thr : c0.sig_thr);
-    c.sig_thr = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(sb >> 32), src) << 32) |
-                                     (unsigned)__builtin_amdgcn_readlane((int)(sb & 0xffffffff), src));
-    c.d0 = *reinterpret_cast<const uint4*>(cdesc + 8 * p);
-    c.d1 = *reinterpret_cast<const uint4*>(cdesc + 8 * p + 4);
-    const uint64_t bit = 1ull << (p & 63);
-    if (ok1[0]) {
-      const unsigned long long key = sft_key(c, false, p, a0[0], a1[0], st1[0], P.ex, P.ey, la[0], lb[0], lc[0], den[0]);
-      if (key != ~0ull) {
-        if (hi) pm01 |= bit;
-        else pm00 |= bit;
-        best0 = key < best0 ? key : best0;
-      }
-    }
-    if (ok1[1]) {
-      const unsigned long long key = sft_key(c, false, p, a0[1], a1[1], st1[1], P.ex, P.ey, la[1], lb[1], lc[1], den[1]);
-      if (key != ~0ull) {
-        if (hi) pm11 |= bit;
-        else pm10 |= bit;
-        best1 = key < best1 ? key : best1;
+  // 1. passing sets (bit p - 64 h of pm[k][h] for feature 64 k + lane) and the round-0 choice
+  const int kact = (n1 + 63) >> 6;
+  uint64_t pm[K][K];
+  unsigned long long best[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    best[k] = ~0ull;
+#pragma unroll
+    for (int h = 0; h < K; h++) pm[k][h] = 0;
+  }
+#pragma unroll
+  for (int h = 0; h < K; h++) {
+    const int pend = min(n2, 64 * (h + 1));
+    for (int p = 64 * h; p < pend; p++) {
+      const int src = p & 63;
+      SftCand cb;  // candidate p broadcast from its lane (scalar registers)
+      cb.usable = __builtin_amdgcn_readlane((int)c[h].usable, src) != 0;
+      if (!cb.usable) continue;  // uniform
+      cb.stereo = __builtin_amdgcn_readlane((int)c[h].stereo, src) != 0;
+      cb.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c[h].x), src));
+      cb.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c[h].y), src));
+      cb.epi_thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c[h].epi_thr), src));
+      const long long sb = __double_as_longlong(c[h].sig_thr);
+      cb.sig_thr = __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(sb >> 32), src) << 32) |
+                                        (unsigned)__builtin_amdgcn_readlane((int)(sb & 0xffffffff), src));
+      cb.d0.x = __builtin_amdgcn_readlane(c[h].d0.x, src);
+      cb.d0.y = __builtin_amdgcn_readlane(c[h].d0.y, src);
+      cb.d0.z = __builtin_amdgcn_readlane(c[h].d0.z, src);
+      cb.d0.w = __builtin_amdgcn_readlane(c[h].d0.w, src);
+      cb.d1.x = __builtin_amdgcn_readlane(c[h].d1.x, src);
+      cb.d1.y = __builtin_amdgcn_readlane(c[h].d1.y, src);
+      cb.d1.z = __builtin_amdgcn_readlane(c[h].d1.z, src);
+      cb.d1.w = __builtin_amdgcn_readlane(c[h].d1.w, src);
+      const uint64_t bit = 1ull << src;
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if (k < kact && ok1[k]) {  // kact: uniform, skips the chunks no KF1 feature fills
+          const unsigned long long key = sft_key(cb, false, p, a0[k], a1[k], st1[k], P.ex, P.ey, la[k], lb[k],
+                                                 lc[k], den[k]);
+          if (key != ~0ull) {
+            pm[k][h] |= bit;
+            best[k] = key < best[k] ? key : best[k];
+          }
+        }
       }
     }
   }
-  int ch[2];
-  ch[0] = best0 == ~0ull ? -1 : 0x7fffffff - (int)(best0 & 0xffffffffull);
-  ch[1] = best1 == ~0ull ? -1 : 0x7fffffff - (int)(best1 & 0xffffffffull);
-  // 2. rounds: claim[p] = first feature choosing p; re-choose among the unclaimed-by-earlier
-  auto rechoose = [&](int i, uint64_t m0, uint64_t m1, const uint4& q0, const uint4& q1) -> int {
-    unsigned long long b = ~0ull;
-    for (int h = 0; h < 2; h++) {
-      uint64_t m = h == 0 ? m0 : m1;
-      while (m) {
-        const int p = 64 * h + __builtin_ctzll(m);
-        m &= m - 1;
-        if (claim[p] < i) continue;  // vbMatched2: taken by an earlier feature of the node
-        const uint4 d0 = *reinterpret_cast<const uint4*>(cdesc + 8 * p);
-        const uint4 d1 = *reinterpret_cast<const uint4*>(cdesc + 8 * p + 4);
-        const unsigned long long key = ((unsigned long long)hamming256(q0, q1, d0, d1) << 32) |
-                                       (unsigned long long)(0x7fffffff - p);
-        b = key < b ? key : b;
-      }
-    }
-    return b == ~0ull ? -1 : 0x7fffffff - (int)(b & 0xffffffffull);
-  };
-  int chA = ch[0], chB = ch[1];
-  const uint4 qa0 = a0[0], qa1 = a1[0], qb0 = a0[1], qb1 = a1[1];
+  int ch[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) ch[k] = best[k] == ~0ull ? -1 : 0x7fffffff - (int)(best[k] & 0xffffffffull);
 #if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 2  // + passing sets (round-0 choices, unresolved)
-  if (lane < n1) P.match12[idx1[0]] = chA >= 0 ? P.fv2.indices[o2 + chA] : -1;
-  if (64 + lane < n1) P.match12[idx1[1]] = chB >= 0 ? P.fv2.indices[o2 + chB] : -1;
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
   return;
 #endif
+  // 2. rounds: claim[p] = first feature choosing p; re-choose among the unclaimed-by-earlier
   for (int round = 0; round <= n1; round++) {
     for (int p = lane; p < n2; p += 64) claim[p] = 0x7fffffff;
     wave_sync();
-    if (chA >= 0) atomicMin(&claim[chA], lane);
-    if (chB >= 0) atomicMin(&claim[chB], 64 + lane);
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if (ch[k] >= 0) atomicMin(&claim[ch[k]], 64 * k + lane);
     wave_sync();
-    const int nA = rechoose(lane, pm00, pm01, qa0, qa1);
-    const int nB = rechoose(64 + lane, pm10, pm11, qb0, qb1);
-    const bool changed = nA != chA || nB != chB;
-    chA = nA;
-    chB = nB;
+    bool changed = false;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const int i = 64 * k + lane;
+      unsigned long long b = ~0ull;
+#pragma unroll
+      for (int h = 0; h < K; h++) {
+        uint64_t m = pm[k][h];
+        while (m) {
+          const int p = 64 * h + __builtin_ctzll(m);
+          m &= m - 1;
+          if (claim[p] < i) continue;  // vbMatched2: taken by an earlier feature of the node
+          const uint4 d0 = *reinterpret_cast<const uint4*>(cdesc + 8 * p);
+          const uint4 d1 = *reinterpret_cast<const uint4*>(cdesc + 8 * p + 4);
+          const unsigned long long key = ((unsigned long long)hamming256(a0[k], a1[k], d0, d1) << 32) |
+                                         (unsigned long long)(0x7fffffff - p);
+          b = key < b ? key : b;
+        }
+      }
+      const int nk = b == ~0ull ? -1 : 0x7fffffff - (int)(b & 0xffffffffull);
+      changed = changed || nk != ch[k];
+      ch[k] = nk;
+    }
     if (wave_ballot(changed) == 0) break;
     wave_sync();  // claim[] is rewritten by the next round
   }
   // every feature of the node gets its final value (-1: no match), written once
-  if (lane < n1) P.match12[idx1[0]] = chA >= 0 ? P.fv2.indices[o2 + chA] : -1;
-  if (64 + lane < n1) P.match12[idx1[1]] = chB >= 0 ? P.fv2.indices[o2 + chB] : -1;
+#pragma unroll
+  for (int k = 0; k < K; k++)
+    if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
 }
 
-__global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
   __shared__ uint32_t s_claim_far[4][SFT_MAX_NODE / 32];  // claims beyond the register chunks
   __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];        // fixpoint path: node candidates
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
@@ -299,8 +337,12 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
 #if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 5  // + node lookup (match12 of the node's features unwritten)
   if (n2 >= 0) return;
 #endif
+  if (e1 - o1 <= 128 && n2 <= 128) {
+    sft_node_fixpoint<2>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
+    return;
+  }
   if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
-    sft_node_fixpoint(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
+    sft_node_fixpoint<4>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
   // large nodes: -1 first, stored before the walk's matches overwrite some of them (the wait
@@ -310,11 +352,12 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
   uint32_t* far = s_claim_far[w];
   if (n2 > SFT_REG_CHUNKS * 64)
     for (int i = lane; i < (n2 + 31) / 32; i += 64) far[i] = 0;
+  const SftOctTab tab = sft_oct_tab(P);
   SftCand c0, c1, c2, c3;
-  sft_load_cand(P, o2, n2, lane, only_stereo, c0);
-  sft_load_cand(P, o2, n2, 64 + lane, only_stereo, c1);
-  sft_load_cand(P, o2, n2, 128 + lane, only_stereo, c2);
-  sft_load_cand(P, o2, n2, 192 + lane, only_stereo, c3);
+  sft_load_cand(P, o2, n2, lane, only_stereo, tab, c0);
+  sft_load_cand(P, o2, n2, 64 + lane, only_stereo, tab, c1);
+  sft_load_cand(P, o2, n2, 128 + lane, only_stereo, tab, c2);
+  sft_load_cand(P, o2, n2, 192 + lane, only_stereo, tab, c3);
   bool cl0 = false, cl1 = false, cl2 = false, cl3 = false;
   const float* F = P.f12;
   const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
@@ -377,7 +420,7 @@ __global__ __launch_bounds__(256) void k_sft_nodes(const orbfe_sft_pair* pairs, 
     for (int cbase = SFT_REG_CHUNKS * 64; cbase < n2; cbase += 64) {  // very large nodes
       SftCand cx;
       const int p = cbase + lane;
-      sft_load_cand(P, o2, n2, p, only_stereo, cx);
+      sft_load_cand(P, o2, n2, p, only_stereo, tab, cx);
       const bool clx = p < n2 && ((far[p >> 5] >> (p & 31)) & 1u);
       k = sft_key(cx, clx, p, a0, a1, st1, P.ex, P.ey, la, lb, lc, den);
       best = k < best ? k : best;

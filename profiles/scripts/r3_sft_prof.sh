@@ -4,6 +4,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/sft_prof -o run --output-format csv -- python3 profiles/scripts/match_only.py 100 > gpurun_out/sft_prof.log 2>&1 &&
-for v in 1 3 4 5; do
+for v in 1 2; do
   ORBFE_LIB=orb_slam2_2021_amd/lib/sd$v/liborbfe.so timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/sft_prof$v -o run --output-format csv -- python3 profiles/scripts/match_only.py 100 > gpurun_out/sft_prof$v.log 2>&1 || exit 1
 done
