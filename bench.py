@@ -120,6 +120,9 @@ def parse(argv=None):
                    help="diagnostic: the pipeline's streams from torch's pool, created after the "
                         "handles (hardware-queue assignment then depends on the stream count; with "
                         "several extractors their side work runs inline)")
+    p.add_argument("--stagger", action="store_true",
+                   help="each sub-batch's extraction waits for the previous sub-batch's pyramid (the handles' "
+                        "pyramid chains never overlap)")
     p.add_argument("--stereo-on-extract", action="store_true",
                    help="ComputeStereoMatches on the extraction stream right after each extraction (rounds 1-3's "
                         "placement; default: on the matching stream ahead of the vocabulary, with two handles per "
@@ -308,7 +311,7 @@ def main():
                            depth=pipe_depth(args), defer=args.defer_matching,
                            stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs,
-                           stereo_on_match=not args.stereo_on_extract)
+                           stereo_on_match=not args.stereo_on_extract, stagger=args.stagger)
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream

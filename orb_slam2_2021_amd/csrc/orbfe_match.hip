@@ -127,7 +127,13 @@ __device__ __forceinline__ unsigned long long sft_key(const SftCand& c, bool cla
 // before i in the node -- iterated from "no claims" until a round reproduces the previous one.
 // That fixpoint is unique and equals the sequential result (feature i's choice is final once
 // those before it are).
-#define SFT_FP_MAX 256
+// 128 (K = 2 only) by default: the K = 4 build's 44 KiB of LDS per workgroup (vs 26 KiB) keeps
+// DistributeOctTree's 80 KiB blocks off the CUs it occupies when the matching stream runs beside
+// the extraction (measured 73.1k vs 78.5k stereo frames/s), though it runs alone in 49 vs ~70 us
+// when a node holds 129-256 features
+#ifndef SFT_FP_MAX
+#define SFT_FP_MAX 128
+#endif
 template <int K>
 __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o1, int n1, int o2, int n2,
                                                   int only_stereo, uint32_t* cdesc, int* claim) {
@@ -280,7 +286,10 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
+#ifndef ORBFE_SFT_WPE
+#define ORBFE_SFT_WPE 4
+#endif
+__global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
   __shared__ uint32_t s_claim_far[4][SFT_MAX_NODE / 32];  // claims beyond the register chunks
   __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];        // fixpoint path: node candidates
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
@@ -341,10 +350,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     sft_node_fixpoint<2>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
+#if SFT_FP_MAX > 128
   if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
     sft_node_fixpoint<4>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
+#endif
   // large nodes: -1 first, stored before the walk's matches overwrite some of them (the wait
   // orders the two stores to one address from different lanes)
   for (int i = o1 + lane; i < e1; i += 64) P.match12[P.fv1.indices[i]] = -1;

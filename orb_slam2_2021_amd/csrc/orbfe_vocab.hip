@@ -263,8 +263,32 @@ __device__ __forceinline__ void bitonic_reg(unsigned long long* ka, unsigned lon
   __syncthreads();
 }
 
+// ascending bitonic sort of P2 keys through LDS, one compare-exchange per thread per stage
+// (rounds 1-3's sort; ORBFE_VOCAB_LDS_SORT selects it)
+__device__ __forceinline__ void bitonic_lds(unsigned long long* skeys, int P2) {
+  const int t = threadIdx.x;
+  for (int k = 2; k <= P2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int pidx = t; pidx < (P2 >> 1); pidx += VOCAB_THREADS) {
+        const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
+        const unsigned long long x = skeys[i], y = skeys[ixj];
+        if ((i & k) == 0 ? (x > y) : (x < y)) {
+          skeys[i] = y;
+          skeys[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // P2 in {1024, 2048, 4096, 8192} (k_vocab pads to at least 1024 keys)
 __device__ __forceinline__ void sort_keys(unsigned long long* ka, unsigned long long* kb, int P2) {
+#if defined(ORBFE_VOCAB_LDS_SORT) && ORBFE_VOCAB_LDS_SORT
+  bitonic_lds(ka, P2);
+  if (kb) bitonic_lds(kb, P2);
+  return;
+#endif
   if (P2 <= 1024)
     bitonic_reg<1>(ka, kb);
   else if (P2 == 2048)
@@ -301,9 +325,12 @@ __device__ __forceinline__ int2 run_starts(const unsigned long long* skeys, int 
 
 // ((0 + f(v[0])) + f(v[1])) + ... over v[0..nw), f = |x| or x*x, one thread; v is readable and
 // zero from nw to nw + 3H (k_vocab zeroes 128 slots)
+#ifndef ORBFE_VOCAB_NORM_H
+#define ORBFE_VOCAB_NORM_H 16
+#endif
 template <bool L2>
 __device__ __forceinline__ double ordered_sum(const double* v, int nw) {
-  constexpr int H = 24;  // words per register set (2 x 24 doubles)
+  constexpr int H = ORBFE_VOCAB_NORM_H;  // words per register set (2 H doubles)
   double A[H], B[H], s = 0.0;
 #pragma unroll
   for (int i = 0; i < H; i++) A[i] = v[i];
@@ -320,27 +347,17 @@ __device__ __forceinline__ double ordered_sum(const double* v, int nw) {
   return s;
 }
 
-__global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsigned long long* fvkeys,
-                                                         const unsigned long long* bowkeys,
-                                                         const int32_t* leaves) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];  // P2 keys, then P2 doubles
-  __shared__ int s_n;
-  __shared__ int s_wsum[VOCAB_THREADS / 64];
-  __shared__ double s_norm;
-  const int img = blockIdx.x, t = threadIdx.x;
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 5  // phase-cost build: an empty k_vocab
-  return;
-#endif
-  const int n = a.empty ? 0 : min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
-  int P2 = 1024;  // sort_keys' smallest size: one key per thread
-  while (P2 < n) P2 <<= 1;
+// One vector of one image: fv -- the FeatureVector from the (node, feature) keys; else the
+// BowVector from the (word, feature) keys. skeys: P2 keys, then P2 + 128 doubles.
+__device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img, int n, int P2,
+                                           const unsigned long long* fvkeys,
+                                           const unsigned long long* bowkeys, const int32_t* leaves,
+                                           unsigned long long* skeys, int* s_n, int* s_wsum, double* s_norm) {
+  const int t = threadIdx.x;
   const long long kbase = (long long)img * a.cap;
-  // blockIdx.y 0: the FeatureVector from the (node, feature) keys; 1: the BowVector from the
-  // (word, feature) keys -- two workgroups per image, each sorting one key set
-  const bool fv = blockIdx.y == 0;
   const unsigned long long* src = fv ? fvkeys : bowkeys;
   for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? src[kbase + i] : ~0ull;
-  if (t == 0) s_n = 0;
+  if (t == 0) *s_n = 0;
   __syncthreads();
 #if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 4  // phase-cost build: key loads only
   return;
@@ -352,9 +369,9 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   int nvalid = 0;
   for (int i = t; i < n; i += VOCAB_THREADS) nvalid += skeys[i] != ~0ull;
   nvalid = wave_sum(nvalid);
-  if (lane_id() == 0) atomicAdd(&s_n, nvalid);
+  if (lane_id() == 0) atomicAdd(s_n, nvalid);
   __syncthreads();
-  const int nv = s_n;  // valid keys sort first; the stopped set is the same for both vectors
+  const int nv = *s_n;  // valid keys sort first; the stopped set is the same for both vectors
   const int per = (nv + VOCAB_THREADS - 1) / VOCAB_THREADS;
   const int beg = min(t * per, nv), end = min(beg + per, nv);
   if (fv) {
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   __syncthreads();
   if (t == 0) {
     // BowVector::normalize (BowVector.cpp:63-85): the norm accumulates in word order -- one
-    // dependent add per word. Thread 0 reads 32 words ahead from LDS into registers (two
+    // dependent add per word. Thread 0 reads the words ahead from LDS into registers (two
     // alternating sets), so the chain is one v_add_f64 per word (|w| as a source modifier); the
     // zero slots past nw add nothing (norm + 0 == norm, norm >= 0).
     double norm = 0.0;
@@ -422,13 +439,43 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
     } else if (a.norm_kind == NORM_DIV_SIZE) {
       norm = (double)nw;  // transform :1176-1182, "unnecessary when normalizing"
     }
-    s_norm = norm;
+    *s_norm = norm;
     a.bow_n[img] = nw;
   }
   __syncthreads();
-  const double norm = s_norm;
+  const double norm = *s_norm;
   const bool divide = a.norm_kind != NORM_NONE && norm > 0.0;
   for (int j = t; j < nw; j += VOCAB_THREADS) wout[j] = divide ? sval[j] / norm : sval[j];
+}
+
+// ORBFE_VOCAB_SPLIT 1: two workgroups per image (blockIdx.y 0: FeatureVector, 1: BowVector);
+// 0: one workgroup per image doing both in turn
+#ifndef ORBFE_VOCAB_SPLIT
+#define ORBFE_VOCAB_SPLIT 1
+#endif
+__global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsigned long long* fvkeys,
+                                                         const unsigned long long* bowkeys,
+                                                         const int32_t* leaves) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];  // P2 keys, then P2 + 128 doubles
+  __shared__ int s_n;
+  __shared__ int s_wsum[VOCAB_THREADS / 64];
+  __shared__ double s_norm;
+  const int img = blockIdx.x;
+#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 5  // phase-cost build: an empty k_vocab
+  return;
+#endif
+  const int n = a.empty ? 0 : min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
+  int P2 = 1024;  // sort_keys' smallest size: one key per thread
+  while (P2 < n) P2 <<= 1;
+  if (ORBFE_VOCAB_SPLIT) {
+    vocab_part(a, blockIdx.y == 0, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
+  } else {
+    vocab_part(a, true, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
+    if (a.bow_words != nullptr) {
+      __syncthreads();
+      vocab_part(a, false, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -753,7 +800,7 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   P2 = P2 < 1024 ? 1024 : P2;  // k_vocab sorts at least 1024 keys
   const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * (P2 + 128) : 0);
   hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
-  hipLaunchKernelGGL(k_vocab, dim3(n_images, d_bow_words ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
+  hipLaunchKernelGGL(k_vocab, dim3(n_images, d_bow_words && ORBFE_VOCAB_SPLIT ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
                      (const unsigned long long*)fvk,
                      (const unsigned long long*)bwk, (const int32_t*)leaves);
   ORBFE_HIP_CHECK(hipGetLastError());

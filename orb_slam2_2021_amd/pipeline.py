@@ -134,7 +134,7 @@ class C3Pipeline:
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
                  nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
                  vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
-                 stereo_on_match: bool = False):
+                 stereo_on_match: bool = False, stagger: bool = False):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -279,6 +279,10 @@ class C3Pipeline:
         self.stereo_on_match = stereo and stereo_on_match and not (self.match_inline or defer or vocab_side
                                                                    or vocab_inline)
         self.stereo_done = [None] * len(self.exts)
+        # stagger: sub-batch i's extraction starts once sub-batch i-1's pyramid is built, so the
+        # handles' latency-bound pyramid chains never run at the same time
+        self.stagger = stagger
+        self.prev_ext = None
         # optional HIP events around the vocabulary / matching / stereo launches
         self.event_sel = set()
         self.events = {"k_vocab": [], "k_sft": [], "k_stereo": []}
@@ -304,8 +308,11 @@ class C3Pipeline:
             # ComputeStereoMatches of this handle's previous sub-batch (matching stream) read the
             # pyramids this extraction overwrites
             s.wait_event(self.stereo_done[k])
+        if self.stagger and self.prev_ext is not None and self.prev_ext is not ext:
+            self.prev_ext.wait_pyramid(s.cuda_stream)
         ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
                                       o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
+        self.prev_ext = ext
         o.ext = ext
         o.k = k
         if self.stereo and not self.stereo_on_match:  # Frame.cc:125, on the extraction stream
@@ -450,7 +457,7 @@ STEP_Z = 1.0  # metres between consecutive frames of the C3 driving sequence (SU
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
              stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
              vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
-             stereo_on_match: bool = False):
+             stereo_on_match: bool = False, stagger: bool = False):
     """The C3 scene of bench.py: KITTI intrinsics, seeded KeyFrame state per keypoint slot (half
     the keypoints stereo unless ComputeStereoMatches provides mvuRight, 30 % with a MapPoint), and
     the KeyFrame pair geometry with F12 and epipole from LocalMapping::ComputeF12
@@ -482,7 +489,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
                       vocab_inline=vocab_inline, vocab_side=vocab_side, pairs=pairs,
-                      stereo_on_match=stereo_on_match)
+                      stereo_on_match=stereo_on_match, stagger=stagger)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo, pairs=pairs)
     return pipe, state
