@@ -2535,6 +2535,9 @@ static bool plan_pyramid(const std::vector<LevelDesc>& lv, const std::vector<int
   return true;
 }
 
+#ifndef ORBFE_OCT_LDS_KB
+#define ORBFE_OCT_LDS_KB 80  // k_octree's LDS per workgroup (two per CU)
+#endif
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   if (h->rows == rows && h->cols == cols && h->geom_mode == h->resize_mode) return ORBFE_OK;
   const int L = h->nlevels;
@@ -2771,7 +2774,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   // blocks share a CU; larger levels use the global scratch path
   const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * h->scan_cap +
                        sizeof(unsigned long long) * sc + sizeof(int) * 16;
-  h->key_lds_cap = fixed < 80 * 1024 ? (int)((80 * 1024 - fixed) / 8) & ~63 : 0;
+  const size_t oct_lds = (size_t)ORBFE_OCT_LDS_KB * 1024;
+  h->key_lds_cap = fixed < oct_lds ? (int)((oct_lds - fixed) / 8) & ~63 : 0;
   if (h->octree_key_cap_override >= 0) h->key_lds_cap = std::min(h->key_lds_cap, h->octree_key_cap_override);
   h->rows = rows;
   h->cols = cols;

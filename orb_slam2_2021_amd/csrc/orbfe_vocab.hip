@@ -22,7 +22,7 @@
 // k=10), popcount the xor, and a 16-lane min of (distance << 23 | sibling) picks the first best
 // child together with everything the next level needs.
 //
-// k_vocab (two 1024-thread workgroups per image) sorts, in one, the (node, feature) keys into the
+// k_vocab (two workgroups per image, VOCAB_THREADS each) sorts, in one, the (node, feature) keys into the
 // FeatureVector CSR (std::map<NodeId, vector<unsigned>> iteration order) and, in the other, the
 // (word, feature) keys into the BowVector: per word the weights are added in feature order
 // (addWeight) or the first kept (addIfNotExist); wave 0 sums the norm in word order, the
@@ -43,7 +43,12 @@
 
 #define VOCAB_MAX_FEATURES 8192
 #define VOCAB_MAX_CHILDREN (1 << 23)  // sibling index field of the min key
-#define VOCAB_THREADS 1024
+// k_vocab workgroup size (a power of two, 256..1024). 512: beside the extraction kernels smaller
+// workgroups find room sooner (bench 81.4k at 512 or 256 vs 78.7k at 1024); alone 66 / 81 / 61 us
+#ifndef ORBFE_VOCAB_THREADS
+#define ORBFE_VOCAB_THREADS 512
+#endif
+#define VOCAB_THREADS ORBFE_VOCAB_THREADS
 
 struct __attribute__((aligned(16))) VocRec {
   uint4 d0, d1;       // the node's descriptor (32 B)
@@ -178,11 +183,11 @@ __global__ __launch_bounds__(256) void k_vocab_descend(VocabArgs a, unsigned lon
   }
 }
 
-// Ascending bitonic sort of P2 = 1024 E keys (one or two arrays) held in registers: element
+// Ascending bitonic sort of P2 = VOCAB_THREADS E keys held in registers: element
 // e = (wave * E + r) * 64 + lane is register r of that lane, so a wave owns 64 E consecutive keys.
 // Stages with j < 64 swap across lanes (ds_bpermute), 64 <= j < 64 E across a lane's registers,
-// and only j >= 64 E (10 of the 55-78 stages) go through LDS with barriers. The keys come from and
-// return to ka / kb (the LDS arrays the rest of k_vocab reads).
+// and only j >= 64 E go through LDS with barriers. The keys come from and return to ka (the LDS
+// array the rest of k_vocab reads).
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
@@ -200,33 +205,23 @@ __device__ __forceinline__ void cx_pair(unsigned long long& lo, unsigned long lo
 }
 
 template <int E>
-__device__ __forceinline__ void bitonic_reg(unsigned long long* ka, unsigned long long* kb) {
-  constexpr int P2 = 1024 * E;
+__device__ __forceinline__ void bitonic_reg(unsigned long long* ka) {
+  constexpr int P2 = VOCAB_THREADS * E;
   const int l = lane_id(), w = wave_id();
-  const bool two = kb != nullptr;
-  unsigned long long va[E], vb[E];
+  unsigned long long va[E];
 #pragma unroll
-  for (int r = 0; r < E; r++) {
-    const int e = (w * E + r) * 64 + l;
-    va[r] = ka[e];
-    vb[r] = two ? kb[e] : 0ull;
-  }
+  for (int r = 0; r < E; r++) va[r] = ka[(w * E + r) * 64 + l];
   for (int k = 2; k <= P2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       if (j >= 64 * E) {  // across waves
         __syncthreads();  // the previous such stage's partner reads are done
 #pragma unroll
-        for (int r = 0; r < E; r++) {
-          const int e = (w * E + r) * 64 + l;
-          ka[e] = va[r];
-          if (two) kb[e] = vb[r];
-        }
+        for (int r = 0; r < E; r++) ka[(w * E + r) * 64 + l] = va[r];
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < E; r++) {
           const int e = (w * E + r) * 64 + l;
           va[r] = cx_keep(va[r], ka[e ^ j], e, j, k);
-          if (two) vb[r] = cx_keep(vb[r], kb[e ^ j], e, j, k);
         }
       } else if (j >= 64) {  // across this lane's registers (static indices per q)
         const int jr = j >> 6;
@@ -234,13 +229,8 @@ __device__ __forceinline__ void bitonic_reg(unsigned long long* ka, unsigned lon
         for (int q = 1; q < E; q <<= 1) {
           if (jr == q) {
 #pragma unroll
-            for (int r = 0; r < E; r++) {
-              if ((r & q) == 0) {
-                const bool asc = ((((w * E + r) * 64 + l) & k) == 0);
-                cx_pair(va[r], va[r | q], asc);
-                if (two) cx_pair(vb[r], vb[r | q], asc);
-              }
-            }
+            for (int r = 0; r < E; r++)
+              if ((r & q) == 0) cx_pair(va[r], va[r | q], ((((w * E + r) * 64 + l) & k) == 0));
           }
         }
       } else {  // across lanes
@@ -248,18 +238,13 @@ __device__ __forceinline__ void bitonic_reg(unsigned long long* ka, unsigned lon
         for (int r = 0; r < E; r++) {
           const int e = (w * E + r) * 64 + l;
           va[r] = cx_keep(va[r], shfl_xor_u64(va[r], j), e, j, k);
-          if (two) vb[r] = cx_keep(vb[r], shfl_xor_u64(vb[r], j), e, j, k);
         }
       }
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < E; r++) {
-    const int e = (w * E + r) * 64 + l;
-    ka[e] = va[r];
-    if (two) kb[e] = vb[r];
-  }
+  for (int r = 0; r < E; r++) ka[(w * E + r) * 64 + l] = va[r];
   __syncthreads();
 }
 
@@ -282,21 +267,24 @@ __device__ __forceinline__ void bitonic_lds(unsigned long long* skeys, int P2) {
   }
 }
 
-// P2 in {1024, 2048, 4096, 8192} (k_vocab pads to at least 1024 keys)
-__device__ __forceinline__ void sort_keys(unsigned long long* ka, unsigned long long* kb, int P2) {
+// P2 a power of two from VOCAB_THREADS to VOCAB_MAX_FEATURES (k_vocab pads to at least one key
+// per thread)
+__device__ __forceinline__ void sort_keys(unsigned long long* ka, int P2) {
 #if defined(ORBFE_VOCAB_LDS_SORT) && ORBFE_VOCAB_LDS_SORT
   bitonic_lds(ka, P2);
-  if (kb) bitonic_lds(kb, P2);
   return;
 #endif
-  if (P2 <= 1024)
-    bitonic_reg<1>(ka, kb);
-  else if (P2 == 2048)
-    bitonic_reg<2>(ka, kb);
-  else if (P2 == 4096)
-    bitonic_reg<4>(ka, kb);
-  else
-    bitonic_reg<8>(ka, kb);
+  const int E = P2 / VOCAB_THREADS;
+  if (E <= 1)
+    bitonic_reg<1>(ka);
+  else if (E == 2)
+    bitonic_reg<2>(ka);
+  else if (E == 4)
+    bitonic_reg<4>(ka);
+  else if (E == 8)
+    bitonic_reg<8>(ka);
+  else  // more than 8 keys per thread (large nfeatures at small workgroups): through LDS
+    bitonic_lds(ka, P2);
 }
 
 // Starts of the runs of equal key>>32 among the nv sorted valid keys: every thread owns a
@@ -362,7 +350,7 @@ __device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img,
 #if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 4  // phase-cost build: key loads only
   return;
 #endif
-  sort_keys(skeys, nullptr, P2);  // stable: the feature index is the low half of every key
+  sort_keys(skeys, P2);  // stable: the feature index is the low half of every key
 #if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 1  // phase-cost build: loads + sorts only
   return;
 #endif
@@ -465,7 +453,7 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   return;
 #endif
   const int n = a.empty ? 0 : min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
-  int P2 = 1024;  // sort_keys' smallest size: one key per thread
+  int P2 = VOCAB_THREADS;  // sort_keys' smallest size: one key per thread
   while (P2 < n) P2 <<= 1;
   if (ORBFE_VOCAB_SPLIT) {
     vocab_part(a, blockIdx.y == 0, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
@@ -797,7 +785,7 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   unsigned long long* bwk = fvk + slots;
   int32_t* leaves = reinterpret_cast<int32_t*>(bwk + slots);
   // P2 keys, then (BowVector workgroups) P2 doubles
-  P2 = P2 < 1024 ? 1024 : P2;  // k_vocab sorts at least 1024 keys
+  P2 = P2 < VOCAB_THREADS ? VOCAB_THREADS : P2;  // k_vocab sorts at least one key per thread
   const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * (P2 + 128) : 0);
   hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
   hipLaunchKernelGGL(k_vocab, dim3(n_images, d_bow_words && ORBFE_VOCAB_SPLIT ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
