@@ -290,8 +290,10 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
 #define ORBFE_SFT_WPE 4
 #endif
 __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
-  __shared__ uint32_t s_claim_far[4][SFT_MAX_NODE / 32];  // claims beyond the register chunks
-  __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];        // fixpoint path: node candidates
+  // per wave: the fixpoint path's node candidates, or the large-node path's claim bits beyond the
+  // register chunks (a wave takes one path; 18 KiB per workgroup in all)
+  static_assert(SFT_MAX_NODE / 32 <= SFT_FP_MAX * 8, "claim bits fit the candidate area");
+  __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
   orbfe_sft_pair P = pairs[blockIdx.y];
   sft_resolve_sizes(P);
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
   // orders the two stores to one address from different lanes)
   for (int i = o1 + lane; i < e1; i += 64) P.match12[P.fv1.indices[i]] = -1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t* far = s_claim_far[w];
+  uint32_t* far = s_fp_desc[w];
   if (n2 > SFT_REG_CHUNKS * 64)
     for (int i = lane; i < (n2 + 31) / 32; i += 64) far[i] = 0;
   const SftOctTab tab = sft_oct_tab(P);
