@@ -2027,17 +2027,21 @@ struct DwX3 {
   uint32_t x, y, z;
 };
 
-__global__ __launch_bounds__(256) void k_describe(ExtractArgs a) {
+#ifndef ORBFE_DESC_WPB
+#define ORBFE_DESC_WPB 4  // k_describe wavefronts per workgroup (4 keypoints each)
+#endif
+constexpr int DESC_THREADS = 64 * ORBFE_DESC_WPB;
+__global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
   __shared__ float4 s_pat[256];
   __shared__ uint32_t s_mom[4 * 279];
-  __shared__ __attribute__((aligned(16))) uint32_t s_win[16][37 * 10];
-  s_pat[threadIdx.x] = c_patf[threadIdx.x];
-  for (int k = threadIdx.x; k < 4 * 279; k += 256) s_mom[k] = (&c_momask[0][0][0])[k];
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * ORBFE_DESC_WPB][37 * 10];
+  for (int k = threadIdx.x; k < 256; k += DESC_THREADS) s_pat[k] = c_patf[k];
+  for (int k = threadIdx.x; k < 4 * 279; k += DESC_THREADS) s_mom[k] = (&c_momask[0][0][0])[k];
   __syncthreads();  // before any wavefront may leave
   const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
   const int img = blk.y;
-  const int slot = (blk.x * 4 + w) * 4 + grp;
+  const int slot = (blk.x * ORBFE_DESC_WPB + w) * 4 + grp;
   const int32_t* lc = a.lvlcnt + (long long)img * a.nlevels;
   if (blk.x == 0 && threadIdx.x == 0) {
     int tot = 0;
@@ -3062,8 +3066,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
 #endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
-    dim3 grid((h->total_key_slots + 15) / 16, n);
-    LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, a));
+    constexpr int per_block = 4 * ORBFE_DESC_WPB;  // keypoints per workgroup
+    dim3 grid((h->total_key_slots + per_block - 1) / per_block, n);
+    LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(DESC_THREADS), 0, st, a));
   }
   ORBFE_HIP_CHECK(hipGetLastError());
   h->last_img0 = d_imgs - (long long)i0 * img_stride;
