@@ -295,15 +295,22 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
   static_assert(SFT_MAX_NODE / 32 <= SFT_FP_MAX * 8, "claim bits fit the candidate area");
   __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
-  orbfe_sft_pair P = pairs[blockIdx.y];
+  // XCD-aware order: the workgroups of one pair run on one XCD, so its KeyFrames' keypoints,
+  // descriptors and FeatureVectors are fetched into one L2 rather than eight
+#if defined(ORBFE_SFT_LINEAR) && ORBFE_SFT_LINEAR
+  const int2 blk = make_int2(blockIdx.x, blockIdx.y);
+#else
+  const int2 blk = xcd_block2d();
+#endif
+  orbfe_sft_pair P = pairs[blk.y];
   sft_resolve_sizes(P);
 #if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 3  // phase-cost builds (match12 left unwritten):
   return;                                             // an empty k_sft_nodes
 #endif
 #if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 4  // the coverage workgroups only
-  if (blockIdx.x != gridDim.x - 1) return;
+  if (blk.x != gridDim.x - 1) return;
 #endif
-  if (blockIdx.x == gridDim.x - 1) {
+  if (blk.x == gridDim.x - 1) {
     // the last workgroup of a pair: KF1 features that no FeatureVector node lists -- a stopped
     // word (weight 0) is not added (TemplatedVocabulary.h:1198-1201) -- never match: -1. Disjoint
     // from the features the node wavefronts write, so no ordering is needed between them.
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
     return;
   }
   const int w = wave_id(), lane = lane_id();
-  const int a = blockIdx.x * 4 + w;
+  const int a = blk.x * 4 + w;
   if (a >= P.fv1.n_nodes || P.kf2.n > SFT_MAX_KF2) return;
   const uint32_t id = P.fv1.node_ids[a];
   const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
