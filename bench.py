@@ -120,6 +120,9 @@ def parse(argv=None):
                    help="diagnostic: the pipeline's streams from torch's pool, created after the "
                         "handles (hardware-queue assignment then depends on the stream count; with "
                         "several extractors their side work runs inline)")
+    p.add_argument("--side-per-stream", action="store_true",
+                   help="one high-priority side stream per extraction stream instead of one shared (more busy "
+                        "streams than hardware queues unless --hw-queues is raised)")
     p.add_argument("--stagger", action="store_true",
                    help="each sub-batch's extraction waits for the previous sub-batch's pyramid (the handles' "
                         "pyramid chains never overlap)")
@@ -252,7 +255,8 @@ def main():
                                                                   match_high=not args.match_normal,
                                                                   side_last=args.inline_side,
                                                                   side_high=not args.side_normal,
-                                                                  cu_split=args.cu_split)
+                                                                  cu_split=args.cu_split,
+                                                                  side_per_stream=args.side_per_stream)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:

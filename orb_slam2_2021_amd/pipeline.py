@@ -65,7 +65,7 @@ class PipelineStreams:
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
                  match_high: bool = False, side_last: bool = False, side_high: bool = True,
-                 cu_split: int = 0):
+                 cu_split: int = 0, side_per_stream: bool = False):
         import torch
         self.device = device
         self._ptrs = []
@@ -104,20 +104,27 @@ class PipelineStreams:
         self.side = make(side_high)
         if match_high and not match_inline and not side_last:  # at the side stream's priority
             self.match = make(True)
+        # side_per_stream: one side stream per extraction stream (handles on extraction stream j
+        # share side stream j) instead of one for all; more busy streams than 4 hardware queues
+        # unless GPU_MAX_HW_QUEUES is raised
+        self.sides = [self.side] + ([make(side_high) for _ in range(n - 1)] if side_per_stream else [])
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
         return self.extract + [self.match]
 
     def attach(self, ext) -> None:
-        """Route `ext`'s side-stream work to the shared side stream (detached again by close())."""
-        ext.set_side_stream(self.side.cuda_stream)
+        """Route `ext`'s side-stream work to the shared side stream (with side_per_stream: the k-th
+        attached handle to side stream k mod n, matching its extraction stream k mod n); detached
+        again by close()."""
+        side = self.sides[len(self._attached) % len(self.sides)]
+        ext.set_side_stream(side.cuda_stream)
         self._attached.append(ext)
 
     def close(self):
         """Wait for the streams, point every attached extractor back at its own side stream, then
         destroy the streams (no handle is left holding a destroyed hipStream_t)."""
-        for s in self.extract + [self.match, self.side]:
+        for s in self.extract + [self.match] + self.sides:
             if s is not None:
                 s.synchronize()
         for e in self._attached:
