@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -602,7 +603,20 @@ struct SbpArgs {
   uint8_t* cand_d;
   uint8_t* cand_l;
   int32_t* cand_n;
+  // rounds >= 2 with the cache: round r-2's owners (round r compares them with round r-1's and
+  // re-evaluates only the queries a changed keypoint can reach); NULL: every query is re-evaluated
+  const int32_t* owner_rm2;
 };
+
+// A keypoint whose owner changed from o1 to o2 between rounds: blocked(k) = owner < q flips exactly
+// for the queries lo < q <= hi (lo = min, hi = max of the two owners), and only a query whose
+// window (|x - kx| < r and |y - ky| < r, the test every candidate passed) holds the keypoint can
+// have it as a candidate. A query no entry reaches keeps its previous result.
+struct SbpChange {
+  float x, y;
+  int lo, hi;
+};
+#define SBP_CHG_MAX 256  // more changed keypoints than this: the round re-evaluates every query
 
 // Keypoint taken before the search starts: Frame::mvpMapPoints with Observations() > 0 (:91-93,
 // :1420-1422) or any non-NULL entry (:384, :1567).
@@ -757,18 +771,55 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
 }
 
 __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
+  __shared__ SbpChange s_chg[SBP_CHG_MAX];
+  __shared__ int s_nchg;
   if (a.round > 1 && a.state[2 + a.round - 1] == 0) {  // previous round reproduced its input
     if (blockIdx.x == 0 && threadIdx.x == 0) a.state[0] = 1;
     return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) a.state[1] = a.round + 1;
+  // the keypoints whose owner differs between rounds r-2 and r-1, gathered by every workgroup
+  // (owner_rm2 is not written during this round: four owner buffers rotate)
+  int nchg = SBP_CHG_MAX + 1;
+  if (a.owner_rm2) {
+    if (threadIdx.x == 0) s_nchg = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < a.F.n; k += 256) {
+      const int o1 = a.owner_rm2[k], o2 = a.owner_prev[k];
+      if (o1 != o2) {
+        const int slot = atomicAdd(&s_nchg, 1);
+        if (slot < SBP_CHG_MAX) {
+          SbpChange c;
+          c.x = a.F.keys_un[k].x;
+          c.y = a.F.keys_un[k].y;
+          c.lo = min(o1, o2);
+          c.hi = max(o1, o2);
+          s_chg[slot] = c;
+        }
+      }
+    }
+    __syncthreads();
+    nchg = s_nchg;
+  }
+  const bool sparse = nchg <= SBP_CHG_MAX;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < a.F.n) a.owner_next[i] = 0x7fffffff;
   bool changed = false;
   if (i < a.m) {
+    bool need = true;
+    if (sparse) {
+      const float qx = a.q[i].x, qy = a.q[i].y, qr = a.q[i].r;
+      need = false;
+      for (int c = 0; c < nchg && !need; c++) {
+        const SbpChange e = s_chg[c];
+        need = e.lo < i && i <= e.hi && fabsf(e.x - qx) < qr && fabsf(e.y - qy) < qr;
+      }
+    }
     auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || a.owner_prev[k] < i; };
     int res;
-    if (!a.cand_n) {
+    if (!need) {
+      res = a.res_prev[i];  // no candidate changed its blocked state for this query
+    } else if (!a.cand_n) {
       res = sbp_one(a, i, blocked);
     } else if (a.round == 0) {
       res = sbp_one<decltype(blocked), true>(a, i, blocked);
@@ -1490,6 +1541,7 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
   p.ocand_l = ar.add(cq);
   p.ocand_n = ar.add(p.cache ? 4 * q1 : 0);
   p.onm = ar.add(4);
+  p.oown3 = ar.add(4 * f1);
 }
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap) {
   SbpPlan p;
@@ -1563,7 +1615,7 @@ static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_fram
   in.res0 = (int32_t*)(A + p.ores0);
   in.res1 = (int32_t*)(A + p.ores1);
   in.own0 = (int32_t*)(A + p.oown0);
-  in.own2 = (int32_t*)(A + p.oown2);
+  in.own2 = (int32_t*)(A + p.oown3);  // round 0's owner_prev (read only without the cache)
   in.state = (int32_t*)(A + p.ostate);
   in.nmatches = (int32_t*)(A + p.onm);
   in.serial = m->d_serial;
@@ -1583,30 +1635,40 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
   a.res_cur = (int32_t*)(A + p.ores0);
   a.res_prev = (int32_t*)(A + p.ores1);
   a.owner_cur = (int32_t*)(A + p.oown0);
-  a.owner_prev = (int32_t*)(A + p.oown2);
+  a.owner_prev = (int32_t*)(A + p.oown3);
   a.owner_next = (int32_t*)(A + p.oown1);
   if (p.nq > 0)
     hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((p.nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                        m->stream, a);
 }
 
-// Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over three:
-// round r claims into own[r % 3], reads own[(r + 2) % 3] and clears own[(r + 1) % 3] for round
-// r + 1, which nobody reads during round r).
+// ORBFE_SBP_DENSE=1: every round re-evaluates every query (rounds 1-3's behaviour, for A/B)
+static bool sbp_dense_rounds() {
+  static const bool dense = std::getenv("ORBFE_SBP_DENSE") && std::atoi(std::getenv("ORBFE_SBP_DENSE")) != 0;
+  return dense;
+}
+
+// Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over four:
+// round r claims into own[r % 4], reads own[(r + 3) % 4] (round r-1) and own[(r + 2) % 4]
+// (round r-2), and clears own[(r + 1) % 4] for round r + 1, which nobody reads during round r).
 static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
                        const SbpMode& md, int r0, int r1, bool defer) {
   uint8_t* A = m->arena;
   const int nq = p.nq;
   SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
   int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
-  int32_t* own[3] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2)};
+  int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
+                     (int32_t*)(A + p.oown3)};
   for (int r = r0; r < r1 && nq > 0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];
-    a.owner_cur = own[r % 3];
-    a.owner_prev = own[(r + 2) % 3];
-    a.owner_next = own[(r + 1) % 3];
+    a.owner_cur = own[r % 4];
+    a.owner_prev = own[(r + 3) % 4];
+    a.owner_next = own[(r + 1) % 4];
+    // round r-2's owners: round r re-evaluates only the queries a keypoint whose owner changed
+    // since can reach
+    a.owner_rm2 = r >= 2 && p.cache && !sbp_dense_rounds() ? own[(r + 2) % 4] : nullptr;
     if (r == 0 && p.cache)
       hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                          m->stream, a);

@@ -170,7 +170,7 @@ bool levels_ok(const orbfe_keypoint* k, int n, int nlevels);
 struct SbpPlan {
   FrameOffsets fo;
   size_t oqd, oqa, og_start, og_items, oq, ores0, ores1, oown0, oown1, oown2, oblk, ostate, obest;
-  size_t ocand_k, ocand_d, ocand_l, ocand_n, onm;
+  size_t ocand_k, ocand_d, ocand_l, ocand_n, onm, oown3;
   bool cache;
   int nq, cand_cap;
 };

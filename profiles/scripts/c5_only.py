@@ -19,13 +19,17 @@ def main():
     frames = [bench.c5_frame(ext, img, tcw) for img, tcw in zip(imgs, poses)]
     m = ORBmatcher(0.8, True)
     m.SearchLocalPoints(frames[0], G, 3.0)
+    m.set_profiling(True)
+    dev = []
     t0 = time.perf_counter()
     for _ in range(reps):
         for F in frames:
             m.SearchLocalPoints(F, G, 3.0)
+            dev.append(m.last_device_ms())
     dt = (time.perf_counter() - t0) / (reps * len(frames))
     print(f"c5: {len(G.flags)} MapPoints, {np.mean([F.N for F in frames]):.0f} keypoints per frame, "
-          f"{1e3 * dt:.3f} ms per search (host buffers), {reps * len(frames)} searches")
+          f"{1e3 * dt:.3f} ms per search (host buffers), device {1e3 * np.mean(dev):.1f} us per search, "
+          f"{reps * len(frames)} searches")
 
 
 if __name__ == "__main__":
