@@ -3,6 +3,8 @@
 set -e
 cd "$(dirname "$0")/../.."
 tail -n 1 gpurun_out/bench_full.log > profiles/r3_bench.json
+cp gpurun_out/pmc_traffic.json gpurun_out/pmc_traffic_c5.json profiles/
+python3 profiles/scripts/valu_summary.py gpurun_out/pmcWait/run_counter_collection.csv > profiles/r3_valu.txt
 cp gpurun_out/prof/run_kernel_stats.csv profiles/r3_kernel_stats.csv
 { echo "# wave-time breakdown, bench (contended): rocprofv3 --pmc of bench.py (refresh_profiles.sh, pmcWait)";
   python3 profiles/pmc_waits.py gpurun_out/pmcWait/run_counter_collection.csv;
