@@ -84,6 +84,7 @@ struct LevelDesc {
 struct CellDesc {
   int16_t level, x0, y0, rw, rh, ox, oy, pad;
   int32_t slot, cap;
+  int32_t pyr_off, pitch;  // the level's (LevelDesc): k_fast's ROI address needs no second descriptor load
 };
 
 struct ExtractArgs {
@@ -993,9 +994,8 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
   const int RS = RSC ? RSC : lay.rs;
 
   const CellDesc cd = a.cells[cell];
-  const LevelDesc ld = a.levels[cd.level];
-  int pitch;
-  const uint8_t* lev = level_ptr(a, ld, img, cd.level, pitch);
+  const int pitch = cd.pitch;
+  const uint8_t* lev = a.pyr + (long long)img * a.pyr_stride + cd.pyr_off;
   const int rw = cd.rw, rh = cd.rh;
   const int mw = rw - 4, mh = rh - 4, dw = rw - 6, dh = rh - 6;
   int32_t* cnt_out = a.cellcnt + (long long)img * a.ncells + cell;
@@ -1017,6 +1017,8 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       const bool in = r < rh && q < nq4;
       __builtin_memcpy(&v[k], lev + (long long)(cd.y0 + (in ? r : 0)) * pitch + x0a + 16 * (in ? q : 0), 16);
     }
+    // the arc-strength map is zeroed while the ROI loads are in flight
+    for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const int i = lane + 64 * k, r = i >> 2, q = i & 3;
@@ -1072,7 +1074,8 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       c = q - r * dw;
     }
   };
-  for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
+  if constexpr (RSC == 0)
+    for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
 #if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 1
   // phase-cost diagnostic builds only (profiles/scripts/r3_fast_phases.sh; -DORBFE_FAST_DIAG=1..3
   // stop after the ROI load, the prefilter, the arc strength): no corners, the work kept alive
@@ -2558,6 +2561,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     std::memset(&d, 0, sizeof(d));
     d.w = h_round((float)cols * h->inv_scale[l]);
     d.h = h_round((float)rows * h->inv_scale[l]);
+    if (d.w > 4095 || d.h > 4095)  // candidate / survivor keys hold x and y in 12 bits each
+      return orbfe_set_error(ORBFE_ERR_ARG, "image too large: width and height must be below 4096");
     const int minB = 16, maxBX = d.w - 16, maxBY = d.h - 16;  // EDGE_THRESHOLD - 3
     const int bw = maxBX - minB, bh = maxBY - minB;
     if (bw < 30 || bh < 30)
@@ -2611,6 +2616,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
         const int dw = c.rw - 6, dh = c.rh - 6;
         c.cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
         c.slot = cand;
+        c.pyr_off = (int32_t)d.pyr_off;
+        c.pitch = d.pitch;
         cand += c.cap;
         rwmax = std::max(rwmax, (int)c.rw);
         rhmax = std::max(rhmax, (int)c.rh);
