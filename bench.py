@@ -83,9 +83,11 @@ def parse(argv=None):
     p.add_argument("--handles-per-stream", type=int, default=2,
                    help="extractor handles per extraction stream (handle k on stream k mod --extractors): "
                         "a handle's pyramids are rebuilt every extractors x this sub-batches")
-    p.add_argument("--hw-queues", type=int, default=0,
+    p.add_argument("--hw-queues", type=int, default=-1,
                    help="GPU_MAX_HW_QUEUES for this process (set before the HIP runtime starts; 0: the "
-                        "environment's, 4 by default): hardware queues the busy streams spread over")
+                        "environment's, 4 by default; -1 (default): 8 when WORLD_SIZE > 1, so that the RCCL "
+                        "stream of the C4 gather gets a queue of its own instead of sharing one with an "
+                        "extraction stream, else the environment's): hardware queues the busy streams spread over")
     p.add_argument("--defer-matching", action="store_true",
                    help="enqueue sub-batch i's vocabulary + matching with sub-batch i+1's extraction, after its "
                         "pyramid (overlapping the FAST / octree / blur / describe phase)")
@@ -139,10 +141,27 @@ def parse(argv=None):
     p.add_argument("--dump-gather", default="",
                    help="test hook: write each rank's last sub-batch (own keypoints + descriptors) and "
                         "rank 0's gathered payloads to this directory")
+    p.add_argument("--c5-workers", type=int, default=4,
+                   help="C5 leg: Tracking-like callers per rank, each with its own extractor + matcher on its "
+                        "own thread (the leg also reports one caller)")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
     return p.parse_args(argv)
+
+
+# N > 1: four busy pipeline streams plus RCCL's stream. With the HIP default of 4 hardware queues
+# the fifth busy stream shares a queue with one of the others, and a receive kernel waiting for its
+# peer then holds that queue (five busy streams on 4 queues measured 54.9k vs 78.9k stereo frames/s
+# in round 2); 8 queues with two extraction streams measured the same as 4 at N = 1 (81.0k both)
+HW_QUEUES_MULTI_RANK = 8
+
+def hw_queue_setting(requested: int, world: int) -> int:
+    """GPU_MAX_HW_QUEUES to set (0: leave the environment's): --hw-queues as given, or with the
+    default (-1) HW_QUEUES_MULTI_RANK when this is one of several ranks."""
+    if requested >= 0:
+        return requested
+    return HW_QUEUES_MULTI_RANK if world > 1 else 0
 
 
 SEQ_SEED = 0x0C3  # the C3 driving sequence (orbfe_synth_sequence_frame)
@@ -233,8 +252,9 @@ class Gatherer:
 
 def main():
     args = parse()
-    if args.hw_queues > 0:  # read once by the HIP runtime at its start (no HIP call before this)
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
+    hw_queues = hw_queue_setting(args.hw_queues, int(os.environ.get("WORLD_SIZE", "1")))
+    if hw_queues > 0:  # read once by the HIP runtime at its start (no HIP call before this)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
     import torch
@@ -461,6 +481,7 @@ def main():
             "stereo_frames_per_gpu_per_subbatch": B, "subbatches_per_step": S_sub,
             "stereo_frames_per_gpu_per_step": B * S_sub, "distinct_input_batches": NB,
             "parallelism": f"frame-sharded x{world}",
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "pipeline": (f"{len(exts)} extractor handles on {n_ext} streams (consecutive sub-batches' "
                          f"extractions overlap), {'matching inline' if args.match_inline else ('' if args.stereo_on_extract else 'ComputeStereoMatches + ') + 'vocabulary + matching on its own stream'}, "
                          f"{pipe_depth(args)} output sets" if pipe_depth(args) > 1 else "one sub-batch at a time"),
@@ -759,7 +780,9 @@ def c5_scene(nfeatures, world, rank, dev, m_points=50000, frames_per_rank=16):
     from orb_slam2_2021_amd import synthetic as S
     from orb_slam2_2021_amd.frames import MapPointGeometry
     from orb_slam2_2021_amd.parallel import broadcast_arrays, shard_frames
-    ext = ORBextractor(nfeatures, 1.2, 8, 12, 7)  # arducam.yaml:126-127
+    import torch
+    gpu = torch.cuda.current_device()  # this rank's GPU (dev may be the host in --rehearse)
+    ext = ORBextractor(nfeatures, 1.2, 8, 12, 7, device=gpu)  # arducam.yaml:126-127
     sc, s2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
     k0, d0 = ext(synth_frame(7, 480, 640))
     rng = np.random.default_rng(0x50C0DE)
@@ -787,7 +810,7 @@ def c5_frame(ext, img, tcw):
                    max_x=640.0, min_y=0.0, max_y=480.0, tcw=tcw, **S.ARDUCAM_CAM)
 
 
-def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
+def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=64):
     """BASELINE config C5: a 640x480 stream through Tracking::SearchLocalPoints' hot part --
     Frame::isInFrustum(pMP, 0.5) for every MapPoint of the local map, then
     ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th=3) (Tracking.cc:1186-1213) -- with
@@ -801,28 +824,50 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
     PMC traffic of the same kernels from profiles/pmc_traffic_c5.json. Rank 0 checks its first
     frame bit-exact against the oracle."""
     import torch
-    from orb_slam2_2021_amd import ORBmatcher
+    from concurrent.futures import ThreadPoolExecutor
+    from orb_slam2_2021_amd import ORBextractor, ORBmatcher
     from orb_slam2_2021_amd.frames import log_scale_factor
     ext, F0, G, imgs, poses, n_total = c5_scene(args.nfeatures, world, rank, dev, m_points, frames_per_rank)
-    m = ORBmatcher(0.8, True)  # Tracking.cc:1206
-    ext(imgs[0])
-    m.SearchLocalPoints(F0, G, 3.0)
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    nm_total, first, frames = 0, None, []
-    for img, tcw in zip(imgs, poses):
-        F = c5_frame(ext, img, tcw)
-        nm, best, nv, _ = m.SearchLocalPoints(F, G, 3.0)
-        nm_total += nm
-        frames.append(F)
-        if first is None:
-            first = (F, nm, best, nv)
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    gpu = torch.cuda.current_device()
+    m = ORBmatcher(0.8, True, device=gpu)  # Tracking.cc:1206
+    # several Tracking-like callers per GPU, each with its own extractor + matcher handle (own
+    # streams) on its own thread: one caller's uploads, extraction and claim rounds overlap the
+    # others' (the frames are independent; ctypes releases the GIL inside the library calls)
+    workers = max(1, args.c5_workers)
+    handles = [(ext, m)] + [(ORBextractor(args.nfeatures, 1.2, 8, 12, 7, device=gpu), ORBmatcher(0.8, True, device=gpu))
+                            for _ in range(workers - 1)]
+    for e, mm in handles:
+        e(imgs[0])
+        mm.SearchLocalPoints(F0, G, 3.0)
+
+    def run(w, nw):
+        e, mm = handles[w]
+        res = []
+        for i in range(w, len(imgs), nw):
+            F = c5_frame(e, imgs[i], poses[i])
+            nm, best, nv, _ = mm.SearchLocalPoints(F, G, 3.0)
+            res.append((i, F, nm, best, nv))
+        return res
+
+    def timed(nw):
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=nw) as pool:
+            res = sorted((r for part in pool.map(lambda w: run(w, nw), range(nw)) for r in part),
+                         key=lambda r: r[0])
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, res
+
+    dt1, _ = timed(1)  # one caller: Tracking's own frame-after-frame pattern
+    dt, res = timed(workers)
+    nm_total = sum(r[2] for r in res)
+    frames = [r[1] for r in res]
+    first = res[0][1:]
     # the device part alone (no extraction, no PCIe)
     m.set_profiling(True)
     dev_ms, rounds = [], []
@@ -839,6 +884,7 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
     achieved = algo / (us * 1e-6) / 1e9
     traffic = c5_pmc_traffic(M)
     out = {"frames_per_s": round(n_total / dt, 1), "ms_per_frame_per_rank": round(1e3 * dt / len(imgs), 3),
+           "callers_per_rank": workers, "frames_per_s_one_caller": round(n_total / dt1, 1),
            "frames": n_total, "ranks": world, "map_points": M,
            "matches_per_frame_rank0": round(nm_total / len(imgs), 1),
            "device_us_per_search": round(us, 2),
@@ -849,7 +895,9 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=16):
                         "algorithmic_bytes_per_frame": int(algo),
                         "measured_in": "HIP events around the device part of each search (orbfe_matcher_set_profiling)"},
            "what": "640x480 frames sharded over ranks, local map replicated (broadcast from rank 0 when N > 1); "
-                   "per frame ORBextractor + orbfe_search_local_points (host buffers, PCIe included)"}
+                   "per frame ORBextractor + orbfe_search_local_points (host buffers, PCIe included), "
+                   f"{workers} callers per rank on their own handles and threads (frames_per_s_one_caller: "
+                   "one caller, frame after frame)"}
     if rank == 0 and not args.no_cpu:
         from oracle import orbref
         F, nm, best, nv = first

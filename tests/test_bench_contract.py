@@ -65,3 +65,13 @@ def test_cli_defaults():
     assert a.pairs == "kf" and a.stereo
     # a step is long enough to be seen (>= 1024 sub-batches of 32 stereo frames)
     assert a.batches_per_step * a.batch >= 32 * 1024
+
+
+def test_hw_queue_setting():
+    # several ranks: RCCL's stream gets a hardware queue of its own beside the four pipeline streams
+    assert bench.hw_queue_setting(-1, 1) == 0
+    assert bench.hw_queue_setting(-1, 2) == bench.HW_QUEUES_MULTI_RANK >= 5
+    assert bench.hw_queue_setting(-1, 8) == bench.HW_QUEUES_MULTI_RANK
+    assert bench.hw_queue_setting(0, 8) == 0  # the environment's
+    assert bench.hw_queue_setting(4, 1) == 4
+    assert bench.parse([]).hw_queues == -1 and bench.parse([]).c5_workers >= 1
