@@ -2030,6 +2030,9 @@ struct DwX3 {
   uint32_t x, y, z;
 };
 
+#ifndef ORBFE_FUSED_BLUR
+#define ORBFE_FUSED_BLUR 0  // 1: k_describe blurs each keypoint's window itself, no k_blur launch
+#endif
 #ifndef ORBFE_DESC_WPB
 #define ORBFE_DESC_WPB 4  // k_describe wavefronts per workgroup (4 keypoints each)
 #endif
@@ -2092,19 +2095,37 @@ __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
     mu[k] = DwX3{0u, 0u, 0u};
     if (l16 + 16 * k < 93) __builtin_memcpy(&mu[k], usrc + (k / 3) * step16 + ur[k % 3] * pitch + 12 * uc[k % 3], 12);
   }
+#if ORBFE_FUSED_BLUR
+  // GaussianBlur fused here: rows cy-21 .. cy+21 of the unblurred level
+  // (REFLECT_101 rows, the padding's reflected columns), lane l16 < 12 one dword at column
+  // xb - 4 + 4 l16; lanes 1..10 produce the blurred window's 10 dwords per row, k_blur's arithmetic
+  (void)bsrc;
+  const uint8_t* levu = a.pyr + lbase;
+  const int bx = xb - 4 + 4 * (l16 < 12 ? l16 : 0);
+  uint32_t rowv[43];
+#pragma unroll
+  for (int i = 0; i < 43; i++)
+    rowv[i] = *reinterpret_cast<const uint32_t*>(levu + (long long)reflect101(cy - 21 + i, ld.h) * pitch + bx);
+#else
   uint2 bw[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) {
     bw[k] = make_uint2(0u, 0u);
     if (l16 + 16 * k < 185) __builtin_memcpy(&bw[k], bsrc + (k / 5) * step16 + br[k % 5] * pitch + 8 * bc[k % 5], 8);
   }
+#endif
 #if defined(ORBFE_DESC_DIAG) && ORBFE_DESC_DIAG == 1  // phase-cost diagnostic builds only (wrong output)
   {
     uint32_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 6; k++) acc ^= mu[k].x ^ mu[k].y ^ mu[k].z;
+#if ORBFE_FUSED_BLUR
+#pragma unroll
+    for (int k = 0; k < 43; k++) acc ^= rowv[k];
+#else
 #pragma unroll
     for (int k = 0; k < 12; k++) acc ^= bw[k].x ^ bw[k].y;
+#endif
     if (acc == 0x12345678u && valid) a.out_desc[0] = 1;  // keeps the loads
     return;
   }
@@ -2133,10 +2154,53 @@ __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
   m10 = group16_sum(m10);
   // the blurred pieces -> LDS (rows of 40 bytes), ahead of the angle arithmetic
   uint8_t* winb = reinterpret_cast<uint8_t*>(s_win[w * 4 + grp]);
+#if ORBFE_FUSED_BLUR
+  {
+    uint32_t seed;
+    asm volatile("v_mov_b32 %0, 0x8000" : "=v"(seed));
+    auto ev = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c020c00u); };  // columns 0, 2
+    auto od = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c01u); };  // columns 1, 3
+    const bool bout = l16 >= 1 && l16 <= 10;
+    uint32_t* wrow = s_win[w * 4 + grp] + (l16 - 1);
+    uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;
+    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;
+#pragma unroll
+    for (int i = 0; i < 43; i++) {
+      const uint32_t C = rowv[i];
+      e0 = e1; e1 = e2; e2 = e3; e3 = e4; e4 = e5; e5 = e6; e6 = ev(C);
+      o0 = o1; o1 = o2; o2 = o3; o3 = o4; o4 = o5; o5 = o6; o6 = od(C);
+      if (i < 6) continue;
+      const uint32_t VE = vtap7(e0, e1, e2, e3, e4, e5, e6), VO = vtap7(o0, o1, o2, o3, o4, o5, o6);
+      const uint32_t LE = from_left(VE), LO = from_left(VO), RE = from_right(VE), RO = from_right(VO);
+      const uint32_t Pm3 = __builtin_amdgcn_perm(LE, LO, 0x07060100u);
+      const uint32_t Pm2 = __builtin_amdgcn_perm(LO, LE, 0x07060302u);
+      const uint32_t Pm1 = __builtin_amdgcn_perm(VE, LO, 0x05040302u);
+      const uint32_t P0 = __builtin_amdgcn_perm(VO, VE, 0x05040100u);
+      const uint32_t P1 = __builtin_amdgcn_perm(VE, VO, 0x07060100u);
+      const uint32_t P2 = __builtin_amdgcn_perm(VO, VE, 0x07060302u);
+      const uint32_t P3 = __builtin_amdgcn_perm(RE, VO, 0x05040302u);
+      const uint32_t P4 = __builtin_amdgcn_perm(RO, RE, 0x05040100u);
+      const uint32_t P5 = __builtin_amdgcn_perm(RE, RO, 0x07060100u);
+      const uint32_t P6 = __builtin_amdgcn_perm(RO, RE, 0x07060302u);
+      auto hz = [seed](uint32_t pa, uint32_t pb, uint32_t pc, uint32_t pd) {
+        uint32_t t = dot2_acc(pd, 0x00000012u, seed);
+        t = dot2_acc(pc, 0x00220031u, t);
+        t = dot2_acc(pb, 0x00360031u, t);
+        return dot2_acc(pa, 0x00220012u, t);
+      };
+      const uint32_t s0 = hz(Pm3, Pm1, P1, P3), s1 = hz(Pm2, P0, P2, P4), s2 = hz(Pm1, P1, P3, P5),
+                     s3 = hz(P0, P2, P4, P6);
+      const uint32_t r = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0c0c0602u),
+                                               __builtin_amdgcn_perm(s1, s0, 0x0c0c0602u), 0x05040100u);
+      if (bout) wrow[(i - 6) * 10] = r;
+    }
+  }
+#else
 #pragma unroll
   for (int k = 0; k < 12; k++)
     if (l16 + 16 * k < 185)
       *reinterpret_cast<uint2*>(winb + (br[k % 5] + 16 * (k / 5)) * 40 + 8 * bc[k % 5]) = bw[k];
+#endif
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
   float ca, sb;
   steer_cos_sin(angle, a.factor_pi, ca, sb);
@@ -3051,7 +3115,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
     LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
 #endif
   }
@@ -3061,14 +3125,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
     LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
 #endif
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   launch_octree(st, 0, h->nlevels);
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1)
+#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
     LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a));
 #endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
