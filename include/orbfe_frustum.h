@@ -50,7 +50,9 @@ typedef struct orbfe_frustum_out {
 /* isInFrustum(pMP, viewing_cos_limit) for every MapPoint of geom not flagged BAD or SEEN, with
  * the frame's camera (F: fx, fy, cx, cy, bf, min/max x/y, nlevels), pose tcw (CurrentFrame.mTcw
  * rows 0..2, 3x4 row-major) and mfLogScaleFactor. *n_in_view = how many passed (nToMatch,
- * Tracking.cc:1197-1201). Host buffers, blocking. */
+ * Tracking.cc:1197-1201). Blocking. The geometry arrays (and the frame view's arrays) may be host
+ * memory or device memory: device inputs -- a local map kept resident in HBM -- are copied on the
+ * device instead of being staged through pinned host memory. Outputs are host buffers. */
 int orbfe_is_in_frustum(orbfe_matcher* m, const orbfe_frame_view* frame,
                         const orbfe_mappoint_geometry* geom, const float* tcw,
                         float log_scale_factor, float viewing_cos_limit,

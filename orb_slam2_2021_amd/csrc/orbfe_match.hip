@@ -1247,6 +1247,7 @@ namespace orbfe_mi {
 int ensure_arena(orbfe_matcher* m, size_t bytes) {
   m->stage_lo = SIZE_MAX;
   m->stage_hi = 0;
+  m->d2d.clear();
   if (bytes > m->arena_bytes) {
     hipFree(m->arena);
     m->arena = nullptr;
@@ -1263,9 +1264,25 @@ int ensure_arena(orbfe_matcher* m, size_t bytes) {
 }
 
 // Stage n host bytes for arena address dst (uploaded by flush_h2d).
+// A caller's array in device memory (a resident local map, a frame left in HBM): hipMemcpyAsync
+// device to device instead of the host staging copy. Pageable host memory reports
+// hipMemoryTypeUnregistered or an error, which is cleared here.
+static bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice;
+}
+
 void stage_h2d(orbfe_matcher* m, const void* dst, const void* src, size_t n) {
   if (n == 0) return;
   const size_t off = (size_t)((const uint8_t*)dst - m->arena);
+  if (is_device_ptr(src)) {
+    m->d2d.emplace_back(off, src, n);
+    return;
+  }
   std::memcpy(m->pinned + off, src, n);
   m->stage_lo = std::min(m->stage_lo, off);
   m->stage_hi = std::max(m->stage_hi, off + n);
@@ -1278,6 +1295,10 @@ int flush_h2d(orbfe_matcher* m) {
                                    hipMemcpyHostToDevice, m->stream));
   m->stage_lo = SIZE_MAX;
   m->stage_hi = 0;
+  for (const auto& c : m->d2d)
+    ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + std::get<0>(c), std::get<1>(c), std::get<2>(c),
+                                   hipMemcpyDeviceToDevice, m->stream));
+  m->d2d.clear();
   return ORBFE_OK;
 }
 

@@ -8,6 +8,7 @@
 
 #include <climits>
 #include <cstring>
+#include <tuple>
 #include <vector>
 
 #include "../../include/orbfe.h"
@@ -44,6 +45,9 @@ struct orbfe_matcher {
   uint8_t* pinned = nullptr;
   size_t pinned_bytes = 0;
   size_t stage_lo = SIZE_MAX, stage_hi = 0;
+  // inputs the caller passed in device memory: arena offset, source, bytes; copied on the device
+  // after the staged span's H2D copy (which may cover their arena regions)
+  std::vector<std::tuple<size_t, const void*, size_t>> d2d;
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)

@@ -198,7 +198,8 @@ class LocalMapPoints:
         self.proj_xr = np.ascontiguousarray(self.proj_xr, np.float32).reshape(m)
         self.level = np.ascontiguousarray(self.level, np.int32).reshape(m)
         self.view_cos = np.ascontiguousarray(self.view_cos, np.float32).reshape(m)
-        self.descriptors = np.ascontiguousarray(self.descriptors, np.uint8).reshape(m, 32)
+        if not getattr(self.descriptors, "is_cuda", False):  # a resident map's stay on the device
+            self.descriptors = np.ascontiguousarray(self.descriptors, np.uint8).reshape(m, 32)
 
     def view(self) -> L.local_mappoints:
         v = L.local_mappoints()
@@ -233,6 +234,45 @@ class MapPointGeometry:
         v.m = len(self.flags)
         for f in ("flags", "world_pos", "normal", "min_distance", "max_distance", "descriptors"):
             setattr(v, f, L.ptr(getattr(self, f)))
+        return v
+
+
+class DeviceMapPointGeometry:
+    """A MapPointGeometry resident in HBM (C5's replicated local map, uploaded or broadcast once):
+    the same SoA fields as contiguous device tensors (any dtype: the bytes are what count). The
+    matcher copies device inputs on the device instead of staging them through the host
+    (orbfe_frustum.h). Built from a MapPointGeometry and a torch device, or from tensors already
+    on the device (parallel.broadcast_arrays' output)."""
+
+    FIELDS = ("flags", "world_pos", "normal", "min_distance", "max_distance", "descriptors")
+
+    def __init__(self, geometry: Optional["MapPointGeometry"] = None, device=None, tensors=None, m=None):
+        import torch
+        if tensors is None:
+            tensors = {f: torch.from_numpy(np.ascontiguousarray(getattr(geometry, f))).to(device)
+                       for f in self.FIELDS}
+            m = len(geometry.flags)
+        if m is None:
+            raise ValueError("m (the MapPoint count) is required with tensors")
+        for f in self.FIELDS:
+            t = tensors[f]
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError(f"{f}: a contiguous device tensor is required")
+            setattr(self, f, t)
+        self.m = int(m)
+        need = {"flags": 1, "world_pos": 12, "normal": 12, "min_distance": 4, "max_distance": 4, "descriptors": 32}
+        for f, b in need.items():
+            if getattr(self, f).numel() * getattr(self, f).element_size() < b * self.m:
+                raise ValueError(f"{f}: fewer than {b} bytes per MapPoint")
+
+    def __len__(self) -> int:
+        return self.m
+
+    def view(self) -> L.mappoint_geometry:
+        v = L.mappoint_geometry()
+        v.m = self.m
+        for f in self.FIELDS:
+            setattr(v, f, L.ptr(getattr(self, f).data_ptr()))
         return v
 
 

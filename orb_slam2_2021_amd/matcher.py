@@ -29,6 +29,11 @@ from .frames import (FeatureVector, Frame, KeyFrame, KeyFrameMapPoints, LastFram
                      LocalMapPoints, MapPointGeometry, epipole, log_scale_factor)
 
 
+def _mp_count(mps) -> int:
+    """MapPoints of a MapPointGeometry (host arrays) or a DeviceMapPointGeometry."""
+    return mps.m if hasattr(mps, "m") else len(mps.flags)
+
+
 class ORBmatcher:
     TH_HIGH = 100  # ORBmatcher.cc:37-39
     TH_LOW = 50
@@ -134,7 +139,7 @@ class ORBmatcher:
             raise ValueError("F.tcw (mTcw) is required")
         sf = scale_factor if scale_factor is not None else float(F.scale_factors[1])
         fv, gv = F.view(), mps.view()
-        o, arrs = self._frustum_out(len(mps.flags))
+        o, arrs = self._frustum_out(_mp_count(mps))
         n = c_int()
         L.check(self._lib.orbfe_is_in_frustum(self._h, byref(fv), byref(gv), L.ptr(F.tcw),
                                               float(log_scale_factor(sf)), float(viewingCosLimit),
@@ -153,8 +158,8 @@ class ORBmatcher:
             raise ValueError("F.tcw (mTcw) is required")
         sf = scale_factor if scale_factor is not None else float(F.scale_factors[1])
         fv, gv = F.view(), mps.view()
-        o, arrs = self._frustum_out(len(mps.flags))
-        best = np.full(len(mps.flags), -1, np.int32)
+        o, arrs = self._frustum_out(_mp_count(mps))
+        best = np.full(_mp_count(mps), -1, np.int32)
         nm, nv = c_int(), c_int()
         L.check(self._lib.orbfe_search_local_points(
             self._h, byref(fv), byref(gv), L.ptr(F.tcw), float(log_scale_factor(sf)),

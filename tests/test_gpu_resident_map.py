@@ -1,0 +1,55 @@
+"""C5's local map resident in HBM (DeviceMapPointGeometry): SearchLocalPoints and isInFrustum with
+the MapPoint SoA in device memory give exactly what the host-array call gives (the matcher copies
+device inputs on the device instead of staging them), on the bench's C5 scene."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene():
+    import bench
+    torch.cuda.set_device(0)
+    ext, F0, G, imgs, poses, _ = bench.c5_scene(2000, 1, 0, None, m_points=50000, frames_per_rank=3)
+    frames = [bench.c5_frame(ext, img, tcw) for img, tcw in zip(imgs, poses)]
+    return G, frames
+
+
+def test_resident_map_search_local_points_equals_host():
+    from orb_slam2_2021_amd import ORBmatcher
+    from orb_slam2_2021_amd.frames import DeviceMapPointGeometry
+    G, frames = _scene()
+    Gd = DeviceMapPointGeometry(G, device=torch.device("cuda", 0))
+    assert len(Gd) == len(G.flags)
+    m = ORBmatcher(0.8, True)
+    for F in frames:
+        nh, bh, vh, lh = m.SearchLocalPoints(F, G, 3.0)
+        nd, bd, vd, ld = m.SearchLocalPoints(F, Gd, 3.0)
+        assert nh > 100 and (nh, vh) == (nd, vd)
+        assert np.array_equal(bh, bd)
+        for f in ("flags", "proj_x", "proj_y", "proj_xr", "level", "view_cos"):
+            assert np.array_equal(getattr(lh, f), getattr(ld, f)), f
+        # alternate host / device calls on one matcher: no stale device copy leaks into a host call
+        n2, b2, _, _ = m.SearchLocalPoints(F, G, 3.0)
+        assert n2 == nh and np.array_equal(b2, bh)
+
+
+def test_resident_map_is_in_frustum_equals_host():
+    from orb_slam2_2021_amd import ORBmatcher
+    from orb_slam2_2021_amd.frames import DeviceMapPointGeometry
+    G, frames = _scene()
+    Gd = DeviceMapPointGeometry(G, device=torch.device("cuda", 0))
+    m = ORBmatcher(0.8, True)
+    nh, lh = m.isInFrustum(frames[0], G)
+    nd, ld = m.isInFrustum(frames[0], Gd)
+    assert nh == nd and nh > 0
+    assert np.array_equal(lh.flags, ld.flags) and np.array_equal(lh.proj_x, ld.proj_x)
+
+
+def test_device_geometry_rejects_host_tensors():
+    from orb_slam2_2021_amd.frames import DeviceMapPointGeometry
+    t = {f: torch.zeros(64, dtype=torch.uint8) for f in DeviceMapPointGeometry.FIELDS}
+    with pytest.raises(ValueError):
+        DeviceMapPointGeometry(tensors=t, m=1)
