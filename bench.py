@@ -810,7 +810,7 @@ def c5_frame(ext, img, tcw):
                    max_x=640.0, min_y=0.0, max_y=480.0, tcw=tcw, **S.ARDUCAM_CAM)
 
 
-def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=64):
+def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=192):
     """BASELINE config C5: a 640x480 stream through Tracking::SearchLocalPoints' hot part --
     Frame::isInFrustum(pMP, 0.5) for every MapPoint of the local map, then
     ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th=3) (Tracking.cc:1186-1213) -- with
@@ -876,7 +876,7 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=64):
     # the device part alone (no extraction, no PCIe)
     m.set_profiling(True)
     dev_ms, rounds = [], []
-    for _ in range(3):
+    for _ in range(1):
         for F in frames:
             m.SearchLocalPoints(F, Gd, 3.0)
             dev_ms.append(m.last_device_ms())
