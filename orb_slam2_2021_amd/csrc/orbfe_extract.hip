@@ -439,16 +439,27 @@ __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
   const int sh = (int)(reinterpret_cast<uintptr_t>(src) & 3);
   const uint32_t* p = reinterpret_cast<const uint32_t*>(src - sh);
   const int nd = (sh + w + 3) >> 2;  // dwords holding columns 0..w-1 (and up to 3 bytes before)
-  for (int i = lane; i < nd; i += 64) {
-    uint32_t v;
-    if (4 * i + 4 <= sh + w) {
-      v = p[i];
-    } else {  // the row's last dword: only its bytes inside the row
-      v = 0;
-      for (int j = 0; j < 4; j++)
-        if (4 * i + j >= sh && 4 * i + j < sh + w) v |= (uint32_t)src[4 * i + j - sh] << (8 * j);
-    }
-    s[i] = v;
+  const int nfull = (sh + w) >> 2;   // dwords wholly inside the row
+  // the row's whole dwords: up to 8 per lane issued before any is stored (one memory latency per
+  // row instead of one per 64 dwords; rows up to 2048 dwords), a strided loop past that
+  constexpr int CU = 8;
+  uint32_t v8[CU];
+#pragma unroll
+  for (int k = 0; k < CU; k++) {
+    const int i = lane + 64 * k;
+    v8[k] = i < nfull ? p[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < CU; k++) {
+    const int i = lane + 64 * k;
+    if (i < nfull) s[i] = v8[k];
+  }
+  for (int i = lane + 64 * CU; i < nfull; i += 64) s[i] = p[i];
+  if (lane == 0 && nfull < nd) {  // the row's last dword: only its bytes inside the row
+    uint32_t v = 0;
+    for (int j = 0; j < 4; j++)
+      if (4 * nfull + j >= sh && 4 * nfull + j < sh + w) v |= (uint32_t)src[4 * nfull + j - sh] << (8 * j);
+    s[nfull] = v;
   }
   wave_sync();
   uint8_t* row = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off - 4 + (long long)y * ld.pitch;
