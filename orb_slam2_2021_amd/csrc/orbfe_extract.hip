@@ -342,13 +342,17 @@ __device__ __forceinline__ uint32_t resize_win_row(const uint32_t W0r0, const ui
 // stream: per-row byte offsets from the row indices in ywin.w, dword-aligned loads from the
 // aligned image base and a per-row v_alignbyte shift; the buffer's extent ends at the last
 // input byte, so the window of a row's last group past the image end reads zeros (unused taps).
+#ifndef ORBFE_RESIZE_PAIRS
+#define ORBFE_RESIZE_PAIRS 1  // k_resize_win: output row pairs per thread (2 and 4 measured slower)
+#endif
 template <bool SRC_IN>
 __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G, uint32_t gmagic) {
+  constexpr int RP = ORBFE_RESIZE_PAIRS;
   const LevelDesc ld = a.levels[l];
   const int item = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
   const int pr = gmagic ? (int)__umulhi((uint32_t)item, gmagic) : item;  // item / G
   const int g = item - pr * G, x = 4 * g;
-  const int y0 = 2 * pr;
+  const int y0 = 2 * RP * pr;
   if (y0 >= ld.h) return;
   const LevelDesc ls = a.levels[l - 1];
   // the source level as dwords from a wave-uniform base; per-lane offsets are 32-bit unsigned
@@ -357,65 +361,78 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
   const uint32_t gi = (uint32_t)(ld.rgrp_begin + g);
   const uint32_t sx0 = (uint32_t)a.rgx0[gi];
   const uint4 sel = a.rgrp[2 * gi], alp16 = a.rgrp[2 * gi + 1];
-  const bool two = y0 + 1 < ld.h;
-  const int4 ya = a.ywin[(uint32_t)(ld.tab_y + y0)], yb = a.ywin[(uint32_t)(ld.tab_y + (two ? y0 + 1 : y0))];
   const uint32_t cx = sx0 >> 2;
-  const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
-  uint32_t wv[4][3];
-  uint32_t W0[4], W1[4];
-  if constexpr (!SRC_IN) {
-    // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
+  // every source row of the thread's RP output row pairs in flight before the first is used
+  uint32_t W0[RP][4], W1[RP][4];
+  int yz[RP][2];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+  for (int q = 0; q < RP; q++) {
+    const int ra = min(y0 + 2 * q, ld.h - 1), rb = min(y0 + 2 * q + 1, ld.h - 1);
+    const int4 ya = a.ywin[(uint32_t)(ld.tab_y + ra)], yb = a.ywin[(uint32_t)(ld.tab_y + rb)];
+    yz[q][0] = ya.z;
+    yz[q][1] = yb.z;
+    uint32_t wv[4][3];
+    if constexpr (!SRC_IN) {
+      const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
+      // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
-    }
-    const int sh = (int)(sx0 & 3u);
+      for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
-      W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
-    }
-  } else {
-    const uint8_t* ib = a.img0 + (long long)img * a.img_stride;
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(ib) & 3u);
-    const LevelDesc l0 = a.levels[0];
-    const long long extent = (long long)(a.n_images - 1 - img) * a.img_stride + (long long)(l0.h - 1) * a.img_pitch + l0.w + mis;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ib - mis), 0, (int)min(extent, 0x7fffffffll), 0x00020000);
-    const uint32_t ri[4] = {(uint32_t)ya.w & 0xffffu, (uint32_t)ya.w >> 16, (uint32_t)yb.w & 0xffffu, (uint32_t)yb.w >> 16};
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint32_t b = ri[r] * (uint32_t)a.img_pitch + sx0 + mis;
-      if ((long long)(b & ~3u) + 12 <= extent) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b & ~3u) + 4 * k, 0, 0);
-      } else {  // the image block's last bytes: a dword past the extent would read as all zeros
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          uint32_t v = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++)
-            v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(b & ~3u) + 4 * k + j, 0, 0) << (8 * j);
-          wv[r][k] = v;
-        }
+        for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
       }
-      W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], b & 3u);
-      W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], b & 3u);
+      const int sh = (int)(sx0 & 3u);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        W0[q][r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
+        W1[q][r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
+      }
+    } else {
+      const uint8_t* ib = a.img0 + (long long)img * a.img_stride;
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(ib) & 3u);
+      const LevelDesc l0 = a.levels[0];
+      const long long extent = (long long)(a.n_images - 1 - img) * a.img_stride + (long long)(l0.h - 1) * a.img_pitch + l0.w + mis;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ib - mis), 0, (int)min(extent, 0x7fffffffll), 0x00020000);
+      const uint32_t ri[4] = {(uint32_t)ya.w & 0xffffu, (uint32_t)ya.w >> 16, (uint32_t)yb.w & 0xffffu, (uint32_t)yb.w >> 16};
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t b = ri[r] * (uint32_t)a.img_pitch + sx0 + mis;
+        if ((long long)(b & ~3u) + 12 <= extent) {
+#pragma unroll
+          for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b & ~3u) + 4 * k, 0, 0);
+        } else {  // the image block's last bytes: a dword past the extent would read as all zeros
+#pragma unroll
+          for (int k = 0; k < 3; k++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+              v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(b & ~3u) + 4 * k + j, 0, 0) << (8 * j);
+            wv[r][k] = v;
+          }
+        }
+        W0[q][r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], b & 3u);
+        W1[q][r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], b & 3u);
+      }
     }
-  }
-  const int2 ba = make_int2(0, ya.z), bb = make_int2(0, yb.z);
-  uint32_t pa, pb;
-  if (x + 4 <= ld.simd_end) {  // every column on the SIMD128 rounding (all but a row's tail)
-    pa = resize_win_row<false>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
-    pb = resize_win_row<false>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
-  } else {
-    pa = resize_win_row<true>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
-    pb = resize_win_row<true>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
   }
   uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-  store_row4(out + __umul24((uint32_t)y0, (uint32_t)ld.pitch), x, ld.w, pa);
-  if (two) store_row4(out + __umul24((uint32_t)(y0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
+  const bool simd = x + 4 <= ld.simd_end;  // every column on the SIMD128 rounding (all but a row's tail)
+#pragma unroll
+  for (int q = 0; q < RP; q++) {
+    const int ya0 = y0 + 2 * q;
+    if (ya0 >= ld.h) break;
+    const int2 ba = make_int2(0, yz[q][0]), bb = make_int2(0, yz[q][1]);
+    uint32_t pa, pb;
+    if (simd) {
+      pa = resize_win_row<false>(W0[q][0], W1[q][0], W0[q][1], W1[q][1], sel, alp16, x, ld, ba);
+      pb = resize_win_row<false>(W0[q][2], W1[q][2], W0[q][3], W1[q][3], sel, alp16, x, ld, bb);
+    } else {
+      pa = resize_win_row<true>(W0[q][0], W1[q][0], W0[q][1], W1[q][1], sel, alp16, x, ld, ba);
+      pb = resize_win_row<true>(W0[q][2], W1[q][2], W0[q][3], W1[q][3], sel, alp16, x, ld, bb);
+    }
+    store_row4(out + __umul24((uint32_t)ya0, (uint32_t)ld.pitch), x, ld.w, pa);
+    if (ya0 + 1 < ld.h) store_row4(out + __umul24((uint32_t)(ya0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
+  }
 }
 
 
@@ -3092,7 +3109,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     for (int l = 1; l < h->nlevels; l++) {
       const LevelDesc& d = h->levels[l];
       if (d.rwin_ok) {
-        const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
+        const int G = (d.w + 3) / 4, items = G * ((d.h + 2 * ORBFE_RESIZE_PAIRS - 1) / (2 * ORBFE_RESIZE_PAIRS));
         const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
         dim3 grid((items + 255) / 256, n);
         if (l == 1 && c0side)
