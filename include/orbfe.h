@@ -117,14 +117,20 @@ int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p,
 int orbfe_get_level_device(orbfe_extractor* h, int image, int level, const uint8_t** d_p,
                            int* rows, int* cols, size_t* step);
 
-/* Per-kernel timing with HIP events recorded on the launch stream around the selected kernels.
- * kernel_mask: 0 = off, -1 = every kernel, else bit k selects kernel k of orbfe_get_kernel_times'
- * order (k_resize, k_fast, k_octree, k_describe, k_copy0, k_blur). orbfe_get_kernel_times
- * synchronises and returns, per kernel, the accumulated milliseconds and launch count. */
-int orbfe_set_profiling(orbfe_extractor* h, int kernel_mask);
-int orbfe_get_kernel_times(orbfe_extractor* h, char* names, int name_len, double* total_ms,
-                           int32_t* launches, int cap, int* n);
-int orbfe_reset_kernel_times(orbfe_extractor* h);
+/* Process-wide device-execution timing of the library's kernels (every handle, every thread).
+ * orbfe_ktimer_select: comma-separated kernel names as rocprofv3 shows them without template
+ * arguments ("k_fast,k_describe"), "*" for every kernel, "" or NULL for none. A selected launch
+ * carries a start and a stop HIP event bound to the dispatch itself (hipExtLaunchKernelGGL), so
+ * its time is the kernel's own execution interval -- what rocprofv3 --kernel-trace reports --
+ * and excludes the queue's wait for earlier packets. orbfe_ktimer_read synchronises on the
+ * pending launches and returns, per kernel timed since the process started (first-timed order),
+ * the accumulated milliseconds and launch count; name_len bytes per name. ORBFE_ERR_CAPACITY
+ * when more than `cap` kernels were timed (*n holds the count). orbfe_ktimer_reset zeroes the
+ * totals. */
+int orbfe_ktimer_select(const char* names);
+int orbfe_ktimer_read(char* names, int name_len, double* total_ms, long long* launches, int cap,
+                      int* n);
+int orbfe_ktimer_reset(void);
 
 /* Stream the handle launches on (hipStream_t as void*). */
 void* orbfe_extractor_stream(orbfe_extractor* h);

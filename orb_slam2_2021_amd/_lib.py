@@ -110,10 +110,9 @@ _SIGNATURES = {
                                 POINTER(c_int), POINTER(c_size_t)]),
     "orbfe_get_level_device": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int),
                                        POINTER(c_int), POINTER(c_size_t)]),
-    "orbfe_set_profiling": (c_int, [c_void_p, c_int]),
-    "orbfe_get_kernel_times": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
-                                       POINTER(c_int)]),
-    "orbfe_reset_kernel_times": (c_int, [c_void_p]),
+    "orbfe_ktimer_select": (c_int, [ctypes.c_char_p]),
+    "orbfe_ktimer_read": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, POINTER(c_int)]),
+    "orbfe_ktimer_reset": (c_int, []),
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
     "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
     "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
@@ -274,3 +273,40 @@ def ptr(a) -> c_void_p:
     if hasattr(a, "data_ptr"):  # torch tensor (device plumbing)
         return c_void_p(a.data_ptr())
     raise TypeError(f"cannot take the address of {type(a)}")
+
+
+# ---- process-wide kernel timer (orbfe_ktimer_*, include/orbfe.h) ----------------------------------
+def ktimer_select(kernels) -> None:
+    """Time these kernels' launches by their own dispatch interval (what rocprofv3's kernel trace
+    reports): an iterable of names ("k_fast", ...), "*" / True for every kernel, None / False /
+    empty for none."""
+    if kernels is True:
+        v = "*"
+    elif not kernels:
+        v = ""
+    elif isinstance(kernels, str):
+        v = kernels
+    else:
+        v = ",".join(kernels)
+    check(lib().orbfe_ktimer_select(v.encode()), "ktimer_select")
+
+
+def ktimer_read() -> dict:
+    """{kernel: (total ms, launches)} of every kernel timed so far (synchronises)."""
+    cap, name_len = 64, 48
+    names = ctypes.create_string_buffer(cap * name_len)
+    total = np.zeros(cap, np.float64)
+    launches = np.zeros(cap, np.int64)
+    n = c_int()
+    check(lib().orbfe_ktimer_read(names, name_len, ptr(total), ptr(launches), cap, ctypes.byref(n)),
+          "ktimer_read")
+    out = {}
+    for k in range(n.value):
+        nm = names.raw[k * name_len:(k + 1) * name_len].split(b"\0", 1)[0].decode()
+        if launches[k] > 0:
+            out[nm] = (float(total[k]), int(launches[k]))
+    return out
+
+
+def ktimer_reset() -> None:
+    check(lib().orbfe_ktimer_reset(), "ktimer_reset")

@@ -30,6 +30,7 @@
 #include "../../include/orbfe_keyframe.h"
 #include "orbfe_device.h"
 #include "orbfe_match_internal.h"
+#include "orbfe_ktimer.h"
 
 using namespace orbfe_mi;
 
@@ -614,9 +615,9 @@ int run_bow(orbfe_matcher* m, int mode, int n_pairs, const orbfe_frame_view* As,
   stage_h2d(m, A + opairs, pairs.data(), sizeof(BowPair) * n_pairs);
   if ((st = flush_h2d(m))) return st;
   const BowPair* dp = (const BowPair*)(A + opairs);
-  hipLaunchKernelGGL(k_bow_init, dim3(n_pairs), dim3(256), 0, m->stream, dp);
-  hipLaunchKernelGGL(k_bow_nodes, dim3((max_nodes + 3) / 4, n_pairs), dim3(256), 0, m->stream, dp, m->nnratio);
-  hipLaunchKernelGGL(k_bow_finish, dim3(n_pairs), dim3(256), 0, m->stream, dp, m->check_ori);
+  ORBFE_LAUNCH("k_bow_init", k_bow_init, dim3(n_pairs), dim3(256), 0, m->stream, dp);
+  ORBFE_LAUNCH("k_bow_nodes", k_bow_nodes, dim3((max_nodes + 3) / 4, n_pairs), dim3(256), 0, m->stream, dp, m->nnratio);
+  ORBFE_LAUNCH("k_bow_finish", k_bow_finish, dim3(n_pairs), dim3(256), 0, m->stream, dp, m->check_ori);
   ORBFE_HIP_CHECK(hipGetLastError());
   size_t off = 0;
   for (int p = 0; p < n_pairs; p++) {  // mode 0: per Frame keypoint; mode 1: per KF1 keypoint
@@ -722,7 +723,7 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   InitQueryArgs qa{n1, n2, d1.keys_un, (const float*)(A + oprev), (float)window_size, (SbpQuery*)(A + p.oq),
                    dec[1], cnt[0], cnt[2], state};
   const int qn = std::max(std::max(n1, n2), INIT_STATE_INTS);
-  hipLaunchKernelGGL(k_init_queries, dim3((qn + 255) / 256), dim3(256), 0, m->stream, qa);
+  ORBFE_LAUNCH("k_init_queries", k_init_queries, dim3((qn + 255) / 256), dim3(256), 0, m->stream, qa);
   sbp_launch_round0(m, p, f2, d2, SbpMode{1, TH_LOW, SBP_BLOCK_NONE, 0, 0});
   // the claim order: fixpoint rounds (each exits at once after convergence), then the finish
   InitFixArgs fa;
@@ -745,7 +746,7 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
     fa.slots_cur = slots[r % 3];
     fa.cnt_cur = cnt[r % 3];
     fa.cnt_next = cnt[(r + 1) % 3];
-    hipLaunchKernelGGL(k_init_round, dim3(gx), dim3(256), 0, m->stream, fa);
+    ORBFE_LAUNCH("k_init_round", k_init_round, dim3(gx), dim3(256), 0, m->stream, fa);
   }
   InitSeqArgs sa;
   std::memset(&sa, 0, sizeof(sa));
@@ -772,7 +773,7 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   }
   const size_t lds = sizeof(int) * (2 * n2s + HISTO_LENGTH + 4);
   if (lds > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_search_for_initialization: F2 too large");
-  hipLaunchKernelGGL(k_init_seq, dim3(1), dim3(64), lds, m->stream, sa);
+  ORBFE_LAUNCH("k_init_seq", k_init_seq, dim3(1), dim3(64), lds, m->stream, sa);
   ORBFE_HIP_CHECK(hipGetLastError());
   int32_t nm = 0;
   ORBFE_HIP_CHECK(hipMemcpyAsync(match12, A + om, 4 * (size_t)n1, hipMemcpyDeviceToHost, m->stream));
@@ -791,7 +792,7 @@ extern "C" int orbfe_compute_distinctive_descriptors_device(orbfe_matcher* m, in
   if (n_points == 0) return ORBFE_OK;
   hipSetDevice(m->device);
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
-  hipLaunchKernelGGL(k_distinctive, dim3((n_points + 3) / 4), dim3(256), 0, s, n_points, d_offsets, d_descriptors,
+  ORBFE_LAUNCH("k_distinctive", k_distinctive, dim3((n_points + 3) / 4), dim3(256), 0, s, n_points, d_offsets, d_descriptors,
                      d_best_index);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;

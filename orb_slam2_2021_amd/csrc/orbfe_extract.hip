@@ -44,6 +44,7 @@
 #include "orb_pattern31.inc"
 #include "orbfe_device.h"
 #include "orbfe_internal.h"
+#include "orbfe_ktimer.h"
 
 // ---------------------------------------------------------------------------------------------
 // errors
@@ -2065,7 +2066,15 @@ struct DwX3 {
 #define ORBFE_DESC_WPB 4  // k_describe wavefronts per workgroup (4 keypoints each)
 #endif
 constexpr int DESC_THREADS = 64 * ORBFE_DESC_WPB;
-__global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
+#ifndef ORBFE_DESC_OCC
+#define ORBFE_DESC_OCC 0
+#endif
+#if ORBFE_DESC_OCC
+#define DESC_OCC_ATTR __attribute__((amdgpu_waves_per_eu(ORBFE_DESC_OCC)))
+#else
+#define DESC_OCC_ATTR
+#endif
+__global__ __launch_bounds__(DESC_THREADS) DESC_OCC_ATTR void k_describe(ExtractArgs a) {
   __shared__ float4 s_pat[256];
   __shared__ uint32_t s_mom[4 * 279];
   __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * ORBFE_DESC_WPB][37 * 10];
@@ -2294,11 +2303,6 @@ inline short h_sat_short(float v) {
 }
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-struct KernelTimer {
-  int kernel;
-  hipEvent_t e0, e1;
-};
-
 }  // namespace
 
 // Fork/join events between the extractor's two streams order device work only (nothing on the
@@ -2450,30 +2454,9 @@ struct orbfe_extractor {
   long long last_img_stride = 0;
   int last_img_pitch = 0, last_n = 0;
   std::vector<uint8_t> level_host;
-  // profiling
-  int profile_mask = 0;  // bit k: time kernel k with HIP events
-  std::vector<KernelTimer> pending;
-  std::vector<hipEvent_t> event_pool;
-  double ktime[8] = {0};
   // Frame::ComputeStereoMatches scratch (orbfe_stereo.hip)
   OrbfeStereoScratch* stereo = nullptr;
-  int klaunch[8] = {0};
 };
-
-static const char* kKernelNames[] = {"k_resize", "k_fast", "k_octree", "k_describe", "k_copy0",
-                                     "k_blur", "k_pyramid"};
-static const int kNumKernels = 7;
-
-static hipEvent_t pool_event(orbfe_extractor* h) {
-  if (!h->event_pool.empty()) {
-    hipEvent_t e = h->event_pool.back();
-    h->event_pool.pop_back();
-    return e;
-  }
-  hipEvent_t e;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
-  return e;
-}
 
 // k_pyramid plan. Groups: levels 1..3 from the input image, then up to 4 levels per group from
 // the previous group's top. Own pieces: x boundaries at multiples of 4 (one writer per 4-column
@@ -2936,22 +2919,6 @@ static size_t fast_lds(const orbfe_extractor* h) {
   return 4 * (size_t)fast_lds_layout(h->roi_w_max, h->roi_h_max, fast_rs(h)).total;
 }
 
-#define LAUNCH_TIMED(h, kid, stream, ...)                          \
-  do {                                                             \
-    hipEvent_t _e0 = nullptr, _e1 = nullptr;                       \
-    const bool _prof = ((h)->profile_mask >> (kid)) & 1;           \
-    if (_prof) {                                                   \
-      _e0 = pool_event(h);                                         \
-      _e1 = pool_event(h);                                         \
-      hipEventRecord(_e0, stream);                                 \
-    }                                                              \
-    __VA_ARGS__;                                                   \
-    if (_prof) {                                                   \
-      hipEventRecord(_e1, stream);                                 \
-      (h)->pending.push_back(KernelTimer{kid, _e0, _e1});          \
-    }                                                              \
-  } while (0)
-
 // How many levels, from level 0 up, get their FAST launch on the side stream as soon as the main
 // stream has built them; the rest run in one launch after the resize chain. Measured on MI355X
 // (C3 bench, stereo frames/s): 1 level 67.6k, 2 levels 68.7k, 3 levels 69.1-69.4k, 4 levels
@@ -3038,9 +3005,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     dim3 grid((c1 - c0 + wpb - 1) / wpb, n);
     const size_t lds = fast_lds(h) / 4 * wpb;
     if (fast_rs(h) == 68)
-      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<68>, grid, dim3(64 * wpb), lds, s, a, c0, c1));
+      ORBFE_LAUNCH("k_fast", k_fast<68>, grid, dim3(64 * wpb), lds, s, a, c0, c1);
     else
-      LAUNCH_TIMED(h, 1, s, hipLaunchKernelGGL(k_fast<0>, grid, dim3(64 * wpb), lds, s, a, c0, c1));
+      ORBFE_LAUNCH("k_fast", k_fast<0>, grid, dim3(64 * wpb), lds, s, a, c0, c1);
     return ORBFE_OK;
   };
   // k_side: the levels whose FAST cells run on the side stream, beside the rest of the pyramid
@@ -3053,7 +3020,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     for (size_t gi = 0; gi < h->pyr_groups.size(); gi++) {
       const PyrGroup& pg = h->pyr_groups[gi];
       dim3 grid(pg.ntx * pg.nty, n);
-      LAUNCH_TIMED(h, 6, st, hipLaunchKernelGGL(k_pyramid, grid, dim3(256), pg.buf0 + pg.buf1 + pg.tab, st, a, pg));
+      ORBFE_LAUNCH("k_pyramid", k_pyramid, grid, dim3(256), pg.buf0 + pg.buf1 + pg.tab, st, a, pg);
       if (gi == 0) {
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
         ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
@@ -3076,12 +3043,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));  // the input is ready on st
         ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
-        LAUNCH_TIMED(h, 4, side, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, side, a));
+        ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, side, a);
 #endif
         ORBFE_HIP_CHECK(hipEventRecord(h->ev_c0, side));
       } else {
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
-        LAUNCH_TIMED(h, 4, st, hipLaunchKernelGGL(k_copy0, grid, dim3(256), lds, st, a));
+        ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, st, a);
 #endif
       }
     }
@@ -3113,12 +3080,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
         const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
         dim3 grid((items + 255) / 256, n);
         if (l == 1 && c0side)
-          LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win<true>, grid, dim3(256), 0, st, a, l, G, gm));
+          ORBFE_LAUNCH("k_resize_win", k_resize_win<true>, grid, dim3(256), 0, st, a, l, G, gm);
         else
-          LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize_win<false>, grid, dim3(256), 0, st, a, l, G, gm));
+          ORBFE_LAUNCH("k_resize_win", k_resize_win<false>, grid, dim3(256), 0, st, a, l, G, gm);
       } else {
         dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
-        LAUNCH_TIMED(h, 0, st, hipLaunchKernelGGL(k_resize, grid, block, 0, st, a, l));
+        ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
       }
       if (l < k_side) side_fast(l);
     }
@@ -3130,7 +3097,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   auto launch_octree = [&](hipStream_t s, int l0, int nl) {
     if (nl <= 0) return;
     dim3 grid(nl, n);
-    LAUNCH_TIMED(h, 2, s, hipLaunchKernelGGL(k_octree, grid, dim3(256), octree_lds(h), s, a, l0));
+    ORBFE_LAUNCH("k_octree", k_octree, grid, dim3(256), octree_lds(h), s, a, l0);
   };
   // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
   // only the pyramid, so it runs on the side stream beside k_octree (a small, latency-bound grid
@@ -3144,7 +3111,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
-    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
+    ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
 #endif
   }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
@@ -3154,20 +3121,20 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
-    LAUNCH_TIMED(h, 5, side, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a));
+    ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
 #endif
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   launch_octree(st, 0, h->nlevels);
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
 #if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
-    LAUNCH_TIMED(h, 5, st, hipLaunchKernelGGL(k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a));
+    ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a);
 #endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
     constexpr int per_block = 4 * ORBFE_DESC_WPB;  // keypoints per workgroup
     dim3 grid((h->total_key_slots + per_block - 1) / per_block, n);
-    LAUNCH_TIMED(h, 3, st, hipLaunchKernelGGL(k_describe, grid, dim3(DESC_THREADS), 0, st, a));
+    ORBFE_LAUNCH("k_describe", k_describe, grid, dim3(DESC_THREADS), 0, st, a);
   }
   ORBFE_HIP_CHECK(hipGetLastError());
   h->last_img0 = d_imgs - (long long)i0 * img_stride;
@@ -3314,11 +3281,6 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   for (auto e : h->ev_out) hipEventDestroy(e);
   if (h->h2d) hipStreamDestroy(h->h2d);
   if (h->d2h) hipStreamDestroy(h->d2h);
-  for (auto& p : h->pending) {
-    hipEventDestroy(p.e0);
-    hipEventDestroy(p.e1);
-  }
-  for (auto e : h->event_pool) hipEventDestroy(e);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->side) hipStreamDestroy(h->side);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -3715,55 +3677,6 @@ extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const u
   *p = h->level_host.data();
   *step = (size_t)(*cols);
   return ORBFE_OK;
-}
-
-extern "C" int orbfe_set_profiling(orbfe_extractor* h, int kernel_mask) {
-  if (!h) return ORBFE_ERR_ARG;
-  h->profile_mask = kernel_mask;
-  return ORBFE_OK;
-}
-
-static int drain_timers(orbfe_extractor* h) {
-  if (h->pending.empty()) return ORBFE_OK;
-  ORBFE_HIP_CHECK(hipEventSynchronize(h->pending.back().e1));
-  for (auto& p : h->pending) {
-    float ms = 0.f;
-    if (hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
-      h->ktime[p.kernel] += ms;
-      h->klaunch[p.kernel] += 1;
-    }
-    h->event_pool.push_back(p.e0);
-    h->event_pool.push_back(p.e1);
-  }
-  h->pending.clear();
-  return ORBFE_OK;
-}
-
-extern "C" int orbfe_get_kernel_times(orbfe_extractor* h, char* names, int name_len,
-                                      double* total_ms, int32_t* launches, int cap, int* n) {
-  if (!h || !n) return ORBFE_ERR_ARG;
-  const int st = drain_timers(h);
-  if (st != ORBFE_OK) return st;
-  *n = kNumKernels;
-  for (int k = 0; k < kNumKernels && k < cap; k++) {
-    if (names && name_len > 0) {
-      std::strncpy(names + (size_t)k * name_len, kKernelNames[k], name_len - 1);
-      names[(size_t)k * name_len + name_len - 1] = 0;
-    }
-    if (total_ms) total_ms[k] = h->ktime[k];
-    if (launches) launches[k] = h->klaunch[k];
-  }
-  return ORBFE_OK;
-}
-
-extern "C" int orbfe_reset_kernel_times(orbfe_extractor* h) {
-  if (!h) return ORBFE_ERR_ARG;
-  const int st = drain_timers(h);
-  for (int k = 0; k < 8; k++) {
-    h->ktime[k] = 0;
-    h->klaunch[k] = 0;
-  }
-  return st;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -33,6 +33,7 @@
 #include "../../include/orbfe_match_batch.h"
 #include "orbfe_device.h"
 #include "orbfe_match_internal.h"
+#include "orbfe_ktimer.h"
 
 using namespace orbfe_mi;
 
@@ -1422,7 +1423,7 @@ extern "C" int orbfe_descriptor_distance_batch(orbfe_matcher* m, const uint8_t* 
   if (st) return st;
   ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + oa, a, 32 * (size_t)n, hipMemcpyHostToDevice, m->stream));
   ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + ob, b, 32 * (size_t)n, hipMemcpyHostToDevice, m->stream));
-  hipLaunchKernelGGL(k_hamming_batch, dim3((n + 255) / 256), dim3(256), 0, m->stream, m->arena + oa,
+  ORBFE_LAUNCH("k_hamming_batch", k_hamming_batch, dim3((n + 255) / 256), dim3(256), 0, m->stream, m->arena + oa,
                      m->arena + ob, n, (int32_t*)(m->arena + oo));
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_HIP_CHECK(hipMemcpyAsync(out, m->arena + oo, 4 * (size_t)n, hipMemcpyDeviceToHost, m->stream));
@@ -1458,9 +1459,9 @@ extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int
   int max_nodes = 1;
   for (int p = 0; p < n_pairs; p++) max_nodes = std::max(max_nodes, pairs[p].fv1.n_nodes);
   // (max_nodes + 3) / 4 workgroups of node wavefronts + one for the features no node lists
-  hipLaunchKernelGGL(k_sft_nodes, dim3((max_nodes + 3) / 4 + 1, n_pairs), dim3(256), 0, s, m->d_pairs,
+  ORBFE_LAUNCH("k_sft_nodes", k_sft_nodes, dim3((max_nodes + 3) / 4 + 1, n_pairs), dim3(256), 0, s, m->d_pairs,
                      only_stereo ? 1 : 0);
-  hipLaunchKernelGGL(k_sft_finish, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, m->check_ori);
+  ORBFE_LAUNCH("k_sft_finish", k_sft_finish, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, m->check_ori);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }
@@ -1599,7 +1600,7 @@ static GridArgs grid_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* 
 
 void sbp_launch_grid(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF) {
   const GridArgs g = grid_args(m->arena, p, F, dF);
-  hipLaunchKernelGGL(k_grid, dim3(1), dim3(1024), sizeof(int) * (GRID_CELLS + 1 + 16 + std::max(F->n, 1)),
+  ORBFE_LAUNCH("k_grid", k_grid, dim3(1), dim3(1024), sizeof(int) * (GRID_CELLS + 1 + 16 + std::max(F->n, 1)),
                      m->stream, g);
 }
 
@@ -1643,7 +1644,7 @@ static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_fram
   in.nq = std::max(p.nq, 1);
   in.nf = std::max(F->n, 1);
   const int nthreads = std::max(std::max(in.nq, in.nf), SBP_ROUND_CAP + 4);
-  hipLaunchKernelGGL(k_sbp_init, dim3((nthreads + 255) / 256), dim3(256), 0, m->stream, in);
+  ORBFE_LAUNCH("k_sbp_init", k_sbp_init, dim3((nthreads + 255) / 256), dim3(256), 0, m->stream, in);
 }
 
 void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
@@ -1659,7 +1660,7 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
   a.owner_prev = (int32_t*)(A + p.oown3);
   a.owner_next = (int32_t*)(A + p.oown1);
   if (p.nq > 0)
-    hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((p.nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+    ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((p.nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                        m->stream, a);
 }
 
@@ -1691,10 +1692,10 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
     // since can reach
     a.owner_rm2 = r >= 2 && p.cache && !sbp_dense_rounds() ? own[(r + 2) % 4] : nullptr;
     if (r == 0 && p.cache)
-      hipLaunchKernelGGL(k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+      ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                          m->stream, a);
     else
-      hipLaunchKernelGGL(k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
+      ORBFE_LAUNCH("k_sbp_round", k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
   }
   SbpFinishArgs f;
   std::memset(&f, 0, sizeof(f));
@@ -1708,8 +1709,8 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
   f.serial_used = m->d_serial;
   f.defer = defer ? 1 : 0;
   if (nq > 0) {
-    hipLaunchKernelGGL(k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
-    hipLaunchKernelGGL(k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
+    ORBFE_LAUNCH("k_sbp_collect", k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
+    ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
   }
 }
 
@@ -1862,7 +1863,7 @@ extern "C" int orbfe_search_by_projection_local(orbfe_matcher* m, const orbfe_fr
     qa.scale_factors = dF.scale_factors;
     qa.th = th;
     qa.q = dq;
-    hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
+    ORBFE_LAUNCH("k_sbp_local_queries", k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
   return run_sbp(m, F, M, SbpMode{0, TH_HIGH, 0, 0}, mps->descriptors, nullptr, plan, make, best_idx, nmatches);
@@ -1927,7 +1928,7 @@ extern "C" int orbfe_search_by_projection_lastframe(orbfe_matcher* m,
     qa.backward = bwd;
     qa.th = th;
     qa.q = dq;
-    hipLaunchKernelGGL(k_sbp_last_queries, dim3((N + 255) / 256), dim3(256), 0, m->stream, qa);
+    ORBFE_LAUNCH("k_sbp_last_queries", k_sbp_last_queries, dim3((N + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
   return run_sbp(m, C, N, SbpMode{1, TH_HIGH, 0, m->check_ori}, L->descriptors, L->angle, plan, make, best_idx,
@@ -2028,7 +2029,7 @@ static int launch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, co
   fa.out.level = (int32_t*)(A + p.o_lvl);
   fa.out.view_cos = (float*)(A + p.o_vc);
   fa.n_in_view = (int32_t*)(A + p.counter);
-  if (G->m > 0) hipLaunchKernelGGL(k_frustum, dim3((G->m + 255) / 256), dim3(256), 0, m->stream, fa);
+  if (G->m > 0) ORBFE_LAUNCH("k_frustum", k_frustum, dim3((G->m + 255) / 256), dim3(256), 0, m->stream, fa);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }
@@ -2102,7 +2103,7 @@ extern "C" int orbfe_search_local_points(orbfe_matcher* m, const orbfe_frame_vie
     qa.scale_factors = dF.scale_factors;
     qa.th = th;
     qa.q = dq;
-    hipLaunchKernelGGL(k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
+    ORBFE_LAUNCH("k_sbp_local_queries", k_sbp_local_queries, dim3((M + 255) / 256), dim3(256), 0, m->stream, qa);
     return ORBFE_OK;
   };
   int st = run_sbp(m, F, M, SbpMode{0, TH_HIGH, 0, 0}, G->descriptors, nullptr, plan, make, best_idx, nmatches);

@@ -7,6 +7,7 @@
 #include "../../include/orbfe.h"
 #include "../../include/orbfe_pack.h"
 #include "orbfe_device.h"
+#include "orbfe_ktimer.h"
 
 static __host__ __device__ inline long long align16(long long x) { return (x + 15) & ~15ll; }
 
@@ -68,7 +69,7 @@ extern "C" int orbfe_pack_keypoints_device(int n_images, const int32_t* d_counts
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_pack_keypoints_device: n_images * cap must stay below 2^31");
   if (out_cap < orbfe_packed_bytes(n_images, (long long)n_images * cap))
     return orbfe_set_error(ORBFE_ERR_CAPACITY, "orbfe_pack_keypoints_device: out_cap below the worst case");
-  hipLaunchKernelGGL(k_pack, dim3(n_images), dim3(256), 0, (hipStream_t)stream, n_images, d_counts, d_kps,
+  ORBFE_LAUNCH("k_pack", k_pack, dim3(n_images), dim3(256), 0, (hipStream_t)stream, n_images, d_counts, d_kps,
                      d_desc, cap, d_out, d_total_bytes);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;

@@ -23,6 +23,7 @@
 #include "../../include/orbfe_keyframe.h"
 #include "orbfe_device.h"
 #include "orbfe_match_internal.h"
+#include "orbfe_ktimer.h"
 
 using namespace orbfe_mi;
 
@@ -243,7 +244,7 @@ void set_pose(ProjQueryArgs& qa, const Pose& p) {
 }
 void launch_queries(orbfe_matcher* m, const SbpPlan& p, ProjQueryArgs qa) {
   qa.q = (SbpQuery*)(m->arena + p.oq);
-  if (qa.m > 0) hipLaunchKernelGGL(k_proj_queries, dim3((qa.m + 255) / 256), dim3(256), 0, m->stream, qa);
+  if (qa.m > 0) ORBFE_LAUNCH("k_proj_queries", k_proj_queries, dim3((qa.m + 255) / 256), dim3(256), 0, m->stream, qa);
 }
 
 // One projection search: plan, stage frame + points, queries, engine, fetch.
@@ -393,7 +394,7 @@ extern "C" int orbfe_search_by_sim3(orbfe_matcher* m, const orbfe_frame_view* kf
   if ((st = sbp_launch(m, p1, kf2, d2, md))) return st;
   if ((st = sbp_launch(m, p2, kf1, d1, md))) return st;
   if (kf1->n > 0)
-    hipLaunchKernelGGL(k_sim3_agree, dim3((kf1->n + 255) / 256), dim3(256), 0, m->stream,
+    ORBFE_LAUNCH("k_sim3_agree", k_sim3_agree, dim3((kf1->n + 255) / 256), dim3(256), 0, m->stream,
                        (const int32_t*)(A + p1.obest), (const int32_t*)(A + p2.obest), kf1->n, kf2->n,
                        (int32_t*)(A + om), (int32_t*)(A + on));
   ORBFE_HIP_CHECK(hipGetLastError());

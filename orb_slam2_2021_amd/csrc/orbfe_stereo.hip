@@ -25,6 +25,7 @@
 #include "../../include/orbfe_stereo.h"
 #include "orbfe_device.h"
 #include "orbfe_internal.h"
+#include "orbfe_ktimer.h"
 
 namespace {
 
@@ -498,13 +499,13 @@ static int launch_stereo(OrbfeStereoScratch* S, const OrbfePyramid& PL, int pl0,
   }
   if (g.nbk == 1) g.rbo[0] = rb_all;
   const size_t lds = sizeof(int) * (g.nbk * (g.rows0 + 1) + 16);
-  hipLaunchKernelGGL(k_stereo_rows, dim3(n_pairs), dim3(ROWS_THREADS), lds, s, g, d_kps, d_counts,
+  ORBFE_LAUNCH("k_stereo_rows", k_stereo_rows, dim3(n_pairs), dim3(ROWS_THREADS), lds, s, g, d_kps, d_counts,
                      S->d_row_start, S->d_buckets);
   ORBFE_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
+  ORBFE_LAUNCH("k_stereo_match", k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
                      d_counts, S->d_row_start, S->d_buckets, d_u_right, d_depth, S->d_sad);
   ORBFE_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_stereo_median, dim3(n_pairs), dim3(256), 0, s, kl0, cap, d_counts, S->d_sad,
+  ORBFE_LAUNCH("k_stereo_median", k_stereo_median, dim3(n_pairs), dim3(256), 0, s, kl0, cap, d_counts, S->d_sad,
                      d_u_right, d_depth);
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;

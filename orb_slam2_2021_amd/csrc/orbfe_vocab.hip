@@ -40,6 +40,7 @@
 #include "../../include/orbfe.h"
 #include "../../include/orbfe_vocab.h"
 #include "orbfe_device.h"
+#include "orbfe_ktimer.h"
 
 #define VOCAB_MAX_FEATURES 8192
 #define VOCAB_MAX_CHILDREN (1 << 23)  // sibling index field of the min key
@@ -787,8 +788,8 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   // P2 keys, then (BowVector workgroups) P2 doubles
   P2 = P2 < VOCAB_THREADS ? VOCAB_THREADS : P2;  // k_vocab sorts at least one key per thread
   const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * (P2 + 128) : 0);
-  hipLaunchKernelGGL(k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
-  hipLaunchKernelGGL(k_vocab, dim3(n_images, d_bow_words && ORBFE_VOCAB_SPLIT ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
+  ORBFE_LAUNCH("k_vocab_descend", k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
+  ORBFE_LAUNCH("k_vocab", k_vocab, dim3(n_images, d_bow_words && ORBFE_VOCAB_SPLIT ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
                      (const unsigned long long*)fvk,
                      (const unsigned long long*)bwk, (const int32_t*)leaves);
   ORBFE_HIP_CHECK(hipGetLastError());

@@ -243,37 +243,6 @@ class ORBextractor:
         return [self.level(l) for l in range(self.nlevels)]
 
     # ---- instrumentation ----------------------------------------------------------------
-    KERNELS = ("k_resize", "k_fast", "k_octree", "k_describe", "k_copy0", "k_blur", "k_pyramid")
-
-    def set_profiling(self, kernels=True) -> None:
-        """True / False, or an iterable of kernel names to time with HIP events."""
-        if kernels is True:
-            mask = -1
-        elif not kernels:
-            mask = 0
-        else:
-            mask = 0
-            for k in kernels:
-                mask |= 1 << self.KERNELS.index(k)
-        L.check(self._lib.orbfe_set_profiling(self._h, mask), "set_profiling")
-
-    def kernel_times(self) -> dict:
-        cap, name_len = 16, 32
-        names = ctypes.create_string_buffer(cap * name_len)
-        total = np.zeros(cap, np.float64)
-        launches = np.zeros(cap, np.int32)
-        n = c_int()
-        L.check(self._lib.orbfe_get_kernel_times(self._h, names, name_len, L.ptr(total),
-                                                 L.ptr(launches), cap, byref(n)), "kernel_times")
-        out = {}
-        for k in range(n.value):
-            nm = names.raw[k * name_len:(k + 1) * name_len].split(b"\0", 1)[0].decode()
-            out[nm] = (float(total[k]), int(launches[k]))
-        return out
-
-    def reset_kernel_times(self) -> None:
-        L.check(self._lib.orbfe_reset_kernel_times(self._h), "reset_kernel_times")
-
     def debug_candidates(self, level: int, image: int = 0) -> np.ndarray:
         n = c_int()
         L.check(self._lib.orbfe_debug_get_candidates(self._h, image, level, None, 0, byref(n)),

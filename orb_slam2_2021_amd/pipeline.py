@@ -290,16 +290,6 @@ class C3Pipeline:
         # handles' latency-bound pyramid chains never run at the same time
         self.stagger = stagger
         self.prev_ext = None
-        # optional HIP events around the vocabulary / matching / stereo launches
-        self.event_sel = set()
-        self.events = {"k_vocab": [], "k_sft": [], "k_stereo": []}
-
-    def _ev(self, name, stream, pair):
-        import torch
-        if name in self.event_sel:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(stream)
-            pair.append(e)
 
     def run(self, d_img_ptr: int, after_match=None):
         """One sub-batch: 2B images of H x W at d_img_ptr (lefts then rights, row pitch W).
@@ -357,14 +347,9 @@ class C3Pipeline:
         """Frame::ComputeStereoMatches (Frame.cc:125) of the set's B pairs on `stream`, from the
         pyramids handle `ext` built for it."""
         B, cap = self.B, self.cap
-        ev = []
-        self._ev("k_stereo", stream, ev)
         ext.compute_stereo_matches_batch_device(B, 0, B, o.kps.data_ptr(), o.desc.data_ptr(),
                                                 o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
                                                 o.ur.data_ptr(), o.dep.data_ptr(), stream=stream.cuda_stream)
-        self._ev("k_stereo", stream, ev)
-        if ev:
-            self.events["k_stereo"].append(tuple(ev))
 
     def _vocab_on_side(self, o):
         self.side.wait_event(o.extracted)
@@ -385,15 +370,10 @@ class C3Pipeline:
             ev.record(m)
         if not (self.vocab_inline or self.vocab_side):
             self._vocab(o, m)
-        ev = []
-        self._ev("k_sft", m, ev)
         if self.n_pairs:
             L.check(self.lib.orbfe_search_for_triangulation_batch_device(
                 o.matcher._h, self.n_pairs, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
                 "sft batch")
-        self._ev("k_sft", m, ev)
-        if ev:
-            self.events["k_sft"].append(tuple(ev))
         if after_match is not None:
             after_match(o)
         o.matched.record(m)
@@ -401,25 +381,12 @@ class C3Pipeline:
     def _vocab(self, o, m):
         """KeyFrame::ComputeBoW of the set's KeyFrame images (n_vocab: the B lefts, or all 2B) on
         stream m."""
-        ev = []
-        self._ev("k_vocab", m, ev)
         bow = (dict(d_bow_words=o.bow_words.data_ptr(), d_bow_weights=o.bow_weights.data_ptr(),
                     d_bow_n=o.bow_n.data_ptr()) if self.bow else {})
         self.voc.transform_batch_device(self.n_vocab, o.desc.data_ptr(), self.cap * 32, o.cnt.data_ptr(),
                                         self.levelsup, o.ids.data_ptr(), o.offs.data_ptr(),
                                         o.idx.data_ptr(), o.nodes.data_ptr(), self.cap,
                                         stream=m.cuda_stream, **bow)
-        self._ev("k_vocab", m, ev)
-        if ev:
-            self.events["k_vocab"].append(tuple(ev))
-
-    def event_times(self) -> dict:
-        """{kernel: (total ms, launches)} of the recorded vocabulary / matching / stereo events."""
-        return {k: (sum(a.elapsed_time(b) for a, b in v), len(v)) for k, v in self.events.items() if v}
-
-    def clear_events(self):
-        for v in self.events.values():
-            v.clear()
 
     def to_host(self, o=None) -> dict:
         """Every output of a sub-batch, per image / pair, as numpy (synchronises)."""

@@ -15,6 +15,6 @@ for f in sorted(glob.glob(f"gpurun_out/{tag}_b*.log") + glob.glob(f"gpurun_out/{
     try:
         d = json.loads(open(f).read().strip().splitlines()[-1])
         print(f.split("/")[-1], d["value"], d.get("parity_bit_exact", ""),
-              {k: v for k, v in d["kernels_ms_per_subbatch"].items()})
+              {k: v for k, v in d["kernels_us_per_subbatch"].items()})
     except Exception as e:  # noqa: BLE001
         print(f, "failed", e)

@@ -10,6 +10,7 @@ import numpy as np
 import torch
 
 from orb_slam2_2021_amd import ORBextractor, synth_frame, synth_sequence_frame
+from orb_slam2_2021_amd import _lib as L
 
 
 def main():
@@ -44,8 +45,8 @@ def main():
         run()
     torch.cuda.synchronize()
     if "--per-kernel" in sys.argv:
-        ext.reset_kernel_times()
-        ext.set_profiling(True)
+        L.ktimer_reset()
+        L.ktimer_select(True)
     t0 = time.perf_counter()
     for _ in range(calls):
         run()
@@ -53,8 +54,8 @@ def main():
     dt = time.perf_counter() - t0
     print(f"extract: {1e6 * dt / calls:.1f} us per 64-image call, {cnt.float().mean().item():.1f} kp/image")
     if "--per-kernel" in sys.argv:
-        ext.set_profiling(False)
-        for k, (ms, n) in sorted(ext.kernel_times().items()):
+        L.ktimer_select(False)
+        for k, (ms, n) in sorted(L.ktimer_read().items()):
             if n:
                 print(f"  {k:14s} {1e3 * ms / calls:9.1f} us/call  {n // calls} launches/call")
 

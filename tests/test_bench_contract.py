@@ -33,9 +33,14 @@ def test_roofline_object():
     px = sum(int(w) * int(h) for w, h in GEO[:, :2])
     assert per_step == 64 * (px + 4 * int(GEO[:, 2].sum())) + 4 * 13_000 * 64
     # SearchForTriangulation bytes follow the pairing: 31 KeyFrame pairs (t, t+1) of 2007 keypoints
-    kt = {"k_sft": (50 * 0.1, 50)}
-    r = bench.roofline(kt, "k_sft", GEO, counts, 0, 64, 50, pipe)
+    kt = {"k_sft_nodes": (50 * 0.1, 50)}
+    r = bench.roofline(kt, "k_sft_nodes", GEO, counts, 0, 64, 50, pipe)
     assert r["algorithmic_bytes_per_subbatch"] == 31 * (64 * 2 * 2007 + 4 * 2007)
+    # every kernel of the C3 step has algorithmic bytes (the dominant one is chosen by device time)
+    for k in ("k_copy0", "k_resize_win", "k_fast", "k_octree", "k_blur", "k_describe", "k_stereo_rows",
+              "k_stereo_match", "k_stereo_median", "k_vocab_descend", "k_vocab", "k_sft_nodes", "k_sft_finish"):
+        r = bench.roofline({k: (50 * 0.1, 50)}, k, GEO, counts, 13_000 * 64, 64, 50, pipe)
+        assert r["algorithmic_bytes_per_subbatch"] > 0 and 0 < r["frac"] < 1, k
 
 
 def test_committed_pmc_traffic_matches_workload():
