@@ -1,0 +1,90 @@
+// ORBextractor_gpu.cc -- the drop-in replacement of the reference's src/ORBextractor.cc for a GPU
+// build of lreithmayr/ORB_SLAM2_2021: every ORBextractor method the reference defines
+// (include/ORBextractor.h:56-100) over liborbfe.so (include/orbfe.hpp). include/ORBextractor.h
+// stays as it is, so Frame.cc / Tracking.cc compile and link unchanged; the GPU handle of each
+// instance lives in a side table keyed by `this` (the header's inline destructor cannot free it:
+// Tracking keeps its two or three extractors for the life of the process, Tracking.cc:125-131).
+//
+// Built only inside the reference's tree, where OpenCV and the reference headers exist
+// (INTEGRATION.md section 4); anywhere else this translation unit is empty.
+#if __has_include(<opencv2/core.hpp>) && __has_include("ORBextractor.h")
+
+#include <cassert>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+
+#include <opencv2/core.hpp>
+
+#include "ORBextractor.h"
+#include "orbfe.hpp"
+
+namespace ORB_SLAM2 {
+
+namespace {
+std::mutex g_mu;
+std::map<const ORBextractor*, std::unique_ptr<orbfe::Extractor>>& handles() {
+  static auto* m = new std::map<const ORBextractor*, std::unique_ptr<orbfe::Extractor>>();
+  return *m;
+}
+orbfe::Extractor& gpu_of(const ORBextractor* e) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return *handles().at(e);
+}
+}  // namespace
+
+// ORBextractor.cc:413-473: the scale / sigma tables and per-level budgets come from the library,
+// computed with the reference's float arithmetic (tests/test_oracle_kat.py pins them)
+ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
+    : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
+      minThFAST(_minThFAST) {
+  std::unique_ptr<orbfe::Extractor> g(
+      new orbfe::Extractor(_nfeatures, _scaleFactor, _nlevels, _iniThFAST, _minThFAST));
+  mvScaleFactor = g->GetScaleFactors();
+  mvInvScaleFactor = g->GetInverseScaleFactors();
+  mvLevelSigma2 = g->GetScaleSigmaSquares();
+  mvInvLevelSigma2 = g->GetInverseScaleSigmaSquares();
+  mnFeaturesPerLevel.assign(g->FeaturesPerLevel().begin(), g->FeaturesPerLevel().end());
+  mvImagePyramid.resize(nlevels);
+  std::lock_guard<std::mutex> lk(g_mu);
+  handles()[this] = std::move(g);
+}
+
+// ORBextractor.cc:1041-1103
+void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask: ignored, :65*/,
+                              std::vector<cv::KeyPoint>& _keypoints, cv::OutputArray _descriptors) {
+  if (_image.empty()) return;  // :1044-1045
+  cv::Mat image = _image.getMat();
+  assert(image.type() == CV_8UC1);  // :1048
+  orbfe::Extractor& g = gpu_of(this);
+  std::vector<orbfe::KeyPoint> kps;
+  std::vector<uint8_t> desc;
+  g(image.data, image.rows, image.cols, image.step, kps, desc);
+  _keypoints.clear();
+  _keypoints.reserve(kps.size());
+  for (const orbfe::KeyPoint& k : kps)  // cv::KeyPoint(x, y, size, angle, response, octave, class_id)
+    _keypoints.emplace_back(k.x, k.y, k.size, k.angle, k.response, k.octave, k.class_id);
+  if (kps.empty()) {
+    _descriptors.release();  // :1062-1063
+  } else {
+    _descriptors.create((int)kps.size(), 32, CV_8U);
+    std::memcpy(_descriptors.getMat().data, desc.data(), desc.size());
+  }
+  // the public mvImagePyramid (ORBextractor.h:100): headers over the handle's host copies of the
+  // levels, valid until the next call (Frame::ComputeStereoMatches reads them right after; the GPU
+  // build's Frame_gpu.cc reads the device pyramids instead and never touches these)
+  for (int l = 0; l < nlevels; l++) {
+    const orbfe::LevelView v = g.level(l);
+    mvImagePyramid[l] = cv::Mat(v.rows, v.cols, CV_8UC1, const_cast<uint8_t*>(v.data), v.step);
+  }
+}
+
+}  // namespace ORB_SLAM2
+
+// the GPU handle of an ORBextractor, for Frame_gpu.cc's ComputeStereoMatches
+orbfe_extractor* orbfe_adapter_extractor_handle(const ORB_SLAM2::ORBextractor* e) {
+  return ORB_SLAM2::gpu_of(e).handle();
+}
+
+#endif

@@ -544,7 +544,8 @@ def main():
         out["host_boundary"] = host_boundary_rate(ext, host[0], others=exts[1:])
         if not args.no_legs:
             out["c2_latency"] = c2_latency(args, host[0][0], host[0][B])
-            out["legs"] = {"c5_search_local_points": c5_leg(args, 1, 0, dev),
+            out["legs"] = {"tracking_sequence": tracking_leg(args),
+                           "c5_search_local_points": c5_leg(args, 1, 0, dev),
                            "keyframe_searches": keyframe_leg(args),
                            "compute_stereo_matches": stereo_leg(args, ext, d_img[0], host[0], B, H, W,
                                                                 pipe.cap, state["cam"]["bf"], state["mb"]),
@@ -915,6 +916,134 @@ def c5_leg(args, world, rank, dev, m_points=50000, frames_per_rank=192):
         nr, br, nvr, _ = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8, kind="native")
         out["cpu_oracle_ms_per_search"] = round(1e3 * (time.perf_counter() - t0), 3)
         out["cpu_bit_exact"] = bool(nr == nm and nvr == nv and np.array_equal(br, best))
+    return out
+
+
+def tracking_leg(args, n_frames=24, n_last=1500, m_local=8000, cpu_frames=4):
+    """Tracking's per-frame device sequence on one GPU (Tracking.cc:210,
+    887-911, 1164-1216), frame after frame as Tracking calls it through the drop-in C ABI:
+      1. the stereo Frame (Frame.cc:113-125): orbfe_stereo_frame = ORBextractor on left + right,
+         then ComputeStereoMatches;
+      2. TrackWithMotionModel's matching: SearchByProjection(CurrentFrame, LastFrame, th = 7,
+         bMono = false), again at 2 th below 20 matches (ORBmatcher(0.9, true));
+      3. SearchLocalPoints: isInFrustum(pMP, 0.5) for the local map, then
+         ORBmatcher(0.8).SearchByProjection(F, vpLocalMapPoints, th = 1) with the motion model's
+         matches holding their keypoints.
+    Frames: the bench's KITTI-shaped driving sequence (1241x376, 1 m per frame). The last frame's
+    MapPoints and the local map are synthetic (S.make_lastframe / S.make_local_map around each
+    frame's keypoints), built before the timed pass. Host buffers in and out (PCIe included):
+    latency per frame = what Tracking waits. Device part: every kernel of the sequence timed by its
+    dispatch (orbfe_ktimer), summed per frame. CPU: the oracle (-O3 -march=native, one thread)
+    runs the same sequence on the first `cpu_frames` frames, which must match bit for bit."""
+    from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_sequence_frame
+    from orb_slam2_2021_amd import _lib as L
+    from orb_slam2_2021_amd import synthetic as S
+    from orb_slam2_2021_amd.frames import log_scale_factor
+    H, W = 376, 1241
+    cam = S.KITTI_CAM
+    mb = cam["bf"] / cam["fx"]
+    frames = [synth_sequence_frame(SEQ_SEED, 200 + t, H, W, right=True) for t in range(n_frames)]
+    ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7)
+    mm = ORBmatcher(0.9, True)   # Tracking.cc:889
+    ml = ORBmatcher(0.8, True)   # Tracking.cc:1207
+    scale, sigma2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+
+    def frame_of(kl, dl, ur, t):
+        return S.Frame(keys_un=kl, descriptors=dl if dl is not None else np.zeros((0, 32), np.uint8), u_right=ur,
+                       mp_state=np.zeros(len(kl), np.uint8), scale_factors=scale, level_sigma2=sigma2,
+                       min_x=0.0, max_x=float(W), min_y=0.0, max_y=float(H), tcw=S.pose(tz=-float(200 + t)), **cam)
+
+    # the synthetic map state around each frame (untimed)
+    scene = []
+    for t, (l, r) in enumerate(frames):
+        kl, dl, _, _, ur, _ = ext.stereo_frame(l, r, cam["bf"], mb)
+        F = frame_of(kl, dl, ur, t)
+        rng = np.random.default_rng(0x7AC0 + t)
+        scene.append((S.make_lastframe(F, n_last, rng, None), S.make_local_map(F, m_local, rng)))
+
+    def run_frame(t):
+        l, r = frames[t]
+        kl, dl, kr, dr, ur, _ = ext.stereo_frame(l, r, cam["bf"], mb)
+        F = frame_of(kl, dl, ur, t)
+        last, local = scene[t]
+        nm1, best1, th = mm.SearchByProjectionMotionModel(F, last, 7.0, False)
+        F.mp_state[best1[best1 >= 0]] = L.ORBFE_MP_OBSERVED  # CurrentFrame.mvpMapPoints[bestIdx2] = pMP
+        nm2, best2, nv, _ = ml.SearchLocalPoints(F, local, 1.0)
+        return (kl, dl, kr, dr, ur, nm1, best1, th, nm2, best2, nv)
+
+    for t in range(3):
+        run_frame(t)
+    lat, outs = [], []
+    for t in range(n_frames):
+        t0 = time.perf_counter()
+        outs.append(run_frame(t))
+        lat.append(time.perf_counter() - t0)
+    L.ktimer_reset()
+    L.ktimer_select(True)
+    for t in range(n_frames):
+        run_frame(t)
+    L.ktimer_select(False)
+    kt = L.ktimer_read()
+    dev_us = {k: round(1e3 * v[0] / n_frames, 2) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}
+    dev_total = sum(v[0] for v in kt.values()) / n_frames * 1e3  # us per frame, kernels back to back
+    # algorithmic bytes per frame (SURVEY 8(d); every input read once, every output written once)
+    geo = ext.geometry(H, W)
+    px = level_pixels(geo)
+    nl_ = float(np.mean([len(o[0]) for o in outs]))
+    nr_ = float(np.mean([len(o[2]) for o in outs]))
+    extract = 2 * (sum(px) + sum(px[1:])) + 60 * (nl_ + nr_)
+    stereo = 72 * nl_ + 48 * nr_ + 44 * nr_ + 8 * nl_
+    sbp_last = n_last * (12 + 32 + 4 + 4 + 1 + 4) + nl_ * (28 + 32 + 4 + 1) + 3072 * 8
+    frustum = m_local * (49 + 21)
+    sbp_local = m_local * (32 + 20) + nl_ * (32 + 16 + 4) + 3072 * 8
+    algo = extract + stereo + sbp_last + frustum + sbp_local
+    achieved = algo / (dev_total * 1e-6) / 1e9
+    out = {"frames": n_frames, "latency_ms": percentiles(lat), "frames_per_s_one_caller": round(n_frames / sum(lat), 1),
+           "device_us_per_frame": round(dev_total, 2), "device_us_per_frame_by_kernel": dev_us,
+           "keypoints_left": round(nl_, 1), "last_frame_mappoints": n_last, "local_map_mappoints": m_local,
+           "motion_model_matches": round(float(np.mean([o[5] for o in outs])), 1),
+           "motion_model_retries": int(sum(o[7] != 7.0 for o in outs)),
+           "local_map_in_view": round(float(np.mean([o[10] for o in outs])), 1),
+           "local_map_matches": round(float(np.mean([o[8] for o in outs])), 1),
+           "roofline": {"kernel": "the whole per-frame sequence (stereo Frame, SearchByProjection(F, LastFrame), "
+                                  "isInFrustum + SearchByProjection(F, local map))",
+                        "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                        "algorithmic_bytes_per_frame": int(algo),
+                        "measured_in": "every kernel of the sequence timed by its dispatch (orbfe_ktimer), summed "
+                                       "per frame"},
+           "what": "Tracking's per-frame device sequence through the host-buffer C ABI, one caller, frame after frame "
+                   "(1241x376 driving sequence; synthetic last-frame MapPoints and local map)"}
+    if not args.no_cpu:
+        from oracle import orbref
+        same, cpu_s = True, 0.0
+        rx = [orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native") for _ in range(2)]
+        inv = rx[0].tables()["inv_scale"]
+        for t in range(min(cpu_frames, n_frames)):
+            l, r = frames[t]
+            t0 = time.perf_counter()
+            kl, dl = rx[0](l)
+            kr, dr = rx[1](r)
+            ur, _ = orbref.compute_stereo_matches(kl, dl, kr, dr, [rx[0].level(i) for i in range(8)],
+                                                  [rx[1].level(i) for i in range(8)], scale, inv, mb, cam["bf"],
+                                                  kind="native")
+            F = frame_of(kl, dl, ur, t)
+            last, local = scene[t]
+            nm1, best1, th = orbref.motion_model_search(F, last, 7.0, False, True, kind="native")
+            F.mp_state[best1[best1 >= 0]] = L.ORBFE_MP_OBSERVED
+            nm2, best2, nv, _ = orbref.search_local_points(F, local, log_scale_factor(1.2), 1.0, 0.8, kind="native")
+            cpu_s += time.perf_counter() - t0
+            g = outs[t]
+            same &= bool(len(g[0]) == len(kl) and g[0].tobytes() == kl.tobytes() and np.array_equal(g[1], dl)
+                         and g[2].tobytes() == kr.tobytes() and np.array_equal(g[3], dr)
+                         and np.array_equal(g[4].view(np.uint32), ur.view(np.uint32))
+                         and (g[5], g[7], g[8], g[10]) == (nm1, th, nm2, nv)
+                         and np.array_equal(g[6], best1) and np.array_equal(g[9], best2))
+        n = min(cpu_frames, n_frames)
+        out["cpu_baseline"] = {"value": round(n / cpu_s, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                               "sample": f"the same sequence on the first {n} frames, oracle -O3 -march=native, 1 thread "
+                                         "(the stereo Frame's two extractions serial here)"}
+        out["cpu_bit_exact"] = same
     return out
 
 

@@ -241,16 +241,28 @@ def search_by_projection_local(F, mps, th: float, nnratio: float):
     return nm.value, best
 
 
-def search_by_projection_lastframe(C, last, th: float, mono: bool, check_ori: bool):
+def search_by_projection_lastframe(C, last, th: float, mono: bool, check_ori: bool, kind: str = "checker"):
     cv, lv = C.view(), last.view()
     best = np.full(len(last.flags), -1, np.int32)
     nm = c_int()
     tcw = np.ascontiguousarray(C.tcw, np.float32)
-    st = lib().orbref_search_by_projection_lastframe(byref(cv), byref(lv), _p(tcw), th,
-                                                     1 if mono else 0, 1 if check_ori else 0,
-                                                     _p(best), byref(nm))
+    st = lib(kind).orbref_search_by_projection_lastframe(byref(cv), byref(lv), _p(tcw), th,
+                                                         1 if mono else 0, 1 if check_ori else 0,
+                                                         _p(best), byref(nm))
     assert st == 0
     return nm.value, best
+
+
+def motion_model_search(C, last, th: float, mono: bool, check_ori: bool = True, kind: str = "checker"):
+    """Tracking::TrackWithMotionModel's matching (src/Tracking.cc:896-911): mvpMapPoints filled
+    with NULL, SearchByProjection(CurrentFrame, LastFrame, th, bMono), and below 20 matches NULL
+    again and the search at 2 th. Returns (nmatches, best_idx, th used)."""
+    C.mp_state = np.zeros(C.N, np.uint8)
+    nm, best = search_by_projection_lastframe(C, last, th, mono, check_ori, kind=kind)
+    if nm < 20:
+        th = 2 * th
+        nm, best = search_by_projection_lastframe(C, last, th, mono, check_ori, kind=kind)
+    return nm, best, th
 
 
 def search_for_triangulation(K1, K2, F12, ex, ey, only_stereo: bool, check_ori: bool):

@@ -119,6 +119,20 @@ class ORBmatcher:
             return nm.value, best
         raise TypeError("points must be LocalMapPoints or LastFrameMapPoints")
 
+    def SearchByProjectionMotionModel(self, F: Frame, last: LastFrameMapPoints, th: float,
+                                      bMono: bool) -> Tuple[int, np.ndarray, float]:
+        """Tracking::TrackWithMotionModel's matching (Tracking.cc:896-911): CurrentFrame's
+        mvpMapPoints are filled with NULL, SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+        runs, and with fewer than 20 matches the map points are cleared again and the search
+        repeats at 2 th. F.mp_state is left all ORBFE_MP_NONE (the fill), as the reference's
+        Frame is before the caller applies best_idx. Returns (nmatches, best_idx, th used)."""
+        F.mp_state = np.zeros(F.N, np.uint8)
+        nm, best = self._search_by_projection_frame(F, last, th, bMono)
+        if nm < 20:
+            th = 2 * th
+            nm, best = self._search_by_projection_frame(F, last, th, bMono)
+        return nm, best, th
+
     # ---- Frame::isInFrustum / Tracking::SearchLocalPoints (orbfe_frustum.h) -----------------
     @staticmethod
     def _frustum_out(m: int):

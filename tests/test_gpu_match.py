@@ -3,7 +3,7 @@ counts must be identical (integer work: bit-exact bar)."""
 import numpy as np
 import pytest
 
-from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame
+from orb_slam2_2021_amd import ORBextractor, ORBmatcher, synth_frame, synth_sequence_frame
 from orb_slam2_2021_amd import synthetic as S
 from oracle import orbref
 
@@ -184,6 +184,49 @@ def test_search_by_projection_lastframe(require_gpu, tum_frame, mono, check_ori,
     assert nm == nr
     assert np.array_equal(best, rb)
     assert nm > 50
+
+
+@pytest.fixture(scope="module")
+def kitti_seq_frame():
+    """The left image of frame 5 of the bench's driving sequence (1241x376), KITTI extractor settings."""
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    k, d = ext(synth_sequence_frame(0x0C3, 5, 376, 1241))
+    return k, d, ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+
+
+# Tracking::TrackWithMotionModel's thresholds (Tracking.cc:900-904): 7 for stereo, 15 otherwise; the
+# camera moving forward (tz = -1 m: LastFrame ahead of mb, the search from nLastOctave up), backward
+# (from level 0 to nLastOctave) and nearly still (nLastOctave - 1 .. + 1); ORBmatcher.cc:1366-1410
+@pytest.mark.parametrize("mono,th", [(False, 7.0), (True, 15.0)])
+@pytest.mark.parametrize("check_ori", [False, True])
+@pytest.mark.parametrize("tz", [-1.0, 1.0, 0.05])
+def test_search_by_projection_lastframe_kitti(require_gpu, kitti_seq_frame, mono, th, check_ori, tz):
+    k, d, scale, sigma2 = kitti_seq_frame
+    rng = np.random.default_rng(int(100 * tz) + 107)
+    C = S.make_frame(k, d, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, mp_frac=0.0,
+                     tcw=S.pose(tz=tz, yaw=0.01))
+    last = S.make_lastframe(C, 1800, rng, None)
+    m = ORBmatcher(0.9, check_ori)  # Tracking.cc:889
+    nm, best = m.SearchByProjection(C, last, th, bMono=mono)
+    nr, rb = orbref.search_by_projection_lastframe(C, last, th, mono, check_ori)
+    assert nm == nr and np.array_equal(best, rb)
+    assert nm > 100
+
+
+@pytest.mark.parametrize("n_last,retried", [(30, True), (1800, False)])
+@pytest.mark.parametrize("mono,th", [(False, 7.0), (True, 15.0)])
+def test_motion_model_retry(require_gpu, kitti_seq_frame, n_last, retried, mono, th):
+    """Tracking.cc:905-911: below 20 matches the search runs again at 2 th on a cleared frame."""
+    k, d, scale, sigma2 = kitti_seq_frame
+    rng = np.random.default_rng(n_last)
+    C = S.make_frame(k, d, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, mp_frac=0.2, tcw=S.pose(tz=-1.0))
+    last = S.make_lastframe(C, n_last, rng, None, match_frac=0.5)
+    m = ORBmatcher(0.9, True)
+    nm, best, th_used = m.SearchByProjectionMotionModel(C, last, th, mono)
+    nr, rb, th_ref = orbref.motion_model_search(C, last, th, mono, True)
+    assert (th_used, nm) == (th_ref, nr) and np.array_equal(best, rb)
+    assert (th_used == 2 * th) == retried
+    assert (C.mp_state == 0).all()  # the fill before each pass (Tracking.cc:897, 909)
 
 
 def test_empty_inputs(require_gpu, tum_frame):
