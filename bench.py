@@ -1016,34 +1016,44 @@ def tracking_leg(args, n_frames=24, n_last=1500, m_local=8000, cpu_frames=4):
                    "(1241x376 driving sequence; synthetic last-frame MapPoints and local map)"}
     if not args.no_cpu:
         from oracle import orbref
-        same, cpu_s = True, 0.0
-        rx = [orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native") for _ in range(2)]
-        inv = rx[0].tables()["inv_scale"]
-        for t in range(min(cpu_frames, n_frames)):
+
+        def oracle_frame(t, kind, rx):
             l, r = frames[t]
-            t0 = time.perf_counter()
             kl, dl = rx[0](l)
             kr, dr = rx[1](r)
             ur, _ = orbref.compute_stereo_matches(kl, dl, kr, dr, [rx[0].level(i) for i in range(8)],
                                                   [rx[1].level(i) for i in range(8)], scale, inv, mb, cam["bf"],
-                                                  kind="native")
+                                                  kind=kind)
             F = frame_of(kl, dl, ur, t)
             last, local = scene[t]
-            nm1, best1, th = orbref.motion_model_search(F, last, 7.0, False, True, kind="native")
+            nm1, best1, th = orbref.motion_model_search(F, last, 7.0, False, True, kind=kind)
             F.mp_state[best1[best1 >= 0]] = L.ORBFE_MP_OBSERVED
-            nm2, best2, nv, _ = orbref.search_local_points(F, local, log_scale_factor(1.2), 1.0, 0.8, kind="native")
-            cpu_s += time.perf_counter() - t0
-            g = outs[t]
-            same &= bool(len(g[0]) == len(kl) and g[0].tobytes() == kl.tobytes() and np.array_equal(g[1], dl)
-                         and g[2].tobytes() == kr.tobytes() and np.array_equal(g[3], dr)
-                         and np.array_equal(g[4].view(np.uint32), ur.view(np.uint32))
-                         and (g[5], g[7], g[8], g[10]) == (nm1, th, nm2, nv)
-                         and np.array_equal(g[6], best1) and np.array_equal(g[9], best2))
+            nm2, best2, nv, _ = orbref.search_local_points(F, local, log_scale_factor(1.2), 1.0, 0.8, kind=kind)
+            return (kl, dl, kr, dr, ur, nm1, best1, th, nm2, best2, nv)
+
         n = min(cpu_frames, n_frames)
+        # timing: the oracle built with the reference's flags (-O3 -march=native)
+        rx = [orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7, kind="native") for _ in range(2)]
+        inv = rx[0].tables()["inv_scale"]
+        t0 = time.perf_counter()
+        for t in range(n):
+            oracle_frame(t, "native", rx)
+        cpu_s = time.perf_counter() - t0
+        # parity: the checker build (-ffp-contract=off), every output of every frame
+        rx = [orbref.RefExtractor(args.nfeatures, 1.2, 8, 20, 7) for _ in range(2)]
+        parts = {k: True for k in ("keypoints", "descriptors", "u_right", "motion_model", "local_points")}
+        for t in range(n):
+            g, c = outs[t], oracle_frame(t, "checker", rx)
+            parts["keypoints"] &= bool(g[0].tobytes() == c[0].tobytes() and g[2].tobytes() == c[2].tobytes())
+            parts["descriptors"] &= bool(np.array_equal(g[1], c[1]) and np.array_equal(g[3], c[3]))
+            parts["u_right"] &= bool(np.array_equal(g[4].view(np.uint32), c[4].view(np.uint32)))
+            parts["motion_model"] &= bool((g[5], g[7]) == (c[5], c[7]) and np.array_equal(g[6], c[6]))
+            parts["local_points"] &= bool((g[8], g[10]) == (c[8], c[10]) and np.array_equal(g[9], c[9]))
         out["cpu_baseline"] = {"value": round(n / cpu_s, 2), "unit": "frames/s", "cores": 1, "kind": "port",
                                "sample": f"the same sequence on the first {n} frames, oracle -O3 -march=native, 1 thread "
                                          "(the stereo Frame's two extractions serial here)"}
-        out["cpu_bit_exact"] = same
+        out["cpu_bit_exact"] = all(parts.values())
+        out["cpu_parity"] = parts
     return out
 
 

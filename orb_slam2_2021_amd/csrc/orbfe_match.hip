@@ -335,7 +335,11 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
   }
   const int w = wave_id(), lane = lane_id();
   const int a = blk.x * 4 + w;
-  if (a >= P.fv1.n_nodes || P.kf2.n > SFT_MAX_KF2) return;
+  if (a >= P.fv1.n_nodes) return;
+  if (P.kf2.n > SFT_MAX_KF2) {  // over capacity (k_sft_finish reports ERR_CAPACITY): no matches
+    for (int i = P.fv1.offsets[a] + lane_id(); i < P.fv1.offsets[a + 1]; i += 64) P.match12[P.fv1.indices[i]] = -1;
+    return;
+  }
   const uint32_t id = P.fv1.node_ids[a];
   const int o1 = P.fv1.offsets[a], e1 = P.fv1.offsets[a + 1];
   // the merge-join visits exactly the common node ids (:705-804): find id among KF2's node ids
@@ -1268,7 +1272,11 @@ int ensure_arena(orbfe_matcher* m, size_t bytes) {
 // A caller's array in device memory (a resident local map, a frame left in HBM): hipMemcpyAsync
 // device to device instead of the host staging copy. Pageable host memory reports
 // hipMemoryTypeUnregistered or an error, which is cleared here.
-static bool is_device_ptr(const void* p) {
+// An error an earlier call left pending on this thread is taken out first and reported by the
+// next flush_h2d, so the query's own cleanup cannot swallow it.
+static bool is_device_ptr(orbfe_matcher* m, const void* p) {
+  const hipError_t prior = hipGetLastError();
+  if (prior != hipSuccess && m->pending_err == hipSuccess) m->pending_err = prior;
   hipPointerAttribute_t at;
   if (hipPointerGetAttributes(&at, p) != hipSuccess) {
     (void)hipGetLastError();
@@ -1280,7 +1288,7 @@ static bool is_device_ptr(const void* p) {
 void stage_h2d(orbfe_matcher* m, const void* dst, const void* src, size_t n) {
   if (n == 0) return;
   const size_t off = (size_t)((const uint8_t*)dst - m->arena);
-  if (is_device_ptr(src)) {
+  if (is_device_ptr(m, src)) {
     m->d2d.emplace_back(off, src, n);
     return;
   }
@@ -1291,6 +1299,14 @@ void stage_h2d(orbfe_matcher* m, const void* dst, const void* src, size_t n) {
 
 // One H2D copy of the staged span (arena regions in between are written by kernels afterwards).
 int flush_h2d(orbfe_matcher* m) {
+  if (m->pending_err != hipSuccess) {
+    const hipError_t e = m->pending_err;
+    m->pending_err = hipSuccess;
+    m->stage_lo = SIZE_MAX;
+    m->stage_hi = 0;
+    m->d2d.clear();
+    return orbfe_set_hip_error(e, "an earlier HIP call (pending before this search)");
+  }
   if (m->stage_hi > m->stage_lo)
     ORBFE_HIP_CHECK(hipMemcpyAsync(m->arena + m->stage_lo, m->pinned + m->stage_lo, m->stage_hi - m->stage_lo,
                                    hipMemcpyHostToDevice, m->stream));
@@ -2064,7 +2080,9 @@ extern "C" int orbfe_is_in_frustum(orbfe_matcher* m, const orbfe_frame_view* F, 
   if (st) return st;
   FrustumArgs fa;
   fill_frustum_args(fa, F, tcw, log_scale_factor, viewing_cos_limit);
+  m->prof_started = m->prof_done = false;  // this call's own device-time window (k_frustum)
   if ((st = launch_frustum(m, m->arena, p, G, fa))) return st;
+  prof_end(m);
   return fetch_frustum(m, m->arena, p, G->m, out, n_in_view);
 }
 

@@ -55,6 +55,7 @@ struct orbfe_matcher {
   // no H2D / D2H) of each SearchByProjection-family call
   int profile = 0;
   bool prof_started = false, prof_done = false;
+  hipError_t pending_err = hipSuccess;  // found by stage_h2d's pointer query, reported by flush_h2d
   hipEvent_t prof_ev0 = nullptr, prof_ev1 = nullptr;
 };
 

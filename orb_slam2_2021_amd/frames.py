@@ -260,6 +260,10 @@ class DeviceMapPointGeometry:
                 raise ValueError(f"{f}: a contiguous device tensor is required")
             setattr(self, f, t)
         self.m = int(m)
+        # the matcher reads these on its own non-blocking stream, which nothing orders after the
+        # stream that wrote them (torch's current stream: the upload, or RCCL's broadcast into them,
+        # parallel.broadcast_arrays): wait for that writer here, once, before any search uses the map
+        torch.cuda.current_stream(self.flags.device).synchronize()
         need = {"flags": 1, "world_pos": 12, "normal": 12, "min_distance": 4, "max_distance": 4, "descriptors": 32}
         for f, b in need.items():
             if getattr(self, f).numel() * getattr(self, f).element_size() < b * self.m:

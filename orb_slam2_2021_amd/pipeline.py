@@ -280,9 +280,12 @@ class C3Pipeline:
         self.last = None
         self._torch = torch
         # stereo_on_match: ComputeStereoMatches on the matching stream (it needs only the extracted
-        # pyramids and keypoints) instead of right after the extraction. Measured on MI355X: no
-        # gain (73.6-73.8k vs 74.2-76.5k stereo frames/s, interleaved) -- the stereo kernels cost
-        # their run time wherever they sit; off by default
+        # pyramids and keypoints) instead of right after the extraction; the handle's next
+        # extraction waits for it (run()). Measured on MI355X: with one handle per extraction
+        # stream no gain (73.6-73.8k vs 74.2-76.5k stereo frames/s, round 3), with two handles per
+        # stream -- the bench's shape, a handle's pyramids rebuilt only every fourth sub-batch --
+        # 78.4-78.5k vs 77.1-77.5k, so bench.py turns it on (its --stereo-on-extract turns it off);
+        # the class default stays off for single-handle callers
         self.stereo_on_match = stereo and stereo_on_match and not (self.match_inline or defer or vocab_side
                                                                    or vocab_inline)
         self.stereo_done = [None] * len(self.exts)

@@ -53,3 +53,28 @@ def test_device_geometry_rejects_host_tensors():
     t = {f: torch.zeros(64, dtype=torch.uint8) for f in DeviceMapPointGeometry.FIELDS}
     with pytest.raises(ValueError):
         DeviceMapPointGeometry(tensors=t, m=1)
+
+
+def test_resident_map_from_tensors_written_on_the_current_stream():
+    """DeviceMapPointGeometry(tensors=...) as parallel.broadcast_arrays hands them over: written on
+    torch's current stream (an asynchronous copy from pinned memory behind a long-running kernel
+    there), then searched on the matcher's own stream at once -- the constructor orders the two."""
+    from orb_slam2_2021_amd import ORBmatcher
+    from orb_slam2_2021_amd.frames import DeviceMapPointGeometry
+    G, frames = _scene()
+    dev = torch.device("cuda", 0)
+    t = {}
+    busy = torch.randn(4096, 4096, device=dev)
+    for _ in range(8):  # keep the current stream busy so an unordered reader would see stale bytes
+        busy = busy @ busy
+        busy = busy / busy.norm()
+    for f in DeviceMapPointGeometry.FIELDS:
+        a = np.ascontiguousarray(getattr(G, f)).view(np.uint8).reshape(-1)
+        d = torch.zeros(a.size, dtype=torch.uint8, device=dev)
+        d.copy_(torch.from_numpy(a).pin_memory(), non_blocking=True)
+        t[f] = d
+    Gd = DeviceMapPointGeometry(tensors=t, m=len(G.flags))
+    m = ORBmatcher(0.8, True)
+    nh, bh, vh, _ = m.SearchLocalPoints(frames[0], G, 3.0)
+    nd, bd, vd, _ = m.SearchLocalPoints(frames[0], Gd, 3.0)
+    assert nh > 100 and (nh, vh) == (nd, vd) and np.array_equal(bh, bd)
