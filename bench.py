@@ -145,6 +145,10 @@ def parse(argv=None):
     p.add_argument("--c5-workers", type=int, default=4,
                    help="C5 leg: Tracking-like callers per rank, each with its own extractor + matcher on its "
                         "own thread (the leg also reports one caller)")
+    p.add_argument("--gather-proxy", type=int, default=0,
+                   help="one-GPU proxy of C4's rank-0 ingestion at N GPUs: after each sub-batch's pack, "
+                        "N-1 device-to-device copies of the packed worst-case payload on a stream of their "
+                        "own (where RCCL's receives run), with N > 1's hardware-queue setting (DESIGN.md section 7)")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
@@ -211,11 +215,13 @@ def spawn_ranks(args) -> int:
 
 class Gatherer:
     """C4: each sub-batch's used keypoints + descriptors to rank 0. The pack kernel runs on the
-    matching stream right after SearchForTriangulation, and the point-to-point transfers of a
-    fixed byte count (the packed worst case; the packed header carries the per-image counts) are
-    enqueued right behind it on the same stream: no size exchange, so the host never waits for
-    the device inside the timed loop (parallel.gather_fixed). The output set is reused only after
-    its payload left (o.matched is recorded behind the transfers)."""
+    matching stream right after SearchForTriangulation; the point-to-point transfers of a fixed
+    byte count (the packed worst case; the packed header carries the per-image counts) run on a
+    communication stream of their own that waits for the pack: no size exchange, so the host never
+    waits for the device inside the timed loop (parallel.gather_fixed), and the matching stream
+    never waits for the transfers (a wait there put two cross-queue hops on the critical chain every
+    sub-batch: --gather-proxy measured 83k -> 54k stereo frames/s at N = 2). The output set is
+    reused only after its payload left (o.released, recorded behind the transfers)."""
 
     def __init__(self, pipe, world, rank, dev, comm_dev):
         import torch
@@ -230,6 +236,10 @@ class Gatherer:
         self.transfers = 0
         self.last = None  # rank 0: the last exchange's per-rank views (alias the receive buffers)
         self.last_set = None
+        self.comm = torch.cuda.Stream(dev)  # created after the pipeline's busy streams
+        from orb_slam2_2021_amd.pipeline import new_event
+        self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
+        self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
 
     def pack(self, o):
         import torch
@@ -239,21 +249,80 @@ class Gatherer:
         pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
                               buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
                               o.mstream.cuda_stream)
-        with torch.cuda.stream(o.mstream):
+        ev = self.packed[id(o)]
+        ev.record(o.mstream)
+        self.comm.wait_event(ev)
+        with torch.cuda.stream(self.comm):
             if self.comm_dev.type == "cpu":  # --rehearse: gloo, staged through the host
-                o.mstream.synchronize()
+                self.comm.synchronize()
                 out = gather_fixed(buf.cpu(), self.cap_bytes, dst=0, recv=self.recv)
             else:
                 out = gather_fixed(buf, self.cap_bytes, dst=0, recv=self.recv)
+        o.released = self.sent[id(o)]
+        o.released.record(self.comm)
         self.transfers += 1
         self.last_set = o
         if self.rank == 0:
             self.last = out
 
 
+class GatherProxy:
+    """--gather-proxy N on one GPU: the cost rank 0 pays for C4's ingestion at N GPUs, without the
+    peers. Per sub-batch, after SearchForTriangulation, the keypoints + descriptors are packed on the
+    matching stream (as Gatherer.pack does), then N - 1 device-to-device copies of the packed
+    worst-case payload (the byte count every peer sends, orbfe_packed_bytes) run on a stream of
+    their own -- RCCL's receive kernels run on RCCL's stream, a fifth busy stream -- and the output
+    set is released only after them (o.released; the matching stream does not wait for them). The copies read and write rank 0's HBM (2x the received bytes)
+    with CU blit kernels, where a real receive writes what xGMI delivers: an upper bound on the HBM
+    side, no model of the links."""
+
+    def __init__(self, pipe, n_gpus, dev):
+        import torch
+        from orb_slam2_2021_amd.parallel import packed_bytes
+        self.pipe, self.n = pipe, n_gpus
+        self.cap_bytes = packed_bytes(pipe.n_img, pipe.n_img * pipe.cap)
+        self.bufs = {id(o): torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for o in pipe.sets}
+        self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
+        self.recv = [torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for _ in range(n_gpus - 1)]
+        self.stream = torch.cuda.Stream(dev)  # created after the pipeline's streams, as RCCL's is
+        from orb_slam2_2021_amd.pipeline import new_event
+        self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
+        self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
+        self.transfers = 0
+
+    def pack(self, o):
+        import torch
+        from orb_slam2_2021_amd.parallel import pack_keypoints_device
+        p, m = self.pipe, o.mstream
+        buf = self.bufs[id(o)]
+        pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                              buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
+        ev = self.packed[id(o)]
+        ev.record(m)
+        self.stream.wait_event(ev)
+        mode = os.environ.get("ORBFE_GPROXY_MODE", "torch")  # diagnostic: which part costs
+        with torch.cuda.stream(self.stream):
+            for r in self.recv:
+                if mode == "torch":
+                    r.copy_(buf, non_blocking=True)
+                elif mode == "kcopy":  # the same bytes moved by the pack kernel (CU copy, no blit)
+                    pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                                          r.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
+                                          self.stream.cuda_stream)
+        o.released = self.sent[id(o)]
+        o.released.record(self.stream)
+        self.transfers += 1
+
+    def describe(self):
+        return {"n_gpus_modelled": self.n, "copies_per_subbatch": self.n - 1, "bytes_per_copy": self.cap_bytes,
+                "received_bytes_per_subbatch": self.cap_bytes * (self.n - 1),
+                "what": "rank 0's ingestion of C4 on one GPU: N-1 device-to-device copies of the packed worst-case "
+                        "payload per sub-batch on their own stream (RCCL's receive stream), 8 hardware queues"}
+
+
 def main():
     args = parse()
-    hw_queues = hw_queue_setting(args.hw_queues, int(os.environ.get("WORLD_SIZE", "1")))
+    hw_queues = hw_queue_setting(args.hw_queues, max(int(os.environ.get("WORLD_SIZE", "1")), args.gather_proxy))
     if hw_queues > 0:  # read once by the HIP runtime at its start (no HIP call before this)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -345,6 +414,8 @@ def main():
         pipe._match = extract_only
     gather = world > 1 and not args.no_gather
     g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
+    if args.gather_proxy > 1 and world == 1:
+        g = GatherProxy(pipe, args.gather_proxy, dev)
     counter = [0]
 
     def sub_batch():
@@ -484,6 +555,7 @@ def main():
                          f"extractions overlap), {'matching inline' if args.match_inline else ('' if args.stereo_on_extract else 'ComputeStereoMatches + ') + 'vocabulary + matching on its own stream'}, "
                          f"{pipe_depth(args)} output sets" if pipe_depth(args) > 1 else "one sub-batch at a time"),
         },
+        **({"gather_proxy": g.describe()} if isinstance(g, GatherProxy) else {}),
         "roofline": roof,
         "pipeline_hbm": {
             "algorithmic_bytes_per_stereo_frame": int(algo_frame),
@@ -500,7 +572,7 @@ def main():
         "stereo_matches_per_pair": (round(float((last.ur >= 0).sum().item()) / B, 1) if args.stereo else None),
         "cpu_baseline": None,
     }
-    if g is not None and rank == 0:
+    if isinstance(g, Gatherer) and rank == 0:
         from orb_slam2_2021_amd.parallel import packed_size
         used = [packed_size(v) for v in g.last]
         out["gather"] = {"bytes_sent_per_rank_per_subbatch": g.cap_bytes,
@@ -508,7 +580,7 @@ def main():
                          "bytes_received_per_subbatch": g.cap_bytes * (world - 1),
                          "what": "packed keypoints + descriptors of ranks 1..N-1 to rank 0, point-to-point, "
                                  "fixed worst-case byte count (no size exchange, no host sync per sub-batch)"}
-    if g is not None and args.dump_gather:
+    if isinstance(g, Gatherer) and args.dump_gather:
         dump_gather(args.dump_gather, g, pipe, rank, world)
     # ---- parity of the last timed sub-batch (every rank checks its own) ----
     if not args.no_parity:

@@ -143,6 +143,14 @@ void* orbfe_extractor_stream(orbfe_extractor* h);
 void* orbfe_extractor_pyramid_event(orbfe_extractor* h);
 /* hipStreamWaitEvent(stream, event, 0) for callers without the HIP headers. */
 int orbfe_stream_wait_event(void* stream, void* event);
+/* An event (hipEvent_t as void*) that only orders device work between streams: no timing and no
+ * system-scope release on record (hipEventDisableTiming | hipEventDisableSystemFence). A pipeline's
+ * cross-stream dependencies recorded with it do not write the GPU caches back to memory each time,
+ * which a default event does; nothing on the host may wait on it for data the device wrote.
+ * orbfe_event_record = hipEventRecord(event, stream). */
+int orbfe_event_create(int device, void** out);
+int orbfe_event_record(void* event, void* stream);
+int orbfe_event_destroy(void* event);
 /* A non-blocking stream on `device` (high_priority: the device's greatest priority, as the
  * extractor's side stream). The runtime maps streams onto a few hardware queues per priority
  * (GPU_MAX_HW_QUEUES, 4 by default), choosing the least-shared queue at creation and the

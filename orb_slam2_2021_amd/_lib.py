@@ -116,6 +116,9 @@ _SIGNATURES = {
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
     "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
     "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
+    "orbfe_event_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "orbfe_event_record": (c_int, [c_void_p, c_void_p]),
+    "orbfe_event_destroy": (c_int, [c_void_p]),
     "orbfe_matcher_set_profiling": (c_int, [c_void_p, c_int]),
     "orbfe_matcher_last_device_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "orbfe_host_register": (c_int, [c_void_p, c_size_t]),

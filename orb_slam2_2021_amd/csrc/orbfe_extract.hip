@@ -3354,6 +3354,27 @@ extern "C" int orbfe_stream_destroy(void* stream) {
   return ORBFE_OK;
 }
 
+extern "C" int orbfe_event_create(int device, void** out) {
+  if (!out) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_event_create: out is NULL");
+  *out = nullptr;
+  hipEvent_t e = nullptr;
+  ORBFE_HIP_CHECK(hipSetDevice(device));
+  ORBFE_HIP_CHECK(hipEventCreateWithFlags(&e, kForkJoinEvent));
+  *out = (void*)e;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_event_record(void* event, void* stream) {
+  if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_event_record: null event");
+  ORBFE_HIP_CHECK(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_event_destroy(void* event) {
+  if (event) ORBFE_HIP_CHECK(hipEventDestroy((hipEvent_t)event));
+  return ORBFE_OK;
+}
+
 extern "C" int orbfe_stream_wait_event(void* stream, void* event) {
   if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stream_wait_event: null event");
   ORBFE_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));

@@ -611,6 +611,10 @@ struct SbpArgs {
   // rounds >= 2 with the cache: round r-2's owners (round r compares them with round r-1's and
   // re-evaluates only the queries a changed keypoint can reach); NULL: every query is re-evaluated
   const int32_t* owner_rm2;
+  // round 0 with the settle path: the inverted candidate index, keypoint k -> the queries whose
+  // window holds it as a candidate (inv[k * SBP_INV_CAP + j], inv_n[k] may exceed the cap); NULL off
+  int32_t* inv;
+  int32_t* inv_n;
 };
 
 // A keypoint whose owner changed from o1 to o2 between rounds: blocked(k) = owner < q flips exactly
@@ -754,7 +758,7 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
 }
 
 struct SbpInit {
-  int32_t *res0, *res1, *own0, *own2, *state, *nmatches, *serial;
+  int32_t *res0, *res1, *own0, *own2, *state, *nmatches, *serial, *inv_n;
   int nq, nf;
 };
 // One launch for the per-call initialisation (results "never", owners unclaimed, counters 0).
@@ -767,6 +771,7 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
   if (i < in.nf) {
     in.own0[i] = 0x7fffffff;
     in.own2[i] = 0x7fffffff;
+    if (in.inv_n) in.inv_n[i] = 0;
   }
   if (i < SBP_ROUND_CAP + 4) in.state[i] = 0;
   if (i == 0) {
@@ -937,6 +942,10 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
         }
         const bool keep = pass && dist < 256;  // a distance of 256 is never best or second
         const uint64_t bm = (wave_ballot(keep) >> rowbase) & 0xffffull;
+        if (keep && a.inv) {  // every candidate, cached or not (a query past cand_cap re-walks them all)
+          const int slot = atomicAdd(&a.inv_n[k], 1);
+          if (slot < SBP_INV_CAP) a.inv[(size_t)k * SBP_INV_CAP + slot] = i;
+        }
         if (keep) {
           const int pos = total + __popcll(bm & ((1ull << j) - 1));
           if (pos < a.cand_cap) {
@@ -990,6 +999,163 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   if (res >= 0 && (q.flags & 2)) atomicMin(&a.owner_cur[res], i);
   const uint64_t changed = wave_ballot(res != a.res_prev[i]);  // plain store, see k_sbp_round
   if (changed && lane_id() == __ffsll((long long)wave_ballot(true)) - 1) a.state[2] = 1;
+}
+
+// ---- the fixpoint's rounds 2.. in one workgroup ---------------------------------------------
+// After round 1 most results are final; the rounds that follow change few of them, and as one
+// launch per round (k_sbp_round) their cost was the launch chain -- 10-16 launches per C5 search,
+// plus host-synchronised continuations when 12 were not enough. Here one 1024-thread workgroup
+// runs them all with the frame's owners in LDS and touches only what a change can reach:
+//   a. the keypoints whose owner differs between rounds r-2 and r-1 (owner = the smallest query
+//      index whose result is the keypoint, among queries whose assignment blocks it);
+//   b. their queries from the inverted candidate index (round 0) with lo < i <= hi: only for those
+//      does blocked(k) = owner < i flip -- the k_sbp_round test, exact rather than by window;
+//   c. re-evaluation from the candidate cache, results updated in place (a round reads only the
+//      previous round's owners, never other results);
+//   d. the owners of the keypoints a changed result left or joined, recomputed from their index
+//      lists (every other keypoint keeps its owner).
+// Settled when no owner changed (the next round would reproduce this one). A keypoint listed by
+// more than SBP_INV_CAP queries makes its rounds scan every query instead (exact, slower); past
+// round_cap the reference's sequential loop runs (as k_sbp_finish does).
+struct SbpSettleArgs {
+  int32_t* res;         // round 1's results, updated in place to the fixpoint
+  const int32_t* own0;  // round 0's owners
+  const int32_t* own1;  // round 1's owners
+  const int32_t* inv;
+  const int32_t* inv_n;
+  int round_cap;
+  int32_t* serial_used;
+  int32_t* blocked_scratch;
+};
+
+__host__ __device__ inline size_t settle_lds(int n, int m) {
+  return sizeof(int) * (4 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 4 * (size_t)((n + 31) / 32);
+}
+
+__global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSettleArgs s) {
+  extern __shared__ int s_lds[];
+  __shared__ int s_cnt, s_dense;
+  const int n = a.F.n, m = a.m, t = threadIdx.x, wv = t >> 6, ln = t & 63;
+  constexpr int NW = SETTLE_THREADS / 64;
+  const int qw = (m + 31) >> 5, kw = (n + 31) >> 5;
+  int* rm2 = s_lds;
+  int* prev = rm2 + n;
+  int* cur = prev + n;
+  int* list = cur + n;  // changed / dirty keypoints
+  uint32_t* qbits = reinterpret_cast<uint32_t*>(list + n);
+  uint32_t* dirty = qbits + qw;
+  for (int k = t; k < n; k += SETTLE_THREADS) {
+    rm2[k] = s.own0[k];
+    prev[k] = s.own1[k];
+  }
+  for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
+  for (int w = t; w < kw; w += SETTLE_THREADS) dirty[w] = 0u;
+  __syncthreads();
+  int round = 2;
+  bool serial = false;
+  for (;; round++) {
+    if (t == 0) {
+      s_cnt = 0;
+      s_dense = 0;
+    }
+    __syncthreads();
+    for (int k = t; k < n; k += SETTLE_THREADS)
+      if (prev[k] != rm2[k]) list[atomicAdd(&s_cnt, 1)] = k;
+    __syncthreads();
+    const int nchg = s_cnt;
+    if (nchg == 0) break;  // round r would reproduce round r-1
+    if (round >= s.round_cap) {
+      serial = true;
+      break;
+    }
+    // b. the queries whose blocked state of a changed keypoint flips: one wavefront per keypoint
+    for (int c = wv; c < nchg; c += NW) {
+      const int k = list[c];
+      const int o1 = rm2[k], o2 = prev[k], lo = min(o1, o2), hi = max(o1, o2);
+      const int cnt = s.inv_n[k];
+      if (cnt > SBP_INV_CAP) {
+        if (ln == 0) s_dense = 1;
+        continue;
+      }
+      for (int j = ln; j < cnt; j += 64) {
+        const int i = s.inv[(size_t)k * SBP_INV_CAP + j];
+        if (lo < i && i <= hi) atomicOr(&qbits[i >> 5], 1u << (i & 31));
+      }
+    }
+    __syncthreads();
+    // c. re-evaluate them from the candidate cache with round r-1's owners
+    const bool dense = s_dense != 0;
+    for (int w = t; w < qw; w += SETTLE_THREADS) {
+      uint32_t bits = dense ? 0xffffffffu : qbits[w];
+      qbits[w] = 0u;
+      while (bits) {
+        const int i = 32 * w + __builtin_ctz(bits);
+        bits &= bits - 1u;
+        if (i >= m) break;
+        const int nc = a.cand_n[i];
+        if (nc == 0) continue;  // no candidate: -1 in every round
+        auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || prev[k] < i; };
+        const int r = nc > 0 ? sbp_cached(a, i, nc, blocked) : sbp_one(a, i, blocked);
+        const int old = s.res[i];
+        if (r != old) {
+          s.res[i] = r;
+          if (a.q[i].flags & 2) {
+            if (old >= 0) atomicOr(&dirty[old >> 5], 1u << (old & 31));
+            if (r >= 0) atomicOr(&dirty[r >> 5], 1u << (r & 31));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // d. round r's owners: round r-1's, recomputed where a result left or joined the keypoint
+    for (int k = t; k < n; k += SETTLE_THREADS) cur[k] = prev[k];
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
+    for (int w = t; w < kw; w += SETTLE_THREADS) {
+      uint32_t bits = dirty[w];
+      dirty[w] = 0u;
+      while (bits) {
+        list[atomicAdd(&s_cnt, 1)] = 32 * w + __builtin_ctz(bits);
+        bits &= bits - 1u;
+      }
+    }
+    __syncthreads();
+    const int nd = s_cnt;
+    for (int c = wv; c < nd; c += NW) {
+      const int k = list[c];
+      const int cnt = s.inv_n[k];
+      int best = 0x7fffffff;
+      if (cnt > SBP_INV_CAP) {  // claimants not all indexed: every query
+        for (int i = ln; i < m; i += 64)
+          if (s.res[i] == k && (a.q[i].flags & 2)) best = min(best, i);
+      } else {
+        for (int j = ln; j < cnt; j += 64) {
+          const int i = s.inv[(size_t)k * SBP_INV_CAP + j];
+          if (s.res[i] == k && (a.q[i].flags & 2)) best = min(best, i);
+        }
+      }
+      best = wave_min(best);
+      if (ln == 0) cur[k] = best;
+    }
+    __syncthreads();
+    int* tmp = rm2;
+    rm2 = prev;
+    prev = cur;
+    cur = tmp;
+  }
+  if (serial && t == 0) {  // the reference loop verbatim (:51-130 / :1371-1450)
+    *s.serial_used = 1;
+    for (int k = 0; k < n; k++) s.blocked_scratch[k] = sbp_pre_blocked(a, k);
+    for (int i = 0; i < m; i++) {
+      const int r = sbp_one(a, i, [&](int k) { return s.blocked_scratch[k] != 0; });
+      s.res[i] = r;
+      if (r >= 0) s.blocked_scratch[r] = (a.q[i].flags & 2) ? 1 : 0;
+    }
+  }
+  if (t == 0) {  // for k_sbp_collect / k_sbp_finish and the round statistics
+    a.state[0] = 1;
+    a.state[1] = round;
+  }
 }
 
 struct SbpFinishArgs {
@@ -1580,6 +1746,9 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
   p.ocand_n = ar.add(p.cache ? 4 * q1 : 0);
   p.onm = ar.add(4);
   p.oown3 = ar.add(4 * f1);
+  p.settle = p.cache && F->n <= SETTLE_MAX_KEYS && p.nq <= SETTLE_MAX_QUERIES && p.nq > 0;
+  p.oinv_n = ar.add(p.settle ? 4 * f1 : 0);
+  p.oinv = ar.add(p.settle ? 4 * f1 * SBP_INV_CAP : 0);
 }
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap) {
   SbpPlan p;
@@ -1647,9 +1816,10 @@ static SbpArgs sbp_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* F,
   return a;
 }
 
-static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F) {
+static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, bool settle = false) {
   uint8_t* A = m->arena;
   SbpInit in;
+  in.inv_n = settle ? (int32_t*)(A + p.oinv_n) : nullptr;
   in.res0 = (int32_t*)(A + p.ores0);
   in.res1 = (int32_t*)(A + p.ores1);
   in.own0 = (int32_t*)(A + p.oown0);
@@ -1689,6 +1859,73 @@ static bool sbp_dense_rounds() {
 // Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over four:
 // round r claims into own[r % 4], reads own[(r + 3) % 4] (round r-1) and own[(r + 2) % 4]
 // (round r-2), and clears own[(r + 1) % 4] for round r + 1, which nobody reads during round r).
+static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs& a, const SbpMode& md,
+                              int32_t* const res_final[2], bool defer) {
+  uint8_t* A = m->arena;
+  SbpFinishArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.s = a;
+  f.res_final[0] = res_final[0];
+  f.res_final[1] = res_final[1];
+  f.best_out = (int32_t*)(A + p.obest);
+  f.nmatches = (int32_t*)(A + p.onm);
+  f.check_ori = md.check_ori;
+  f.q_angle = (const float*)(A + p.oqa);
+  f.serial_used = m->d_serial;
+  f.defer = defer ? 1 : 0;
+  ORBFE_LAUNCH("k_sbp_collect", k_sbp_collect, dim3((p.nq + 255) / 256), dim3(256), 0, m->stream, f);
+  ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
+}
+
+// Rounds 0 and 1 grid-wide (round 0 fills the candidate cache and the inverted index), the rest in
+// k_sbp_settle, then collect / finish: five launches whatever the depth of the claim order.
+static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
+                              const orbfe_frame_view& dF, const SbpMode& md) {
+  uint8_t* A = m->arena;
+  const int nq = p.nq;
+  SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
+  int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
+  int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
+                     (int32_t*)(A + p.oown3)};
+  for (int r = 0; r < 2; r++) {
+    a.round = r;
+    a.res_cur = res[r & 1];
+    a.res_prev = res[(r + 1) & 1];
+    a.owner_cur = own[r % 4];
+    a.owner_prev = own[(r + 3) % 4];
+    a.owner_next = own[(r + 1) % 4];
+    a.owner_rm2 = nullptr;
+    if (r == 0) {
+      a.inv = (int32_t*)(A + p.oinv);
+      a.inv_n = (int32_t*)(A + p.oinv_n);
+      ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+                   m->stream, a);
+      a.inv = a.inv_n = nullptr;
+    } else {
+      ORBFE_LAUNCH("k_sbp_round", k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
+    }
+  }
+  SbpSettleArgs st;
+  st.res = res[1];
+  st.own0 = own[0];
+  st.own1 = own[1];
+  st.inv = (const int32_t*)(A + p.oinv);
+  st.inv_n = (const int32_t*)(A + p.oinv_n);
+  st.round_cap = m->round_cap;
+  st.serial_used = m->d_serial;
+  st.blocked_scratch = (int32_t*)(A + p.oblk);
+  const size_t lds = settle_lds(F->n, nq);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)k_sbp_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)settle_lds(SETTLE_MAX_KEYS, SETTLE_MAX_QUERIES));
+    attr_set = true;
+  }
+  ORBFE_LAUNCH("k_sbp_settle", k_sbp_settle, dim3(1), dim3(SETTLE_THREADS), lds, m->stream, a, st);
+  int32_t* fin[2] = {res[1], res[1]};
+  sbp_finish_launch(m, p, a, md, fin, false);
+}
+
 static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
                        const SbpMode& md, int r0, int r1, bool defer) {
   uint8_t* A = m->arena;
@@ -1713,29 +1950,28 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
     else
       ORBFE_LAUNCH("k_sbp_round", k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
   }
-  SbpFinishArgs f;
-  std::memset(&f, 0, sizeof(f));
-  f.s = a;
-  f.res_final[0] = res[0];
-  f.res_final[1] = res[1];
-  f.best_out = (int32_t*)(A + p.obest);
-  f.nmatches = (int32_t*)(A + p.onm);
-  f.check_ori = md.check_ori;
-  f.q_angle = (const float*)(A + p.oqa);
-  f.serial_used = m->d_serial;
-  f.defer = defer ? 1 : 0;
-  if (nq > 0) {
-    ORBFE_LAUNCH("k_sbp_collect", k_sbp_collect, dim3((nq + 255) / 256), dim3(256), 0, m->stream, f);
-    ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
-  }
+  if (nq > 0) sbp_finish_launch(m, p, a, md, res, defer);
+}
+
+// ORBFE_SBP_SETTLE=0: the fixpoint as one launch per round (rounds 1-3's engine, for A/B)
+static bool sbp_settle_enabled() {
+  static const bool on = !(std::getenv("ORBFE_SBP_SETTLE") && std::atoi(std::getenv("ORBFE_SBP_SETTLE")) == 0);
+  return on;
 }
 
 int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
                const SbpMode& md, bool defer) {
   sbp_launch_grid(m, p, F, dF);
-  sbp_launch_init(m, p, F);
-  const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
-  sbp_rounds(m, p, F, dF, md, 0, rounds, defer && m->round_cap > rounds);
+  // the settle path unless rounds are restricted (orbfe_matcher_set_max_rounds: the serial
+  // fallback's tests) or no assignment blocks anything (one round is the result)
+  const bool settle = p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
+  sbp_launch_init(m, p, F, settle);
+  if (settle) {
+    sbp_settle_rounds(m, p, F, dF, md);
+  } else {
+    const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
+    sbp_rounds(m, p, F, dF, md, 0, rounds, defer && m->round_cap > rounds);
+  }
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
 }

@@ -26,6 +26,10 @@
 #define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
 #define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
 #define SBP_CAND 48          // default per-query candidate cache of the projection searches
+#define SBP_INV_CAP 1024     // queries per keypoint in the settle path's inverted candidate index
+#define SETTLE_THREADS 1024  // k_sbp_settle: one workgroup for the fixpoint's rounds 2..
+#define SETTLE_MAX_KEYS 4096       // settle path: frame keypoints (owners in LDS) ...
+#define SETTLE_MAX_QUERIES 131072  // ... and queries (a bitmap in LDS)
 #define ORBFE_MAX_LEVELS_M 32
 
 struct orbfe_matcher {
@@ -175,8 +179,9 @@ bool levels_ok(const orbfe_keypoint* k, int n, int nlevels);
 struct SbpPlan {
   FrameOffsets fo;
   size_t oqd, oqa, og_start, og_items, oq, ores0, ores1, oown0, oown1, oown2, oblk, ostate, obest;
-  size_t ocand_k, ocand_d, ocand_l, ocand_n, onm, oown3;
+  size_t ocand_k, ocand_d, ocand_l, ocand_n, onm, oown3, oinv, oinv_n;
   bool cache;
+  bool settle;  // the fixpoint's rounds 2.. in k_sbp_settle (cache, frame and query bounds)
   int nq, cand_cap;
 };
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap = SBP_CAND);

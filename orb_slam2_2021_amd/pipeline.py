@@ -53,6 +53,45 @@ def nodes_at_level_bound(tree, levelsup: int, cap: int) -> int:
     return max(1, min(cap, n))
 
 
+class DevEvent:
+    """A cross-stream ordering event of the library (orbfe_event_create): no timing and no
+    system-scope cache write-back on record, which a default (torch) event performs -- the
+    pipeline's events only order device work between its streams; the host synchronises with
+    torch.cuda.synchronize(). Same record(stream) / stream.wait_event(ev) interface as
+    torch.cuda.Event. ORBFE_TORCH_EVENTS=1 selects torch's events instead (A/B)."""
+
+    def __init__(self, device: int):
+        import ctypes
+        p = ctypes.c_void_p()
+        L.check(L.lib().orbfe_event_create(int(device), ctypes.byref(p)), "orbfe_event_create")
+        self._e = p
+
+    def record(self, stream) -> None:
+        import ctypes
+        L.check(L.lib().orbfe_event_record(self._e, ctypes.c_void_p(stream.cuda_stream)), "orbfe_event_record")
+
+    def wait(self, stream) -> None:  # torch.cuda.Stream.wait_event(ev) calls ev.wait(stream)
+        import ctypes
+        L.check(L.lib().orbfe_stream_wait_event(ctypes.c_void_p(stream.cuda_stream), self._e),
+                "orbfe_stream_wait_event")
+
+    def __del__(self):
+        try:
+            if self._e:
+                L.lib().orbfe_event_destroy(self._e)
+        except Exception:  # interpreter shutdown
+            pass
+
+
+def new_event(device: int):
+    """An ordering event for the pipeline's cross-stream dependencies (DevEvent by default)."""
+    import os
+    import torch
+    if os.environ.get("ORBFE_TORCH_EVENTS", "0") == "1":
+        return torch.cuda.Event()
+    return DevEvent(device)
+
+
 class PipelineStreams:
     """The pipeline's concurrently busy streams, created natively in one go: one extraction stream
     per extractor, the matching stream, and (several extractors) one high-priority side stream
@@ -221,9 +260,12 @@ class C3Pipeline:
                     p.kf2_n_dev = self.cnt.data_ptr() + b * 4
                     p.fv1_nodes_dev = self.nodes.data_ptr() + a * 4
                     p.fv2_nodes_dev = self.nodes.data_ptr() + b * 4
-                self.extracted = torch.cuda.Event()
-                self.vocabbed = torch.cuda.Event()
-                self.matched = torch.cuda.Event()
+                self.extracted = new_event(dev.index)
+                self.vocabbed = new_event(dev.index)
+                self.matched = new_event(dev.index)
+                # set by an after_match hook whose work on another stream still reads the set (the
+                # C4 gather): the set is reused only after it as well
+                self.released = None
                 self.mstream = None  # the stream the last matching of this set ran on
 
             def view(self, i):
@@ -304,6 +346,8 @@ class C3Pipeline:
         B, H, W, cap = self.B, self.H, self.W, self.cap
         s, ext = self.streams[k % len(self.streams)], self.exts[k]
         s.wait_event(o.matched)  # the matching that last read this set is done
+        if o.released is not None:  # and whatever an after_match hook still runs on it (the gather)
+            s.wait_event(o.released)
         if self.stereo_on_match and self.stereo_done[k] is not None:
             # ComputeStereoMatches of this handle's previous sub-batch (matching stream) read the
             # pyramids this extraction overwrites
@@ -369,8 +413,9 @@ class C3Pipeline:
         if self.stereo and self.stereo_on_match:
             # off the extraction chain: the handle's next extraction waits for it (run())
             self._stereo(o, o.ext, m)
-            ev = self.stereo_done[o.k] = self._torch.cuda.Event()
-            ev.record(m)
+            if self.stereo_done[o.k] is None:  # one per handle, re-recorded (earlier waits keep the old record)
+                self.stereo_done[o.k] = new_event(self.dev.index)
+            self.stereo_done[o.k].record(m)
         if not (self.vocab_inline or self.vocab_side):
             self._vocab(o, m)
         if self.n_pairs:
