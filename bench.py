@@ -223,7 +223,7 @@ class Gatherer:
     sub-batch: --gather-proxy measured 83k -> 54k stereo frames/s at N = 2). The output set is
     reused only after its payload left (o.released, recorded behind the transfers)."""
 
-    def __init__(self, pipe, world, rank, dev, comm_dev):
+    def __init__(self, pipe, world, rank, dev, comm_dev, comm=None):
         import torch
         from orb_slam2_2021_amd.parallel import packed_bytes
         self.pipe, self.world, self.rank = pipe, world, rank
@@ -236,7 +236,9 @@ class Gatherer:
         self.transfers = 0
         self.last = None  # rank 0: the last exchange's per-rank views (alias the receive buffers)
         self.last_set = None
-        self.comm = torch.cuda.Stream(dev)  # created after the pipeline's busy streams
+        # the pipeline's comm stream (a hardware queue of its own, PipelineStreams); torch's pool
+        # only with --torch-streams
+        self.comm = comm if comm is not None else torch.cuda.Stream(dev)
         from orb_slam2_2021_amd.pipeline import new_event
         self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
         self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
@@ -276,7 +278,7 @@ class GatherProxy:
     with CU blit kernels, where a real receive writes what xGMI delivers: an upper bound on the HBM
     side, no model of the links."""
 
-    def __init__(self, pipe, n_gpus, dev):
+    def __init__(self, pipe, n_gpus, dev, comm=None):
         import torch
         from orb_slam2_2021_amd.parallel import packed_bytes
         self.pipe, self.n = pipe, n_gpus
@@ -284,7 +286,7 @@ class GatherProxy:
         self.bufs = {id(o): torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for o in pipe.sets}
         self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
         self.recv = [torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for _ in range(n_gpus - 1)]
-        self.stream = torch.cuda.Stream(dev)  # created after the pipeline's streams, as RCCL's is
+        self.stream = comm if comm is not None else torch.cuda.Stream(dev)  # PipelineStreams.comm
         from orb_slam2_2021_amd.pipeline import new_event
         self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
         self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
@@ -346,7 +348,8 @@ def main():
                                                                   side_last=args.inline_side,
                                                                   side_high=not args.side_normal,
                                                                   cu_split=args.cu_split,
-                                                                  side_per_stream=args.side_per_stream)
+                                                                  side_per_stream=args.side_per_stream,
+                                                                  comm=world > 1 or args.gather_proxy > 1)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -413,9 +416,10 @@ def main():
             o.matched.record(m)
         pipe._match = extract_only
     gather = world > 1 and not args.no_gather
-    g = Gatherer(pipe, world, rank, dev, comm_dev) if gather else None
+    comm = pstreams.comm if pstreams is not None and pstreams.comm is not None else None
+    g = Gatherer(pipe, world, rank, dev, comm_dev, comm) if gather else None
     if args.gather_proxy > 1 and world == 1:
-        g = GatherProxy(pipe, args.gather_proxy, dev)
+        g = GatherProxy(pipe, args.gather_proxy, dev, comm)
     counter = [0]
 
     def sub_batch():

@@ -774,10 +774,8 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
     if (in.inv_n) in.inv_n[i] = 0;
   }
   if (i < SBP_ROUND_CAP + 4) in.state[i] = 0;
-  if (i == 0) {
-    *in.nmatches = 0;
-    *in.serial = 0;
-  }
+  if (i < 4) in.serial[i] = 0;  // [0] serial walk, [1..3] k_sbp_settle's statistics
+  if (i == 0) *in.nmatches = 0;
 }
 
 __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
@@ -1085,6 +1083,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     __syncthreads();
     // c. re-evaluate them from the candidate cache with round r-1's owners
     const bool dense = s_dense != 0;
+    if (t == 0 && dense) s.serial_used[1] += 1;
     for (int w = t; w < qw; w += SETTLE_THREADS) {
       uint32_t bits = dense ? 0xffffffffu : qbits[w];
       qbits[w] = 0u;
@@ -1094,6 +1093,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
         if (i >= m) break;
         const int nc = a.cand_n[i];
         if (nc == 0) continue;  // no candidate: -1 in every round
+        atomicAdd(&s.serial_used[2], 1);
         auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || prev[k] < i; };
         const int r = nc > 0 ? sbp_cached(a, i, nc, blocked) : sbp_one(a, i, blocked);
         const int old = s.res[i];
@@ -1121,6 +1121,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     }
     __syncthreads();
     const int nd = s_cnt;
+    if (t == 0) s.serial_used[3] += nd;
     for (int c = wv; c < nd; c += NW) {
       const int k = list[c];
       const int cnt = s.inv_n[k];
@@ -2191,6 +2192,13 @@ extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
   if (!m || rounds < 1 || rounds > SBP_MAX_ROUNDS) return ORBFE_ERR_ARG;
   m->max_rounds = rounds;
   m->round_cap = rounds;  // a fixed budget: the serial walk past it (tests of the fallback)
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out3) {
+  if (!m || !out3) return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  ORBFE_HIP_CHECK(hipMemcpy(out3, m->d_serial + 1, 3 * sizeof(int32_t), hipMemcpyDeviceToHost));
   return ORBFE_OK;
 }
 

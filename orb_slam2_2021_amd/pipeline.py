@@ -104,7 +104,7 @@ class PipelineStreams:
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
                  match_high: bool = False, side_last: bool = False, side_high: bool = True,
-                 cu_split: int = 0, side_per_stream: bool = False):
+                 cu_split: int = 0, side_per_stream: bool = False, comm: bool = False):
         import torch
         self.device = device
         self._ptrs = []
@@ -147,6 +147,11 @@ class PipelineStreams:
         # share side stream j) instead of one for all; more busy streams than 4 hardware queues
         # unless GPU_MAX_HW_QUEUES is raised
         self.sides = [self.side] + ([make(side_high) for _ in range(n - 1)] if side_per_stream else [])
+        # comm: a stream for the C4 gather's transfers, created here with the others so that it gets
+        # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
+        # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
+        # that stream's kernels: measured 83k -> 52k stereo frames/s on one GPU (--gather-proxy)
+        self.comm = make(False) if comm else None
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
@@ -163,7 +168,7 @@ class PipelineStreams:
     def close(self):
         """Wait for the streams, point every attached extractor back at its own side stream, then
         destroy the streams (no handle is left holding a destroyed hipStream_t)."""
-        for s in self.extract + [self.match] + self.sides:
+        for s in self.extract + [self.match, self.comm] + self.sides:
             if s is not None:
                 s.synchronize()
         for e in self._attached:

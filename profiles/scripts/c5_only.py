@@ -38,9 +38,12 @@ def main():
     dt = (time.perf_counter() - t0) / (reps * len(frames))
     n = reps * len(frames)
     rounds = m.last_stats()[0]
+    st = np.zeros(3, np.int32)
+    L.check(L.lib().orbfe_debug_matcher_settle_stats(m._h, L.ptr(st)), "settle_stats")
     print(f"c5: {len(G.flags)} MapPoints, {np.mean([F.N for F in frames]):.0f} keypoints per frame, "
           f"{1e3 * dt:.3f} ms per search (host buffers), device {1e3 * np.mean(dev):.1f} us per search, "
-          f"{reps * len(frames)} searches, {rounds} rounds in the last")
+          f"{reps * len(frames)} searches, {rounds} rounds in the last; settle (last search): dense rounds "
+          f"{st[0]}, queries re-evaluated {st[1]}, owners recomputed {st[2]}")
     if "--per-kernel" in sys.argv:
         L.ktimer_select(False)
         for k, (ms, c) in sorted(L.ktimer_read().items(), key=lambda kv: -kv[1][0]):
