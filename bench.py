@@ -88,57 +88,24 @@ def parse(argv=None):
                         "environment's, 4 by default; -1 (default): 8 when WORLD_SIZE > 1, so that the RCCL "
                         "stream of the C4 gather gets a queue of its own instead of sharing one with an "
                         "extraction stream, else the environment's): hardware queues the busy streams spread over")
-    p.add_argument("--defer-matching", action="store_true",
-                   help="enqueue sub-batch i's vocabulary + matching with sub-batch i+1's extraction, after its "
-                        "pyramid (overlapping the FAST / octree / blur / describe phase)")
     p.add_argument("--fast-side", type=int, default=4,
                    help="FAST of levels 0..K-1 on the extractor's side stream as each level is built "
                         "(0: the library default, levels 0..2, best with one handle; 4 with the pipeline's four "
                         "handles: 82.9k vs 82.0k stereo frames/s, interleaved, round 4)")
     p.add_argument("--diag-skip-matching", action="store_true",
                    help="diagnostic, not the metric: skip ComputeBoW + SearchForTriangulation (extraction-only rate)")
-    p.add_argument("--side-normal", action="store_true",
-                   help="the shared side stream at normal priority (default: high)")
-    p.add_argument("--copy0-side", action="store_true",
-                   help="level 1 from the caller's image, the level-0 copy on the side stream "
-                        "(orbfe_debug_set_copy0_side; measured slower)")
     p.add_argument("--inline-side", action="store_true",
                    help="diagnostic: every handle's side-stream work on its own launch stream (with "
                         "--extractors 1 --pipeline 1 every kernel runs alone)")
     p.add_argument("--blur-mode", type=int, default=-1,
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
-                        "side stream, 1 after it on the launch stream, 2 on the side stream once the pyramid is "
-                        "built (default: 0 with one handle, 1 with several)")
-    p.add_argument("--vocab-side", action="store_true",
-                   help="ComputeBoW on the shared side stream (deferred by one sub-batch), only "
-                        "SearchForTriangulation on the matching stream")
-    p.add_argument("--vocab-inline", action="store_true",
-                   help="ComputeBoW on the extraction streams, only SearchForTriangulation on the matching stream")
-    p.add_argument("--match-normal", action="store_true",
-                   help="the matching stream at normal priority (default: high, beside the shared side "
-                        "stream, so that the latency-bound vocabulary + SFT chain keeps up with two handles)")
+                        "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
     p.add_argument("--match-inline", action="store_true",
                    help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
-    p.add_argument("--torch-streams", action="store_true",
-                   help="diagnostic: the pipeline's streams from torch's pool, created after the "
-                        "handles (hardware-queue assignment then depends on the stream count; with "
-                        "several extractors their side work runs inline)")
-    p.add_argument("--side-per-stream", action="store_true",
-                   help="one high-priority side stream per extraction stream instead of one shared (more busy "
-                        "streams than hardware queues unless --hw-queues is raised)")
-    p.add_argument("--stagger", action="store_true",
-                   help="each sub-batch's extraction waits for the previous sub-batch's pyramid (the handles' "
-                        "pyramid chains never overlap)")
     p.add_argument("--stereo-on-extract", action="store_true",
                    help="ComputeStereoMatches on the extraction stream right after each extraction (rounds 1-3's "
                         "placement; default: on the matching stream ahead of the vocabulary, with two handles per "
                         "extraction stream so no extraction waits for it: 78.4-78.5k vs 77.1-77.5k)")
-    p.add_argument("--cu-split", type=int, default=0,
-                   help="each extractor handle's stream on its own share of the CUs (hipExtStreamCreateWithCUMask; "
-                        "1: contiguous CU ranges, 2: interleaved), side work inline on it")
-    p.add_argument("--tiled-pyramid", action="store_true",
-                   help="the tiled k_pyramid launches instead of the default k_copy0 + one k_resize launch per "
-                        "level (comparison; measured slower)")
     p.add_argument("--dump-gather", default="",
                    help="test hook: write each rank's last sub-batch (own keypoints + descriptors) and "
                         "rank 0's gathered payloads to this directory")
@@ -297,22 +264,27 @@ class GatherProxy:
         from orb_slam2_2021_amd.parallel import pack_keypoints_device
         p, m = self.pipe, o.mstream
         buf = self.bufs[id(o)]
-        pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
-                              buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
+        mode = os.environ.get("ORBFE_GPROXY_MODE", "torch")  # diagnostic: which part costs
+        if mode != "evonly":
+            pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                                  buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
+        if mode == "packonly":
+            return
+        if mode == "same":  # the copies on the matching stream itself, no cross-stream events
+            with torch.cuda.stream(m):
+                for r in self.recv:
+                    r.copy_(buf, non_blocking=True)
+            return
         ev = self.packed[id(o)]
         ev.record(m)
         self.stream.wait_event(ev)
-        mode = os.environ.get("ORBFE_GPROXY_MODE", "torch")  # diagnostic: which part costs
         with torch.cuda.stream(self.stream):
             for r in self.recv:
                 if mode == "torch":
                     r.copy_(buf, non_blocking=True)
-                elif mode == "kcopy":  # the same bytes moved by the pack kernel (CU copy, no blit)
-                    pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
-                                          r.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
-                                          self.stream.cuda_stream)
-        o.released = self.sent[id(o)]
-        o.released.record(self.stream)
+        if mode != "norelease":
+            o.released = self.sent[id(o)]
+            o.released.record(self.stream)
         self.transfers += 1
 
     def describe(self):
@@ -343,13 +315,8 @@ def main():
     # one, so that each opens its own hardware queue (PipelineStreams)
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
-    pstreams = None if args.torch_streams else PipelineStreams(gpu, n_ext, match_inline=args.match_inline,
-                                                                  match_high=not args.match_normal,
-                                                                  side_last=args.inline_side,
-                                                                  side_high=not args.side_normal,
-                                                                  cu_split=args.cu_split,
-                                                                  side_per_stream=args.side_per_stream,
-                                                                  comm=world > 1 or args.gather_proxy > 1)
+    pstreams = PipelineStreams(gpu, n_ext, match_inline=args.match_inline, side_last=args.inline_side,
+                               comm=world > 1 or args.gather_proxy > 1)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -373,18 +340,14 @@ def main():
     host = make_inputs(args, world, rank)
     d_img = torch.from_numpy(host).to(dev)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
-    if args.tiled_pyramid:
-        ext.debug_force_level_launches(False)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
     if args.fast_side > 0:
         ext.debug_set_fast_side_levels(args.fast_side)
     if args.blur_mode >= 0:
         ext.debug_set_blur_mode(args.blur_mode)
-    if args.inline_side or args.cu_split:
+    if args.inline_side:
         ext.debug_set_inline_side(True)
-    if args.copy0_side:
-        ext.debug_set_copy0_side(True)
     exts = [ext]
     n_handles = n_ext * max(1, args.handles_per_stream)
     if n_handles > 1:
@@ -392,7 +355,7 @@ def main():
         # shares one high-priority stream (PipelineStreams.side)
         exts += [ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index) for _ in range(n_handles - 1)]
         for e in exts:
-            if pstreams is None or args.inline_side or args.cu_split:
+            if args.inline_side:
                 e.debug_set_inline_side(True)
             if args.fast_side > 0:
                 e.debug_set_fast_side_levels(args.fast_side)
@@ -400,15 +363,9 @@ def main():
             # and the shared side stream is better left to FAST alone: the blur follows the octree
             # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
-            if args.copy0_side:
-                e.debug_set_copy0_side(True)
-            if args.tiled_pyramid:
-                e.debug_force_level_launches(False)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
-                           depth=pipe_depth(args), defer=args.defer_matching,
-                           stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                           vocab_inline=args.vocab_inline, vocab_side=args.vocab_side, pairs=args.pairs,
-                           stereo_on_match=not args.stereo_on_extract, stagger=args.stagger)
+                           depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
+                           pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream
@@ -416,7 +373,7 @@ def main():
             o.matched.record(m)
         pipe._match = extract_only
     gather = world > 1 and not args.no_gather
-    comm = pstreams.comm if pstreams is not None and pstreams.comm is not None else None
+    comm = pstreams.comm
     g = Gatherer(pipe, world, rank, dev, comm_dev, comm) if gather else None
     if args.gather_proxy > 1 and world == 1:
         g = GatherProxy(pipe, args.gather_proxy, dev, comm)
@@ -427,9 +384,6 @@ def main():
         counter[0] += 1
         pipe.run(d_img[j].data_ptr(), after_match=g.pack if g else None)
 
-    def drain():  # every enqueued sub-batch matched (and gathered)
-        pipe.flush(after_match=g.pack if g else None)
-
     def barrier():
         if world > 1:
             dist.barrier()
@@ -438,7 +392,6 @@ def main():
     torch.cuda.set_stream(pipe.stream)
     for _ in range(args.warmup * S_sub):
         sub_batch()
-    drain()
     torch.cuda.synchronize()
     # host cost of enqueueing one sub-batch (untimed): 32 sub-batches right after a synchronize,
     # while the device queues are still short enough that no launch blocks
@@ -446,7 +399,6 @@ def main():
     for _ in range(32):
         sub_batch()
     host_us = (time.perf_counter() - th0) / 32 * 1e6
-    drain()
     torch.cuda.synchronize()
     # probe pass (untimed): every kernel's launches timed by their own dispatch interval
     # (orbfe_ktimer: start / stop events bound to the dispatch, the interval rocprofv3's kernel
@@ -456,7 +408,6 @@ def main():
     L.ktimer_select(True)
     for _ in range(args.probe_subbatches):
         sub_batch()
-    drain()
     torch.cuda.synchronize()
     L.ktimer_select(False)
     probe = L.ktimer_read()
@@ -484,7 +435,6 @@ def main():
             sub_batch()
             if ev:
                 set_events(False)
-    drain()
     t_enq = time.perf_counter()  # every launch of the timed region enqueued
     torch.cuda.synchronize()
     barrier()

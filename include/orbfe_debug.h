@@ -25,13 +25,8 @@ int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, 
 /* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
  * global-memory path for every level; < 0 restores the automatic size). */
 int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
-/* 1 (default): k_copy0 + one k_resize launch per level; 0: build the pyramid with the tiled
- * k_pyramid launches (groups of levels, no k_copy0) when the geometry allows (measured slower,
- * DESIGN.md section 5). */
-int orbfe_debug_force_level_launches(orbfe_extractor* h, int on);
-/* Per-level pyramid path only: FAST of levels 0..k-1 on the side stream, each launched as soon
- * as its level is built, the rest in one launch after the resize chain (k <= 0: the default,
- * levels 0..2). The tiled path runs the first group's levels on the side stream. */
+/* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the rest
+ * in one launch after the resize chain (k <= 0: the default, levels 0..2). */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);
 /* 1: run the side-stream work (k_blur, the early FAST levels) on the launch stream, for callers
  * that overlap whole extractions on several streams of their own; 0 (default): the handle's
@@ -41,12 +36,8 @@ int orbfe_debug_set_inline_side(orbfe_extractor* h, int on);
  * handles whose extractions overlap); NULL restores the handle's own side stream. */
 int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
 /* Where GaussianBlur runs: 0 (default) on the side stream beside DistributeOctTree, 1 on the
- * launch stream after DistributeOctTree, 2 on the side stream as soon as the pyramid is built. */
+ * launch stream after DistributeOctTree (several handles sharing one side stream). */
 int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode);
-/* 1: with a side stream and the window resize, level 1 is resized from the caller's image and
- * the copy into pyramid level 0 runs on the side stream beside the resize chain; 0 (default,
- * measured faster): the copy first on the launch stream, level 1 from the copied level 0. */
-int orbfe_debug_set_copy0_side(orbfe_extractor* h, int on);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

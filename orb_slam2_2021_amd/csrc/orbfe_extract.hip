@@ -117,11 +117,6 @@ struct ExtractArgs {
   int ini_th, min_th;
   int roi_w_max, roi_h_max;
   int node_cap, sort_cap, scan_cap, key_lds_cap;
-  const int4* pyr_xt;     // k_pyramid: per (tile column, level) {own0, own1, comp0, comp1}
-  const int4* pyr_yt;     // k_pyramid: per (tile row, level) {own0, own1, comp0, comp1}
-  const int2* pyr_blob;   // k_pyramid: per tile column / row {blob start, blob dwords}
-  const uint32_t* pyr_xblob;  // k_pyramid: resize tap records per tile column
-  const uint32_t* pyr_yblob;  // k_pyramid: ytab rows per tile row
   const uint4* rgrp;      // k_resize: per 4-column group {sel[4]}, {alpha[4]} (2 x uint4)
   const int* rgx0;        // k_resize: first source column of each group
   int umax[16];
@@ -235,7 +230,7 @@ __device__ __forceinline__ void store_row4(uint8_t* row, int x, int w, uint32_t 
 
 // ---------------------------------------------------------------------------------------------
 // k_resize: level l from level l-1 (ComputePyramid, ORBextractor.cc:1105-1135), one launch per
-// level -- the fallback of k_pyramid for scale factors whose taps do not fit an 8-byte window.
+// level -- the fallback of k_resize_win for scale factors whose taps do not fit an 8-byte window.
 #define RESIZE_ROWS 8  // output rows per thread (the column taps are loaded once)
 __global__ __launch_bounds__(256) void k_resize(ExtractArgs a, int l) {
   const LevelDesc ld = a.levels[l];
@@ -337,23 +332,14 @@ __device__ __forceinline__ uint32_t resize_win_row(const uint32_t W0r0, const ui
 
 // Items (4-column group, row pair) of the level are numbered row-major and dealt to the threads
 // linearly, so only the last wave of an image's grid has idle lanes (a 2-D grid of 256-column
-// blocks left up to a third of the lanes idle on the right edge of every row band).
-// SRC_IN (level 1 only): the source is the caller's image itself (any pitch and alignment) rather
-// than level 0 of the pyramid, so that k_copy0 can run beside the resize chain on the side
-// stream: per-row byte offsets from the row indices in ywin.w, dword-aligned loads from the
-// aligned image base and a per-row v_alignbyte shift; the buffer's extent ends at the last
-// input byte, so the window of a row's last group past the image end reads zeros (unused taps).
-#ifndef ORBFE_RESIZE_PAIRS
-#define ORBFE_RESIZE_PAIRS 1  // k_resize_win: output row pairs per thread (2 and 4 measured slower)
-#endif
-template <bool SRC_IN>
+// blocks left up to a third of the lanes idle on the right edge of every row band). One row pair
+// per thread (2 and 4 pairs with every source row in flight measured slower).
 __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G, uint32_t gmagic) {
-  constexpr int RP = ORBFE_RESIZE_PAIRS;
   const LevelDesc ld = a.levels[l];
   const int item = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
   const int pr = gmagic ? (int)__umulhi((uint32_t)item, gmagic) : item;  // item / G
   const int g = item - pr * G, x = 4 * g;
-  const int y0 = 2 * RP * pr;
+  const int y0 = 2 * pr;
   if (y0 >= ld.h) return;
   const LevelDesc ls = a.levels[l - 1];
   // the source level as dwords from a wave-uniform base; per-lane offsets are 32-bit unsigned
@@ -363,82 +349,40 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
   const uint32_t sx0 = (uint32_t)a.rgx0[gi];
   const uint4 sel = a.rgrp[2 * gi], alp16 = a.rgrp[2 * gi + 1];
   const uint32_t cx = sx0 >> 2;
-  // every source row of the thread's RP output row pairs in flight before the first is used
-  uint32_t W0[RP][4], W1[RP][4];
-  int yz[RP][2];
+  const int4 ya = a.ywin[(uint32_t)(ld.tab_y + y0)], yb = a.ywin[(uint32_t)(ld.tab_y + min(y0 + 1, ld.h - 1))];
+  const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
+  // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
+  uint32_t wv[4][3];
 #pragma unroll
-  for (int q = 0; q < RP; q++) {
-    const int ra = min(y0 + 2 * q, ld.h - 1), rb = min(y0 + 2 * q + 1, ld.h - 1);
-    const int4 ya = a.ywin[(uint32_t)(ld.tab_y + ra)], yb = a.ywin[(uint32_t)(ld.tab_y + rb)];
-    yz[q][0] = ya.z;
-    yz[q][1] = yb.z;
-    uint32_t wv[4][3];
-    if constexpr (!SRC_IN) {
-      const uint32_t rows[4] = {(uint32_t)ya.x + cx, (uint32_t)ya.y + cx, (uint32_t)yb.x + cx, (uint32_t)yb.y + cx};
-      // raw buffer loads from the wave-uniform base: 32-bit byte offsets, no per-lane 64-bit math
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(src), 0, 0x7fffffff, 0x00020000);
+  for (int r = 0; r < 4; r++) {
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
+    for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
+  }
+  const int sh = (int)(sx0 & 3u);
+  uint32_t W0[4], W1[4];
 #pragma unroll
-        for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * rows[r]) + 4 * k, 0, 0);
-      }
-      const int sh = (int)(sx0 & 3u);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        W0[q][r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
-        W1[q][r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
-      }
-    } else {
-      const uint8_t* ib = a.img0 + (long long)img * a.img_stride;
-      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(ib) & 3u);
-      const LevelDesc l0 = a.levels[0];
-      const long long extent = (long long)(a.n_images - 1 - img) * a.img_stride + (long long)(l0.h - 1) * a.img_pitch + l0.w + mis;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ib - mis), 0, (int)min(extent, 0x7fffffffll), 0x00020000);
-      const uint32_t ri[4] = {(uint32_t)ya.w & 0xffffu, (uint32_t)ya.w >> 16, (uint32_t)yb.w & 0xffffu, (uint32_t)yb.w >> 16};
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const uint32_t b = ri[r] * (uint32_t)a.img_pitch + sx0 + mis;
-        if ((long long)(b & ~3u) + 12 <= extent) {
-#pragma unroll
-          for (int k = 0; k < 3; k++) wv[r][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(b & ~3u) + 4 * k, 0, 0);
-        } else {  // the image block's last bytes: a dword past the extent would read as all zeros
-#pragma unroll
-          for (int k = 0; k < 3; k++) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(b & ~3u) + 4 * k + j, 0, 0) << (8 * j);
-            wv[r][k] = v;
-          }
-        }
-        W0[q][r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], b & 3u);
-        W1[q][r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], b & 3u);
-      }
-    }
+  for (int r = 0; r < 4; r++) {
+    W0[r] = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
+    W1[r] = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
   }
   uint8_t* out = a.pyr + (long long)img * a.pyr_stride + ld.pyr_off;
-  const bool simd = x + 4 <= ld.simd_end;  // every column on the SIMD128 rounding (all but a row's tail)
-#pragma unroll
-  for (int q = 0; q < RP; q++) {
-    const int ya0 = y0 + 2 * q;
-    if (ya0 >= ld.h) break;
-    const int2 ba = make_int2(0, yz[q][0]), bb = make_int2(0, yz[q][1]);
-    uint32_t pa, pb;
-    if (simd) {
-      pa = resize_win_row<false>(W0[q][0], W1[q][0], W0[q][1], W1[q][1], sel, alp16, x, ld, ba);
-      pb = resize_win_row<false>(W0[q][2], W1[q][2], W0[q][3], W1[q][3], sel, alp16, x, ld, bb);
-    } else {
-      pa = resize_win_row<true>(W0[q][0], W1[q][0], W0[q][1], W1[q][1], sel, alp16, x, ld, ba);
-      pb = resize_win_row<true>(W0[q][2], W1[q][2], W0[q][3], W1[q][3], sel, alp16, x, ld, bb);
-    }
-    store_row4(out + __umul24((uint32_t)ya0, (uint32_t)ld.pitch), x, ld.w, pa);
-    if (ya0 + 1 < ld.h) store_row4(out + __umul24((uint32_t)(ya0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
+  const int2 ba = make_int2(0, ya.z), bb = make_int2(0, yb.z);
+  uint32_t pa, pb;
+  if (x + 4 <= ld.simd_end) {  // every column on the SIMD128 rounding (all but a row's tail)
+    pa = resize_win_row<false>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
+    pb = resize_win_row<false>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
+  } else {
+    pa = resize_win_row<true>(W0[0], W1[0], W0[1], W1[1], sel, alp16, x, ld, ba);
+    pb = resize_win_row<true>(W0[2], W1[2], W0[3], W1[3], sel, alp16, x, ld, bb);
   }
+  store_row4(out + __umul24((uint32_t)y0, (uint32_t)ld.pitch), x, ld.w, pa);
+  if (y0 + 1 < ld.h) store_row4(out + __umul24((uint32_t)(y0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
 }
 
 
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
-// padding columns) -- the per-level path's level 0; k_pyramid's first group does this itself.
+// padding columns).
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
   // One wavefront per row. The caller's row (any pitch, any byte alignment) comes in as coalesced
   // aligned dwords into LDS (byte loads only for a last dword that would run past the row); the
@@ -503,189 +447,6 @@ __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
     const int col = lane < 3 ? -1 - k : w + k;                        // -1..-3, w..w+2
     const int from = lane < 3 ? min(1 + k, w - 1) : max(w - 2 - k, 0);  // REFLECT_101
     row[4 + col] = sb[from];
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_pyramid: ComputePyramid (ORBextractor.cc:1105-1135) as a few launches of 2-D tiles, each
-// building a group of consecutive levels src+1..top from level src (the caller's image for the
-// first group, whose tiles also write level 0 into the padded pyramid block: k_copy0's job).
-// A workgroup owns one tile of the group's top level and the matching (4-column aligned) piece
-// of every lower level; it loads the source region its cone of bilinear taps reaches into LDS
-// and computes each level's region -- its own piece plus the halo the next level reads, which
-// neighbouring tiles compute too (identical bytes) -- from the previous level's region in LDS,
-// writing only its own pieces to HBM. No dependency between workgroups; every level stays the
-// uint8 rounding of the level below, exactly the reference chain. Host tables per (tile column,
-// level) and (tile row, level): {own0, own1, comp0, comp1}, comp x bounds multiples of 4; per
-// tile column a blob of the resize taps of its 4-column groups (12 dwords: first source column,
-// 4 selectors, 4 alphas) level after level, per tile row a blob of its ytab rows. Every global
-// load of a workgroup (blobs, source region) is issued up front; the levels then run from LDS.
-struct PyrGroup {
-  int src, top;      // source level and top level of the group
-  int ntx, nty;      // tiles of the top level
-  int tx_off, ty_off;  // pyr_xt / pyr_yt index of tile (0, level src)
-  int bx_off, by_off;  // pyr_blob index of tile column 0 / tile row 0
-  int buf0, buf1;    // LDS bytes of the two ping-pong region buffers
-  int tab;           // LDS bytes of the staged blobs
-  int dbg;           // experiment switches (0 in production)
-};
-#define PYR_REC 12   // dwords per 4-column group record
-
-// LDS row pitch of a region with comp x bounds [c0, c1): the 12-byte window of the last
-// 4-column group may run 11 bytes past the region
-__host__ __device__ __forceinline__ int pyr_lds_pitch(int c0, int c1) { return c1 - c0 + 12; }
-
-
-typedef __attribute__((address_space(1))) const uint32_t global_u32;  // global_load, not flat_load
-// i / n as __umulhi(i, ceil(2^32 / n)), exact for i * n < 2^32; n == 1 has no 32-bit magic
-// (magic 0 marks it)
-__device__ __forceinline__ uint32_t magic_div(uint32_t n) { return n <= 1 ? 0u : (uint32_t)((0x100000000ull + n - 1) / n); }
-__device__ __forceinline__ int div_magic(int i, uint32_t m) { return m ? (int)__umulhi((uint32_t)i, m) : i; }
-
-// Own piece of level ld (rows oy.x..oy.y, columns ox.x..ox.y) from its LDS region (comp origin
-// (cx.z, cy.z), pitch P) to the padded pyramid block, one dword per item. Tiles on the image
-// edges also write the REFLECT_101 columns -3..-1 (dword -4..-1) and w..w+2 (in the dwords up to
-// column w+2) that k_blur reads; bytes past w+2 are never read.
-__device__ __forceinline__ void pyr_copy_own(const uint8_t* reg, int P, int4 ox, int4 oy, int cx0, int cy0,
-                                             const LevelDesc& ld, uint8_t* out, int t) {
-  const int w = ld.w;
-  const int d0 = ox.x == 0 ? -1 : ox.x >> 2;
-  const int d1 = ox.y == w ? ((w + 2) >> 2) + 1 : ox.y >> 2;
-  const int nd = d1 - d0, items = nd * (oy.y - oy.x);
-  const uint32_t m = magic_div((uint32_t)nd);
-  for (int i = t; i < items; i += 256) {
-    const int r = div_magic(i, m), x = 4 * (d0 + i - r * nd), y = oy.x + r;
-    const uint8_t* row = reg + __umul24((uint32_t)(y - cy0), (uint32_t)P);
-    uint32_t v;
-    if (x >= 0 && x + 4 <= w) {
-      v = *reinterpret_cast<const uint32_t*>(row + x - cx0);
-    } else {
-      v = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int c = x + j, sc = c < 0 ? -c : (c >= w ? 2 * w - 2 - c : c);
-        if (c >= -3 && c <= w + 2) v |= (uint32_t)row[sc - cx0] << (8 * j);
-      }
-    }
-    *reinterpret_cast<uint32_t*>(out + (long long)y * ld.pitch + x) = v;
-  }
-}
-
-#define PYR_LOADS 8  // source-region dwords in flight per thread
-__global__ __launch_bounds__(256) void k_pyramid(ExtractArgs a, PyrGroup g) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int2 blk = xcd_block2d();
-  const int img = blk.y, tyi = blk.x / g.ntx, txi = blk.x - tyi * g.ntx;
-  const int t = threadIdx.x, NL = g.top - g.src + 1;
-  const int4* XT = a.pyr_xt + g.tx_off + txi * NL;
-  const int4* YT = a.pyr_yt + g.ty_off + tyi * NL;
-  uint32_t* const tabs = reinterpret_cast<uint32_t*>(smem + g.buf0 + g.buf1);
-  const int2 bx = a.pyr_blob[g.bx_off + txi], by = a.pyr_blob[g.by_off + tyi];
-  uint8_t* const pyr = a.pyr + (long long)img * a.pyr_stride;
-  // 1. blobs and the source level's region -> LDS; all loads of a thread in flight together
-  {
-    const int4 cx = XT[0], cy = YT[0];
-    const LevelDesc ls = a.levels[g.src];
-    const int nt = bx.y + by.y;
-    uint32_t tv[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = t + 256 * k;
-      tv[k] = i < bx.y ? a.pyr_xblob[bx.x + i] : (i < nt ? a.pyr_yblob[by.x + i - bx.y] : 0u);
-    }
-    for (int i = t + 1024; i < nt; i += 256) tabs[i] = i < bx.y ? a.pyr_xblob[bx.x + i] : a.pyr_yblob[by.x + i - bx.y];
-    const int P = pyr_lds_pitch(cx.z, cx.w), G = (cx.w - cx.z) >> 2, items = G * (cy.w - cy.z);
-    const uint32_t gm = magic_div((uint32_t)G);
-    const uint8_t* in = g.src == 0 ? a.img0 + (long long)img * a.img_stride : pyr + ls.pyr_off;
-    const long long ipitch = g.src == 0 ? a.img_pitch : ls.pitch;
-    for (int i0 = 0; i0 < items; i0 += 256 * PYR_LOADS) {
-      uint32_t v[PYR_LOADS];
-#pragma unroll
-      for (int k = 0; k < PYR_LOADS; k++) {
-        const int i = min(i0 + t + 256 * k, items - 1);
-        const int r = div_magic(i, gm), x = cx.z + 4 * (i - r * G);
-        const uintptr_t pa = reinterpret_cast<uintptr_t>(in + (long long)(cy.z + r) * ipitch + x);
-        // the aligned dwords holding bytes x..x+3 (any caller pitch); the second only when it
-        // holds a byte of the row, so nothing past the caller's buffer is touched
-        const global_u32* q = (const global_u32*)(pa & ~(uintptr_t)3);
-        const int sh = (int)(pa & 3);
-        if (g.dbg & 4) { v[k] = pa; continue; }
-        const uint32_t w0 = q[0], w1 = (sh != 0 && x - sh + 4 < ls.w) ? q[1] : 0u;
-        v[k] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-      }
-#pragma unroll
-      for (int k = 0; k < PYR_LOADS; k++) {
-        const int i = i0 + t + 256 * k;
-        if (i < items) {
-          const int r = div_magic(i, gm);
-          *reinterpret_cast<uint32_t*>(smem + __umul24((uint32_t)r, (uint32_t)P) + 4 * (i - r * G)) = v[k];
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (t + 256 * k < nt) tabs[t + 256 * k] = tv[k];
-    __syncthreads();
-    if (g.src == 0 && !(g.dbg & 2)) pyr_copy_own(smem, P, cx, cy, cx.z, cy.z, ls, pyr + ls.pyr_off, t);
-  }
-  if (g.dbg & 1) return;
-  // 2. levels src+1..top, each from the previous level's region in LDS into its own region
-  //    buffer, then (after the barrier) its own piece to HBM
-  int xo = 0, yo = bx.y;  // this level's records / ytab rows in the staged blobs (dwords)
-  for (int l = g.src + 1; l <= g.top; l++) {
-    const int j = l - g.src;
-    const int4 sx = XT[j - 1], sy = YT[j - 1], ox = XT[j], oy = YT[j];
-    // (offsets from smem itself, so that the compiler keeps these LDS accesses as ds_* ops)
-    const uint8_t* S = smem + (((j - 1) & 1) ? g.buf0 : 0);
-    uint8_t* D = smem + ((j & 1) ? g.buf0 : 0);
-    const int SP = pyr_lds_pitch(sx.z, sx.w), DP = pyr_lds_pitch(ox.z, ox.w);
-    const LevelDesc ld = a.levels[l];
-    const int sh_max = a.levels[l - 1].h - 1;
-    const int G = (ox.w - ox.z) >> 2, R = oy.w - oy.z, R2 = (R + 1) >> 1;
-    // groups [0, Gm) lie below simd_end (the SIMD128 rounding only); [Gm, G) reach it. Both rows
-    // of a pair are computed and stored (the region buffers hold one spare row for odd R).
-    const int Gm = min(G, max(0, ((ld.simd_end & ~3) - ox.z) >> 2));
-    auto item = [&](auto tail, int pr, int gx) {
-      const int x = ox.z + 4 * gx, r0 = 2 * pr;
-      const uint32_t* rec = tabs + xo + PYR_REC * gx;
-      const int lc = (int)rec[0] - sx.z, sh = lc & 3;
-      const uint4 sel = *reinterpret_cast<const uint4*>(rec + 4), alp = *reinterpret_cast<const uint4*>(rec + 8);
-      const int2 ya = *reinterpret_cast<const int2*>(tabs + yo + 2 * r0);
-      const int2 yb = *reinterpret_cast<const int2*>(tabs + yo + 2 * min(r0 + 1, R - 1));
-      const int rows[4] = {ya.x, ya.x + 1, yb.x, yb.x + 1};
-      uint32_t W0[4], W1[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(
-            S + __umul24((uint32_t)(min(max(rows[r], 0), sh_max) - sy.z), (uint32_t)SP) + (lc & ~3));
-        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2];
-        W0[r] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        W1[r] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-      }
-      uint32_t* d = reinterpret_cast<uint32_t*>(D + __umul24((uint32_t)r0, (uint32_t)DP) + 4 * gx);
-      d[0] = resize_win_row<decltype(tail)::value>(W0[0], W1[0], W0[1], W1[1], sel, alp, x, ld, ya);
-      d[DP >> 2] = resize_win_row<decltype(tail)::value>(W0[2], W1[2], W0[3], W1[3], sel, alp, x, ld, yb);
-    };
-    {
-      const int items = Gm * R2;
-      const uint32_t gm = magic_div((uint32_t)Gm);
-      for (int i = t; i < items; i += 256) {
-        const int pr = div_magic(i, gm);
-        item(std::false_type{}, pr, i - pr * Gm);
-      }
-    }
-    if (Gm < G) {
-      const int Gt = G - Gm, items = Gt * R2;
-      const uint32_t gm = magic_div((uint32_t)Gt);
-      for (int i = t; i < items; i += 256) {
-        const int pr = div_magic(i, gm);
-        item(std::true_type{}, pr, Gm + i - pr * Gt);
-      }
-    }
-    __syncthreads();
-    if (!(g.dbg & 2)) pyr_copy_own(D, DP, ox, oy, ox.z, oy.z, ld, pyr + ld.pyr_off, t);
-    xo += PYR_REC * G;
-    yo += 2 * R;
   }
 }
 
@@ -1105,13 +866,6 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
   };
   if constexpr (RSC == 0)
     for (int i = lane; i < (mw * mh + 3) >> 2; i += 64) reinterpret_cast<uint32_t*>(m8)[i] = 0u;
-#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 1
-  // phase-cost diagnostic builds only (profiles/scripts/r3_fast_phases.sh; -DORBFE_FAST_DIAG=1..3
-  // stop after the ROI load, the prefilter, the arc strength): no corners, the work kept alive
-  wave_sync();
-  if (lane == 0) *cnt_out = (int)m8[lane] + roi[lane] == 1000 ? 1 : 0;
-  return;
-#endif
   wave_sync();
   const uint8_t* R = roi + xo;  // pixel (r, c) of the ROI at R[r * RS + c]
   uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
@@ -1176,10 +930,6 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       }
     }
     wave_sync();
-#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 2
-    if (lane == 0) *cnt_out = nlist == 100000 ? 1 : 0;
-    return;
-#endif
     // 2b+3. on the survivors, two list entries per lane in packed 16-bit halves: the arc strength
     //     (OpenCV cornerScore + 1) of the corners at t goes to m8 and, compacted in order, back
     //     into the list
@@ -1210,10 +960,6 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       ncorner += __popcll(b0) + __popcll(b1);
     }
     wave_sync();
-#if defined(ORBFE_FAST_DIAG) && ORBFE_FAST_DIAG == 3
-    if (lane == 0) *cnt_out = ncorner == 100000 ? 1 : 0;
-    return;
-#endif
     // 4. NMS over the corners at t (out-of-region neighbours and non-corners score 0)
     for (int j0 = 0; j0 < ncorner; j0 += 64) {
       const int j = j0 + lane;
@@ -2059,32 +1805,19 @@ struct DwX3 {
   uint32_t x, y, z;
 };
 
-#ifndef ORBFE_FUSED_BLUR
-#define ORBFE_FUSED_BLUR 0  // 1: k_describe blurs each keypoint's window itself, no k_blur launch
-#endif
-#ifndef ORBFE_DESC_WPB
-#define ORBFE_DESC_WPB 4  // k_describe wavefronts per workgroup (4 keypoints each)
-#endif
-constexpr int DESC_THREADS = 64 * ORBFE_DESC_WPB;
-#ifndef ORBFE_DESC_OCC
-#define ORBFE_DESC_OCC 0
-#endif
-#if ORBFE_DESC_OCC
-#define DESC_OCC_ATTR __attribute__((amdgpu_waves_per_eu(ORBFE_DESC_OCC)))
-#else
-#define DESC_OCC_ATTR
-#endif
-__global__ __launch_bounds__(DESC_THREADS) DESC_OCC_ATTR void k_describe(ExtractArgs a) {
+constexpr int DESC_WPB = 4;  // k_describe wavefronts per workgroup (4 keypoints each)
+constexpr int DESC_THREADS = 64 * DESC_WPB;
+__global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
   __shared__ float4 s_pat[256];
   __shared__ uint32_t s_mom[4 * 279];
-  __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * ORBFE_DESC_WPB][37 * 10];
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * DESC_WPB][37 * 10];
   for (int k = threadIdx.x; k < 256; k += DESC_THREADS) s_pat[k] = c_patf[k];
   for (int k = threadIdx.x; k < 4 * 279; k += DESC_THREADS) s_mom[k] = (&c_momask[0][0][0])[k];
   __syncthreads();  // before any wavefront may leave
   const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
   const int img = blk.y;
-  const int slot = (blk.x * ORBFE_DESC_WPB + w) * 4 + grp;
+  const int slot = (blk.x * DESC_WPB + w) * 4 + grp;
   const int32_t* lc = a.lvlcnt + (long long)img * a.nlevels;
   if (blk.x == 0 && threadIdx.x == 0) {
     int tot = 0;
@@ -2132,41 +1865,12 @@ __global__ __launch_bounds__(DESC_THREADS) DESC_OCC_ATTR void k_describe(Extract
     mu[k] = DwX3{0u, 0u, 0u};
     if (l16 + 16 * k < 93) __builtin_memcpy(&mu[k], usrc + (k / 3) * step16 + ur[k % 3] * pitch + 12 * uc[k % 3], 12);
   }
-#if ORBFE_FUSED_BLUR
-  // GaussianBlur fused here: rows cy-21 .. cy+21 of the unblurred level
-  // (REFLECT_101 rows, the padding's reflected columns), lane l16 < 12 one dword at column
-  // xb - 4 + 4 l16; lanes 1..10 produce the blurred window's 10 dwords per row, k_blur's arithmetic
-  (void)bsrc;
-  const uint8_t* levu = a.pyr + lbase;
-  const int bx = xb - 4 + 4 * (l16 < 12 ? l16 : 0);
-  uint32_t rowv[43];
-#pragma unroll
-  for (int i = 0; i < 43; i++)
-    rowv[i] = *reinterpret_cast<const uint32_t*>(levu + (long long)reflect101(cy - 21 + i, ld.h) * pitch + bx);
-#else
   uint2 bw[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) {
     bw[k] = make_uint2(0u, 0u);
     if (l16 + 16 * k < 185) __builtin_memcpy(&bw[k], bsrc + (k / 5) * step16 + br[k % 5] * pitch + 8 * bc[k % 5], 8);
   }
-#endif
-#if defined(ORBFE_DESC_DIAG) && ORBFE_DESC_DIAG == 1  // phase-cost diagnostic builds only (wrong output)
-  {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < 6; k++) acc ^= mu[k].x ^ mu[k].y ^ mu[k].z;
-#if ORBFE_FUSED_BLUR
-#pragma unroll
-    for (int k = 0; k < 43; k++) acc ^= rowv[k];
-#else
-#pragma unroll
-    for (int k = 0; k < 12; k++) acc ^= bw[k].x ^ bw[k].y;
-#endif
-    if (acc == 0x12345678u && valid) a.out_desc[0] = 1;  // keeps the loads
-    return;
-  }
-#endif
   // 2. IC_Angle moments (:75-102) over the 749-pixel circle: bytes with |u| <= umax[|v|] (masks in
   //    LDS), sums of I and col * I by byte dot products
   const uint32_t* mt = s_mom + ((cx - 15) & 3) * 279;
@@ -2191,61 +1895,14 @@ __global__ __launch_bounds__(DESC_THREADS) DESC_OCC_ATTR void k_describe(Extract
   m10 = group16_sum(m10);
   // the blurred pieces -> LDS (rows of 40 bytes), ahead of the angle arithmetic
   uint8_t* winb = reinterpret_cast<uint8_t*>(s_win[w * 4 + grp]);
-#if ORBFE_FUSED_BLUR
-  {
-    uint32_t seed;
-    asm volatile("v_mov_b32 %0, 0x8000" : "=v"(seed));
-    auto ev = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c020c00u); };  // columns 0, 2
-    auto od = [](uint32_t d) { return __builtin_amdgcn_perm(0u, d, 0x0c030c01u); };  // columns 1, 3
-    const bool bout = l16 >= 1 && l16 <= 10;
-    uint32_t* wrow = s_win[w * 4 + grp] + (l16 - 1);
-    uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0, e4 = 0, e5 = 0, e6 = 0;
-    uint32_t o0 = 0, o1 = 0, o2 = 0, o3 = 0, o4 = 0, o5 = 0, o6 = 0;
-#pragma unroll
-    for (int i = 0; i < 43; i++) {
-      const uint32_t C = rowv[i];
-      e0 = e1; e1 = e2; e2 = e3; e3 = e4; e4 = e5; e5 = e6; e6 = ev(C);
-      o0 = o1; o1 = o2; o2 = o3; o3 = o4; o4 = o5; o5 = o6; o6 = od(C);
-      if (i < 6) continue;
-      const uint32_t VE = vtap7(e0, e1, e2, e3, e4, e5, e6), VO = vtap7(o0, o1, o2, o3, o4, o5, o6);
-      const uint32_t LE = from_left(VE), LO = from_left(VO), RE = from_right(VE), RO = from_right(VO);
-      const uint32_t Pm3 = __builtin_amdgcn_perm(LE, LO, 0x07060100u);
-      const uint32_t Pm2 = __builtin_amdgcn_perm(LO, LE, 0x07060302u);
-      const uint32_t Pm1 = __builtin_amdgcn_perm(VE, LO, 0x05040302u);
-      const uint32_t P0 = __builtin_amdgcn_perm(VO, VE, 0x05040100u);
-      const uint32_t P1 = __builtin_amdgcn_perm(VE, VO, 0x07060100u);
-      const uint32_t P2 = __builtin_amdgcn_perm(VO, VE, 0x07060302u);
-      const uint32_t P3 = __builtin_amdgcn_perm(RE, VO, 0x05040302u);
-      const uint32_t P4 = __builtin_amdgcn_perm(RO, RE, 0x05040100u);
-      const uint32_t P5 = __builtin_amdgcn_perm(RE, RO, 0x07060100u);
-      const uint32_t P6 = __builtin_amdgcn_perm(RO, RE, 0x07060302u);
-      auto hz = [seed](uint32_t pa, uint32_t pb, uint32_t pc, uint32_t pd) {
-        uint32_t t = dot2_acc(pd, 0x00000012u, seed);
-        t = dot2_acc(pc, 0x00220031u, t);
-        t = dot2_acc(pb, 0x00360031u, t);
-        return dot2_acc(pa, 0x00220012u, t);
-      };
-      const uint32_t s0 = hz(Pm3, Pm1, P1, P3), s1 = hz(Pm2, P0, P2, P4), s2 = hz(Pm1, P1, P3, P5),
-                     s3 = hz(P0, P2, P4, P6);
-      const uint32_t r = __builtin_amdgcn_perm(__builtin_amdgcn_perm(s3, s2, 0x0c0c0602u),
-                                               __builtin_amdgcn_perm(s1, s0, 0x0c0c0602u), 0x05040100u);
-      if (bout) wrow[(i - 6) * 10] = r;
-    }
-  }
-#else
 #pragma unroll
   for (int k = 0; k < 12; k++)
     if (l16 + 16 * k < 185)
       *reinterpret_cast<uint2*>(winb + (br[k % 5] + 16 * (k / 5)) * 40 + 8 * bc[k % 5]) = bw[k];
-#endif
   const float angle = fast_atan2_dev((float)m01, (float)m10, a.atan);
   float ca, sb;
   steer_cos_sin(angle, a.factor_pi, ca, sb);
   wave_sync();
-#if defined(ORBFE_DESC_DIAG) && ORBFE_DESC_DIAG == 2
-  if (__float_as_uint(ca + sb) == 0x12345678u && valid) a.out_desc[0] = 1;  // keeps the angle work
-  return;
-#endif
   // 3. the 256 steered tests (:105-151) on the LDS window, pixel (dy, dx) at byte
   //    (dy + 18) * 40 + (dx + cx - xb); test p = 16 j + l16 lands in bit l16 of the group's
   //    16-bit slice of ballot j = descriptor bytes 2j, 2j+1
@@ -2390,15 +2047,13 @@ struct orbfe_extractor {
   int umax[16];
   int resize_mode = ORBFE_RESIZE_SIMD128;
   int octree_key_cap_override = -1;  // orbfe_debug_set_octree_key_cap
-  int force_level_launches = 1;      // orbfe_debug_force_level_launches (default: per-level launches)
   int fast_side_levels = -1;         // orbfe_debug_set_fast_side_levels (-1: the default, 3 levels)
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr, ev_c0 = nullptr;
-  int copy0_side = 0;  // orbfe_debug_set_copy0_side (measured slower, off)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
   hipEvent_t ev_pyr = nullptr;              // pyramid complete (orbfe_extractor_pyramid_event)
   std::vector<hipEvent_t> ev_lvl;           // level l built (per-level FAST on the side stream)
   // geometry
@@ -2416,13 +2071,6 @@ struct orbfe_extractor {
   int4* d_ywin = nullptr;
   uint4* d_rgrp = nullptr;
   int* d_rgx0 = nullptr;
-  int4* d_pyr_xt = nullptr;          // k_pyramid tile tables
-  int4* d_pyr_yt = nullptr;
-  int2* d_pyr_blob = nullptr;
-  uint32_t* d_pyr_xblob = nullptr;
-  uint32_t* d_pyr_yblob = nullptr;
-  std::vector<PyrGroup> pyr_groups;  // k_pyramid plan (empty: per-level launches)
-  size_t pyramid_lds = 0;
   // batch buffers
   int batch_cap = 0;
   uint8_t* d_in = nullptr;
@@ -2458,168 +2106,7 @@ struct orbfe_extractor {
   OrbfeStereoScratch* stereo = nullptr;
 };
 
-// k_pyramid plan. Groups: levels 1..3 from the input image, then up to 4 levels per group from
-// the previous group's top. Own pieces: x boundaries at multiples of 4 (one writer per 4-column
-// group of store_row4), y boundaries by rows; the compute regions grow top-down by the bilinear
-// taps' reach (clamped rows, sx + 1 only below xmax). Tiles shrink until the two LDS region
-// buffers fit 48 KiB. False (per-level launches) when a level's taps need more than the
-// 8-byte window (rwin_ok) or with a single level.
-struct PyrPlan {
-  std::vector<PyrGroup> groups;
-  std::vector<int4> tx, ty;
-  std::vector<int2> blob;
-  std::vector<uint32_t> xblob, yblob;
-  size_t lds_max = 0;
-};
-static bool plan_pyramid(const std::vector<LevelDesc>& lv, const std::vector<int2>& xt, const std::vector<int2>& yt,
-                         const std::vector<uint4>& rgrp, const std::vector<int>& rgx0, PyrPlan& pp) {
-  std::vector<PyrGroup>& groups = pp.groups;
-  std::vector<int4>& tx = pp.tx;
-  std::vector<int4>& ty = pp.ty;
-  size_t& lds_max = pp.lds_max;
-  const int L = (int)lv.size();
-  if (L < 2) return false;
-  for (int l = 1; l < L; l++)
-    if (!lv[l].rwin_ok) return false;
-  auto a4 = [](int v) { return (v + 3) & ~3; };
-  int src = 0;
-  lds_max = 0;
-  while (src < L - 1) {
-    const int top = src == 0 ? std::min(3, L - 1) : std::min(src + 4, L - 1);
-    const int NL = top - src + 1;
-    int TW = src == 0 ? 64 : 32, TH = src == 0 ? 32 : 16;
-    if (const char* e = std::getenv(src == 0 ? "ORBFE_PYR_TILE_A" : "ORBFE_PYR_TILE_B")) std::sscanf(e, "%dx%d", &TW, &TH);
-    for (;;) {
-      const int ntx = std::max(1, std::min((lv[top].w + TW - 1) / TW, (lv[top].w + 3) / 4));
-      const int nty = std::max(1, std::min((lv[top].h + TH - 1) / TH, lv[top].h));
-      auto own_x = [&](int l, int k) {
-        if (k <= 0) return 0;
-        if (k >= ntx) return lv[l].w;
-        return std::min(lv[l].w, 4 * (int)((long long)k * ((lv[l].w + 3) / 4) / ntx));
-      };
-      auto own_y = [&](int l, int k) { return (int)((long long)k * lv[l].h / nty); };
-      std::vector<int4> gx((size_t)ntx * NL), gy((size_t)nty * NL);
-      for (int k = 0; k < ntx; k++) {
-        int4* e = &gx[(size_t)k * NL];
-        for (int l = src; l <= top; l++)
-          e[l - src] = (l == src && src > 0) ? make_int4(0, 0, 0, 0) : make_int4(own_x(l, k), own_x(l, k + 1), 0, 0);
-        e[NL - 1].z = e[NL - 1].x;
-        e[NL - 1].w = a4(e[NL - 1].y);
-        for (int l = top; l > src; l--) {
-          const LevelDesc& d = lv[l];
-          const int c0 = std::min(e[l - src].z, d.w - 1), c1 = std::min(e[l - src].w - 1, d.w - 1);
-          const int s0 = xt[d.tab_x + c0].x;
-          const int s1 = c1 < d.xmax ? xt[d.tab_x + c1].x + 1 : xt[d.tab_x + c1].x;
-          int4& p = e[l - 1 - src];
-          const bool has_own = p.y > p.x;
-          const int o0 = has_own ? std::min(s0, p.x) : s0, o1 = has_own ? std::max(s1 + 1, p.y) : s1 + 1;
-          p.z = o0 & ~3;
-          p.w = std::min(a4(o1), a4(lv[l - 1].w));
-        }
-      }
-      for (int k = 0; k < nty; k++) {
-        int4* e = &gy[(size_t)k * NL];
-        for (int l = src; l <= top; l++)
-          e[l - src] = (l == src && src > 0) ? make_int4(0, 0, 0, 0) : make_int4(own_y(l, k), own_y(l, k + 1), 0, 0);
-        e[NL - 1].z = e[NL - 1].x;
-        e[NL - 1].w = e[NL - 1].y;
-        for (int l = top; l > src; l--) {
-          const LevelDesc& d = lv[l];
-          const int hs = lv[l - 1].h;
-          const int s0 = std::min(std::max(yt[d.tab_y + e[l - src].z].x, 0), hs - 1);
-          const int s1 = std::min(std::max(yt[d.tab_y + e[l - src].w - 1].x + 1, 0), hs - 1);
-          int4& p = e[l - 1 - src];
-          const bool has_own = p.y > p.x;
-          p.z = has_own ? std::min(s0, p.x) : s0;
-          p.w = has_own ? std::max(s1 + 1, p.y) : s1 + 1;
-        }
-      }
-      // LDS: regions of levels src..top, even offsets in buffer 0, odd in buffer 1
-      size_t b[2] = {0, 0};
-      bool empty = false;
-      for (int kx = 0; kx < ntx; kx++)
-        for (int ky = 0; ky < nty; ky++)
-          for (int l = src; l <= top; l++) {
-            const int4 ex = gx[(size_t)kx * NL + l - src], ey = gy[(size_t)ky * NL + l - src];
-            if (ex.w <= ex.z || ey.w <= ey.z) empty = true;
-            // every level's region stays in LDS until its own piece is copied out; one spare
-            // row for the second row of an odd last pair
-            const size_t bytes = (size_t)pyr_lds_pitch(ex.z, ex.w) * (ey.w - ey.z + 1);
-            b[(l - src) & 1] = std::max(b[(l - src) & 1], bytes);
-          }
-      b[0] = align_up(b[0], 16);
-      b[1] = align_up(b[1], 16);
-      // staged blobs: per tile column the tap records of its 4-column groups, per tile row its
-      // ytab rows, levels src+1..top in order
-      size_t tab = 0, bxmax = 0, bymax = 0;
-      for (int k = 0; k < ntx; k++) {
-        size_t n = 0;
-        for (int l = src + 1; l <= top; l++) n += PYR_REC * (size_t)((gx[(size_t)k * NL + l - src].w - gx[(size_t)k * NL + l - src].z) >> 2);
-        bxmax = std::max(bxmax, n);
-      }
-      for (int k = 0; k < nty; k++) {
-        size_t n = 0;
-        for (int l = src + 1; l <= top; l++) n += 2 * (size_t)(gy[(size_t)k * NL + l - src].w - gy[(size_t)k * NL + l - src].z);
-        bymax = std::max(bymax, n);
-      }
-      tab = align_up(4 * (bxmax + bymax), 16);
-      if (!empty && b[0] + b[1] + tab <= 48 * 1024) {
-        PyrGroup pg;
-        pg.src = src;
-        pg.top = top;
-        pg.ntx = ntx;
-        pg.nty = nty;
-        pg.tx_off = (int)tx.size();
-        pg.ty_off = (int)ty.size();
-        pg.buf0 = (int)b[0];
-        pg.buf1 = (int)b[1];
-        pg.tab = (int)tab;
-        pg.dbg = std::getenv("ORBFE_PYR_DEBUG") ? std::atoi(std::getenv("ORBFE_PYR_DEBUG")) : 0;
-        pg.bx_off = (int)pp.blob.size();
-        for (int k = 0; k < ntx; k++) {
-          const int start = (int)pp.xblob.size();
-          for (int l = src + 1; l <= top; l++) {
-            const int4 e = gx[(size_t)k * NL + l - src];
-            for (int q = e.z >> 2; q < (e.w >> 2); q++) {
-              const int gi = lv[l].rgrp_begin + q;
-              const uint4 sl = rgrp[2 * gi], al = rgrp[2 * gi + 1];
-              const uint32_t rec[PYR_REC] = {(uint32_t)rgx0[gi], 0, 0, 0, sl.x, sl.y, sl.z, sl.w, al.x, al.y, al.z, al.w};
-              pp.xblob.insert(pp.xblob.end(), rec, rec + PYR_REC);
-            }
-          }
-          pp.blob.push_back(make_int2(start, (int)pp.xblob.size() - start));
-        }
-        pg.by_off = (int)pp.blob.size();
-        for (int k = 0; k < nty; k++) {
-          const int start = (int)pp.yblob.size();
-          for (int l = src + 1; l <= top; l++) {
-            const int4 e = gy[(size_t)k * NL + l - src];
-            for (int y = e.z; y < e.w; y++) {
-              const int2 v = yt[lv[l].tab_y + y];
-              pp.yblob.push_back((uint32_t)v.x);
-              pp.yblob.push_back((uint32_t)v.y);
-            }
-          }
-          pp.blob.push_back(make_int2(start, (int)pp.yblob.size() - start));
-        }
-        tx.insert(tx.end(), gx.begin(), gx.end());
-        ty.insert(ty.end(), gy.begin(), gy.end());
-        groups.push_back(pg);
-        lds_max = std::max(lds_max, b[0] + b[1] + tab);
-        break;
-      }
-      if (empty || (TW <= 8 && TH <= 4)) return false;
-      if (TW >= 2 * TH) TW /= 2;
-      else TH /= 2;
-    }
-    src = top;
-  }
-  return true;
-}
-
-#ifndef ORBFE_OCT_LDS_KB
-#define ORBFE_OCT_LDS_KB 80  // k_octree's LDS per workgroup (two per CU)
-#endif
+constexpr int OCT_LDS_KB = 80;  // k_octree's LDS per workgroup (two per CU)
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   if (h->rows == rows && h->cols == cols && h->geom_mode == h->resize_mode) return ORBFE_OK;
   const int L = h->nlevels;
@@ -2739,7 +2226,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
         const short b0 = h_sat_short((1.f - fy) * 2048.f), b1 = h_sat_short(fy * 2048.f);
         yt.push_back(make_int2(sy, (int)(((unsigned)(unsigned short)b1 << 16) | (unsigned short)b0)));
         const int r0 = std::min(std::max(sy, 0), s.h - 1), r1 = std::min(std::max(sy + 1, 0), s.h - 1);
-        yw.push_back(make_int4(r0 * (s.pitch / 4), r1 * (s.pitch / 4), yt.back().y, r0 | (r1 << 16)));
+        yw.push_back(make_int4(r0 * (s.pitch / 4), r1 * (s.pitch / 4), yt.back().y, 0));
       }
       d.xmax = xmax;
       // 4-column groups: the taps of output columns 4g..4g+3 as byte selectors into the 8-byte
@@ -2775,19 +2262,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
       d.simd_end = se;
     }
   }
-  // k_pyramid tile plan (see the kernel): groups of levels, 2-D tiles of each group's top level
-  PyrPlan pp;
-  if (!plan_pyramid(lv, xt, yt, rgrp, rgx0, pp)) pp.groups.clear();
   // release old geometry buffers and upload new ones
   hipSetDevice(h->device);
-  hipFree(h->d_pyr_xt);
-  hipFree(h->d_pyr_yt);
-  hipFree(h->d_pyr_blob);
-  hipFree(h->d_pyr_xblob);
-  hipFree(h->d_pyr_yblob);
-  h->d_pyr_xt = h->d_pyr_yt = nullptr;
-  h->d_pyr_blob = nullptr;
-  h->d_pyr_xblob = h->d_pyr_yblob = nullptr;
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   h->d_rgrp = nullptr;
@@ -2798,19 +2274,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMemcpy(h->d_rgrp, rgrp.data(), sizeof(uint4) * rgrp.size(), hipMemcpyHostToDevice));
     ORBFE_HIP_CHECK(hipMemcpy(h->d_rgx0, rgx0.data(), sizeof(int) * rgx0.size(), hipMemcpyHostToDevice));
   }
-  if (!pp.groups.empty()) {
-    auto up = [](void** d, const void* src, size_t bytes) -> hipError_t {
-      hipError_t e = hipMalloc(d, std::max<size_t>(bytes, 4));
-      return e == hipSuccess ? hipMemcpy(*d, src, bytes, hipMemcpyHostToDevice) : e;
-    };
-    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_xt, pp.tx.data(), sizeof(int4) * pp.tx.size()));
-    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_yt, pp.ty.data(), sizeof(int4) * pp.ty.size()));
-    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_blob, pp.blob.data(), sizeof(int2) * pp.blob.size()));
-    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_xblob, pp.xblob.data(), sizeof(uint32_t) * pp.xblob.size()));
-    ORBFE_HIP_CHECK(up((void**)&h->d_pyr_yblob, pp.yblob.data(), sizeof(uint32_t) * pp.yblob.size()));
-  }
-  h->pyr_groups = pp.groups;
-  h->pyramid_lds = pp.lds_max;
   hipFree(h->d_levels);
   hipFree(h->d_cells);
   hipFree(h->d_xtab);
@@ -2860,7 +2323,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   // blocks share a CU; larger levels use the global scratch path
   const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * h->scan_cap +
                        sizeof(unsigned long long) * sc + sizeof(int) * 16;
-  const size_t oct_lds = (size_t)ORBFE_OCT_LDS_KB * 1024;
+  const size_t oct_lds = (size_t)OCT_LDS_KB * 1024;
   h->key_lds_cap = fixed < oct_lds ? (int)((oct_lds - fixed) / 8) & ~63 : 0;
   if (h->octree_key_cap_override >= 0) h->key_lds_cap = std::min(h->key_lds_cap, h->octree_key_cap_override);
   h->rows = rows;
@@ -2954,9 +2417,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.img_pitch = pitch;
   a.pyr = h->d_pyr + (long long)i0 * h->pyr_stride;
   a.blur = h->d_blur + (long long)i0 * h->pyr_stride;
-#if defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1  // ablation build: no GaussianBlur (wrong output)
-  a.blur = a.pyr;
-#endif
   a.pyr_stride = h->pyr_stride;
   a.cand = h->d_cand + (long long)i0 * h->cand_stride;
   a.cand_stride = h->cand_stride;
@@ -2979,11 +2439,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.sort_cap = h->sort_cap;
   a.scan_cap = h->scan_cap;
   a.key_lds_cap = h->key_lds_cap;
-  a.pyr_xt = h->d_pyr_xt;
-  a.pyr_yt = h->d_pyr_yt;
-  a.pyr_blob = h->d_pyr_blob;
-  a.pyr_xblob = h->d_pyr_xblob;
-  a.pyr_yblob = h->d_pyr_yblob;
   a.rgrp = h->d_rgrp;
   a.rgx0 = h->d_rgx0;
   for (int v = 0; v < 16; v++) a.umax[v] = h->umax[v];
@@ -3010,86 +2465,43 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       ORBFE_LAUNCH("k_fast", k_fast<0>, grid, dim3(64 * wpb), lds, s, a, c0, c1);
     return ORBFE_OK;
   };
-  // k_side: the levels whose FAST cells run on the side stream, beside the rest of the pyramid
-  // launches
-  int k_side = 0;
-  bool c0side = false;
-  if (!h->pyr_groups.empty() && !h->force_level_launches) {
-    // the first group writes levels 0..top
-    k_side = h->pyr_groups[0].top + 1;
-    for (size_t gi = 0; gi < h->pyr_groups.size(); gi++) {
-      const PyrGroup& pg = h->pyr_groups[gi];
-      dim3 grid(pg.ntx * pg.nty, n);
-      ORBFE_LAUNCH("k_pyramid", k_pyramid, grid, dim3(256), pg.buf0 + pg.buf1 + pg.tab, st, a, pg);
-      if (gi == 0) {
-        ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));
-        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
-        launch_fast(side, 0, k_side < h->nlevels ? h->levels[k_side].cell_begin : a.ncells);
-      }
+  {
+    const LevelDesc& d = h->levels[0];
+    dim3 grid((d.h + 3) / 4, n);
+    const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
+    ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, st, a);
+  }
+  // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main stream
+  // has built it, beside the chain of small dependent resize launches that leaves most CUs idle;
+  // levels k..L-1 follow the chain on the main stream
+  const int k_side = fast_side_split(h);
+  if ((int)h->ev_lvl.size() < h->nlevels) {
+    for (int l = (int)h->ev_lvl.size(); l < h->nlevels; l++) {
+      hipEvent_t e = nullptr;
+      ORBFE_HIP_CHECK(hipEventCreateWithFlags(&e, kForkJoinEvent));
+      h->ev_lvl.push_back(e);
     }
-  } else {
-    // c0side (debug option, off): level 1 is resized from the caller's image, so k_copy0 runs on
-    // the side stream beside the resize chain (followed there by FAST of level 0); the main
-    // stream joins it before the pyramid counts as complete. Measured on MI355X: 66.3k vs 72.3k
-    // stereo frames/s with one handle, 79.4-82.8k vs 84.6k with two (the side stream's FAST of
-    // level 0 then waits for the copy, and with two handles the other handle's side work too).
-    c0side = h->copy0_side && side != st && h->nlevels > 1 && h->levels[1].rwin_ok &&
-             h->levels[0].h < 65536;
-    {
-      const LevelDesc& d = h->levels[0];
-      dim3 grid((d.h + 3) / 4, n);
-      const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
-      if (c0side) {
-        ORBFE_HIP_CHECK(hipEventRecord(h->ev_l0, st));  // the input is ready on st
-        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_l0, 0));
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
-        ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, side, a);
-#endif
-        ORBFE_HIP_CHECK(hipEventRecord(h->ev_c0, side));
-      } else {
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 2)  // ablation build: no level-0 copy
-        ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, st, a);
-#endif
-      }
+  }
+  auto side_fast = [&](int l) -> int {
+    const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
+    ORBFE_HIP_CHECK(hipEventRecord(e, st));
+    ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
+    const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
+    return launch_fast(side, h->levels[l].cell_begin, c1);
+  };
+  side_fast(0);
+  for (int l = 1; l < h->nlevels; l++) {
+    const LevelDesc& d = h->levels[l];
+    if (d.rwin_ok) {
+      const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
+      const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
+      dim3 grid((items + 255) / 256, n);
+      ORBFE_LAUNCH("k_resize_win", k_resize_win, grid, dim3(256), 0, st, a, l, G, gm);
+    } else {
+      dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
+      ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
     }
-    // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main
-    // stream has built it, beside the chain of small dependent resize launches that leaves most
-    // CUs idle; levels k..L-1 follow the chain on the main stream
-    k_side = fast_side_split(h);
-    if ((int)h->ev_lvl.size() < h->nlevels) {
-      for (int l = (int)h->ev_lvl.size(); l < h->nlevels; l++) {
-        hipEvent_t e = nullptr;
-        ORBFE_HIP_CHECK(hipEventCreateWithFlags(&e, kForkJoinEvent));
-        h->ev_lvl.push_back(e);
-      }
-    }
-    auto side_fast = [&](int l) -> int {
-      if (!(l == 0 && c0side)) {  // with c0side level 0 is the side stream's own k_copy0
-        const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
-        ORBFE_HIP_CHECK(hipEventRecord(e, st));
-        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
-      }
-      const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
-      return launch_fast(side, h->levels[l].cell_begin, c1);
-    };
-    side_fast(0);
-    for (int l = 1; l < h->nlevels; l++) {
-      const LevelDesc& d = h->levels[l];
-      if (d.rwin_ok) {
-        const int G = (d.w + 3) / 4, items = G * ((d.h + 2 * ORBFE_RESIZE_PAIRS - 1) / (2 * ORBFE_RESIZE_PAIRS));
-        const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
-        dim3 grid((items + 255) / 256, n);
-        if (l == 1 && c0side)
-          ORBFE_LAUNCH("k_resize_win", k_resize_win<true>, grid, dim3(256), 0, st, a, l, G, gm);
-        else
-          ORBFE_LAUNCH("k_resize_win", k_resize_win<false>, grid, dim3(256), 0, st, a, l, G, gm);
-      } else {
-        dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
-        ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
-      }
-      if (l < k_side) side_fast(l);
-    }
-    if (c0side) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_c0, 0));  // level 0 is in the pyramid
+    if (l < k_side) side_fast(l);
   }
   if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
   ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3108,31 +2520,21 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));  // the pyramid is complete on st
   const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
-  if (h->blur_mode == 2) {  // the blur on the side stream as soon as the pyramid is complete
-    ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_pyr, 0));
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
-    ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
-#endif
-  }
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
-#endif
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   launch_octree(st, 0, h->nlevels);
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
-#if !(defined(ORBFE_DIAG_SKIP) && ORBFE_DIAG_SKIP == 1) && !ORBFE_FUSED_BLUR
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a);
-#endif
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
   {
-    constexpr int per_block = 4 * ORBFE_DESC_WPB;  // keypoints per workgroup
+    constexpr int per_block = 4 * DESC_WPB;  // keypoints per workgroup
     dim3 grid((h->total_key_slots + per_block - 1) / per_block, n);
     ORBFE_LAUNCH("k_describe", k_describe, grid, dim3(DESC_THREADS), 0, st, a);
   }
@@ -3210,7 +2612,6 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
       hipEventCreateWithFlags(&h->ev_fork, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_l0, kForkJoinEvent) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_c0, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_f0, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pyr, hipEventDisableTiming) != hipSuccess) {
     delete h;
@@ -3260,11 +2661,6 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_ywin);
-  hipFree(h->d_pyr_blob);
-  hipFree(h->d_pyr_xblob);
-  hipFree(h->d_pyr_yblob);
-  hipFree(h->d_pyr_xt);
-  hipFree(h->d_pyr_yt);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   hipFree(h->d_in);
@@ -3286,7 +2682,6 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->ev_l0) hipEventDestroy(h->ev_l0);
-  if (h->ev_c0) hipEventDestroy(h->ev_c0);
   if (h->ev_f0) hipEventDestroy(h->ev_f0);
   if (h->ev_pyr) hipEventDestroy(h->ev_pyr);
   for (hipEvent_t e : h->ev_lvl) hipEventDestroy(e);
@@ -3779,14 +3174,8 @@ extern "C" int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_set_copy0_side(orbfe_extractor* h, int on) {
-  if (!h) return ORBFE_ERR_ARG;
-  h->copy0_side = on ? 1 : 0;
-  return ORBFE_OK;
-}
-
 extern "C" int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode) {
-  if (!h || mode < 0 || mode > 2) return ORBFE_ERR_ARG;
+  if (!h || mode < 0 || mode > 1) return ORBFE_ERR_ARG;
   h->blur_mode = mode;
   return ORBFE_OK;
 }
@@ -3812,12 +3201,6 @@ extern "C" int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k) {
 extern "C" int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16) {
   if (!h || !umax16) return ORBFE_ERR_ARG;
   for (int v = 0; v < 16; v++) umax16[v] = h->umax[v];
-  return ORBFE_OK;
-}
-
-extern "C" int orbfe_debug_force_level_launches(orbfe_extractor* h, int on) {
-  if (!h) return ORBFE_ERR_ARG;
-  h->force_level_launches = on ? 1 : 0;
   return ORBFE_OK;
 }
 

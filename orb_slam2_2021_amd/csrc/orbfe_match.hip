@@ -122,20 +122,17 @@ __device__ __forceinline__ unsigned long long sft_key(const SftCand& c, bool cla
   return ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
 }
 
-// Nodes with at most 64 K features on each side (K = 2, or 4 up to SFT_FP_MAX): lanes take KF1
+// Nodes with at most 64 K features on each side (K = 2: up to SFT_FP_MAX = 128): lanes take KF1
 // features (K per lane), every lane finds its passing KF2 candidates once (dist <= TH_LOW, the
 // epipole and epipolar checks: the candidate set S_i of the reference loop), then the claim order
 // of :772-777 is solved as a fixpoint -- choice(i) = best of S_i minus the choices of features
 // before i in the node -- iterated from "no claims" until a round reproduces the previous one.
 // That fixpoint is unique and equals the sequential result (feature i's choice is final once
 // those before it are).
-// 128 (K = 2 only) by default: the K = 4 build's 44 KiB of LDS per workgroup (vs 26 KiB) keeps
-// DistributeOctTree's 80 KiB blocks off the CUs it occupies when the matching stream runs beside
-// the extraction (measured 73.1k vs 78.5k stereo frames/s), though it runs alone in 49 vs ~70 us
-// when a node holds 129-256 features
-#ifndef SFT_FP_MAX
-#define SFT_FP_MAX 128
-#endif
+// (K = 4 for nodes of 129-256 features ran alone in 49 vs ~70 us, but its 44 KiB of LDS per
+// workgroup (vs 26 KiB) kept DistributeOctTree's 80 KiB blocks off the CUs it occupied beside the
+// extraction: 73.1k vs 78.5k stereo frames/s)
+constexpr int SFT_FP_MAX = 128;
 template <int K>
 __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o1, int n1, int o2, int n2,
                                                   int only_stereo, uint32_t* cdesc, int* claim) {
@@ -175,12 +172,6 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     }
   }
   wave_sync();
-#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 1  // phase-cost build: loads only (no matches)
-#pragma unroll
-  for (int k = 0; k < K; k++)
-    if (64 * k + lane < n1) P.match12[idx1[k]] = -1;
-  return;
-#endif
   const float* F = P.f12;
   const float f0 = F[0], f1 = F[1], f2 = F[2], f3 = F[3], f4 = F[4], f5 = F[5], f6 = F[6],
               f7 = F[7], f8 = F[8];
@@ -242,12 +233,6 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
   int ch[K];
 #pragma unroll
   for (int k = 0; k < K; k++) ch[k] = best[k] == ~0ull ? -1 : 0x7fffffff - (int)(best[k] & 0xffffffffull);
-#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 2  // + passing sets (round-0 choices, unresolved)
-#pragma unroll
-  for (int k = 0; k < K; k++)
-    if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
-  return;
-#endif
   // 2. rounds: claim[p] = first feature choosing p; re-choose among the unclaimed-by-earlier
   for (int round = 0; round <= n1; round++) {
     for (int p = lane; p < n2; p += 64) claim[p] = 0x7fffffff;
@@ -288,10 +273,7 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
 }
 
-#ifndef ORBFE_SFT_WPE
-#define ORBFE_SFT_WPE 4
-#endif
-__global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
+__global__ __launch_bounds__(256, 4) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
   // per wave: the fixpoint path's node candidates, or the large-node path's claim bits beyond the
   // register chunks (a wave takes one path; 18 KiB per workgroup in all)
   static_assert(SFT_MAX_NODE / 32 <= SFT_FP_MAX * 8, "claim bits fit the candidate area");
@@ -299,19 +281,9 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
   __shared__ int s_fp_claim[4][SFT_FP_MAX];
   // XCD-aware order: the workgroups of one pair run on one XCD, so its KeyFrames' keypoints,
   // descriptors and FeatureVectors are fetched into one L2 rather than eight
-#if defined(ORBFE_SFT_LINEAR) && ORBFE_SFT_LINEAR
-  const int2 blk = make_int2(blockIdx.x, blockIdx.y);
-#else
   const int2 blk = xcd_block2d();
-#endif
   orbfe_sft_pair P = pairs[blk.y];
   sft_resolve_sizes(P);
-#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 3  // phase-cost builds (match12 left unwritten):
-  return;                                             // an empty k_sft_nodes
-#endif
-#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 4  // the coverage workgroups only
-  if (blk.x != gridDim.x - 1) return;
-#endif
   if (blk.x == gridDim.x - 1) {
     // the last workgroup of a pair: KF1 features that no FeatureVector node lists -- a stopped
     // word (weight 0) is not added (TemplatedVocabulary.h:1198-1201) -- never match: -1. Disjoint
@@ -358,19 +330,10 @@ __global__ __launch_bounds__(256, ORBFE_SFT_WPE) void k_sft_nodes(const orbfe_sf
     return;
   }
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
-#if defined(ORBFE_SFT_DIAG) && ORBFE_SFT_DIAG == 5  // + node lookup (match12 of the node's features unwritten)
-  if (n2 >= 0) return;
-#endif
-  if (e1 - o1 <= 128 && n2 <= 128) {
+  if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
     sft_node_fixpoint<2>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
-#if SFT_FP_MAX > 128
-  if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
-    sft_node_fixpoint<4>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
-    return;
-  }
-#endif
   // large nodes: -1 first, stored before the walk's matches overwrite some of them (the wait
   // orders the two stores to one address from different lanes)
   for (int i = o1 + lane; i < e1; i += 64) P.match12[P.fv1.indices[i]] = -1;
@@ -612,7 +575,8 @@ struct SbpArgs {
   // re-evaluates only the queries a changed keypoint can reach); NULL: every query is re-evaluated
   const int32_t* owner_rm2;
   // round 0 with the settle path: the inverted candidate index, keypoint k -> the queries whose
-  // window holds it as a candidate (inv[k * SBP_INV_CAP + j], inv_n[k] may exceed the cap); NULL off
+  // window holds it as a candidate (inv[k * SBP_INV_CAP + j] = query | claims << 31, claims = the
+  // query's assignment blocks its keypoint; inv_n[k] may exceed the cap); NULL off
   int32_t* inv;
   int32_t* inv_n;
 };
@@ -942,7 +906,7 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
         const uint64_t bm = (wave_ballot(keep) >> rowbase) & 0xffffull;
         if (keep && a.inv) {  // every candidate, cached or not (a query past cand_cap re-walks them all)
           const int slot = atomicAdd(&a.inv_n[k], 1);
-          if (slot < SBP_INV_CAP) a.inv[(size_t)k * SBP_INV_CAP + slot] = i;
+          if (slot < SBP_INV_CAP) a.inv[(size_t)k * SBP_INV_CAP + slot] = (int32_t)((uint32_t)i | ((q.flags & 2u) << 30));
         }
         if (keep) {
           const int pos = total + __popcll(bm & ((1ull << j) - 1));
@@ -999,6 +963,52 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   if (changed && lane_id() == __ffsll((long long)wave_ballot(true)) - 1) a.state[2] = 1;
 }
 
+// sbp_cached with the 16 lanes of a DPP row (lane j takes cache entries j, j + 16, ...): the
+// sequential best / second-best bookkeeping is the two smallest (dist, position) keys over the
+// unblocked entries (see k_sbp_round0), merged over the row. Every lane returns the result.
+template <class Blocked>
+__device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int n, int j, Blocked blocked) {
+  const unsigned long long NONE = ~0ull;
+  unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
+  int kb1 = -1;
+  const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
+  const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
+  const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
+  for (int c = j; c < n; c += 16) {
+    const int k = ck[c];
+    if (blocked(k)) continue;
+    const unsigned long long key =
+        ((unsigned long long)cd[c] << 40) | ((unsigned long long)c << 8) | (unsigned long long)cl[c];
+    if (key < k1) {
+      k2 = k1;
+      k1 = key;
+      kb1 = k;
+    } else if (key < k2) {
+      k2 = key;
+    }
+  }
+#pragma unroll
+  for (int s2 = 8; s2 > 0; s2 >>= 1) {
+    const unsigned long long o1 = __shfl_xor(k1, s2, 16), o2 = __shfl_xor(k2, s2, 16);
+    const int ob = __shfl_xor(kb1, s2, 16);
+    k2 = min_u64(max_u64(k1, o1), min_u64(k2, o2));
+    if (o1 < k1) {
+      k1 = o1;
+      kb1 = ob;
+    }
+  }
+  if (k1 == NONE) return -1;
+  SbpBest bb;
+  bb.bestDist = (int)(k1 >> 40);
+  bb.bestLevel = (int)(k1 & 0xff);
+  bb.bestIdx = kb1;
+  if (k2 != NONE) {
+    bb.bestDist2 = (int)(k2 >> 40);
+    bb.bestLevel2 = (int)(k2 & 0xff);
+  }
+  return bb.result(a.mode, a.nnratio, a.dist_th);
+}
+
 // ---- the fixpoint's rounds 2.. in one workgroup ---------------------------------------------
 // After round 1 most results are final; the rounds that follow change few of them, and as one
 // launch per round (k_sbp_round) their cost was the launch chain -- 10-16 launches per C5 search,
@@ -1008,17 +1018,19 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
 //      index whose result is the keypoint, among queries whose assignment blocks it);
 //   b. their queries from the inverted candidate index (round 0) with lo < i <= hi: only for those
 //      does blocked(k) = owner < i flip -- the k_sbp_round test, exact rather than by window;
-//   c. re-evaluation from the candidate cache, results updated in place (a round reads only the
-//      previous round's owners, never other results);
+//   c. re-evaluation from the candidate cache, 16 lanes per query (one query's cache walk as a
+//      chain of dependent loads on one thread cost ~40 us per round), results updated in place (a
+//      round reads only the previous round's owners, never other results);
 //   d. the owners of the keypoints a changed result left or joined, recomputed from their index
 //      lists (every other keypoint keeps its owner).
 // Settled when no owner changed (the next round would reproduce this one). A keypoint listed by
 // more than SBP_INV_CAP queries makes its rounds scan every query instead (exact, slower); past
 // round_cap the reference's sequential loop runs (as k_sbp_finish does).
 struct SbpSettleArgs {
-  int32_t* res;         // round 1's results, updated in place to the fixpoint
-  const int32_t* own0;  // round 0's owners
-  const int32_t* own1;  // round 1's owners
+  int32_t* res;         // round R0-1's results, updated in place to the fixpoint
+  const int32_t* own0;  // round R0-2's owners
+  const int32_t* own1;  // round R0-1's owners
+  int round0;           // R0: the first round run here
   const int32_t* inv;
   const int32_t* inv_n;
   int round_cap;
@@ -1027,29 +1039,38 @@ struct SbpSettleArgs {
 };
 
 __host__ __device__ inline size_t settle_lds(int n, int m) {
-  return sizeof(int) * (4 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 4 * (size_t)((n + 31) / 32);
+  return sizeof(int) * (4 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
 }
+constexpr int SETTLE_INV_PER_LANE = SBP_INV_CAP / 64;  // index entries per lane, loaded together
 
 __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSettleArgs s) {
   extern __shared__ int s_lds[];
-  __shared__ int s_cnt, s_dense;
+  __shared__ int s_cnt, s_dense, s_nq;
   const int n = a.F.n, m = a.m, t = threadIdx.x, wv = t >> 6, ln = t & 63;
   constexpr int NW = SETTLE_THREADS / 64;
   const int qw = (m + 31) >> 5, kw = (n + 31) >> 5;
+  if (a.state[0] != 0) return;  // the grid-wide rounds settled already (k_sbp_round's early exit)
   int* rm2 = s_lds;
   int* prev = rm2 + n;
   int* cur = prev + n;
   int* list = cur + n;  // changed / dirty keypoints
   uint32_t* qbits = reinterpret_cast<uint32_t*>(list + n);
   uint32_t* dirty = qbits + qw;
+  uint32_t* pre = dirty + kw;  // keypoints taken before the search (sbp_pre_blocked)
   for (int k = t; k < n; k += SETTLE_THREADS) {
     rm2[k] = s.own0[k];
     prev[k] = s.own1[k];
   }
+  for (int w = t; w < kw; w += SETTLE_THREADS) {
+    uint32_t b = 0;
+    for (int k = 32 * w; k < min(n, 32 * w + 32); k++) b |= sbp_pre_blocked(a, k) ? 1u << (k & 31) : 0u;
+    pre[w] = b;
+  }
   for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
   for (int w = t; w < kw; w += SETTLE_THREADS) dirty[w] = 0u;
+  if (t == 0) s_nq = 0;
   __syncthreads();
-  int round = 2;
+  int round = s.round0;
   bool serial = false;
   for (;; round++) {
     if (t == 0) {
@@ -1075,38 +1096,51 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
         if (ln == 0) s_dense = 1;
         continue;
       }
-      for (int j = ln; j < cnt; j += 64) {
-        const int i = s.inv[(size_t)k * SBP_INV_CAP + j];
-        if (lo < i && i <= hi) atomicOr(&qbits[i >> 5], 1u << (i & 31));
+      // every entry's load in flight before the first is used (one memory latency per keypoint)
+      const int32_t* L = s.inv + (size_t)k * SBP_INV_CAP;
+      int e[SETTLE_INV_PER_LANE];
+#pragma unroll
+      for (int u = 0; u < SETTLE_INV_PER_LANE; u++) e[u] = ln + 64 * u < cnt ? L[ln + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < SETTLE_INV_PER_LANE; u++) {
+        const int i = e[u] & 0x7fffffff;
+        if (ln + 64 * u < cnt && lo < i && i <= hi) atomicOr(&qbits[i >> 5], 1u << (i & 31));
       }
     }
     __syncthreads();
     // c. re-evaluate them from the candidate cache with round r-1's owners
     const bool dense = s_dense != 0;
     if (t == 0 && dense) s.serial_used[1] += 1;
-    for (int w = t; w < qw; w += SETTLE_THREADS) {
-      uint32_t bits = dense ? 0xffffffffu : qbits[w];
-      qbits[w] = 0u;
-      while (bits) {
-        const int i = 32 * w + __builtin_ctz(bits);
-        bits &= bits - 1u;
-        if (i >= m) break;
-        const int nc = a.cand_n[i];
-        if (nc == 0) continue;  // no candidate: -1 in every round
-        atomicAdd(&s.serial_used[2], 1);
-        auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || prev[k] < i; };
-        const int r = nc > 0 ? sbp_cached(a, i, nc, blocked) : sbp_one(a, i, blocked);
-        const int old = s.res[i];
-        if (r != old) {
-          s.res[i] = r;
-          if (a.q[i].flags & 2) {
-            if (old >= 0) atomicOr(&dirty[old >> 5], 1u << (old & 31));
-            if (r >= 0) atomicOr(&dirty[r >> 5], 1u << (r & 31));
+    {
+      // one 16-lane row per bitmap word (64 rows); the row's lanes walk its set bits together
+      const int row = t >> 4, j = t & 15;
+      for (int w = row; w < qw; w += SETTLE_THREADS / 16) {
+        uint32_t bits = dense ? 0xffffffffu : qbits[w];
+        while (bits) {
+          const int i = 32 * w + __builtin_ctz(bits);
+          bits &= bits - 1u;
+          if (i >= m) break;
+          const int nc = a.cand_n[i];
+          if (nc == 0) continue;  // no candidate: -1 in every round
+          auto blocked = [&](int k) { return ((pre[k >> 5] >> (k & 31)) & 1u) || prev[k] < i; };
+          const int r = nc > 0 ? sbp_cached_row(a, i, nc, j, blocked)
+                               : (j == 0 ? sbp_one(a, i, blocked) : 0);
+          if (j == 0) {
+            atomicAdd(&s_nq, 1);
+            const int old = s.res[i];
+            if (r != old) {
+              s.res[i] = r;
+              if (a.q[i].flags & 2) {
+                if (old >= 0) atomicOr(&dirty[old >> 5], 1u << (old & 31));
+                if (r >= 0) atomicOr(&dirty[r >> 5], 1u << (r & 31));
+              }
+            }
           }
         }
       }
     }
     __syncthreads();
+    for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
     // d. round r's owners: round r-1's, recomputed where a result left or joined the keypoint
     for (int k = t; k < n; k += SETTLE_THREADS) cur[k] = prev[k];
     if (t == 0) s_cnt = 0;
@@ -1129,11 +1163,16 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
       if (cnt > SBP_INV_CAP) {  // claimants not all indexed: every query
         for (int i = ln; i < m; i += 64)
           if (s.res[i] == k && (a.q[i].flags & 2)) best = min(best, i);
-      } else {
-        for (int j = ln; j < cnt; j += 64) {
-          const int i = s.inv[(size_t)k * SBP_INV_CAP + j];
-          if (s.res[i] == k && (a.q[i].flags & 2)) best = min(best, i);
-        }
+      } else {  // the claiming entries' results, all loads in flight together
+        const int32_t* L = s.inv + (size_t)k * SBP_INV_CAP;
+        int e[SETTLE_INV_PER_LANE], r[SETTLE_INV_PER_LANE];
+#pragma unroll
+        for (int u = 0; u < SETTLE_INV_PER_LANE; u++) e[u] = ln + 64 * u < cnt ? L[ln + 64 * u] : 0;
+#pragma unroll
+        for (int u = 0; u < SETTLE_INV_PER_LANE; u++) r[u] = e[u] < 0 ? s.res[e[u] & 0x7fffffff] : -2;
+#pragma unroll
+        for (int u = 0; u < SETTLE_INV_PER_LANE; u++)
+          if (r[u] == k) best = min(best, e[u] & 0x7fffffff);
       }
       best = wave_min(best);
       if (ln == 0) cur[k] = best;
@@ -1154,8 +1193,10 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     }
   }
   if (t == 0) {  // for k_sbp_collect / k_sbp_finish and the round statistics
+    s.serial_used[2] = s_nq;
     a.state[0] = 1;
-    a.state[1] = round;
+    a.state[1] = round;  // rounds run (the last computed one + 1)
+    a.state[SBP_FINAL_SLOT] = ((s.round0 - 1) & 1) + 1;  // the results stay in round R0-1's buffer
   }
 }
 
@@ -1178,12 +1219,18 @@ __device__ __forceinline__ bool sbp_converged(const SbpArgs& a) {
   return a.state[0] != 0 || (rounds >= 2 && a.state[2 + rounds - 1] == 0);
 }
 
+// The final results: round state[1]-1's buffer, or the one k_sbp_settle updated in place.
+__device__ __forceinline__ const int32_t* sbp_final(const SbpFinishArgs& f) {
+  const int slot = f.s.state[SBP_FINAL_SLOT];
+  return slot ? f.res_final[slot - 1] : f.res_final[(f.s.state[1] - 1) & 1];
+}
+
 // Converged without a rotation filter (the local search): results and count, grid-wide.
 __global__ __launch_bounds__(256) void k_sbp_collect(SbpFinishArgs f) {
   const SbpArgs& a = f.s;
   if (f.check_ori || !sbp_converged(a)) return;  // k_sbp_finish handles those
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int32_t* res = f.res_final[(a.state[1] - 1) & 1];
+  const int32_t* res = sbp_final(f);
   int c = 0;
   if (i < a.m) {
     const int r = res[i];
@@ -1203,10 +1250,9 @@ __global__ __launch_bounds__(256) void k_sbp_finish(SbpFinishArgs f, int32_t* bl
   __shared__ int s_misc[8];
   const SbpArgs& a = f.s;
   const int t = threadIdx.x;
-  const int rounds = a.state[1];
   const bool converged = sbp_converged(a);
   if (converged && !f.check_ori) return;  // done by k_sbp_collect
-  const int32_t* res = f.res_final[(rounds - 1) & 1];
+  const int32_t* res = sbp_final(f);
   if (!converged && f.defer) {  // the host continues the rounds (sbp_fetch)
     if (t == 0) *f.serial_used = 2;
     return;
@@ -1851,12 +1897,6 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
                        m->stream, a);
 }
 
-// ORBFE_SBP_DENSE=1: every round re-evaluates every query (rounds 1-3's behaviour, for A/B)
-static bool sbp_dense_rounds() {
-  static const bool dense = std::getenv("ORBFE_SBP_DENSE") && std::atoi(std::getenv("ORBFE_SBP_DENSE")) != 0;
-  return dense;
-}
-
 // Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over four:
 // round r claims into own[r % 4], reads own[(r + 3) % 4] (round r-1) and own[(r + 2) % 4]
 // (round r-2), and clears own[(r + 1) % 4] for round r + 1, which nobody reads during round r).
@@ -1878,8 +1918,14 @@ static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs&
   ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
 }
 
-// Rounds 0 and 1 grid-wide (round 0 fills the candidate cache and the inverted index), the rest in
-// k_sbp_settle, then collect / finish: five launches whatever the depth of the claim order.
+// Rounds 0 .. R0-1 grid-wide (round 0 fills the candidate cache and the inverted index; the early
+// rounds change many owners, work one workgroup would take long over), the rest in k_sbp_settle,
+// then collect / finish: R0 + 3 launches whatever the depth of the claim order.
+static int sbp_settle_from() {
+  static const int r0 = std::getenv("ORBFE_SBP_SETTLE_FROM") ? std::max(2, std::atoi(std::getenv("ORBFE_SBP_SETTLE_FROM")))
+                                                             : SBP_SETTLE_FROM;
+  return r0;
+}
 static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
                               const orbfe_frame_view& dF, const SbpMode& md) {
   uint8_t* A = m->arena;
@@ -1888,14 +1934,15 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
   int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
   int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
                      (int32_t*)(A + p.oown3)};
-  for (int r = 0; r < 2; r++) {
+  const int R0 = sbp_settle_from();
+  for (int r = 0; r < R0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
     a.res_prev = res[(r + 1) & 1];
     a.owner_cur = own[r % 4];
     a.owner_prev = own[(r + 3) % 4];
     a.owner_next = own[(r + 1) % 4];
-    a.owner_rm2 = nullptr;
+    a.owner_rm2 = r >= 2 ? own[(r + 2) % 4] : nullptr;
     if (r == 0) {
       a.inv = (int32_t*)(A + p.oinv);
       a.inv_n = (int32_t*)(A + p.oinv_n);
@@ -1907,9 +1954,10 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
     }
   }
   SbpSettleArgs st;
-  st.res = res[1];
-  st.own0 = own[0];
-  st.own1 = own[1];
+  st.res = res[(R0 - 1) & 1];  // round R0-1's results and the owners of rounds R0-2, R0-1
+  st.own0 = own[(R0 - 2) % 4];
+  st.own1 = own[(R0 - 1) % 4];
+  st.round0 = R0;
   st.inv = (const int32_t*)(A + p.oinv);
   st.inv_n = (const int32_t*)(A + p.oinv_n);
   st.round_cap = m->round_cap;
@@ -1923,8 +1971,7 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
     attr_set = true;
   }
   ORBFE_LAUNCH("k_sbp_settle", k_sbp_settle, dim3(1), dim3(SETTLE_THREADS), lds, m->stream, a, st);
-  int32_t* fin[2] = {res[1], res[1]};
-  sbp_finish_launch(m, p, a, md, fin, false);
+  sbp_finish_launch(m, p, a, md, res, false);
 }
 
 static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
@@ -1944,7 +1991,7 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
     a.owner_next = own[(r + 1) % 4];
     // round r-2's owners: round r re-evaluates only the queries a keypoint whose owner changed
     // since can reach
-    a.owner_rm2 = r >= 2 && p.cache && !sbp_dense_rounds() ? own[(r + 2) % 4] : nullptr;
+    a.owner_rm2 = r >= 2 && p.cache ? own[(r + 2) % 4] : nullptr;
     if (r == 0 && p.cache)
       ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
                          m->stream, a);

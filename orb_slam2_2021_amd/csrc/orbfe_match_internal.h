@@ -23,11 +23,13 @@
 #define GRID_CELLS (GRID_COLS * GRID_ROWS)
 #define SBP_MAX_ROUNDS 12      // rounds of the first launch (no host sync)
 #define SBP_ROUND_CAP 1024     // rounds a host-synchronous search may continue to before the serial walk
+#define SBP_FINAL_SLOT (SBP_ROUND_CAP + 3)  // state[]: 1 + the result buffer k_sbp_settle left final (0: by parity)
 #define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
 #define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
 #define SBP_CAND 48          // default per-query candidate cache of the projection searches
 #define SBP_INV_CAP 1024     // queries per keypoint in the settle path's inverted candidate index
-#define SETTLE_THREADS 1024  // k_sbp_settle: one workgroup for the fixpoint's rounds 2..
+#define SETTLE_THREADS 1024  // k_sbp_settle: one workgroup for the fixpoint's rounds R0..
+#define SBP_SETTLE_FROM 4    // R0: rounds 0 .. R0-1 grid-wide (ORBFE_SBP_SETTLE_FROM overrides)
 #define SETTLE_MAX_KEYS 4096       // settle path: frame keypoints (owners in LDS) ...
 #define SETTLE_MAX_QUERIES 131072  // ... and queries (a bitmap in LDS)
 #define ORBFE_MAX_LEVELS_M 32

@@ -52,12 +52,9 @@ struct StereoGeom {
 
 // ---- k_stereo_rows ----------------------------------------------------------------------------
 // 256 threads: the rows table runs on the matching stream beside the extraction kernels, where
-// smaller workgroups find room sooner (1024-thread workgroups of k_vocab measured -3.7 %)
-#ifndef ORBFE_STEREO_ROWS_THREADS
-#define ORBFE_STEREO_ROWS_THREADS 256
-#endif
-constexpr int ROWS_THREADS = ORBFE_STEREO_ROWS_THREADS;
-static_assert(ROWS_THREADS == 256 || ROWS_THREADS == 1024, "k_stereo_rows scans with 256 or 1024 threads");
+// smaller workgroups find room sooner (1024 threads measured no faster; 1024-thread workgroups of
+// k_vocab measured -3.7 %)
+constexpr int ROWS_THREADS = 256;
 
 // Counting sort of pair p's right keypoints into buckets (octave, floor(y)); bucket entry
 // {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544.
@@ -80,10 +77,7 @@ __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, cons
   };
   for (int i = t; i < nR; i += ROWS_THREADS) atomicAdd(&s_hist[bucket(K[i].y, K[i].octave)], 1);
   __syncthreads();
-  if (ROWS_THREADS == 1024)
-    block_scan_excl_1024(s_hist, ntab, wsum);
-  else
-    block_scan_excl(s_hist, ntab, wsum);
+  block_scan_excl(s_hist, ntab, wsum);
   int32_t* rs = row_start + (long long)p * ntab;
   for (int r = t; r < ntab; r += ROWS_THREADS) rs[r] = s_hist[r];
   __syncthreads();

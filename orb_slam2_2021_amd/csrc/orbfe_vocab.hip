@@ -44,12 +44,9 @@
 
 #define VOCAB_MAX_FEATURES 8192
 #define VOCAB_MAX_CHILDREN (1 << 23)  // sibling index field of the min key
-// k_vocab workgroup size (a power of two, 256..1024). 512: beside the extraction kernels smaller
-// workgroups find room sooner (bench 81.4k at 512 or 256 vs 78.7k at 1024); alone 66 / 81 / 61 us
-#ifndef ORBFE_VOCAB_THREADS
-#define ORBFE_VOCAB_THREADS 512
-#endif
-#define VOCAB_THREADS ORBFE_VOCAB_THREADS
+// k_vocab workgroup size. 512: beside the extraction kernels smaller workgroups find room sooner
+// (bench 81.4k at 512 or 256 vs 78.7k at 1024); alone 66 / 81 / 61 us
+#define VOCAB_THREADS 512
 
 struct __attribute__((aligned(16))) VocRec {
   uint4 d0, d1;       // the node's descriptor (32 B)
@@ -271,10 +268,6 @@ __device__ __forceinline__ void bitonic_lds(unsigned long long* skeys, int P2) {
 // P2 a power of two from VOCAB_THREADS to VOCAB_MAX_FEATURES (k_vocab pads to at least one key
 // per thread)
 __device__ __forceinline__ void sort_keys(unsigned long long* ka, int P2) {
-#if defined(ORBFE_VOCAB_LDS_SORT) && ORBFE_VOCAB_LDS_SORT
-  bitonic_lds(ka, P2);
-  return;
-#endif
   const int E = P2 / VOCAB_THREADS;
   if (E <= 1)
     bitonic_reg<1>(ka);
@@ -314,12 +307,9 @@ __device__ __forceinline__ int2 run_starts(const unsigned long long* skeys, int 
 
 // ((0 + f(v[0])) + f(v[1])) + ... over v[0..nw), f = |x| or x*x, one thread; v is readable and
 // zero from nw to nw + 3H (k_vocab zeroes 128 slots)
-#ifndef ORBFE_VOCAB_NORM_H
-#define ORBFE_VOCAB_NORM_H 16
-#endif
 template <bool L2>
 __device__ __forceinline__ double ordered_sum(const double* v, int nw) {
-  constexpr int H = ORBFE_VOCAB_NORM_H;  // words per register set (2 H doubles)
+  constexpr int H = 16;  // words per register set (2 H doubles)
   double A[H], B[H], s = 0.0;
 #pragma unroll
   for (int i = 0; i < H; i++) A[i] = v[i];
@@ -348,13 +338,7 @@ __device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img,
   for (int i = t; i < P2; i += VOCAB_THREADS) skeys[i] = i < n ? src[kbase + i] : ~0ull;
   if (t == 0) *s_n = 0;
   __syncthreads();
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 4  // phase-cost build: key loads only
-  return;
-#endif
   sort_keys(skeys, P2);  // stable: the feature index is the low half of every key
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 1  // phase-cost build: loads + sorts only
-  return;
-#endif
   int nvalid = 0;
   for (int i = t; i < n; i += VOCAB_THREADS) nvalid += skeys[i] != ~0ull;
   nvalid = wave_sum(nvalid);
@@ -383,9 +367,6 @@ __device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img,
     }
     return;
   }
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 2  // + FeatureVector CSR
-  return;
-#endif
   double* sval = reinterpret_cast<double*>(skeys + P2);
   uint32_t* words = a.bow_words + kbase;
   double* wout = a.bow_weights + kbase;
@@ -415,11 +396,7 @@ __device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img,
     // alternating sets), so the chain is one v_add_f64 per word (|w| as a source modifier); the
     // zero slots past nw add nothing (norm + 0 == norm, norm >= 0).
     double norm = 0.0;
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 3  // everything but the serial norm
-    const bool sum = false;
-#else
     const bool sum = a.norm_kind == NORM_L1 || a.norm_kind == NORM_L2;
-#endif
     if (sum) {
       if (a.norm_kind == NORM_L2)
         norm = sqrt(ordered_sum<true>(sval, nw));
@@ -437,11 +414,8 @@ __device__ __forceinline__ void vocab_part(const VocabArgs& a, bool fv, int img,
   for (int j = t; j < nw; j += VOCAB_THREADS) wout[j] = divide ? sval[j] / norm : sval[j];
 }
 
-// ORBFE_VOCAB_SPLIT 1: two workgroups per image (blockIdx.y 0: FeatureVector, 1: BowVector);
-// 0: one workgroup per image doing both in turn
-#ifndef ORBFE_VOCAB_SPLIT
-#define ORBFE_VOCAB_SPLIT 1
-#endif
+// Two workgroups per image (blockIdx.y 0: FeatureVector, 1: BowVector; one workgroup doing both
+// in turn measured slower)
 __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsigned long long* fvkeys,
                                                          const unsigned long long* bowkeys,
                                                          const int32_t* leaves) {
@@ -450,21 +424,10 @@ __global__ __launch_bounds__(VOCAB_THREADS) void k_vocab(VocabArgs a, const unsi
   __shared__ int s_wsum[VOCAB_THREADS / 64];
   __shared__ double s_norm;
   const int img = blockIdx.x;
-#if defined(ORBFE_VOCAB_DIAG) && ORBFE_VOCAB_DIAG == 5  // phase-cost build: an empty k_vocab
-  return;
-#endif
   const int n = a.empty ? 0 : min(a.counts ? a.counts[img] : a.fixed_count, a.cap);
   int P2 = VOCAB_THREADS;  // sort_keys' smallest size: one key per thread
   while (P2 < n) P2 <<= 1;
-  if (ORBFE_VOCAB_SPLIT) {
-    vocab_part(a, blockIdx.y == 0, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
-  } else {
-    vocab_part(a, true, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
-    if (a.bow_words != nullptr) {
-      __syncthreads();
-      vocab_part(a, false, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
-    }
-  }
+  vocab_part(a, blockIdx.y == 0, img, n, P2, fvkeys, bowkeys, leaves, skeys, &s_n, s_wsum, &s_norm);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -789,7 +752,7 @@ static int launch_vocab(orbfe_vocabulary* v, int n_images, const uint8_t* d_desc
   P2 = P2 < VOCAB_THREADS ? VOCAB_THREADS : P2;  // k_vocab sorts at least one key per thread
   const size_t lds = sizeof(unsigned long long) * P2 + (d_bow_words ? sizeof(double) * (P2 + 128) : 0);
   ORBFE_LAUNCH("k_vocab_descend", k_vocab_descend, dim3((cap + 15) / 16, n_images), dim3(256), 0, s, a, fvk, bwk, leaves);
-  ORBFE_LAUNCH("k_vocab", k_vocab, dim3(n_images, d_bow_words && ORBFE_VOCAB_SPLIT ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
+  ORBFE_LAUNCH("k_vocab", k_vocab, dim3(n_images, d_bow_words ? 2 : 1), dim3(VOCAB_THREADS), lds, s, a,
                      (const unsigned long long*)fvk,
                      (const unsigned long long*)bwk, (const int32_t*)leaves);
   ORBFE_HIP_CHECK(hipGetLastError());

@@ -282,13 +282,9 @@ class ORBextractor:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
-    def debug_set_copy0_side(self, on: bool = True) -> None:
-        """Level 1 resized from the caller's image, the level-0 copy on the side stream (default off)."""
-        L.check(self._lib.orbfe_debug_set_copy0_side(self._h, 1 if on else 0), "set_copy0_side")
-
     def debug_set_blur_mode(self, mode: int) -> None:
         """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream
-        after it, 2 side stream as soon as the pyramid is built."""
+        after it (several handles sharing one side stream)."""
         L.check(self._lib.orbfe_debug_set_blur_mode(self._h, int(mode)), "set_blur_mode")
 
     def set_side_stream(self, stream: int) -> None:
@@ -298,12 +294,6 @@ class ORBextractor:
     def debug_set_inline_side(self, on: bool = True) -> None:
         """Run the side-stream work (k_blur, early FAST levels) on the launch stream."""
         L.check(self._lib.orbfe_debug_set_inline_side(self._h, 1 if on else 0), "set_inline_side")
-
-    def debug_force_level_launches(self, on: bool = True) -> None:
-        """True (the library default): k_copy0 + one k_resize launch per level; False: the tiled
-        k_pyramid launches (measured slower, kept for comparison)."""
-        L.check(self._lib.orbfe_debug_force_level_launches(self._h, 1 if on else 0),
-                "force_level_launches")
 
     def geometry(self, rows: int, cols: int) -> np.ndarray:
         info = np.zeros(7 * self.nlevels, np.int32)

@@ -84,11 +84,8 @@ class DevEvent:
 
 
 def new_event(device: int):
-    """An ordering event for the pipeline's cross-stream dependencies (DevEvent by default)."""
-    import os
-    import torch
-    if os.environ.get("ORBFE_TORCH_EVENTS", "0") == "1":
-        return torch.cuda.Event()
+    """An ordering event for the pipeline's cross-stream dependencies: a DevEvent (torch's timing-
+    capable events with their system-scope fence measured 0.6 % slower)."""
     return DevEvent(device)
 
 
@@ -103,50 +100,30 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 match_high: bool = False, side_last: bool = False, side_high: bool = True,
-                 cu_split: int = 0, side_per_stream: bool = False, comm: bool = False):
+                 side_last: bool = False, comm: bool = False):
         import torch
         self.device = device
         self._ptrs = []
         self._attached = []
-        self.cu_split = cu_split
-
-        def wrap(p):
-            self._ptrs.append(p.value)
-            return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
 
         def make(high):
             p = ctypes.c_void_p()
             L.check(L.lib().orbfe_stream_create(device, 1 if high else 0, ctypes.byref(p)), "stream_create")
-            return wrap(p)
-
-        def make_masked(k, n):
-            # cu_split 1: contiguous CU ranges; 2: CU i to extractor i mod n (every XCD's CUs shared)
-            ncu = torch.cuda.get_device_properties(device).multi_processor_count
-            bits = [(i * n // ncu == k) if cu_split == 1 else (i % n == k) for i in range(ncu)]
-            words = np.zeros((ncu + 31) // 32, np.uint32)
-            for i, b in enumerate(bits):
-                if b:
-                    words[i // 32] |= np.uint32(1 << (i % 32))
-            p = ctypes.c_void_p()
-            L.check(L.lib().orbfe_stream_create_masked(device, words.ctypes.data, len(words), ctypes.byref(p)),
-                    "stream_create_masked")
-            return wrap(p)
+            self._ptrs.append(p.value)
+            return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
 
         n = max(1, n_extractors)
-        self.extract = [make_masked(k, n) if cu_split else make(False) for k in range(n)]
-        # match_inline: each sub-batch's vocabulary + matching follow its extraction on the same
-        # stream (the other extractors' streams provide the overlap)
-        self.match = None if match_inline or match_high else make(False)
-        if match_high and not match_inline and side_last:
+        self.extract = [make(False) for _ in range(n)]
+        # the matching stream at high priority, beside the shared side stream, so that the
+        # latency-bound vocabulary + SFT chain keeps up with the extraction handles (normal priority
+        # and the other placements measured slower: DESIGN.md section 5); match_inline: each
+        # sub-batch's vocabulary + matching follow its extraction on the same stream instead
+        self.match = None
+        if not match_inline and side_last:
             self.match = make(True)
-        self.side = make(side_high)
-        if match_high and not match_inline and not side_last:  # at the side stream's priority
+        self.side = make(True)
+        if not match_inline and not side_last:
             self.match = make(True)
-        # side_per_stream: one side stream per extraction stream (handles on extraction stream j
-        # share side stream j) instead of one for all; more busy streams than 4 hardware queues
-        # unless GPU_MAX_HW_QUEUES is raised
-        self.sides = [self.side] + ([make(side_high) for _ in range(n - 1)] if side_per_stream else [])
         # comm: a stream for the C4 gather's transfers, created here with the others so that it gets
         # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
@@ -158,17 +135,14 @@ class PipelineStreams:
         return self.extract + [self.match]
 
     def attach(self, ext) -> None:
-        """Route `ext`'s side-stream work to the shared side stream (with side_per_stream: the k-th
-        attached handle to side stream k mod n, matching its extraction stream k mod n); detached
-        again by close()."""
-        side = self.sides[len(self._attached) % len(self.sides)]
-        ext.set_side_stream(side.cuda_stream)
+        """Route `ext`'s side-stream work to the shared side stream; detached again by close()."""
+        ext.set_side_stream(self.side.cuda_stream)
         self._attached.append(ext)
 
     def close(self):
         """Wait for the streams, point every attached extractor back at its own side stream, then
         destroy the streams (no handle is left holding a destroyed hipStream_t)."""
-        for s in self.extract + [self.match, self.comm] + self.sides:
+        for s in self.extract + [self.match, self.comm, self.side]:
             if s is not None:
                 s.synchronize()
         for e in self._attached:
@@ -183,9 +157,8 @@ class C3Pipeline:
     def __init__(self, ext, voc, tree, B: int, H: int, W: int, cam: dict, F12: np.ndarray,
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
-                 nnratio: float = 0.6, check_ori: bool = False, defer: bool = False, streams=None,
-                 vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
-                 stereo_on_match: bool = False, stagger: bool = False):
+                 nnratio: float = 0.6, check_ori: bool = False, streams=None, pairs: str = "stereo",
+                 stereo_on_match: bool = False):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -193,23 +166,6 @@ class C3Pipeline:
         self.exts = list(ext) if isinstance(ext, (list, tuple)) else [ext]
         ext = self.exts[0]
         depth = max(depth, len(self.exts) + 1)
-        # defer: sub-batch i's vocabulary + matching are enqueued with sub-batch i+1's extraction
-        # and wait for its pyramid, so they overlap its FAST / octree / blur / describe phase
-        # rather than the latency-bound copy + resize chain (measured on MI355X: 63.7k vs 68.8k
-        # stereo frames/s -- the matching then stretches DistributeOctTree 80 -> 142 us; off by
-        # default)
-        self.defer = defer
-        # vocab_inline: ComputeBoW runs on the extraction stream right after the descriptors, the
-        # matching stream only SearchForTriangulation (a shorter serial chain per sub-batch there)
-        self.vocab_inline = vocab_inline
-        # vocab_side: sub-batch i's ComputeBoW is enqueued on the shared side stream during
-        # sub-batch i+1's call (behind i+1's side-stream FAST, ahead of i+2's, by which time i is
-        # extracted), the matching stream runs SearchForTriangulation only
-        self.vocab_side = vocab_side
-        self.side = None
-        if defer or vocab_side:
-            depth = max(depth, 3)
-        self.pending = None
         self.ext, self.voc = ext, voc
         self.B, self.H, self.W = B, H, W
         self.n_img = 2 * B
@@ -266,7 +222,6 @@ class C3Pipeline:
                     p.fv1_nodes_dev = self.nodes.data_ptr() + a * 4
                     p.fv2_nodes_dev = self.nodes.data_ptr() + b * 4
                 self.extracted = new_event(dev.index)
-                self.vocabbed = new_event(dev.index)
                 self.matched = new_event(dev.index)
                 # set by an after_match hook whose work on another stream still reads the set (the
                 # C4 gather): the set is reused only after it as well
@@ -308,9 +263,7 @@ class C3Pipeline:
         if isinstance(streams, PipelineStreams):
             for e in self.exts:
                 streams.attach(e)
-            self.side = streams.side
             streams = streams.ordered()
-        assert not vocab_side or self.side is not None, "vocab_side needs PipelineStreams"
         if streams is None:
             streams = [torch.cuda.Stream(dev) for _ in range(len(self.exts) + 1)]
         # several handles may share an extraction stream (handle k on stream k mod S): a handle's
@@ -321,7 +274,6 @@ class C3Pipeline:
         self.stream = self.streams[0]
         # vocabulary + matching (+ gather); None: on each sub-batch's extraction stream
         self.match_inline = streams[-1] is None
-        assert not (self.match_inline and defer), "deferred matching needs the matching stream"
         self.mstream = self.stream if self.match_inline else streams[-1]
         self.counter = 0
         self.last = None
@@ -333,13 +285,8 @@ class C3Pipeline:
         # stream -- the bench's shape, a handle's pyramids rebuilt only every fourth sub-batch --
         # 78.4-78.5k vs 77.1-77.5k, so bench.py turns it on (its --stereo-on-extract turns it off);
         # the class default stays off for single-handle callers
-        self.stereo_on_match = stereo and stereo_on_match and not (self.match_inline or defer or vocab_side
-                                                                   or vocab_inline)
+        self.stereo_on_match = stereo and stereo_on_match and not self.match_inline
         self.stereo_done = [None] * len(self.exts)
-        # stagger: sub-batch i's extraction starts once sub-batch i-1's pyramid is built, so the
-        # handles' latency-bound pyramid chains never run at the same time
-        self.stagger = stagger
-        self.prev_ext = None
 
     def run(self, d_img_ptr: int, after_match=None):
         """One sub-batch: 2B images of H x W at d_img_ptr (lefts then rights, row pitch W).
@@ -357,43 +304,18 @@ class C3Pipeline:
             # ComputeStereoMatches of this handle's previous sub-batch (matching stream) read the
             # pyramids this extraction overwrites
             s.wait_event(self.stereo_done[k])
-        if self.stagger and self.prev_ext is not None and self.prev_ext is not ext:
-            self.prev_ext.wait_pyramid(s.cuda_stream)
         ext.extract_batch_device(self.n_img, d_img_ptr, H * W, H, W, W, o.kps.data_ptr(),
-                                      o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
-        self.prev_ext = ext
+                                 o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
         o.ext = ext
         o.k = k
         if self.stereo and not self.stereo_on_match:  # Frame.cc:125, on the extraction stream
             self._stereo(o, ext, s)
-        if self.vocab_inline:
-            self._vocab(o, s)
         o.extracted.record(s)
         self.last = o
         if self.match_inline:
             self.mstream = s
-        if self.vocab_side:
-            if self.pending is not None:
-                self._vocab_on_side(self.pending)
-                self._match(self.pending, after_match)
-            self.pending = o
-            return o
-        if not self.defer:
-            self._match(o, after_match)
-            return o
-        if self.pending is not None:
-            ext.wait_pyramid(self.mstream.cuda_stream)  # this extraction's pyramid is built
-            self._match(self.pending, after_match)
-        self.pending = o
+        self._match(o, after_match)
         return o
-
-    def flush(self, after_match=None):
-        """Deferred modes: enqueue the matching of the last sub-batch."""
-        if self.pending is not None:
-            if self.vocab_side:
-                self._vocab_on_side(self.pending)
-            self._match(self.pending, after_match)
-            self.pending = None
 
     def _stereo(self, o, ext, stream):
         """Frame::ComputeStereoMatches (Frame.cc:125) of the set's B pairs on `stream`, from the
@@ -403,17 +325,10 @@ class C3Pipeline:
                                                 o.cnt.data_ptr(), cap, self.cam["bf"], self.mb,
                                                 o.ur.data_ptr(), o.dep.data_ptr(), stream=stream.cuda_stream)
 
-    def _vocab_on_side(self, o):
-        self.side.wait_event(o.extracted)
-        self._vocab(o, self.side)
-        o.vocabbed.record(self.side)
-
     def _match(self, o, after_match):
         B, cap = self.B, self.cap
         m = o.mstream = self.mstream
-        if self.vocab_side:
-            m.wait_event(o.vocabbed)
-        elif not self.match_inline:
+        if not self.match_inline:
             m.wait_event(o.extracted)
         if self.stereo and self.stereo_on_match:
             # off the extraction chain: the handle's next extraction waits for it (run())
@@ -421,8 +336,7 @@ class C3Pipeline:
             if self.stereo_done[o.k] is None:  # one per handle, re-recorded (earlier waits keep the old record)
                 self.stereo_done[o.k] = new_event(self.dev.index)
             self.stereo_done[o.k].record(m)
-        if not (self.vocab_inline or self.vocab_side):
-            self._vocab(o, m)
+        self._vocab(o, m)
         if self.n_pairs:
             L.check(self.lib.orbfe_search_for_triangulation_batch_device(
                 o.matcher._h, self.n_pairs, ctypes.cast(o.pairs, ctypes.c_void_p), 0, ctypes.c_void_p(m.cuda_stream)),
@@ -482,9 +396,8 @@ STEP_Z = 1.0  # metres between consecutive frames of the C3 driving sequence (SU
 
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
-             stereo: bool = False, levelsup: int = 4, defer: bool = False, streams=None,
-             vocab_inline: bool = False, vocab_side: bool = False, pairs: str = "stereo",
-             stereo_on_match: bool = False, stagger: bool = False):
+             stereo: bool = False, levelsup: int = 4, streams=None, pairs: str = "stereo",
+             stereo_on_match: bool = False):
     """The C3 scene of bench.py: KITTI intrinsics, seeded KeyFrame state per keypoint slot (half
     the keypoints stereo unless ComputeStereoMatches provides mvuRight, 30 % with a MapPoint), and
     the KeyFrame pair geometry with F12 and epipole from LocalMapping::ComputeF12
@@ -514,9 +427,8 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
     pipe = C3Pipeline(exts, voc, tree, B, H, W, cam, F12, (ex, ey),
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
-                      levelsup=levelsup, stereo=stereo, defer=defer, streams=streams,
-                      vocab_inline=vocab_inline, vocab_side=vocab_side, pairs=pairs,
-                      stereo_on_match=stereo_on_match, stagger=stagger)
+                      levelsup=levelsup, stereo=stereo, streams=streams, pairs=pairs,
+                      stereo_on_match=stereo_on_match)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo, pairs=pairs)
     return pipe, state

@@ -1,5 +1,5 @@
 """Extraction only, C3 shape (64 images of 1241x376 per call), for PMC passes on the extractor
-kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel] [--side=K] [--tiled]
+kernels: python profiles/scripts/extract_only.py [calls] [--per-kernel] [--side=K]
 [--seq] (--seq: the bench's driving-sequence frames instead of orbfe_synth_frame)"""
 import os
 import sys
@@ -29,8 +29,6 @@ def main():
     for a in sys.argv:
         if a.startswith("--side="):
             ext.debug_set_fast_side_levels(int(a.split("=")[1]))
-        if a == "--tiled":
-            ext.debug_force_level_launches(False)
     cap = ext.max_keypoints(H, W)
     kps = torch.empty(2 * B * cap * 28, dtype=torch.uint8, device=dev)
     desc = torch.empty(2 * B * cap * 32, dtype=torch.uint8, device=dev)

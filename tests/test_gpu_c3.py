@@ -68,7 +68,7 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
 
 @pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match,handles",
                          [(False, False, 1, "stereo", True, 2), (True, False, 0, "stereo", True, 2),
-                          (False, True, 2, "stereo", False, 2), (False, True, 1, "kf", True, 2),
+                          (False, True, 0, "stereo", False, 2), (False, True, 1, "kf", True, 2),
                           (True, True, 1, "kf", True, 2), (False, True, 1, "kf", False, 2),
                           (False, True, 1, "kf", True, 4)])
 def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match,
@@ -86,7 +86,7 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
     exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(handles)]
     for e in exts:
         e.debug_set_blur_mode(blur_mode)
-    streams = PipelineStreams(0, 2, match_inline=match_inline, match_high=not match_inline)
+    streams = PipelineStreams(0, 2, match_inline=match_inline)
     pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs,
                         stereo_on_match=stereo_on_match)
     batches = [frames(B, 0, pairs), frames(B, 1000, pairs), frames(B, 2000, pairs)]

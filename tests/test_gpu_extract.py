@@ -72,34 +72,27 @@ def test_other_parameters(require_gpu):
         assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
 
-@pytest.mark.parametrize("level_launches", [False, True])
-def test_scalar_resize_mode(require_gpu, level_launches):
+def test_scalar_resize_mode(require_gpu):
     img = synth_frame(2, 376, 1241)
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
-    ext.debug_force_level_launches(level_launches)
     ext.set_resize_mode(ORBFE_RESIZE_SCALAR)
     ref.set_resize_mode(ORBFE_RESIZE_SCALAR)
     assert_same_extraction(ext, ref, img)
 
 
 @pytest.mark.parametrize("shape", [(376, 1241), (480, 640), (260, 1500), (900, 700)])
-def test_pyramid_paths_agree(require_gpu, shape):
-    """The tiled k_pyramid launches (groups of levels from LDS regions, level 0 copied by the first
-    group) and the per-level k_copy0 + k_resize launches give the reference pyramid on wide, tall
-    and KITTI/TUM shapes."""
+def test_pyramid_shapes(require_gpu, shape):
+    """k_copy0 + the per-level k_resize_win launches give the reference pyramid on wide, tall and
+    KITTI/TUM shapes."""
     img = synth_frame(9, *shape)
-    ref = RefExtractor(1000, 1.2, 8, 20, 7)
-    for forced in (False, True):
-        ext = ORBextractor(1000, 1.2, 8, 20, 7)
-        ext.debug_force_level_launches(forced)
-        assert_same_extraction(ext, ref, img)
+    assert_same_extraction(ORBextractor(1000, 1.2, 8, 20, 7), RefExtractor(1000, 1.2, 8, 20, 7), img)
 
 
 @pytest.mark.parametrize("params,shape", [((800, 1.1, 12, 20, 7), (480, 640)), ((300, 1.2, 1, 20, 7), (240, 333)),
                                           ((500, 1.2, 2, 20, 7), (377, 643)), ((1500, 1.5, 5, 20, 7), (601, 1023))])
-def test_pyramid_group_splits(require_gpu, params, shape):
-    """k_pyramid's level groups (1..3 from the image, then up to 4 per group) for 1, 2, 5 and 12
-    levels on odd widths; every level's bytes, and the rest of the extraction, vs the oracle."""
+def test_pyramid_level_counts(require_gpu, params, shape):
+    """1, 2, 5 and 12 levels on odd widths (scale factors 1.1-1.5); every level's bytes, and the rest
+    of the extraction, vs the oracle."""
     img = synth_frame(17, *shape)
     assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
@@ -217,12 +210,11 @@ def test_library_umax_equals_oracle(require_gpu):
     assert u.tolist() == RefExtractor(2000, 1.2, 8, 20, 7).tables()["umax"].tolist()
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_blur_placements(require_gpu, mode):
-    """GaussianBlur after DistributeOctTree on the launch stream (1) or on the side stream as soon as
-    the pyramid is built (2): the same blurred levels, keypoints and descriptors as the oracle."""
+def test_blur_after_octree(require_gpu):
+    """GaussianBlur after DistributeOctTree on the launch stream (the several-handle placement): the
+    same blurred levels, keypoints and descriptors as the oracle."""
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
-    ext.debug_set_blur_mode(mode)
+    ext.debug_set_blur_mode(1)
     assert_same_extraction(ext, ref, synth_frame(4, 376, 1241))
     imgs = [synth_frame(30 + i, 376, 1241) for i in range(3)]
     outs = ext.extract_batch(imgs)
@@ -230,11 +222,9 @@ def test_blur_placements(require_gpu, mode):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
-@pytest.mark.parametrize("copy0_side", [True, False])
-def test_device_input_odd_pitch_and_alignment(require_gpu, copy0_side):
-    """extract_batch_device on images at an odd byte offset with an odd row pitch: level 1 is then
-    resized straight from the unaligned caller rows (the level-0 copy beside it on the side
-    stream) or from the copied level 0; both equal the oracle, image by image."""
+def test_device_input_odd_pitch_and_alignment(require_gpu):
+    """extract_batch_device on images at an odd byte offset with an odd row pitch (k_copy0's
+    unaligned loads and last-dword byte path) equals the oracle, image by image."""
     import torch
     from orb_slam2_2021_amd import _lib as L
     n, rows, cols, pitch = 3, 376, 1241, 1247
@@ -245,7 +235,6 @@ def test_device_input_odd_pitch_and_alignment(require_gpu, copy0_side):
         v[:, :cols] = imgs[i]
     d = torch.from_numpy(buf).to("cuda")
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
-    ext.debug_set_copy0_side(copy0_side)
     cap = ext.max_keypoints(rows, cols)
     kps = torch.empty(n * cap * 28, dtype=torch.uint8, device="cuda")
     desc = torch.empty(n * cap * 32, dtype=torch.uint8, device="cuda")
