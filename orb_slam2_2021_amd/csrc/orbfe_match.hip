@@ -966,19 +966,33 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
 // sbp_cached with the 16 lanes of a DPP row (lane j takes cache entries j, j + 16, ...): the
 // sequential best / second-best bookkeeping is the two smallest (dist, position) keys over the
 // unblocked entries (see k_sbp_round0), merged over the row. Every lane returns the result.
+// The first SBP_ROW_PRE entries of each lane are loaded together with the entry count (one memory
+// latency per query instead of a count -> entries chain); entries past them (a cache larger than
+// SBP_CAND) follow in a loop.
+#define SBP_ROW_PRE (SBP_CAND / 16)
 template <class Blocked>
-__device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int n, int j, Blocked blocked) {
+__device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int j, Blocked blocked, int& n_out) {
   const unsigned long long NONE = ~0ull;
   unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
   int kb1 = -1;
   const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
   const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
   const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
-  for (int c = j; c < n; c += 16) {
-    const int k = ck[c];
-    if (blocked(k)) continue;
-    const unsigned long long key =
-        ((unsigned long long)cd[c] << 40) | ((unsigned long long)c << 8) | (unsigned long long)cl[c];
+  int pk[SBP_ROW_PRE], pd[SBP_ROW_PRE], pl[SBP_ROW_PRE];
+#pragma unroll
+  for (int u = 0; u < SBP_ROW_PRE; u++) {
+    const int c = j + 16 * u;
+    const bool in = c < a.cand_cap;
+    pk[u] = in ? ck[c] : 0;
+    pd[u] = in ? cd[c] : 0;
+    pl[u] = in ? cl[c] : 0;
+  }
+  const int n = a.cand_n[i];
+  n_out = n;
+  if (n <= 0) return -1;  // (n < 0: the caller walks the grid instead)
+  auto add = [&](int c, int k, int d, int l) {
+    if (blocked(k)) return;
+    const unsigned long long key = ((unsigned long long)d << 40) | ((unsigned long long)c << 8) | (unsigned long long)l;
     if (key < k1) {
       k2 = k1;
       k1 = key;
@@ -986,7 +1000,11 @@ __device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int n, in
     } else if (key < k2) {
       k2 = key;
     }
-  }
+  };
+#pragma unroll
+  for (int u = 0; u < SBP_ROW_PRE; u++)
+    if (j + 16 * u < n) add(j + 16 * u, pk[u], pd[u], pl[u]);
+  for (int c = j + 16 * SBP_ROW_PRE; c < n; c += 16) add(c, ck[c], cd[c], cl[c]);
 #pragma unroll
   for (int s2 = 8; s2 > 0; s2 >>= 1) {
     const unsigned long long o1 = __shfl_xor(k1, s2, 16), o2 = __shfl_xor(k2, s2, 16);
@@ -1039,7 +1057,7 @@ struct SbpSettleArgs {
 };
 
 __host__ __device__ inline size_t settle_lds(int n, int m) {
-  return sizeof(int) * (4 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
+  return sizeof(int) * (5 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
 }
 constexpr int SETTLE_INV_PER_LANE = SBP_INV_CAP / 64;  // index entries per lane, loaded together
 
@@ -1057,9 +1075,11 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
   uint32_t* qbits = reinterpret_cast<uint32_t*>(list + n);
   uint32_t* dirty = qbits + qw;
   uint32_t* pre = dirty + kw;  // keypoints taken before the search (sbp_pre_blocked)
+  int* inv_cnt = reinterpret_cast<int*>(pre + kw);  // inv_n, read every round
   for (int k = t; k < n; k += SETTLE_THREADS) {
     rm2[k] = s.own0[k];
     prev[k] = s.own1[k];
+    inv_cnt[k] = s.inv_n[k];
   }
   for (int w = t; w < kw; w += SETTLE_THREADS) {
     uint32_t b = 0;
@@ -1091,7 +1111,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     for (int c = wv; c < nchg; c += NW) {
       const int k = list[c];
       const int o1 = rm2[k], o2 = prev[k], lo = min(o1, o2), hi = max(o1, o2);
-      const int cnt = s.inv_n[k];
+      const int cnt = inv_cnt[k];
       if (cnt > SBP_INV_CAP) {
         if (ln == 0) s_dense = 1;
         continue;
@@ -1120,11 +1140,11 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
           const int i = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1u;
           if (i >= m) break;
-          const int nc = a.cand_n[i];
-          if (nc == 0) continue;  // no candidate: -1 in every round
           auto blocked = [&](int k) { return ((pre[k >> 5] >> (k & 31)) & 1u) || prev[k] < i; };
-          const int r = nc > 0 ? sbp_cached_row(a, i, nc, j, blocked)
-                               : (j == 0 ? sbp_one(a, i, blocked) : 0);
+          int nc;
+          int r = sbp_cached_row(a, i, j, blocked, nc);
+          if (nc == 0) continue;  // no candidate: -1 in every round
+          if (nc < 0) r = j == 0 ? sbp_one(a, i, blocked) : 0;  // past the cache: the grid walk
           if (j == 0) {
             atomicAdd(&s_nq, 1);
             const int old = s.res[i];
@@ -1158,7 +1178,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     if (t == 0) s.serial_used[3] += nd;
     for (int c = wv; c < nd; c += NW) {
       const int k = list[c];
-      const int cnt = s.inv_n[k];
+      const int cnt = inv_cnt[k];
       int best = 0x7fffffff;
       if (cnt > SBP_INV_CAP) {  // claimants not all indexed: every query
         for (int i = ln; i < m; i += 64)

@@ -29,6 +29,7 @@ events on two streams.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import numpy as np
@@ -128,7 +129,7 @@ class PipelineStreams:
         # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
         # that stream's kernels: measured 83k -> 52k stereo frames/s on one GPU (--gather-proxy)
-        self.comm = make(False) if comm else None
+        self.comm = (make(os.environ.get("ORBFE_COMM_PRIO", "normal") == "high") if comm else None)
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
