@@ -275,12 +275,49 @@ class GatherProxy:
                 for r in self.recv:
                     r.copy_(buf, non_blocking=True)
             return
-        ev = self.packed[id(o)]
-        ev.record(m)
+        if mode in ("waitonly", "reconly", "nowait", "waitext"):  # factorial diagnostics
+            ev = self.packed[id(o)]
+            if mode != "nowait":
+                ev.record(m)
+            if mode == "waitonly":
+                self.stream.wait_event(ev)
+            if mode == "waitext":  # an extraction stream's pending event instead of the matching stream's
+                self.stream.wait_event(o.extracted)
+            if mode == "nowait":
+                with torch.cuda.stream(self.stream):
+                    for r in self.recv:
+                        r.copy_(buf, non_blocking=True)
+            return
+        if mode == "poll":  # hand over only packs already complete (the wait is then a no-op)
+            ev = self.packed[id(o)]
+            ev.record(m)
+            q = self.__dict__.setdefault("_pending", [])
+            q.append((ev, buf, o))
+            while q and (q[0][0].query() or len(q) > len(p.sets) // 2):
+                e0, b0, o0 = q.pop(0)
+                self.stream.wait_event(e0)
+                with torch.cuda.stream(self.stream):
+                    for r in self.recv:
+                        r.copy_(b0, non_blocking=True)
+                o0.released = self.sent[id(o0)]
+                o0.released.record(self.stream)
+            self.transfers += 1
+            return
+        if mode == "tev":  # torch's timing events for the hand-over
+            ev = torch.cuda.Event()
+            ev.record(m)
+        else:
+            ev = self.packed[id(o)]
+            ev.record(m)
+        if mode == "lag":  # the hand-over one sub-batch late: the copies wait for an older pack
+            prev, self._prev = getattr(self, "_prev", None), (ev, buf)
+            if prev is None:
+                return
+            ev, buf = prev
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):
             for r in self.recv:
-                if mode == "torch":
+                if mode in ("torch", "tev", "lag", "side"):
                     r.copy_(buf, non_blocking=True)
         if mode != "norelease":
             o.released = self.sent[id(o)]
@@ -376,7 +413,8 @@ def main():
     comm = pstreams.comm
     g = Gatherer(pipe, world, rank, dev, comm_dev, comm) if gather else None
     if args.gather_proxy > 1 and world == 1:
-        g = GatherProxy(pipe, args.gather_proxy, dev, comm)
+        g = GatherProxy(pipe, args.gather_proxy, dev,
+                        pstreams.side if os.environ.get("ORBFE_GPROXY_MODE") == "side" else comm)
     counter = [0]
 
     def sub_batch():

@@ -150,6 +150,8 @@ int orbfe_stream_wait_event(void* stream, void* event);
  * orbfe_event_record = hipEventRecord(event, stream). */
 int orbfe_event_create(int device, void** out);
 int orbfe_event_record(void* event, void* stream);
+/* 0: the event's work is complete (or it was never recorded), 1: not yet, < 0: error. */
+int orbfe_event_query(void* event);
 int orbfe_event_destroy(void* event);
 /* A non-blocking stream on `device` (high_priority: the device's greatest priority, as the
  * extractor's side stream). The runtime maps streams onto a few hardware queues per priority

@@ -47,8 +47,9 @@ int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float* d_cos, float* d_sin, void* stream);
 /* The last SearchByProjection's k_sbp_settle statistics: rounds that scanned every query (a
  * keypoint listed by more queries than the inverted index holds), queries re-evaluated, keypoint
- * owners recomputed (all summed over its rounds; zeros when the per-round launches ran). */
-int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out3);
+ * owners recomputed (all summed over its rounds; zeros when the per-round launches ran), then the
+ * kernel's wall-clock ticks (100 MHz) in its prologue and in its steps a-d, summed over rounds. */
+int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out8);
 
 #ifdef __cplusplus
 }

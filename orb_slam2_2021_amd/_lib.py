@@ -119,6 +119,7 @@ _SIGNATURES = {
     "orbfe_event_create": (c_int, [c_int, POINTER(c_void_p)]),
     "orbfe_event_record": (c_int, [c_void_p, c_void_p]),
     "orbfe_event_destroy": (c_int, [c_void_p]),
+    "orbfe_event_query": (c_int, [c_void_p]),
     "orbfe_matcher_set_profiling": (c_int, [c_void_p, c_int]),
     "orbfe_matcher_last_device_ms": (c_int, [c_void_p, POINTER(c_float)]),
     "orbfe_debug_matcher_settle_stats": (c_int, [c_void_p, c_void_p]),

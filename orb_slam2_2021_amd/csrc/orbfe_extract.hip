@@ -2765,6 +2765,14 @@ extern "C" int orbfe_event_record(void* event, void* stream) {
   return ORBFE_OK;
 }
 
+extern "C" int orbfe_event_query(void* event) {
+  if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_event_query: null event");
+  const hipError_t e = hipEventQuery((hipEvent_t)event);
+  if (e == hipErrorNotReady) return 1;
+  ORBFE_HIP_CHECK(e);
+  return 0;
+}
+
 extern "C" int orbfe_event_destroy(void* event) {
   if (event) ORBFE_HIP_CHECK(hipEventDestroy((hipEvent_t)event));
   return ORBFE_OK;

@@ -738,7 +738,7 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
     if (in.inv_n) in.inv_n[i] = 0;
   }
   if (i < SBP_ROUND_CAP + 4) in.state[i] = 0;
-  if (i < 4) in.serial[i] = 0;  // [0] serial walk, [1..3] k_sbp_settle's statistics
+  if (i < 16) in.serial[i] = 0;  // [0] serial walk, [1..9] k_sbp_settle's statistics
   if (i == 0) *in.nmatches = 0;
 }
 
@@ -963,25 +963,25 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   if (changed && lane_id() == __ffsll((long long)wave_ballot(true)) - 1) a.state[2] = 1;
 }
 
-// sbp_cached with the 16 lanes of a DPP row (lane j takes cache entries j, j + 16, ...): the
-// sequential best / second-best bookkeeping is the two smallest (dist, position) keys over the
-// unblocked entries (see k_sbp_round0), merged over the row. Every lane returns the result.
-// The first SBP_ROW_PRE entries of each lane are loaded together with the entry count (one memory
-// latency per query instead of a count -> entries chain); entries past them (a cache larger than
-// SBP_CAND) follow in a loop.
-#define SBP_ROW_PRE (SBP_CAND / 16)
-template <class Blocked>
-__device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int j, Blocked blocked, int& n_out) {
+// sbp_cached with a group of L lanes (lane j takes cache entries j, j + L, ...): the sequential
+// best / second-best bookkeeping is the two smallest (dist, position) keys over the unblocked
+// entries (see k_sbp_round0), merged over the group. The first SBP_CAND / L entries of each lane are
+// loaded together with the entry count (one memory latency per query instead of a count -> entries
+// chain); entries past them (a cache larger than SBP_CAND) follow in a loop. Every lane returns the
+// result; n_out is the entry count (< 0: past the cache, the caller walks the grid instead).
+template <int L, class Blocked>
+__device__ __forceinline__ int sbp_cached_group(const SbpArgs& a, int i, int j, Blocked blocked, int& n_out) {
+  constexpr int PRE = SBP_CAND / L;
   const unsigned long long NONE = ~0ull;
   unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
   int kb1 = -1;
   const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
   const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
   const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
-  int pk[SBP_ROW_PRE], pd[SBP_ROW_PRE], pl[SBP_ROW_PRE];
+  int pk[PRE], pd[PRE], pl[PRE];
 #pragma unroll
-  for (int u = 0; u < SBP_ROW_PRE; u++) {
-    const int c = j + 16 * u;
+  for (int u = 0; u < PRE; u++) {
+    const int c = j + L * u;
     const bool in = c < a.cand_cap;
     pk[u] = in ? ck[c] : 0;
     pd[u] = in ? cd[c] : 0;
@@ -989,7 +989,7 @@ __device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int j, Bl
   }
   const int n = a.cand_n[i];
   n_out = n;
-  if (n <= 0) return -1;  // (n < 0: the caller walks the grid instead)
+  if (n <= 0) return -1;
   auto add = [&](int c, int k, int d, int l) {
     if (blocked(k)) return;
     const unsigned long long key = ((unsigned long long)d << 40) | ((unsigned long long)c << 8) | (unsigned long long)l;
@@ -1002,13 +1002,13 @@ __device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int j, Bl
     }
   };
 #pragma unroll
-  for (int u = 0; u < SBP_ROW_PRE; u++)
-    if (j + 16 * u < n) add(j + 16 * u, pk[u], pd[u], pl[u]);
-  for (int c = j + 16 * SBP_ROW_PRE; c < n; c += 16) add(c, ck[c], cd[c], cl[c]);
+  for (int u = 0; u < PRE; u++)
+    if (j + L * u < n) add(j + L * u, pk[u], pd[u], pl[u]);
+  for (int c = j + L * PRE; c < n; c += L) add(c, ck[c], cd[c], cl[c]);
 #pragma unroll
-  for (int s2 = 8; s2 > 0; s2 >>= 1) {
-    const unsigned long long o1 = __shfl_xor(k1, s2, 16), o2 = __shfl_xor(k2, s2, 16);
-    const int ob = __shfl_xor(kb1, s2, 16);
+  for (int s2 = L / 2; s2 > 0; s2 >>= 1) {
+    const unsigned long long o1 = __shfl_xor(k1, s2, L), o2 = __shfl_xor(k2, s2, L);
+    const int ob = __shfl_xor(kb1, s2, L);
     k2 = min_u64(max_u64(k1, o1), min_u64(k2, o2));
     if (o1 < k1) {
       k1 = o1;
@@ -1027,18 +1027,25 @@ __device__ __forceinline__ int sbp_cached_row(const SbpArgs& a, int i, int j, Bl
   return bb.result(a.mode, a.nnratio, a.dist_th);
 }
 
-// ---- the fixpoint's rounds 2.. in one workgroup ---------------------------------------------
-// After round 1 most results are final; the rounds that follow change few of them, and as one
-// launch per round (k_sbp_round) their cost was the launch chain -- 10-16 launches per C5 search,
-// plus host-synchronised continuations when 12 were not enough. Here one 1024-thread workgroup
-// runs them all with the frame's owners in LDS and touches only what a change can reach:
+// ---- the fixpoint's tail in one workgroup ---------------------------------------------------
+// The grid-wide rounds (k_sbp_round, one launch each) settle most searches in 8-12 rounds, but a
+// C5 search needs 8-23 (KITTI-shaped local map: half of them more than 12), and a chain of launches
+// must be sized on the host: too short and the host synchronises to continue it, too long and the
+// empty launches cost ~4 us each. Rounds R0.. therefore run in this one 1024-thread workgroup, with
+// the frame's owners in LDS, touching only what a change can reach. Measured (C5, device time per
+// search, round 4): R0 = 2 / 3 / 4 / 6 / 8 / 10: 691 / 421 / 335 / 296 / 294 / 301 us, the
+// launch chain with host continuation 295-300 us; a settle round costs ~16 us against ~12 us
+// grid-wide (one workgroup's dependent global loads), so it takes over only at R0 = 8 -- equal
+// device time without the host synchronisation. Per round:
 //   a. the keypoints whose owner differs between rounds r-2 and r-1 (owner = the smallest query
 //      index whose result is the keypoint, among queries whose assignment blocks it);
 //   b. their queries from the inverted candidate index (round 0) with lo < i <= hi: only for those
 //      does blocked(k) = owner < i flip -- the k_sbp_round test, exact rather than by window;
-//   c. re-evaluation from the candidate cache, 16 lanes per query (one query's cache walk as a
-//      chain of dependent loads on one thread cost ~40 us per round), results updated in place (a
-//      round reads only the previous round's owners, never other results);
+//   c. re-evaluation from the candidate cache: the flagged queries compacted into an LDS list
+//      (they cluster in index ranges: a row of lanes per bitmap word left a few rows doing all
+//      the work) and dealt to groups of SETTLE_L lanes, each query's cache entries, count, result
+//      and flags loaded together; results updated in place (a round reads only the previous
+//      round's owners, never other results);
 //   d. the owners of the keypoints a changed result left or joined, recomputed from their index
 //      lists (every other keypoint keeps its owner).
 // Settled when no owner changed (the next round would reproduce this one). A keypoint listed by
@@ -1056,18 +1063,24 @@ struct SbpSettleArgs {
   int32_t* blocked_scratch;
 };
 
+#define SETTLE_QCAP 4096  // flagged queries per pass of step c (LDS list)
+#define SETTLE_L 4        // lanes per re-evaluated query
 __host__ __device__ inline size_t settle_lds(int n, int m) {
-  return sizeof(int) * (5 * (size_t)n) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
+  return sizeof(int) * (5 * (size_t)n + SETTLE_QCAP) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
 }
 constexpr int SETTLE_INV_PER_LANE = SBP_INV_CAP / 64;  // index entries per lane, loaded together
 
 __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSettleArgs s) {
   extern __shared__ int s_lds[];
   __shared__ int s_cnt, s_dense, s_nq;
+  __shared__ int s_wsum[SETTLE_THREADS / 64];
   const int n = a.F.n, m = a.m, t = threadIdx.x, wv = t >> 6, ln = t & 63;
   constexpr int NW = SETTLE_THREADS / 64;
   const int qw = (m + 31) >> 5, kw = (n + 31) >> 5;
   if (a.state[0] != 0) return;  // the grid-wide rounds settled already (k_sbp_round's early exit)
+  // phase clock (thread 0, wall clock ticks): [0] prologue, [1] a, [2] b, [3] c, [4] d
+  unsigned long long tck[5] = {0, 0, 0, 0, 0}, tlast = 0;
+  if (t == 0) tlast = wall_clock64();
   int* rm2 = s_lds;
   int* prev = rm2 + n;
   int* cur = prev + n;
@@ -1076,20 +1089,32 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
   uint32_t* dirty = qbits + qw;
   uint32_t* pre = dirty + kw;  // keypoints taken before the search (sbp_pre_blocked)
   int* inv_cnt = reinterpret_cast<int*>(pre + kw);  // inv_n, read every round
-  for (int k = t; k < n; k += SETTLE_THREADS) {
-    rm2[k] = s.own0[k];
-    prev[k] = s.own1[k];
-    inv_cnt[k] = s.inv_n[k];
-  }
-  for (int w = t; w < kw; w += SETTLE_THREADS) {
-    uint32_t b = 0;
-    for (int k = 32 * w; k < min(n, 32 * w + 32); k++) b |= sbp_pre_blocked(a, k) ? 1u << (k & 31) : 0u;
-    pre[w] = b;
-  }
+  int* qlist = inv_cnt + n;                           // step c's compacted queries
   for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
-  for (int w = t; w < kw; w += SETTLE_THREADS) dirty[w] = 0u;
+  for (int w = t; w < kw; w += SETTLE_THREADS) {
+    dirty[w] = 0u;
+    pre[w] = 0u;
+  }
   if (t == 0) s_nq = 0;
   __syncthreads();
+  for (int k = t; k < n; k += SETTLE_THREADS) {  // one thread per keypoint, all loads together
+    const int o0 = s.own0[k], o1 = s.own1[k], c = s.inv_n[k];
+    const bool pb = sbp_pre_blocked(a, k);
+    rm2[k] = o0;
+    prev[k] = o1;
+    inv_cnt[k] = c;
+    if (pb) atomicOr(&pre[k >> 5], 1u << (k & 31));
+  }
+
+  auto tick = [&](int ph) {
+    if (t == 0) {
+      const unsigned long long now = wall_clock64();
+      tck[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  __syncthreads();
+  tick(0);
   int round = s.round0;
   bool serial = false;
   for (;; round++) {
@@ -1101,6 +1126,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
     for (int k = t; k < n; k += SETTLE_THREADS)
       if (prev[k] != rm2[k]) list[atomicAdd(&s_cnt, 1)] = k;
     __syncthreads();
+    tick(1);
     const int nchg = s_cnt;
     if (nchg == 0) break;  // round r would reproduce round r-1
     if (round >= s.round_cap) {
@@ -1128,38 +1154,72 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
       }
     }
     __syncthreads();
+    tick(2);
     // c. re-evaluate them from the candidate cache with round r-1's owners
     const bool dense = s_dense != 0;
     if (t == 0 && dense) s.serial_used[1] += 1;
     {
-      // one 16-lane row per bitmap word (64 rows); the row's lanes walk its set bits together
-      const int row = t >> 4, j = t & 15;
-      for (int w = row; w < qw; w += SETTLE_THREADS / 16) {
-        uint32_t bits = dense ? 0xffffffffu : qbits[w];
-        while (bits) {
-          const int i = 32 * w + __builtin_ctz(bits);
-          bits &= bits - 1u;
-          if (i >= m) break;
+      // compaction: thread t owns words [t per, (t + 1) per); exclusive scan of their popcounts
+      const int per = (qw + SETTLE_THREADS - 1) / SETTLE_THREADS;
+      const int w0 = min(t * per, qw), w1 = min(w0 + per, qw);
+      auto word = [&](int w) -> uint32_t {
+        uint32_t b = dense ? 0xffffffffu : qbits[w];
+        if (32 * w + 32 > m) b &= (1u << (m - 32 * w)) - 1u;  // (m - 32 w) in 1..31 here
+        return b;
+      };
+      int mine = 0;
+      for (int w = w0; w < w1; w++) mine += __popc(word(w));
+      int inc = mine;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (ln >= o) inc += y;
+      }
+      if (ln == 63) s_wsum[wv] = inc;
+      __syncthreads();
+      int off = inc - mine, total = 0;
+      for (int q = 0; q < NW; q++) {
+        if (q < wv) off += s_wsum[q];
+        total += s_wsum[q];
+      }
+      const int g = t / SETTLE_L, j = t % SETTLE_L;
+      for (int base = 0; base < total; base += SETTLE_QCAP) {
+        int pos = off;
+        for (int w = w0; w < w1 && pos < base + SETTLE_QCAP; w++) {
+          uint32_t bits = word(w);
+          while (bits) {
+            const int i = 32 * w + __builtin_ctz(bits);
+            bits &= bits - 1u;
+            if (pos >= base && pos < base + SETTLE_QCAP) qlist[pos - base] = i;
+            pos++;
+          }
+        }
+        __syncthreads();
+        const int cnt = min(SETTLE_QCAP, total - base);
+        for (int e = g; e < cnt; e += SETTLE_THREADS / SETTLE_L) {
+          const int i = qlist[e];
+          const int old = s.res[i];
+          const int fl = a.q[i].flags;
           auto blocked = [&](int k) { return ((pre[k >> 5] >> (k & 31)) & 1u) || prev[k] < i; };
           int nc;
-          int r = sbp_cached_row(a, i, j, blocked, nc);
+          int r = sbp_cached_group<SETTLE_L>(a, i, j, blocked, nc);
           if (nc == 0) continue;  // no candidate: -1 in every round
           if (nc < 0) r = j == 0 ? sbp_one(a, i, blocked) : 0;  // past the cache: the grid walk
           if (j == 0) {
             atomicAdd(&s_nq, 1);
-            const int old = s.res[i];
             if (r != old) {
               s.res[i] = r;
-              if (a.q[i].flags & 2) {
+              if (fl & 2) {
                 if (old >= 0) atomicOr(&dirty[old >> 5], 1u << (old & 31));
                 if (r >= 0) atomicOr(&dirty[r >> 5], 1u << (r & 31));
               }
             }
           }
         }
+        __syncthreads();  // qlist is rewritten by the next pass
       }
     }
-    __syncthreads();
+    tick(3);
     for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
     // d. round r's owners: round r-1's, recomputed where a result left or joined the keypoint
     for (int k = t; k < n; k += SETTLE_THREADS) cur[k] = prev[k];
@@ -1198,6 +1258,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
       if (ln == 0) cur[k] = best;
     }
     __syncthreads();
+    tick(4);
     int* tmp = rm2;
     rm2 = prev;
     prev = cur;
@@ -1214,6 +1275,7 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
   }
   if (t == 0) {  // for k_sbp_collect / k_sbp_finish and the round statistics
     s.serial_used[2] = s_nq;
+    for (int ph = 0; ph < 5; ph++) s.serial_used[4 + ph] = (int32_t)tck[ph];
     a.state[0] = 1;
     a.state[1] = round;  // rounds run (the last computed one + 1)
     a.state[SBP_FINAL_SLOT] = ((s.round0 - 1) & 1) + 1;  // the results stay in round R0-1's buffer
@@ -1610,7 +1672,7 @@ extern "C" int orbfe_matcher_create(float nnratio, int check_orientation, int de
   m->check_ori = check_orientation ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&m->d_serial, sizeof(int32_t) * 4) != hipSuccess) {
+      hipMalloc(&m->d_serial, sizeof(int32_t) * 16) != hipSuccess) {
     delete m;
     return orbfe_set_error(ORBFE_ERR_HIP, "orbfe_matcher_create: HIP setup failed");
   }
@@ -2262,10 +2324,10 @@ extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out3) {
-  if (!m || !out3) return ORBFE_ERR_ARG;
+extern "C" int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out8) {
+  if (!m || !out8) return ORBFE_ERR_ARG;
   ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
-  ORBFE_HIP_CHECK(hipMemcpy(out3, m->d_serial + 1, 3 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  ORBFE_HIP_CHECK(hipMemcpy(out8, m->d_serial + 1, 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
   return ORBFE_OK;
 }
 

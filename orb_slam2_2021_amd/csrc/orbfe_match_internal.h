@@ -29,7 +29,7 @@
 #define SBP_CAND 48          // default per-query candidate cache of the projection searches
 #define SBP_INV_CAP 1024     // queries per keypoint in the settle path's inverted candidate index
 #define SETTLE_THREADS 1024  // k_sbp_settle: one workgroup for the fixpoint's rounds R0..
-#define SBP_SETTLE_FROM 4    // R0: rounds 0 .. R0-1 grid-wide (ORBFE_SBP_SETTLE_FROM overrides)
+#define SBP_SETTLE_FROM 8    // R0: rounds 0 .. R0-1 grid-wide (ORBFE_SBP_SETTLE_FROM overrides)
 #define SETTLE_MAX_KEYS 4096       // settle path: frame keypoints (owners in LDS) ...
 #define SETTLE_MAX_QUERIES 131072  // ... and queries (a bitmap in LDS)
 #define ORBFE_MAX_LEVELS_M 32
@@ -183,7 +183,7 @@ struct SbpPlan {
   size_t oqd, oqa, og_start, og_items, oq, ores0, ores1, oown0, oown1, oown2, oblk, ostate, obest;
   size_t ocand_k, ocand_d, ocand_l, ocand_n, onm, oown3, oinv, oinv_n;
   bool cache;
-  bool settle;  // the fixpoint's rounds 2.. in k_sbp_settle (cache, frame and query bounds)
+  bool settle;  // the fixpoint's rounds R0.. in k_sbp_settle (cache, frame and query bounds)
   int nq, cand_cap;
 };
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap = SBP_CAND);

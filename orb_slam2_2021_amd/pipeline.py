@@ -59,7 +59,7 @@ class DevEvent:
     system-scope cache write-back on record, which a default (torch) event performs -- the
     pipeline's events only order device work between its streams; the host synchronises with
     torch.cuda.synchronize(). Same record(stream) / stream.wait_event(ev) interface as
-    torch.cuda.Event. ORBFE_TORCH_EVENTS=1 selects torch's events instead (A/B)."""
+    torch.cuda.Event."""
 
     def __init__(self, device: int):
         import ctypes
@@ -70,6 +70,12 @@ class DevEvent:
     def record(self, stream) -> None:
         import ctypes
         L.check(L.lib().orbfe_event_record(self._e, ctypes.c_void_p(stream.cuda_stream)), "orbfe_event_record")
+
+    def query(self) -> bool:
+        """True when the recorded work is complete (hipEventQuery)."""
+        r = L.lib().orbfe_event_query(self._e)
+        L.check(min(r, 0), "orbfe_event_query")
+        return r == 0
 
     def wait(self, stream) -> None:  # torch.cuda.Stream.wait_event(ev) calls ev.wait(stream)
         import ctypes
@@ -120,11 +126,12 @@ class PipelineStreams:
         # and the other placements measured slower: DESIGN.md section 5); match_inline: each
         # sub-batch's vocabulary + matching follow its extraction on the same stream instead
         self.match = None
+        mhigh = os.environ.get("ORBFE_MATCH_PRIO", "high") == "high"
         if not match_inline and side_last:
-            self.match = make(True)
+            self.match = make(mhigh)
         self.side = make(True)
         if not match_inline and not side_last:
-            self.match = make(True)
+            self.match = make(mhigh)
         # comm: a stream for the C4 gather's transfers, created here with the others so that it gets
         # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold

@@ -5,6 +5,7 @@ kernel's dispatch-bound device time per search, orbfe_ktimer; --resident: the ma
 import os
 import sys
 import time
+from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
@@ -29,21 +30,24 @@ def main():
     if "--per-kernel" in sys.argv:
         L.ktimer_reset()
         L.ktimer_select(True)
-    dev = []
+    dev, rounds_all = [], []
     t0 = time.perf_counter()
     for _ in range(reps):
         for F in frames:
             m.SearchLocalPoints(F, G, 3.0)
             dev.append(m.last_device_ms())
+            rounds_all.append(m.last_stats()[0])
     dt = (time.perf_counter() - t0) / (reps * len(frames))
     n = reps * len(frames)
     rounds = m.last_stats()[0]
-    st = np.zeros(3, np.int32)
+    st = np.zeros(8, np.int32)
     L.check(L.lib().orbfe_debug_matcher_settle_stats(m._h, L.ptr(st)), "settle_stats")
     print(f"c5: {len(G.flags)} MapPoints, {np.mean([F.N for F in frames]):.0f} keypoints per frame, "
           f"{1e3 * dt:.3f} ms per search (host buffers), device {1e3 * np.mean(dev):.1f} us per search, "
           f"{reps * len(frames)} searches, {rounds} rounds in the last; settle (last search): dense rounds "
-          f"{st[0]}, queries re-evaluated {st[1]}, owners recomputed {st[2]}")
+          f"{st[0]}, queries re-evaluated {st[1]}, owners recomputed {st[2]}; ticks (10 ns) prologue / a / b / c / d "
+          f"{st[3]} / {st[4]} / {st[5]} / {st[6]} / {st[7]}")
+    print("rounds per search:", dict(sorted(Counter(rounds_all).items())))
     if "--per-kernel" in sys.argv:
         L.ktimer_select(False)
         for k, (ms, c) in sorted(L.ktimer_read().items(), key=lambda kv: -kv[1][0]):
