@@ -182,13 +182,14 @@ def spawn_ranks(args) -> int:
 
 class Gatherer:
     """C4: each sub-batch's used keypoints + descriptors to rank 0. The pack kernel runs on the
-    matching stream right after SearchForTriangulation; the point-to-point transfers of a fixed
-    byte count (the packed worst case; the packed header carries the per-image counts) run on a
-    communication stream of their own that waits for the pack: no size exchange, so the host never
-    waits for the device inside the timed loop (parallel.gather_fixed), and the matching stream
-    never waits for the transfers (a wait there put two cross-queue hops on the critical chain every
-    sub-batch: --gather-proxy measured 83k -> 54k stereo frames/s at N = 2). The output set is
-    reused only after its payload left (o.released, recorded behind the transfers)."""
+    matching stream right after SearchForTriangulation, and the point-to-point transfers of a fixed
+    byte count (the packed worst case; the packed header carries the per-image counts) follow it on
+    the same stream as one RCCL group (orb_slam2_2021_amd.rccl): no size exchange, so the host never
+    waits for the device inside the timed loop, and no cross-stream event (an idle stream made to
+    wait for the matching stream's pack every sub-batch cost 37 % of the throughput on one GPU,
+    DESIGN.md section 7). The set's o.matched follows the transfers on the stream. ORBFE_GATHER=torch
+    (and --rehearse) use torch.distributed's process group instead (parallel.gather_fixed on a comm
+    stream that waits for the pack; o.released recorded behind the transfers)."""
 
     def __init__(self, pipe, world, rank, dev, comm_dev, comm=None):
         import torch
@@ -203,12 +204,19 @@ class Gatherer:
         self.transfers = 0
         self.last = None  # rank 0: the last exchange's per-rank views (alias the receive buffers)
         self.last_set = None
-        # the pipeline's comm stream (a hardware queue of its own, PipelineStreams); torch's pool
-        # only with --torch-streams
+        # the pipeline's comm stream (a hardware queue of its own, PipelineStreams)
         self.comm = comm if comm is not None else torch.cuda.Stream(dev)
         from orb_slam2_2021_amd.pipeline import new_event
         self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
         self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
+        self.rccl = None
+        if comm_dev.type != "cpu" and os.environ.get("ORBFE_GATHER", "rccl") == "rccl":
+            from orb_slam2_2021_amd.rccl import RcclComm
+            try:
+                self.rccl = RcclComm.from_process_group()
+            except (OSError, RuntimeError, AttributeError) as e:  # every rank fails alike (library / init)
+                print(f"rank {rank}: RCCL communicator unavailable ({e}); C4 through torch.distributed",
+                      file=sys.stderr)
 
     def pack(self, o):
         import torch
@@ -218,6 +226,16 @@ class Gatherer:
         pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
                               buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(),
                               o.mstream.cuda_stream)
+        if self.rccl is not None:  # the transfers on the matching stream, behind the pack
+            recv = [r.data_ptr() for r in self.recv] if self.rank == 0 else None
+            self.rccl.gather(buf.data_ptr(), self.cap_bytes, recv, 0, o.mstream.cuda_stream)
+            o.released = None
+            self.transfers += 1
+            self.last_set = o
+            if self.rank == 0:
+                self.last = [buf[:self.cap_bytes] if r == 0 else self.recv[r][:self.cap_bytes]
+                             for r in range(self.world)]
+            return
         ev = self.packed[id(o)]
         ev.record(o.mstream)
         self.comm.wait_event(ev)
@@ -258,6 +276,10 @@ class GatherProxy:
         self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
         self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
         self.transfers = 0
+        self.rccl = None
+        if os.environ.get("ORBFE_GPROXY_MODE", "torch") == "rccl":
+            from orb_slam2_2021_amd.rccl import RcclComm, unique_id
+            self.rccl = RcclComm(1, 0, unique_id())
 
     def pack(self, o):
         import torch
@@ -265,6 +287,12 @@ class GatherProxy:
         p, m = self.pipe, o.mstream
         buf = self.bufs[id(o)]
         mode = os.environ.get("ORBFE_GPROXY_MODE", "torch")  # diagnostic: which part costs
+        if self.rccl is not None:  # RCCL self send / receive pairs on the matching stream
+            pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                                  buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
+            self.rccl.self_copies(buf.data_ptr(), self.cap_bytes, [r.data_ptr() for r in self.recv], m.cuda_stream)
+            self.transfers += 1
+            return
         if mode != "evonly":
             pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
                                   buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)

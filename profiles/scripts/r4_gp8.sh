@@ -7,4 +7,6 @@ ORBFE_GPROXY_MODE=waitext timeout -k 10 120 python bench.py $A --gather-proxy 2 
 ORBFE_MATCH_PRIO=normal timeout -k 10 120 python bench.py $A --hw-queues 8 > gpurun_out/g10_mnormal.log 2>&1 &&
 ORBFE_MATCH_PRIO=normal ORBFE_GPROXY_MODE=waitonly timeout -k 10 120 python bench.py $A --gather-proxy 2 > gpurun_out/g10_mnormal_wait.log 2>&1 &&
 ORBFE_MATCH_PRIO=normal timeout -k 10 120 python bench.py $A --gather-proxy 8 > gpurun_out/g10_mnormal_p8.log 2>&1 &&
-ORBFE_GPROXY_MODE=poll timeout -k 10 120 python bench.py $A --gather-proxy 2 > gpurun_out/g10_poll.log 2>&1
+ORBFE_GPROXY_MODE=poll timeout -k 10 120 python bench.py $A --gather-proxy 2 > gpurun_out/g10_poll.log 2>&1 &&
+ORBFE_GPROXY_MODE=rccl timeout -k 10 120 python bench.py $A --gather-proxy 2 > gpurun_out/g10_rccl2.log 2>&1 &&
+ORBFE_GPROXY_MODE=rccl timeout -k 10 120 python bench.py $A --gather-proxy 8 > gpurun_out/g10_rccl8.log 2>&1

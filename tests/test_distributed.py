@@ -236,3 +236,14 @@ def test_bench_rank_refuses_world_mismatch(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert "WORLD_SIZE=2" in str(e.value.code)
+
+
+def test_rccl_binding_resolves_the_p2p_api():
+    """The C4 transfer binding (orb_slam2_2021_amd.rccl) finds torch's librccl and every entry it
+    calls, without touching a GPU."""
+    from orb_slam2_2021_amd import rccl
+    lib = rccl.lib()
+    for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclSend", "ncclRecv", "ncclGroupStart",
+              "ncclGroupEnd", "ncclCommDestroy", "ncclGetErrorString"):
+        assert getattr(lib, f) is not None
+    assert lib.ncclGetErrorString(0)
