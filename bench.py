@@ -112,6 +112,8 @@ def parse(argv=None):
     p.add_argument("--c5-workers", type=int, default=4,
                    help="C5 leg: Tracking-like callers per rank, each with its own extractor + matcher on its "
                         "own thread (the leg also reports one caller)")
+    p.add_argument("--gather-every", type=int, default=1,
+                   help="--gather-proxy: the packed payloads of K sub-batches per RCCL group")
     p.add_argument("--gather-proxy", type=int, default=0,
                    help="one-GPU proxy of C4's rank-0 ingestion at N GPUs: after each sub-batch's pack, "
                         "N-1 device-to-device copies of the packed worst-case payload on a stream of their "
@@ -228,7 +230,7 @@ class Gatherer:
                               o.mstream.cuda_stream)
         if self.rccl is not None:  # the transfers on the matching stream, behind the pack
             recv = [r.data_ptr() for r in self.recv] if self.rank == 0 else None
-            self.rccl.gather(buf.data_ptr(), self.cap_bytes, recv, 0, o.mstream.cuda_stream)
+            self.rccl.gather([buf.data_ptr()], self.cap_bytes, [recv] if recv else None, 0, o.mstream.cuda_stream)
             o.released = None
             self.transfers += 1
             self.last_set = o
@@ -255,108 +257,48 @@ class Gatherer:
 
 class GatherProxy:
     """--gather-proxy N on one GPU: the cost rank 0 pays for C4's ingestion at N GPUs, without the
-    peers. Per sub-batch, after SearchForTriangulation, the keypoints + descriptors are packed on the
-    matching stream (as Gatherer.pack does), then N - 1 device-to-device copies of the packed
-    worst-case payload (the byte count every peer sends, orbfe_packed_bytes) run on a stream of
-    their own -- RCCL's receive kernels run on RCCL's stream, a fifth busy stream -- and the output
-    set is released only after them (o.released; the matching stream does not wait for them). The copies read and write rank 0's HBM (2x the received bytes)
-    with CU blit kernels, where a real receive writes what xGMI delivers: an upper bound on the HBM
-    side, no model of the links."""
+    peers. Per sub-batch the keypoints + descriptors are packed on the matching stream (as
+    Gatherer.pack does); every --gather-every K sub-batches the K packed payloads go through N - 1
+    RCCL send / receive pairs each of a world-1 communicator with itself, one group on the matching
+    stream (Gatherer's transfer path, orb_slam2_2021_amd.rccl). The self pairs read and write rank
+    0's HBM (the send side too, which a real root does not pay): an upper bound on the root's HBM
+    and CU cost, no model of the xGMI links."""
 
-    def __init__(self, pipe, n_gpus, dev, comm=None):
+    def __init__(self, pipe, n_gpus, dev, every=1):
         import torch
         from orb_slam2_2021_amd.parallel import packed_bytes
-        self.pipe, self.n = pipe, n_gpus
+        from orb_slam2_2021_amd.rccl import RcclComm, unique_id
+        self.pipe, self.n, self.every = pipe, n_gpus, max(1, every)
         self.cap_bytes = packed_bytes(pipe.n_img, pipe.n_img * pipe.cap)
         self.bufs = {id(o): torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for o in pipe.sets}
         self.sizes = {id(o): torch.zeros(1, dtype=torch.int64, device=dev) for o in pipe.sets}
-        self.recv = [torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev) for _ in range(n_gpus - 1)]
-        self.stream = comm if comm is not None else torch.cuda.Stream(dev)  # PipelineStreams.comm
-        from orb_slam2_2021_amd.pipeline import new_event
-        self.packed = {id(o): new_event(dev.index) for o in pipe.sets}
-        self.sent = {id(o): new_event(dev.index) for o in pipe.sets}
+        self.recv = [torch.empty(self.cap_bytes, dtype=torch.uint8, device=dev)
+                     for _ in range((n_gpus - 1) * self.every)]
+        self.rccl = RcclComm(1, 0, unique_id())
+        self.pending = []
         self.transfers = 0
-        self.rccl = None
-        if os.environ.get("ORBFE_GPROXY_MODE", "torch") == "rccl":
-            from orb_slam2_2021_amd.rccl import RcclComm, unique_id
-            self.rccl = RcclComm(1, 0, unique_id())
 
     def pack(self, o):
-        import torch
         from orb_slam2_2021_amd.parallel import pack_keypoints_device
         p, m = self.pipe, o.mstream
         buf = self.bufs[id(o)]
-        mode = os.environ.get("ORBFE_GPROXY_MODE", "torch")  # diagnostic: which part costs
-        if self.rccl is not None:  # RCCL self send / receive pairs on the matching stream
-            pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
-                                  buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
-            self.rccl.self_copies(buf.data_ptr(), self.cap_bytes, [r.data_ptr() for r in self.recv], m.cuda_stream)
-            self.transfers += 1
-            return
-        if mode != "evonly":
-            pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
-                                  buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
-        if mode == "packonly":
-            return
-        if mode == "same":  # the copies on the matching stream itself, no cross-stream events
-            with torch.cuda.stream(m):
-                for r in self.recv:
-                    r.copy_(buf, non_blocking=True)
-            return
-        if mode in ("waitonly", "reconly", "nowait", "waitext"):  # factorial diagnostics
-            ev = self.packed[id(o)]
-            if mode != "nowait":
-                ev.record(m)
-            if mode == "waitonly":
-                self.stream.wait_event(ev)
-            if mode == "waitext":  # an extraction stream's pending event instead of the matching stream's
-                self.stream.wait_event(o.extracted)
-            if mode == "nowait":
-                with torch.cuda.stream(self.stream):
-                    for r in self.recv:
-                        r.copy_(buf, non_blocking=True)
-            return
-        if mode == "poll":  # hand over only packs already complete (the wait is then a no-op)
-            ev = self.packed[id(o)]
-            ev.record(m)
-            q = self.__dict__.setdefault("_pending", [])
-            q.append((ev, buf, o))
-            while q and (q[0][0].query() or len(q) > len(p.sets) // 2):
-                e0, b0, o0 = q.pop(0)
-                self.stream.wait_event(e0)
-                with torch.cuda.stream(self.stream):
-                    for r in self.recv:
-                        r.copy_(b0, non_blocking=True)
-                o0.released = self.sent[id(o0)]
-                o0.released.record(self.stream)
-            self.transfers += 1
-            return
-        if mode == "tev":  # torch's timing events for the hand-over
-            ev = torch.cuda.Event()
-            ev.record(m)
-        else:
-            ev = self.packed[id(o)]
-            ev.record(m)
-        if mode == "lag":  # the hand-over one sub-batch late: the copies wait for an older pack
-            prev, self._prev = getattr(self, "_prev", None), (ev, buf)
-            if prev is None:
-                return
-            ev, buf = prev
-        self.stream.wait_event(ev)
-        with torch.cuda.stream(self.stream):
-            for r in self.recv:
-                if mode in ("torch", "tev", "lag", "side"):
-                    r.copy_(buf, non_blocking=True)
-        if mode != "norelease":
-            o.released = self.sent[id(o)]
-            o.released.record(self.stream)
+        pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
+                              buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
+        self.pending.append(buf.data_ptr())
+        if len(self.pending) == self.every:
+            # (a set's payload buffer is rewritten only by its next pack, behind this on the stream)
+            k = self.n - 1
+            recv = [[r.data_ptr() for r in self.recv[j * k:(j + 1) * k]] for j in range(len(self.pending))]
+            self.rccl.self_copies(self.pending, self.cap_bytes, recv, m.cuda_stream)
+            self.pending = []
         self.transfers += 1
 
     def describe(self):
-        return {"n_gpus_modelled": self.n, "copies_per_subbatch": self.n - 1, "bytes_per_copy": self.cap_bytes,
-                "received_bytes_per_subbatch": self.cap_bytes * (self.n - 1),
-                "what": "rank 0's ingestion of C4 on one GPU: N-1 device-to-device copies of the packed worst-case "
-                        "payload per sub-batch on their own stream (RCCL's receive stream), 8 hardware queues"}
+        return {"n_gpus_modelled": self.n, "payloads_per_subbatch": self.n - 1, "bytes_per_payload": self.cap_bytes,
+                "received_bytes_per_subbatch": self.cap_bytes * (self.n - 1), "gather_every": self.every,
+                "what": "rank 0's ingestion of C4 on one GPU: N-1 RCCL self send / receive pairs of the packed "
+                        "worst-case payload per sub-batch on the matching stream, batched every K sub-batches "
+                        "into one group; the send side's HBM traffic is counted too (an upper bound)"}
 
 
 def main():
@@ -381,7 +323,7 @@ def main():
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
     pstreams = PipelineStreams(gpu, n_ext, match_inline=args.match_inline, side_last=args.inline_side,
-                               comm=world > 1 or args.gather_proxy > 1)
+                               comm=world > 1)
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -441,8 +383,7 @@ def main():
     comm = pstreams.comm
     g = Gatherer(pipe, world, rank, dev, comm_dev, comm) if gather else None
     if args.gather_proxy > 1 and world == 1:
-        g = GatherProxy(pipe, args.gather_proxy, dev,
-                        pstreams.side if os.environ.get("ORBFE_GPROXY_MODE") == "side" else comm)
+        g = GatherProxy(pipe, args.gather_proxy, dev, every=args.gather_every)
     counter = [0]
 
     def sub_batch():

@@ -91,32 +91,37 @@ class RcclComm:
         dist.broadcast_object_list(box, src=0)
         return cls(world, rank, box[0])
 
-    def gather(self, send_ptr: int, nbytes: int, recv_ptrs: Optional[Sequence[int]], root: int,
-               stream: int) -> None:
-        """Every rank's first `nbytes` at send_ptr to `root`: rank r's bytes land at recv_ptrs[r]
-        on the root (root's own entry is ignored: its payload stays where it is). One RCCL group
-        on `stream` (a hipStream_t address), ordered by the stream alone."""
+    def gather(self, send_ptrs: Sequence[int], nbytes: int, recv_ptrs: Optional[Sequence[Sequence[int]]],
+               root: int, stream: int) -> None:
+        """Every rank's payloads to `root`, one RCCL group on `stream` (a hipStream_t address),
+        ordered by the stream alone: send_ptrs[j] holds this rank's j-th payload (its first
+        `nbytes`); on the root, rank r's j-th payload lands at recv_ptrs[j][r] (the root's own
+        entries are ignored: its payloads stay where they are)."""
         l, c, s = lib(), self._comm, c_void_p(stream)
         _check(l.ncclGroupStart(), "ncclGroupStart")
         try:
-            if self.rank == root:
-                for r in range(self.nranks):
-                    if r != root:
-                        _check(l.ncclRecv(c_void_p(recv_ptrs[r]), nbytes, NCCL_UINT8, r, c, s), "ncclRecv")
-            else:
-                _check(l.ncclSend(c_void_p(send_ptr), nbytes, NCCL_UINT8, root, c, s), "ncclSend")
+            for j, sp in enumerate(send_ptrs):
+                if self.rank == root:
+                    for r in range(self.nranks):
+                        if r != root:
+                            _check(l.ncclRecv(c_void_p(recv_ptrs[j][r]), nbytes, NCCL_UINT8, r, c, s), "ncclRecv")
+                else:
+                    _check(l.ncclSend(c_void_p(sp), nbytes, NCCL_UINT8, root, c, s), "ncclSend")
         finally:
             _check(l.ncclGroupEnd(), "ncclGroupEnd")
 
-    def self_copies(self, send_ptr: int, nbytes: int, recv_ptrs: Sequence[int], stream: int) -> None:
-        """len(recv_ptrs) send / receive pairs of this rank with itself in one group (the one-GPU
-        proxy of a root receiving from that many peers)."""
+    def self_copies(self, send_ptrs: Sequence[int], nbytes: int, recv_ptrs: Sequence[Sequence[int]],
+                    stream: int) -> None:
+        """For payload j (send_ptrs[j]), one send / receive pair of this rank with itself into each
+        of recv_ptrs[j], all in one group (the one-GPU proxy of a root receiving from that many
+        peers)."""
         l, c, s = lib(), self._comm, c_void_p(stream)
         _check(l.ncclGroupStart(), "ncclGroupStart")
         try:
-            for p in recv_ptrs:
-                _check(l.ncclSend(c_void_p(send_ptr), nbytes, NCCL_UINT8, self.rank, c, s), "ncclSend")
-                _check(l.ncclRecv(c_void_p(p), nbytes, NCCL_UINT8, self.rank, c, s), "ncclRecv")
+            for sp, rp in zip(send_ptrs, recv_ptrs):
+                for p in rp:
+                    _check(l.ncclSend(c_void_p(sp), nbytes, NCCL_UINT8, self.rank, c, s), "ncclSend")
+                    _check(l.ncclRecv(c_void_p(p), nbytes, NCCL_UINT8, self.rank, c, s), "ncclRecv")
         finally:
             _check(l.ncclGroupEnd(), "ncclGroupEnd")
 

@@ -150,7 +150,7 @@ def test_rccl_self_transfers_on_a_stream(require_gpu):
         dst = [torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(3)]
         with torch.cuda.stream(s):
             src.copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda"))
-        comm.self_copies(src.data_ptr(), n, [d.data_ptr() for d in dst], s.cuda_stream)
+        comm.self_copies([src.data_ptr()], n, [[d.data_ptr() for d in dst]], s.cuda_stream)
         s.synchronize()
         for d in dst:
             assert torch.equal(d, src)
