@@ -61,9 +61,11 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per mode")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the all-core CPU baseline (0: the affinity mask, capped by OMP_NUM_THREADS)")
-    p.add_argument("--event-every", type=int, default=4,
-                   help="HIP events around the dominant kernel on every n-th timed sub-batch")
-    p.add_argument("--probe-subbatches", type=int, default=24)
+    p.add_argument("--event-every", type=int, default=8,
+                   help="every kernel timed by dispatch-bound events on every n-th group of timed sub-batches "
+                        "(all kernels on every 4th group cost 2.2 %% of the value, round 4)")
+    p.add_argument("--probe-subbatches", type=int, default=24,
+                   help="with --no-kernel-events: sub-batches of the untimed pass that times every kernel")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-gather", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true")
@@ -407,28 +409,19 @@ def main():
         sub_batch()
     host_us = (time.perf_counter() - th0) / 32 * 1e6
     torch.cuda.synchronize()
-    # probe pass (untimed): every kernel's launches timed by their own dispatch interval
-    # (orbfe_ktimer: start / stop events bound to the dispatch, the interval rocprofv3's kernel
-    # trace reports) -> device time per sub-batch per kernel; the dominant kernel is the largest
+    # timed region: every kernel's launches on every n-th group of sub-batches timed by their own
+    # dispatch interval (orbfe_ktimer: start / stop events bound to the dispatch, the interval
+    # rocprofv3's kernel trace reports) -> device time per sub-batch per kernel, measured under the
+    # timed region's own contention; the dominant kernel is the largest
     from orb_slam2_2021_amd import _lib as L
-    L.ktimer_reset()
-    L.ktimer_select(True)
-    for _ in range(args.probe_subbatches):
-        sub_batch()
-    torch.cuda.synchronize()
-    L.ktimer_select(False)
-    probe = L.ktimer_read()
-    dominant = max(probe, key=lambda k: probe[k][0])
-    # timed region: the dominant kernel and k_fast (the path's FAST row) timed the same way on
-    # every n-th group of sub-batches
-    watch = [dominant] + (["k_fast"] if dominant != "k_fast" and "k_fast" in probe else [])
+    kt_overhead = L.ktimer_calibrate(dev.index)  # on a private stream, the pipeline idle
     L.ktimer_reset()
     ev_every = max(1, args.event_every)
     timed_events = 0
 
     def set_events(on):
         if not args.no_kernel_events:
-            L.ktimer_select(watch if on else None)
+            L.ktimer_select(True if on else None)
 
     barrier()
     torch.cuda.synchronize()
@@ -447,6 +440,16 @@ def main():
     barrier()
     t1 = time.perf_counter()
     timed = L.ktimer_read()
+    if not timed:  # --no-kernel-events: a short untimed pass with every kernel timed instead
+        L.ktimer_select(True)
+        for _ in range(args.probe_subbatches):
+            sub_batch()
+        torch.cuda.synchronize()
+        L.ktimer_select(False)
+        timed, timed_events = L.ktimer_read(), args.probe_subbatches
+    corr = {k: (ms - c * kt_overhead * 1e-3, c) for k, (ms, c) in timed.items()}  # overhead off each launch
+    dominant = max(corr, key=lambda k: corr[k][0])
+    watch = [dominant] + (["k_fast"] if dominant != "k_fast" and "k_fast" in timed else [])
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
@@ -462,11 +465,9 @@ def main():
     geo = ext.geometry(H, W)
     rooflines = []
     for kname in watch:
-        use_timed = kname in timed and not args.no_kernel_events
-        r = roofline(timed if use_timed else probe, kname, geo, counts, cand, n_img,
-                     timed_events if use_timed else args.probe_subbatches, pipe)
+        r = roofline(timed, kname, geo, counts, cand, n_img, timed_events, pipe, kt_overhead)
         r["measured_in"] = ((f"timed region, every {ev_every}th group of sub-batches ({timed_events} sub-batches)"
-                             if use_timed else "probe pass")
+                             if not args.no_kernel_events else "an untimed pass after the timed region")
                             + ": start / stop HIP events bound to each launch's dispatch (hipExtLaunchKernelGGL, "
                               "orbfe_ktimer), the kernel's own execution interval as rocprofv3 --kernel-trace reports it")
         r["traffic"], r["traffic_source"] = pmc_traffic(kname, W, H, B, args)
@@ -475,7 +476,7 @@ def main():
             r["traffic"] = int(r["traffic"] / r["launches_per_subbatch"])
         rooflines.append(r)
     roof = rooflines[0]
-    roof["dominant_by"] = "device time per sub-batch in the probe pass (all kernels timed)"
+    roof["dominant_by"] = "device time per sub-batch, every kernel timed on the same sub-batches"
     if len(rooflines) > 1:
         roof["also"] = rooflines[1:]
     algo_frame = pipeline_bytes_per_stereo_frame(geo, counts, B, pipe.n_pairs)
@@ -510,6 +511,7 @@ def main():
                                             f"levelsup {args.levelsup}, TF_IDF / L1",
             "stereo_frames_per_gpu_per_subbatch": B, "subbatches_per_step": S_sub,
             "stereo_frames_per_gpu_per_step": B * S_sub, "distinct_input_batches": NB,
+            "extractor_handles": len(exts), "event_every": ev_every,
             "parallelism": f"frame-sharded x{world}",
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "pipeline": (f"{len(exts)} extractor handles on {n_ext} streams (consecutive sub-batches' "
@@ -523,10 +525,12 @@ def main():
             "achieved_GBps": round(algo_frame * value / world / 1e9, 3),
             "frac_of_peak": round(algo_frame * value / world / 1e9 / HBM_PEAK_GBS, 6),
         },
-        "kernels_us_per_subbatch": {k: round(1e3 * v[0] / args.probe_subbatches, 2)
-                                    for k, v in sorted(probe.items(), key=lambda kv: -kv[1][0])},
-        "kernels_us_per_subbatch_what": ("device execution per sub-batch in the probe pass (dispatch-bound events, "
-                                         "the contended pipeline; sums exceed the period because kernels overlap)"),
+        "kernels_us_per_subbatch": {k: round(1e3 * v[0] / timed_events, 2)
+                                    for k, v in sorted(corr.items(), key=lambda kv: -kv[1][0])},
+        "kernels_us_per_subbatch_what": ("device execution per sub-batch on the timed region's event sub-batches "
+                                         "(dispatch-bound events less the timer's per-dispatch overhead, "
+                                         f"{kt_overhead:.2f} us; the contended pipeline; sums exceed the period "
+                                         "because kernels overlap)"),
         "keypoints_per_image": round(float(counts.mean()), 1),
         "sft_matches_per_pair": round(float(nm[:pipe.n_pairs].mean()), 1),
         "sft_pairs_per_subbatch": pipe.n_pairs,
@@ -618,7 +622,7 @@ def level_pixels(geo):
     return [int(w) * int(h) for w, h in geo[:, :2]]
 
 
-def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches, pipe):
+def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches, pipe, overhead_us=0.0):
     """Roofline of kernel `dom`: ALGORITHMIC bytes per sub-batch / its device time per sub-batch
     (kt: {kernel: (total ms, launches)} over `subbatches` sub-batches; a kernel may run as several
     launches per sub-batch, e.g. k_resize_win once per level and k_fast as levels 0-2 beside the
@@ -664,11 +668,14 @@ def roofline(kt, dom, geo, counts, n_cand, n_img, subbatches, pipe):
     }
     total_ms, launches = kt[dom]
     per_launch = max(round(launches / max(subbatches, 1)), 1)  # launches per sub-batch
-    sub_s = total_ms / 1e3 / max(subbatches, 1)
+    raw_s = total_ms / 1e3 / max(subbatches, 1)
+    # the timer's own per-dispatch overhead (orbfe_ktimer_calibrate) off every launch
+    sub_s = max(raw_s - launches * overhead_us * 1e-6 / max(subbatches, 1), 1e-9)
     algo = per_sub.get(dom)
     out = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
            "traffic": None, "kernel_us_per_subbatch": round(sub_s * 1e6, 2),
-           "avg_launch_us": round(sub_s * 1e6 / per_launch, 2), "launches_per_subbatch": per_launch}
+           "avg_launch_us": round(sub_s * 1e6 / per_launch, 2), "launches_per_subbatch": per_launch,
+           "avg_launch_us_events": round(raw_s * 1e6 / per_launch, 2), "timer_overhead_us": round(overhead_us, 2)}
     if algo is not None:
         achieved = algo / sub_s / 1e9
         out.update({"achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 6),

@@ -131,6 +131,11 @@ int orbfe_ktimer_select(const char* names);
 int orbfe_ktimer_read(char* names, int name_len, double* total_ms, long long* launches, int cap,
                       int* n);
 int orbfe_ktimer_reset(void);
+/* The timer's own per-dispatch overhead: the median event interval of n launches of an empty
+ * one-workgroup kernel on a private stream of `device`, in microseconds. The dispatch-bound events
+ * include the dispatch's marker / launch latency beyond the kernel's execution, which rocprofv3's
+ * kernel trace does not count; bench.py subtracts it per launch. */
+int orbfe_ktimer_calibrate(int device, int n, double* overhead_us);
 
 /* Stream the handle launches on (hipStream_t as void*). */
 void* orbfe_extractor_stream(orbfe_extractor* h);

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_float, c_int, c_int32,
+from ctypes import (POINTER, byref, Structure, c_char, c_char_p, c_double, c_float, c_int, c_int32,
                     c_size_t, c_uint8, c_uint32, c_uint64, c_void_p)
 
 import numpy as np
@@ -113,6 +113,7 @@ _SIGNATURES = {
     "orbfe_ktimer_select": (c_int, [ctypes.c_char_p]),
     "orbfe_ktimer_read": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, POINTER(c_int)]),
     "orbfe_ktimer_reset": (c_int, []),
+    "orbfe_ktimer_calibrate": (c_int, [c_int, c_int, POINTER(c_double)]),
     "orbfe_extractor_stream": (c_void_p, [c_void_p]),
     "orbfe_extractor_pyramid_event": (c_void_p, [c_void_p]),
     "orbfe_stream_wait_event": (c_int, [c_void_p, c_void_p]),
@@ -313,3 +314,10 @@ def ktimer_read() -> dict:
 
 def ktimer_reset() -> None:
     check(lib().orbfe_ktimer_reset(), "ktimer_reset")
+
+
+def ktimer_calibrate(device: int = 0, n: int = 64) -> float:
+    """The timer's per-dispatch overhead in microseconds (orbfe_ktimer_calibrate)."""
+    v = c_double()
+    check(lib().orbfe_ktimer_calibrate(int(device), int(n), byref(v)), "ktimer_calibrate")
+    return float(v.value)

@@ -138,6 +138,36 @@ extern "C" int orbfe_ktimer_read(char* names, int name_len, double* total_ms, lo
   return (int)s.names.size() > cap ? ORBFE_ERR_CAPACITY : ORBFE_OK;
 }
 
+// An empty one-workgroup kernel: the event interval it reports is the timer's own per-dispatch
+// overhead (the marker and dispatch latency the dispatch-bound events include beyond the kernel's
+// execution, which rocprofv3's kernel trace does not count).
+__global__ void k_ktimer_nop() {}
+
+extern "C" int orbfe_ktimer_calibrate(int device, int n, double* overhead_us) {
+  if (!overhead_us || n <= 0) return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<float> t;
+  hipError_t err = hipEventCreate(&e0);
+  if (err == hipSuccess) err = hipEventCreate(&e1);
+  for (int i = 0; err == hipSuccess && i <= n; i++) {
+    hipExtLaunchKernelGGL(k_ktimer_nop, dim3(1), dim3(64), 0, s, e0, e1, 0);
+    err = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, e0, e1);
+    if (err == hipSuccess && i > 0) t.push_back(ms);  // (the first launch loads the code object)
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipStreamDestroy(s);
+  ORBFE_HIP_CHECK(err);
+  std::sort(t.begin(), t.end());
+  *overhead_us = 1e3 * (double)t[t.size() / 2];  // median
+  return ORBFE_OK;
+}
+
 extern "C" int orbfe_ktimer_reset(void) {
   using namespace orbfe_kt;
   State& s = st();
