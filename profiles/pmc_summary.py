@@ -6,7 +6,8 @@ counts half the bytes of wide coalesced reads, so it is doubled; WRITE_SIZE (KiB
 usage: pmc_summary.py FETCH_CSV WRITE_CSV [OUT_JSON]
 Per sub-batch (one C3 batch of 64 images; bench.py's `traffic_bytes_per_step` key keeps its
 round-1 name) = mean per launch x launches per sub-batch (k_resize_win: one per pyramid level;
-k_fast: levels 0..2 each beside the resize chain + levels 3..7; every other kernel once).
+k_fast: levels 0..K-1 each beside the resize chain + the rest; every other kernel once), counted as
+each kernel's launches over k_describe's.
 """
 import csv
 import json
@@ -36,7 +37,9 @@ def per_kernel(path, counter):
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    lps = {"k_resize_win": 7, "k_resize": 7, "k_fast": 4}
+    # launches per sub-batch: each kernel's launch count over k_describe's (one per sub-batch)
+    ref = fetch.get("k_describe", (0, 0))[1]
+    lps = {k: max(1, round(c / ref)) for k, (_, c) in fetch.items()} if ref else {}
     kernels = {}
     for k in sorted(set(fetch) & set(write)):
         if k.startswith("__amd") or k.startswith("at::") or "native" in k:
