@@ -61,9 +61,9 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU baseline time per mode")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="threads of the all-core CPU baseline (0: the affinity mask, capped by OMP_NUM_THREADS)")
-    p.add_argument("--event-every", type=int, default=8,
+    p.add_argument("--event-every", type=int, default=16,
                    help="every kernel timed by dispatch-bound events on every n-th group of timed sub-batches "
-                        "(all kernels on every 4th group cost 2.2 %% of the value, round 4)")
+                        "(every 4th group cost 2.2 %% of the value, every 8th 1.1 %%, round 4)")
     p.add_argument("--probe-subbatches", type=int, default=24,
                    help="with --no-kernel-events: sub-batches of the untimed pass that times every kernel")
     p.add_argument("--no-cpu", action="store_true")
