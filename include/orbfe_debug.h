@@ -50,6 +50,9 @@ int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float* d_cos, fl
  * owners recomputed (all summed over its rounds; zeros when the per-round launches ran), then the
  * kernel's wall-clock ticks (100 MHz) in its prologue and in its steps a-d, summed over rounds. */
 int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out8);
+/* The first SearchByProjection round k_sbp_settle runs for this matcher (2 .. 12; 0 restores the
+ * default, round 8): tests drive the settle kernel through most of the fixpoint with 2. */
+int orbfe_debug_matcher_set_settle_from(orbfe_matcher* m, int round0);
 
 #ifdef __cplusplus
 }

@@ -2003,10 +2003,10 @@ static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs&
 // Rounds 0 .. R0-1 grid-wide (round 0 fills the candidate cache and the inverted index; the early
 // rounds change many owners, work one workgroup would take long over), the rest in k_sbp_settle,
 // then collect / finish: R0 + 3 launches whatever the depth of the claim order.
-static int sbp_settle_from() {
+static int sbp_settle_from(const orbfe_matcher* m) {
   static const int r0 = std::getenv("ORBFE_SBP_SETTLE_FROM") ? std::max(2, std::atoi(std::getenv("ORBFE_SBP_SETTLE_FROM")))
                                                              : SBP_SETTLE_FROM;
-  return r0;
+  return m->settle_from >= 2 ? m->settle_from : r0;
 }
 static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
                               const orbfe_frame_view& dF, const SbpMode& md) {
@@ -2016,7 +2016,7 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
   int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
   int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
                      (int32_t*)(A + p.oown3)};
-  const int R0 = sbp_settle_from();
+  const int R0 = sbp_settle_from(m);
   for (int r = 0; r < R0; r++) {
     a.round = r;
     a.res_cur = res[r & 1];
@@ -2321,6 +2321,12 @@ extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
   if (!m || rounds < 1 || rounds > SBP_MAX_ROUNDS) return ORBFE_ERR_ARG;
   m->max_rounds = rounds;
   m->round_cap = rounds;  // a fixed budget: the serial walk past it (tests of the fallback)
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_matcher_set_settle_from(orbfe_matcher* m, int round0) {
+  if (!m || (round0 != 0 && (round0 < 2 || round0 > SBP_MAX_ROUNDS))) return ORBFE_ERR_ARG;
+  m->settle_from = round0;
   return ORBFE_OK;
 }
 

@@ -57,6 +57,7 @@ struct orbfe_matcher {
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
+  int settle_from = 0;            // orbfe_debug_matcher_set_settle_from (0: SBP_SETTLE_FROM)
   // orbfe_matcher_set_profiling: HIP events around the device part (first kernel .. last kernel,
   // no H2D / D2H) of each SearchByProjection-family call
   int profile = 0;

@@ -140,3 +140,36 @@ def test_c5_shape_50k_mappoints(require_gpu):
     # but makes the same matches here
     nnm, nbest, nnv, _ = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8, kind="native")
     assert (nnm, nnv) == (nm, nv) and np.array_equal(nbest, best)
+
+
+@pytest.mark.parametrize("settle_from", [2, 3, 5])
+def test_c5_shape_settle_kernel_through_most_rounds(require_gpu, settle_from):
+    """SearchByProjection's one-workgroup fixpoint (k_sbp_settle) taking over from round 2, 3 or 5
+    instead of 8, so it runs most of the claim order's rounds on the C5 scene (8-23 rounds per
+    search on these frames): the same best_idx as the oracle and as the default schedule, over
+    several frames, and its statistics show it re-evaluated queries."""
+    from orb_slam2_2021_amd import _lib as L
+    ext = ORBextractor(2000, 1.2, 8, 12, 7)
+    k0, d0 = ext(synth_frame(7, 480, 640))
+    rng = np.random.default_rng(0x50C0DE)
+    sc, s2 = ext.GetScaleFactors(), ext.GetScaleSigmaSquares()
+    F0 = S.make_frame(k0, d0, sc, s2, 480, 640, S.ARDUCAM_CAM, rng, mp_frac=0.0, tcw=S.pose(tx=0.1, yaw=0.02))
+    G = S.make_local_map(F0, 50000, rng)
+    m, ref = ORBmatcher(0.8, True), ORBmatcher(0.8, True)
+    L.check(L.lib().orbfe_debug_matcher_set_settle_from(m._h, settle_from), "set_settle_from")
+    reevaluated = 0
+    for seed, tx in ((103, 0.106), (104, 0.112), (105, 0.094)):
+        k, d = ext(synth_frame(seed, 480, 640))
+        F = S.Frame(keys_un=k, descriptors=d, u_right=np.full(len(k), -1.0, np.float32),
+                    mp_state=np.zeros(len(k), np.uint8), scale_factors=sc, level_sigma2=s2, min_x=0.0, max_x=640.0,
+                    min_y=0.0, max_y=480.0, tcw=S.pose(tx=tx, yaw=0.023), **S.ARDUCAM_CAM)
+        nm, best, nv, _ = m.SearchLocalPoints(F, G, 3.0)
+        st = np.zeros(8, np.int32)
+        L.check(L.lib().orbfe_debug_matcher_settle_stats(m._h, L.ptr(st)), "settle_stats")
+        reevaluated += int(st[1])
+        rnm, rbest, rnv, _ = ref.SearchLocalPoints(F, G, 3.0)
+        assert (nm, nv) == (rnm, rnv) and np.array_equal(best, rbest)
+        wnm, wbest, wnv, _ = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8)
+        assert (nm, nv) == (wnm, wnv) and np.array_equal(best, wbest), \
+            f"best_idx differs at {np.flatnonzero(best != wbest)[:5]}"
+    assert reevaluated > 0

@@ -213,6 +213,25 @@ def test_search_by_projection_lastframe_kitti(require_gpu, kitti_seq_frame, mono
     assert nm > 100
 
 
+@pytest.mark.parametrize("check_ori", [False, True])
+def test_search_by_projection_lastframe_settle_from_round_2(require_gpu, kitti_seq_frame, check_ori):
+    """The last-frame search with the one-workgroup fixpoint kernel taking over from round 2 (every
+    round after the first two in k_sbp_settle): the oracle's result, with the rotation filter's
+    undo codes."""
+    from orb_slam2_2021_amd import _lib as L
+    k, d, scale, sigma2 = kitti_seq_frame
+    rng = np.random.default_rng(211)
+    C = S.make_frame(k, d, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, mp_frac=0.0,
+                     tcw=S.pose(tz=-1.0, yaw=0.01))
+    last = S.make_lastframe(C, 1800, rng, None)
+    m = ORBmatcher(0.9, check_ori)
+    L.check(L.lib().orbfe_debug_matcher_set_settle_from(m._h, 2), "set_settle_from")
+    nm, best = m.SearchByProjection(C, last, 15.0, bMono=True)
+    nr, rb = orbref.search_by_projection_lastframe(C, last, 15.0, True, check_ori)
+    assert nm == nr and np.array_equal(best, rb)
+    assert nm > 100
+
+
 @pytest.mark.parametrize("n_last,retried", [(30, True), (1800, False)])
 @pytest.mark.parametrize("mono,th", [(False, 7.0), (True, 15.0)])
 def test_motion_model_retry(require_gpu, kitti_seq_frame, n_last, retried, mono, th):
