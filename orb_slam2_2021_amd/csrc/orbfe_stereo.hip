@@ -57,15 +57,11 @@ struct StereoGeom {
 constexpr int ROWS_THREADS = 256;
 
 // Counting sort of pair p's right keypoints into buckets (octave, floor(y)); bucket entry
-// {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544. Then the
-// same counting sort of the left keypoints into `order` (their indices by (octave, floor(y))):
-// k_stereo_match takes them in that order, so the 16 keypoints of a workgroup read neighbouring
-// rows of the pyramids and the same bucket rows (the extraction order is the octree's).
+// {x bits, (minr & 0xffff) | maxr << 16, octave, iR} with minr/maxr as Frame.cc:543-544.
 __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, const orbfe_keypoint* __restrict__ kps,
                                                               const int32_t* __restrict__ counts,
                                                               int32_t* __restrict__ row_start,
-                                                              uint4* __restrict__ buckets,
-                                                              int32_t* __restrict__ order) {
+                                                              uint4* __restrict__ buckets) {
   extern __shared__ int s_hist[];  // nbk*(rows0+1) counters, then 16 ints of scan scratch
   const int ntab = g.nbk * (g.rows0 + 1);
   int* wsum = s_hist + ntab;
@@ -96,17 +92,6 @@ __global__ __launch_bounds__(ROWS_THREADS) void k_stereo_rows(StereoGeom g, cons
     B[slot] = make_uint4(__float_as_uint(x), ((unsigned)minr & 0xffffu) | ((unsigned)maxr << 16),
                          (unsigned)oct, (unsigned)i);
   }
-  __syncthreads();
-  const int imgL = g.kL0 + p;
-  const int nL = min(counts[imgL], g.cap);
-  const orbfe_keypoint* KL = kps + (long long)imgL * g.cap;
-  for (int r = t; r < ntab; r += ROWS_THREADS) s_hist[r] = 0;
-  __syncthreads();
-  for (int i = t; i < nL; i += ROWS_THREADS) atomicAdd(&s_hist[bucket(KL[i].y, KL[i].octave)], 1);
-  __syncthreads();
-  block_scan_excl(s_hist, ntab, wsum);
-  int32_t* O = order + (long long)p * g.cap;
-  for (int i = t; i < nL; i += ROWS_THREADS) O[atomicAdd(&s_hist[bucket(KL[i].y, KL[i].octave)], 1)] = i;
 }
 
 // ---- median filter ---------------------------------------------------------------------------
@@ -381,19 +366,15 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoGeom g, const orbfe_
                                                       const int32_t* __restrict__ counts,
                                                       const int32_t* __restrict__ row_start,
                                                       const uint4* __restrict__ buckets,
-                                                      const int32_t* __restrict__ order,
                                                       float* __restrict__ u_right, float* __restrict__ depth,
                                                       int32_t* __restrict__ sad_out) {
   const int2 blk = xcd_block2d();
   const int p = blk.y;
   const int j = threadIdx.x & 15;
-  const int e = blk.x * 16 + (threadIdx.x >> 4);  // position in k_stereo_rows' (octave, row) order
+  const int i = blk.x * 16 + (threadIdx.x >> 4);
   const int imgL = g.kL0 + p, imgR = g.kR0 + p;
   const int nL = min(counts[imgL], g.cap);
-  if (e < nL) {
-    const int i = order[(long long)p * g.cap + e];
-    stereo_one(g, kps, desc, row_start, buckets, u_right, depth, sad_out, p, i, j, imgL, imgR);
-  }
+  if (i < nL) stereo_one(g, kps, desc, row_start, buckets, u_right, depth, sad_out, p, i, j, imgL, imgR);
 }
 
 // One block per pair. (A last-block-done tail in k_stereo_match would save this launch, but on
@@ -416,7 +397,6 @@ struct OrbfeStereoScratch {
   size_t row_start_n = 0;
   uint4* d_buckets = nullptr;
   int32_t* d_sad = nullptr;
-  int32_t* d_order = nullptr;  // left keypoints by (octave, row), k_stereo_rows
   size_t slots_n = 0;
   // host-buffer entry points
   orbfe_keypoint* d_kps = nullptr;
@@ -432,7 +412,6 @@ void orbfe_internal_stereo_free(OrbfeStereoScratch* s) {
   if (!s) return;
   hipFree(s->d_row_start);
   hipFree(s->d_buckets);
-  hipFree(s->d_order);
   hipFree(s->d_sad);
   hipFree(s->d_kps);
   hipFree(s->d_desc);
@@ -471,13 +450,10 @@ static int launch_stereo(OrbfeStereoScratch* S, const OrbfePyramid& PL, int pl0,
   if (sl_n > S->slots_n) {
     hipFree(S->d_buckets);
     hipFree(S->d_sad);
-    hipFree(S->d_order);
     S->d_buckets = nullptr;
     S->d_sad = nullptr;
-    S->d_order = nullptr;
     ORBFE_HIP_CHECK(hipMalloc(&S->d_buckets, sl_n * sizeof(uint4)));
     ORBFE_HIP_CHECK(hipMalloc(&S->d_sad, sl_n * sizeof(int32_t)));
-    ORBFE_HIP_CHECK(hipMalloc(&S->d_order, sl_n * sizeof(int32_t)));
     S->slots_n = sl_n;
   }
   StereoGeom g;
@@ -518,10 +494,10 @@ static int launch_stereo(OrbfeStereoScratch* S, const OrbfePyramid& PL, int pl0,
   if (g.nbk == 1) g.rbo[0] = rb_all;
   const size_t lds = sizeof(int) * (g.nbk * (g.rows0 + 1) + 16);
   ORBFE_LAUNCH("k_stereo_rows", k_stereo_rows, dim3(n_pairs), dim3(ROWS_THREADS), lds, s, g, d_kps, d_counts,
-                     S->d_row_start, S->d_buckets, S->d_order);
+                     S->d_row_start, S->d_buckets);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_LAUNCH("k_stereo_match", k_stereo_match, dim3((cap + 15) / 16, n_pairs), dim3(256), 0, s, g, d_kps, d_desc,
-                     d_counts, S->d_row_start, S->d_buckets, S->d_order, d_u_right, d_depth, S->d_sad);
+                     d_counts, S->d_row_start, S->d_buckets, d_u_right, d_depth, S->d_sad);
   ORBFE_HIP_CHECK(hipGetLastError());
   ORBFE_LAUNCH("k_stereo_median", k_stereo_median, dim3(n_pairs), dim3(256), 0, s, kl0, cap, d_counts, S->d_sad,
                      d_u_right, d_depth);
