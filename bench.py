@@ -593,6 +593,9 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        if isinstance(g, Gatherer) and g.rccl is not None:
+            torch.cuda.synchronize()
+            g.rccl.close()
         dist.destroy_process_group()
 
 
