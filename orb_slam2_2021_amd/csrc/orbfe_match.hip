@@ -1982,8 +1982,10 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
 // Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over four:
 // round r claims into own[r % 4], reads own[(r + 3) % 4] (round r-1) and own[(r + 2) % 4]
 // (round r-2), and clears own[(r + 1) % 4] for round r + 1, which nobody reads during round r).
+// `settled`: the settle path ran (the fixpoint is complete on the device, k_sbp_settle ran the
+// serial walk itself if it had to), so without a rotation filter k_sbp_finish has nothing to do.
 static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs& a, const SbpMode& md,
-                              int32_t* const res_final[2], bool defer) {
+                              int32_t* const res_final[2], bool defer, bool settled = false) {
   uint8_t* A = m->arena;
   SbpFinishArgs f;
   std::memset(&f, 0, sizeof(f));
@@ -1996,8 +1998,10 @@ static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs&
   f.q_angle = (const float*)(A + p.oqa);
   f.serial_used = m->d_serial;
   f.defer = defer ? 1 : 0;
-  ORBFE_LAUNCH("k_sbp_collect", k_sbp_collect, dim3((p.nq + 255) / 256), dim3(256), 0, m->stream, f);
-  ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
+  if (!md.check_ori)  // (k_sbp_collect returns at once with the rotation filter)
+    ORBFE_LAUNCH("k_sbp_collect", k_sbp_collect, dim3((p.nq + 255) / 256), dim3(256), 0, m->stream, f);
+  if (md.check_ori || !settled)
+    ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
 }
 
 // Rounds 0 .. R0-1 grid-wide (round 0 fills the candidate cache and the inverted index; the early
@@ -2053,7 +2057,7 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
     attr_set = true;
   }
   ORBFE_LAUNCH("k_sbp_settle", k_sbp_settle, dim3(1), dim3(SETTLE_THREADS), lds, m->stream, a, st);
-  sbp_finish_launch(m, p, a, md, res, false);
+  sbp_finish_launch(m, p, a, md, res, false, true);
 }
 
 static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
