@@ -809,154 +809,6 @@ __global__ __launch_bounds__(256) void k_sbp_round(SbpArgs a) {
   if (wave_ballot(changed) && lane_id() == 0) a.state[2 + a.round] = 1;
 }
 
-// ---- the fixpoint's rounds in one launch (grid barriers) -----------------------------------------
-// k_sbp_round's work for rounds r0 .. r1-1 in one launch of G workgroups that all stay resident
-// (G = half the CUs: they fit beside any other kernels once those finish), separated by a grid
-// barrier instead of a kernel boundary. The per-XCD L2s are not coherent with each other, so
-// every access another workgroup's round can read -- the claim owners, their clearing, the
-// round flags, the barrier counter -- is an agent-scope atomic (performed or re-read at the
-// device's coherence point; no cache write-back or invalidate), and each wavefront waits for its
-// memory operations (s_waitcnt) before the workgroup arrives. The results are read only by the
-// thread that owns the query until the kernel ends. A barrier that waits too long (a workgroup
-// that never arrived) marks the fixpoint unsettled, and k_sbp_finish runs the reference's
-// sequential walk instead: a timeout costs time, never a wrong match.
-__device__ __forceinline__ int ld_ag(const int32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_ag(int32_t* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct SbpPersistArgs {
-  int32_t* res[2];
-  int32_t* own[4];
-  int32_t* bar;    // arrivals (zeroed by k_sbp_init)
-  int32_t* fault;  // a barrier timed out
-  int r0, r1;
-};
-#define SBP_PERSIST_SPIN (1 << 18)  // barrier polls (about 1 us each) before giving up
-
-__global__ __launch_bounds__(256) void k_sbp_persist(SbpArgs a, SbpPersistArgs pa) {
-  __shared__ SbpChange s_chg[SBP_CHG_MAX];
-  __shared__ int s_nchg, s_stop;
-  // round r-1's owners (read by every candidate test) and round r-2's, fetched once per round from
-  // the coherence point into LDS; the two arrays swap roles each round
-  extern __shared__ int s_own[];
-  int* lds_prev = s_own;
-  int* lds_rm2 = s_own + a.F.n;
-  const int t = threadIdx.x, G = gridDim.x, stride = G * 256, gid = blockIdx.x * 256 + t;
-  int arrived = 0;
-  int r = pa.r0;
-  for (; r < pa.r1; r++) {
-    // round r-1 reproduced round r-2 (every workgroup reads the same flags after the barrier)
-    if (t == 0) s_stop = (r > 1 && ld_ag(&a.state[2 + r - 1]) == 0) || ld_ag(pa.fault) != 0;
-    __syncthreads();
-    if (s_stop) break;
-    if (blockIdx.x == 0 && t == 0) st_ag(&a.state[1], r + 1);
-    int32_t* own_cur = pa.own[r % 4];
-    const int32_t* own_prev = pa.own[(r + 3) % 4];
-    int32_t* own_next = pa.own[(r + 1) % 4];
-    const int32_t* own_rm2 = r >= 2 && a.cand_n ? pa.own[(r + 2) % 4] : nullptr;
-    int32_t* res_cur = pa.res[r & 1];
-    const int32_t* res_prev = pa.res[(r + 1) & 1];
-    {  // this round's owner snapshot (round r-1); round r-2's is last round's snapshot
-      int* tmp = lds_rm2;
-      lds_rm2 = lds_prev;
-      lds_prev = tmp;
-      constexpr int U = 8;  // loads in flight per thread
-      for (int k0 = 0; k0 < a.F.n; k0 += 256 * U) {
-        int v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int k = k0 + t + 256 * u;
-          v[u] = k < a.F.n ? ld_ag(own_prev + k) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int k = k0 + t + 256 * u;
-          if (k < a.F.n) lds_prev[k] = v[u];
-        }
-      }
-      if (t == 0) s_nchg = 0;
-      __syncthreads();
-    }
-    int nchg = SBP_CHG_MAX + 1;
-    if (own_rm2) {  // the keypoints whose owner changed between rounds r-2 and r-1 (k_sbp_round)
-      for (int k = t; k < a.F.n; k += 256) {
-        const int o1 = lds_rm2[k], o2 = lds_prev[k];
-        if (o1 != o2) {
-          const int slot = atomicAdd(&s_nchg, 1);
-          if (slot < SBP_CHG_MAX) {
-            SbpChange c;
-            c.x = a.F.keys_un[k].x;
-            c.y = a.F.keys_un[k].y;
-            c.lo = min(o1, o2);
-            c.hi = max(o1, o2);
-            s_chg[slot] = c;
-          }
-        }
-      }
-      __syncthreads();
-      nchg = s_nchg;
-    }
-    const bool sparse = nchg <= SBP_CHG_MAX;
-    for (int k = gid; k < a.F.n; k += stride) st_ag(own_next + k, 0x7fffffff);
-    bool changed = false;
-    for (int i = gid; i < a.m; i += stride) {
-      bool need = true;
-      if (sparse) {
-        const float qx = a.q[i].x, qy = a.q[i].y, qr = a.q[i].r;
-        need = false;
-        for (int c = 0; c < nchg && !need; c++) {
-          const SbpChange e = s_chg[c];
-          need = e.lo < i && i <= e.hi && fabsf(e.x - qx) < qr && fabsf(e.y - qy) < qr;
-        }
-      }
-      const int prev_res = res_prev[i];
-      auto blocked = [&](int k) { return sbp_pre_blocked(a, k) || lds_prev[k] < i; };
-      int res;
-      if (!need) {
-        res = prev_res;
-      } else if (!a.cand_n) {
-        res = sbp_one(a, i, blocked);
-      } else {
-        const int n = a.cand_n[i];
-        res = n >= 0 ? sbp_cached(a, i, n, blocked) : sbp_one(a, i, blocked);
-      }
-      res_cur[i] = res;
-      if (res >= 0 && (a.q[i].flags & 2))
-        __hip_atomic_fetch_min(own_cur + res, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      changed = changed || res != prev_res;
-    }
-    if (wave_ballot(changed) && lane_id() == 0) st_ag(&a.state[2 + r], 1);
-    // grid barrier: this wavefront's claims, clears and flags are performed before it arrives
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    arrived += G;
-    if (t == 0) {
-      __hip_atomic_fetch_add(pa.bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int spins = 0;
-      while (ld_ag(pa.bar) < arrived) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > SBP_PERSIST_SPIN) {
-          st_ag(pa.fault, 1);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (blockIdx.x == 0 && t == 0) {
-    if (ld_ag(pa.fault) != 0) {  // unsettled: k_sbp_finish walks the claim order sequentially
-      st_ag(&a.state[0], 0);
-      st_ag(&a.state[1], pa.r1);
-      st_ag(&a.state[2 + pa.r1 - 1], 1);
-    } else if (r < pa.r1) {
-      st_ag(&a.state[0], 1);  // settled
-    }
-  }
-}
-
 // Round 0 with the candidate cache, 16 lanes (one DPP row) per MapPoint. The window's grid cells
 // are taken 16 at a time in GetFeaturesInArea order (ix outer, iy inner, Frame.cc:394-430), one
 // cell per lane: a counting pass and a 16-lane scan place each lane's candidates in that order in
@@ -2209,7 +2061,7 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
 }
 
 static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
-                       const SbpMode& md, int r0, int r1, bool defer, bool finish = true) {
+                       const SbpMode& md, int r0, int r1, bool defer) {
   uint8_t* A = m->arena;
   const int nq = p.nq;
   SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
@@ -2232,39 +2084,7 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
     else
       ORBFE_LAUNCH("k_sbp_round", k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
   }
-  if (nq > 0 && finish) sbp_finish_launch(m, p, a, md, res, defer);
-}
-
-// ORBFE_SBP_PERSIST=1: rounds 1.. in one launch with grid barriers (k_sbp_persist)
-static bool sbp_persist_enabled() {
-  static const bool on = std::getenv("ORBFE_SBP_PERSIST") && std::atoi(std::getenv("ORBFE_SBP_PERSIST")) != 0;
-  return on;
-}
-
-static void sbp_persist_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
-                               const orbfe_frame_view& dF, const SbpMode& md) {
-  uint8_t* A = m->arena;
-  int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
-  int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
-                     (int32_t*)(A + p.oown3)};
-  sbp_rounds(m, p, F, dF, md, 0, 1, false, false);  // round 0: candidate cache, first results
-  SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
-  SbpPersistArgs pa;
-  for (int k = 0; k < 2; k++) pa.res[k] = res[k];
-  for (int k = 0; k < 4; k++) pa.own[k] = own[k];
-  pa.bar = m->d_serial + 12;
-  pa.fault = m->d_serial + 13;
-  pa.r0 = 1;
-  pa.r1 = std::min(m->round_cap, SBP_ROUND_CAP);
-  static int cus = 0;
-  if (!cus) {
-    hipDeviceProp_t prop;
-    cus = hipGetDeviceProperties(&prop, m->device) == hipSuccess ? prop.multiProcessorCount : 64;
-  }
-  const int G = std::max(1, std::min(cus / 2, (std::max(p.nq, F->n) + 255) / 256));
-  ORBFE_LAUNCH("k_sbp_persist", k_sbp_persist, dim3(G), dim3(256), 2 * sizeof(int) * std::max(F->n, 1), m->stream,
-               a, pa);
-  sbp_finish_launch(m, p, a, md, res, false);
+  if (nq > 0) sbp_finish_launch(m, p, a, md, res, defer);
 }
 
 // ORBFE_SBP_SETTLE=0: the fixpoint as one launch per round (rounds 1-3's engine, for A/B)
@@ -2278,13 +2098,9 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   sbp_launch_grid(m, p, F, dF);
   // the settle path unless rounds are restricted (orbfe_matcher_set_max_rounds: the serial
   // fallback's tests) or no assignment blocks anything (one round is the result)
-  const bool persist = !md.no_claims && p.cache && p.nq > 0 && F->n <= SETTLE_MAX_KEYS &&
-                       m->round_cap >= SBP_MAX_ROUNDS && sbp_persist_enabled();
-  const bool settle = !persist && p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
+  const bool settle = p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
   sbp_launch_init(m, p, F, settle);
-  if (persist) {
-    sbp_persist_rounds(m, p, F, dF, md);
-  } else if (settle) {
+  if (settle) {
     sbp_settle_rounds(m, p, F, dF, md);
   } else {
     const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
