@@ -29,7 +29,6 @@ events on two streams.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import numpy as np
@@ -126,17 +125,16 @@ class PipelineStreams:
         # and the other placements measured slower: DESIGN.md section 5); match_inline: each
         # sub-batch's vocabulary + matching follow its extraction on the same stream instead
         self.match = None
-        mhigh = os.environ.get("ORBFE_MATCH_PRIO", "high") == "high"
         if not match_inline and side_last:
-            self.match = make(mhigh)
+            self.match = make(True)
         self.side = make(True)
         if not match_inline and not side_last:
-            self.match = make(mhigh)
+            self.match = make(True)
         # comm: a stream for the C4 gather's transfers, created here with the others so that it gets
         # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
         # that stream's kernels: measured 83k -> 52k stereo frames/s on one GPU (--gather-proxy)
-        self.comm = (make(os.environ.get("ORBFE_COMM_PRIO", "normal") == "high") if comm else None)
+        self.comm = make(False) if comm else None
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
