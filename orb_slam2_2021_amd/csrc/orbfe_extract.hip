@@ -1730,11 +1730,8 @@ __global__ __launch_bounds__(256) void k_blur(ExtractArgs a) {
 // k_describe: one wavefront per surviving keypoint. IC_Angle (:75-102) sums the integer moments of
 // the 749-pixel circle straight from the level (L1/L2 hits); the 256 steered tests (:105-151) read
 // the blurred level; bits land as 4 wave ballots (64 pairs each = 8 descriptor bytes).
-// k_describe tables: the 256 test pairs as floats (x0, y0, x1, y1), and for each alignment
-// s = (cx - 15) & 3 the byte masks of the 31 x 9 dwords of the IC_Angle window that keep the
-// circle |u| <= umax[|v|] (ORBextractor.cc:82-98)
+// k_describe's table: the 256 test pairs as floats (x0, y0, x1, y1)
 __constant__ float4 c_patf[256];
-__constant__ uint32_t c_momask[4][31][9];
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -1799,20 +1796,23 @@ __global__ __launch_bounds__(256) void k_steer_trig(uint32_t bits0, uint32_t n, 
 // Four keypoints per wavefront, 16 lanes each, so the per-keypoint scalar work (level lookup,
 // fastAtan2, the cos/sin of computeOrbDescriptor) is shared by 4 keypoints. A wavefront issues all
 // of its global loads before their first use (the IC_Angle window as 12-byte pieces, the blurred
-// window as 8-byte pieces); the test pattern and the circle masks are copied to LDS once per
-// block, so the moments and the 256 tests read no global memory.
+// window as 8-byte pieces); the test pattern is copied to LDS once per block and the circle masks
+// are computed, so the moments and the 256 tests read no global memory.
 struct DwX3 {
   uint32_t x, y, z;
 };
 
 constexpr int DESC_WPB = 4;  // k_describe wavefronts per workgroup (4 keypoints each)
 constexpr int DESC_THREADS = 64 * DESC_WPB;
+// umax[0..15] (ORBextractor.cc:82-98; each <= 15) as 4-bit fields of two dwords: IC_Angle's
+// circle masks are computed per dword, not looked up (a 4.4 KiB mask table in LDS left k_describe
+// at 32 KiB per workgroup, two beside a DistributeOctTree block; 27 KiB without it: 84.0k vs
+// 82.8k)
+__constant__ uint32_t c_umax4[2];
 __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
   __shared__ float4 s_pat[256];
-  __shared__ uint32_t s_mom[4 * 279];
   __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * DESC_WPB][37 * 10];
   for (int k = threadIdx.x; k < 256; k += DESC_THREADS) s_pat[k] = c_patf[k];
-  for (int k = threadIdx.x; k < 4 * 279; k += DESC_THREADS) s_mom[k] = (&c_momask[0][0][0])[k];
   __syncthreads();  // before any wavefront may leave
   const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
@@ -1871,19 +1871,25 @@ __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
     bw[k] = make_uint2(0u, 0u);
     if (l16 + 16 * k < 185) __builtin_memcpy(&bw[k], bsrc + (k / 5) * step16 + br[k % 5] * pitch + 8 * bc[k % 5], 8);
   }
-  // 2. IC_Angle moments (:75-102) over the 749-pixel circle: bytes with |u| <= umax[|v|] (masks in
-  //    LDS), sums of I and col * I by byte dot products
-  const uint32_t* mt = s_mom + ((cx - 15) & 3) * 279;
+  // 2. IC_Angle moments (:75-102) over the 749-pixel circle: bytes with |u| <= umax[|v|] (a byte
+  //    mask per dword from umax), sums of I and col * I by byte dot products
+  const int msh = (cx - 15) & 3;
+  const uint32_t um_lo = c_umax4[0], um_hi = c_umax4[1];
   int m01 = 0, m10 = 0;
 #pragma unroll
   for (int k = 0; k < 6; k++) {
     if (l16 + 16 * k < 93) {
       const int r = ur[k % 3] + 16 * (k / 3), v = r - 15;
       const uint32_t d3[3] = {mu[k].x, mu[k].y, mu[k].z};
+      const int av = v < 0 ? -v : v;
+      const int um = (int)(((av < 8 ? um_lo : um_hi) >> (4 * (av & 7))) & 15u);
 #pragma unroll
       for (int d = 0; d < 3; d++) {
         const int c = 3 * uc[k % 3] + d;  // dword of the row
-        const uint32_t px = d3[d] & mt[r * 9 + c];
+        // bytes b of dword c with |u| <= um, u = -15 - msh + 4 c + b
+        const int blo = min(max(15 + msh - 4 * c - um, 0), 4), bhi = min(max(16 + msh - 4 * c + um, 0), 4);
+        const uint32_t msk = blo < bhi ? (uint32_t)((((1ull << (8 * (bhi - blo))) - 1ull)) << (8 * blo)) : 0u;
+        const uint32_t px = d3[d] & msk;
         const int sI = (int)__builtin_amdgcn_udot4(px, 0x01010101u, 0u, false);
         const int sC = (int)__builtin_amdgcn_udot4(px, (uint32_t)(4 * c) * 0x01010101u + 0x03020100u, 0u, false);
         m10 += sC + (xa - cx) * sI;  // sum u I with u = xa + col - cx
@@ -2624,22 +2630,13 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
     float patf[1024];
     for (int i = 0; i < 1024; i++) patf[i] = (float)kOrbPattern31[i];
     if (pat_err == hipSuccess) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_patf), patf, sizeof(patf));
-    // IC_Angle circle masks: window dword c of row v covers u = -15 - s + 4c .. +3
-    uint32_t masks[4][31][9];
+    // IC_Angle's circle |u| <= umax[|v|], v = -15..15: 749 pixels (the kernel builds each window
+    // dword's byte mask from these 4-bit fields)
+    uint32_t um4[2] = {0u, 0u};
     int npx = 0;
-    for (int sh = 0; sh < 4; sh++)
-      for (int r = 0; r < 31; r++)
-        for (int c = 0; c < 9; c++) {
-          const int um = h->umax[std::abs(r - 15)];
-          uint32_t m = 0;
-          for (int b = 0; b < 4; b++) {
-            const int u = -15 - sh + 4 * c + b;
-            if (u >= -um && u <= um) m |= 0xffu << (8 * b);
-          }
-          masks[sh][r][c] = m;
-          if (sh == 0) npx += __builtin_popcount(m) / 8;
-        }
-    if (pat_err == hipSuccess && npx == 749) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_momask), masks, sizeof(masks));
+    for (int v = -15; v <= 15; v++) npx += 2 * h->umax[std::abs(v)] + 1;
+    for (int v = 0; v < 16; v++) um4[v >> 3] |= (uint32_t)h->umax[v] << (4 * (v & 7));
+    if (pat_err == hipSuccess && npx == 749) pat_err = hipMemcpyToSymbol(HIP_SYMBOL(c_umax4), um4, sizeof(um4));
     else if (pat_err == hipSuccess) pat_err = hipErrorInvalidValue;
   });
   if (pat_err != hipSuccess) {
