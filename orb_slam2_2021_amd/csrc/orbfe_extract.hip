@@ -1810,26 +1810,9 @@ constexpr int DESC_THREADS = 64 * DESC_WPB;
 // 82.8k)
 __constant__ uint32_t c_umax4[2];
 __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
-#ifndef ORBFE_DESC_H16
-#define ORBFE_DESC_H16 0
-#endif
-#if ORBFE_DESC_H16
-  typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
-  __shared__ h16x4 s_pat[256];  // small integers: exact in fp16
-  for (int k = threadIdx.x; k < 256; k += DESC_THREADS) {
-    const float4 f = c_patf[k];
-    s_pat[k] = (h16x4){(_Float16)f.x, (_Float16)f.y, (_Float16)f.z, (_Float16)f.w};
-  }
-  auto pat = [&](int p) {
-    const h16x4 h = s_pat[p];
-    return make_float4((float)h.x, (float)h.y, (float)h.z, (float)h.w);
-  };
-#else
   __shared__ float4 s_pat[256];
-  for (int k = threadIdx.x; k < 256; k += DESC_THREADS) s_pat[k] = c_patf[k];
-  auto pat = [&](int p) { return s_pat[p]; };
-#endif
   __shared__ __attribute__((aligned(16))) uint32_t s_win[4 * DESC_WPB][37 * 10];
+  for (int k = threadIdx.x; k < 256; k += DESC_THREADS) s_pat[k] = c_patf[k];
   __syncthreads();  // before any wavefront may leave
   const int w = wave_id(), lane = lane_id(), grp = lane >> 4, l16 = lane & 15;
   const int2 blk = xcd_block2d();
@@ -1937,7 +1920,7 @@ __global__ __launch_bounds__(DESC_THREADS) void k_describe(ExtractArgs a) {
     // row = cvRound(x sin + y cos), col = cvRound(x cos - y sin) (:115-117): the products and the
     // sum in packed fp32 (separately rounded, as the reference), cvRound's half-even by adding
     // 1.5 * 2^23 and reading the integer out of the mantissa
-    const float4 P = pat(p);
+    const float4 P = s_pat[p];
     const f32x2 sc = {sb, ca}, cs = {ca, -sb}, magic = {12582912.0f, 12582912.0f};
     const f32x2 q0 = (f32x2){P.x, P.x} * sc + (f32x2){P.y, P.y} * cs + magic;
     const f32x2 q1 = (f32x2){P.z, P.z} * sc + (f32x2){P.w, P.w} * cs + magic;
