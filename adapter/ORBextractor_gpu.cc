@@ -7,6 +7,13 @@
 //
 // Built only inside the reference's tree, where OpenCV and the reference headers exist
 // (INTEGRATION.md section 4); anywhere else this translation unit is empty.
+//
+// ORBFE_ADAPTER_GPU_STEREO=1 (set when Frame_gpu.cc replaces Frame::ComputeStereoMatches): the
+// public mvImagePyramid is left empty and no pyramid leaves the GPU. 0 (default): the CPU
+// ComputeStereoMatches reads host copies of the levels.
+#ifndef ORBFE_ADAPTER_GPU_STEREO
+#define ORBFE_ADAPTER_GPU_STEREO 0
+#endif
 #if __has_include(<opencv2/core.hpp>) && __has_include("ORBextractor.h")
 
 #include <cassert>
@@ -47,6 +54,11 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   mvInvLevelSigma2 = g->GetInverseScaleSigmaSquares();
   mnFeaturesPerLevel.assign(g->FeaturesPerLevel().begin(), g->FeaturesPerLevel().end());
   mvImagePyramid.resize(nlevels);
+#if !ORBFE_ADAPTER_GPU_STEREO
+  // the CPU Frame::ComputeStereoMatches reads mvImagePyramid after every call: the library copies
+  // each pyramid down beside the rest of the extraction, so operator() pays no extra copy or wait
+  g->SetHostPyramid(true);
+#endif
   std::lock_guard<std::mutex> lk(g_mu);
   handles()[this] = std::move(g);
 }
@@ -58,26 +70,37 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask: ign
   cv::Mat image = _image.getMat();
   assert(image.type() == CV_8UC1);  // :1048
   orbfe::Extractor& g = gpu_of(this);
-  std::vector<orbfe::KeyPoint> kps;
-  std::vector<uint8_t> desc;
-  g(image.data, image.rows, image.cols, image.step, kps, desc);
-  _keypoints.clear();
-  _keypoints.reserve(kps.size());
-  for (const orbfe::KeyPoint& k : kps)  // cv::KeyPoint(x, y, size, angle, response, octave, class_id)
-    _keypoints.emplace_back(k.x, k.y, k.size, k.angle, k.response, k.octave, k.class_id);
-  if (kps.empty()) {
+  // cv::KeyPoint is orbfe_keypoint's layout (pt.x, pt.y, size, angle, response, octave, class_id):
+  // the keypoints land in the caller's vector directly
+  static_assert(sizeof(cv::KeyPoint) == sizeof(orbfe_keypoint), "cv::KeyPoint is 28 bytes");
+  const int cap = orbfe::check(orbfe_max_keypoints(g.handle(), image.rows, image.cols), "orbfe_max_keypoints");
+  thread_local std::vector<uint8_t> desc;  // one operator() per thread at a time (Frame.cc:113-116)
+  desc.resize((size_t)cap * 32);
+  _keypoints.resize(cap);
+  int n = 0;
+  orbfe::check(orbfe_extract(g.handle(), image.data, image.rows, image.cols, image.step,
+                             reinterpret_cast<orbfe_keypoint*>(_keypoints.data()), cap, desc.data(), &n),
+               "orbfe_extract");
+  _keypoints.resize(n);
+  if (n == 0) {
     _descriptors.release();  // :1062-1063
   } else {
-    _descriptors.create((int)kps.size(), 32, CV_8U);
-    std::memcpy(_descriptors.getMat().data, desc.data(), desc.size());
+    _descriptors.create(n, 32, CV_8U);
+    std::memcpy(_descriptors.getMat().data, desc.data(), (size_t)n * 32);
   }
-  // the public mvImagePyramid (ORBextractor.h:100): headers over the handle's host copies of the
-  // levels, valid until the next call (Frame::ComputeStereoMatches reads them right after; the GPU
-  // build's Frame_gpu.cc reads the device pyramids instead and never touches these)
+#if !ORBFE_ADAPTER_GPU_STEREO
+  // the public mvImagePyramid (ORBextractor.h:100): headers over the handle's host copy of this
+  // call's pyramid (every level at once, prefetched during the extraction), valid until the next
+  // call, as the reference's own levels are; Frame::ComputeStereoMatches reads them right after
   for (int l = 0; l < nlevels; l++) {
     const orbfe::LevelView v = g.level(l);
     mvImagePyramid[l] = cv::Mat(v.rows, v.cols, CV_8UC1, const_cast<uint8_t*>(v.data), v.step);
   }
+#else
+  // a build with Frame_gpu.cc reads the device pyramids (orbfe_compute_stereo_matches); nothing
+  // else in the reference reads mvImagePyramid (Frame.cc:529,620-640 are its only readers), so
+  // no level is copied to the host
+#endif
 }
 
 }  // namespace ORB_SLAM2

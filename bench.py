@@ -118,18 +118,21 @@ def parse(argv=None):
                    help="--gather-proxy: the packed payloads of K sub-batches per RCCL group")
     p.add_argument("--gather-proxy", type=int, default=0,
                    help="one-GPU proxy of C4's rank-0 ingestion at N GPUs: after each sub-batch's pack, "
-                        "N-1 device-to-device copies of the packed worst-case payload on a stream of their "
-                        "own (where RCCL's receives run), with N > 1's hardware-queue setting (DESIGN.md section 7)")
+                        "N-1 RCCL self send / receive pairs of the packed worst-case payload (a world-1 "
+                        "communicator) as one group on the matching stream, where Gatherer's transfers run, "
+                        "with N > 1's hardware-queue setting (DESIGN.md section 7)")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
     return p.parse_args(argv)
 
 
-# N > 1: four busy pipeline streams plus RCCL's stream. With the HIP default of 4 hardware queues
-# the fifth busy stream shares a queue with one of the others, and a receive kernel waiting for its
-# peer then holds that queue (five busy streams on 4 queues measured 54.9k vs 78.9k stereo frames/s
-# in round 2); 8 queues with two extraction streams measured the same as 4 at N = 1 (81.0k both)
+# N > 1: the C4 transfers run on the matching stream (Gatherer), but RCCL's own internal streams
+# and torch.distributed's collective stream (the barrier / all-reduce around the timed region, the
+# ORBFE_GATHER=torch path) come on top of the four busy pipeline streams. With the HIP default of 4
+# hardware queues an extra busy stream shares a queue with a pipeline stream, and a receive kernel
+# waiting for its peer then holds that queue (five busy streams on 4 queues measured 54.9k vs 78.9k
+# stereo frames/s in round 2); 8 queues with two extraction streams measured the same as 4 at N = 1
 HW_QUEUES_MULTI_RANK = 8
 
 def hw_queue_setting(requested: int, world: int) -> int:

@@ -107,11 +107,21 @@ int orbfe_extract_batch_device(orbfe_extractor* h, int n_images, const uint8_t* 
                                orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
                                int32_t* d_counts, void* stream);
 
-/* Lazy D2H of pyramid level `level` of image `image` of the last extract call (mvImagePyramid,
- * read by Frame::ComputeStereoMatches, Frame.cc:529,620-640). *p stays valid until the next
- * extract call on this handle. */
+/* Host view of pyramid level `level` of image `image` of the last extract call (mvImagePyramid,
+ * read by Frame::ComputeStereoMatches, Frame.cc:529,620-640). The handle keeps one host copy per
+ * image holding all its levels (rows `*step` bytes apart): the first access to an image copies
+ * its whole pyramid in one DMA, unless the handle prefetched it (orbfe_extractor_set_host_pyramid).
+ * Every level of every image of the call stays valid at once, until the next extract call on
+ * this handle, as the reference's mvImagePyramid[0..nlevels-1] do. */
 int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p, int* rows,
                     int* cols, size_t* step);
+
+/* enable != 0: every later host-buffer extract call (orbfe_extract, orbfe_extract_batch) also
+ * copies each image's pyramid to the handle's host block as soon as it is built, on a copy stream
+ * beside the rest of the extraction, so orbfe_get_level returns without a copy. For callers that
+ * read mvImagePyramid on the CPU after every call (the reference's Frame::ComputeStereoMatches).
+ * Off by default: a GPU ComputeStereoMatches (orbfe_stereo.h) reads the device pyramids. */
+int orbfe_extractor_set_host_pyramid(orbfe_extractor* h, int enable);
 
 /* Device pointer of the same level (no copy), for device-side consumers. */
 int orbfe_get_level_device(orbfe_extractor* h, int image, int level, const uint8_t** d_p,

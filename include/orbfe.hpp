@@ -93,12 +93,16 @@ class Extractor {
     descriptors.resize((size_t)n * ORBFE_DESC_BYTES);
   }
 
-  // mvImagePyramid[level] of the last call (ORBextractor.h:100), host copy on first access.
+  // mvImagePyramid[level] of the last call (ORBextractor.h:100): a view of the handle's host copy
+  // of that image's pyramid (one DMA on the first access to the image, none when prefetched);
+  // every level's view stays valid until the next call.
   LevelView level(int level, int image = 0) {
     LevelView v;
     check(orbfe_get_level(h_, image, level, &v.data, &v.rows, &v.cols, &v.step), "orbfe_get_level");
     return v;
   }
+  // Copy each call's pyramid to the host beside the extraction (orbfe_extractor_set_host_pyramid).
+  void SetHostPyramid(bool on) { check(orbfe_extractor_set_host_pyramid(h_, on ? 1 : 0), "set_host_pyramid"); }
 
   // getters (ORBextractor.h:70-98)
   int GetLevels() const { return nlevels_; }

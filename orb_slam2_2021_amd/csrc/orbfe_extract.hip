@@ -2107,7 +2107,18 @@ struct orbfe_extractor {
   const uint8_t* last_img0 = nullptr;
   long long last_img_stride = 0;
   int last_img_pitch = 0, last_n = 0;
-  std::vector<uint8_t> level_host;
+  hipStream_t last_stream = nullptr;  // the stream the last call's pyramids were built on
+  // mvImagePyramid on the host (orbfe_get_level): one pinned block holding every image of the last
+  // call at the device layout (levels packed, rows `pitch` apart), so all levels of all images stay
+  // valid together until the next extract call. An image is copied on its first access, or during
+  // the extraction itself when the handle prefetches (orbfe_extractor_set_host_pyramid).
+  unsigned long long gen = 0;            // extract calls so far (the block's validity)
+  uint8_t* h_pyr = nullptr;
+  size_t h_pyr_bytes = 0;
+  std::vector<unsigned long long> h_pyr_gen;  // per image: the call whose pyramid the block holds
+  int host_pyramid = 0;                  // prefetch the pyramids to h_pyr in the host-buffer calls
+  hipEvent_t ev_hpyr = nullptr;          // the prefetch copies are done
+  bool hpyr_pending = false;
   // Frame::ComputeStereoMatches scratch (orbfe_stereo.hip)
   OrbfeStereoScratch* stereo = nullptr;
 };
@@ -2549,6 +2560,28 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   h->last_img_stride = img_stride;
   h->last_img_pitch = pitch;
   h->last_n = i0 + n;
+  h->last_stream = st;
+  return ORBFE_OK;
+}
+
+// The host block of orbfe_get_level, sized for n images of the current geometry. Called once per
+// extract call before any image of that call is copied into it, so a reallocation never moves a
+// level the caller still holds from the same call.
+static int ensure_host_pyramid(orbfe_extractor* h, int n) {
+  const size_t need = (size_t)h->pyr_stride * n;
+  if (need > h->h_pyr_bytes) {
+    if (h->hpyr_pending) {
+      ORBFE_HIP_CHECK(hipEventSynchronize(h->ev_hpyr));
+      h->hpyr_pending = false;
+    }
+    if (h->h_pyr) hipHostFree(h->h_pyr);
+    h->h_pyr = nullptr;
+    h->h_pyr_bytes = 0;
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_pyr, need, hipHostMallocDefault));
+    h->h_pyr_bytes = need;
+  }
+  if ((int)h->h_pyr_gen.size() < n) h->h_pyr_gen.resize(n, 0);
+  if (!h->ev_hpyr) ORBFE_HIP_CHECK(hipEventCreateWithFlags(&h->ev_hpyr, hipEventDisableTiming));
   return ORBFE_OK;
 }
 
@@ -2668,6 +2701,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (h->h_out) hipHostFree(h->h_out);
   if (h->h2d) hipStreamSynchronize(h->h2d);
   if (h->d2h) hipStreamSynchronize(h->d2h);
+  if (h->h_pyr) hipHostFree(h->h_pyr);
+  if (h->ev_hpyr) hipEventDestroy(h->ev_hpyr);
   delete h->pool;
   for (auto e : h->ev_in) hipEventDestroy(e);
   for (auto e : h->ev_ext) hipEventDestroy(e);
@@ -2765,7 +2800,13 @@ extern "C" int orbfe_event_record(void* event, void* stream) {
 extern "C" int orbfe_event_query(void* event) {
   if (!event) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_event_query: null event");
   const hipError_t e = hipEventQuery((hipEvent_t)event);
-  if (e == hipErrorNotReady) return 1;
+  if (e == hipErrorNotReady) {
+    // a runtime that records NotReady as the thread's last error would fail the next
+    // hipGetLastError check (a matcher's pending_err, ORBFE_HIP_CHECK) on this thread; an
+    // earlier, real error stays recorded
+    if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+    return 1;
+  }
   ORBFE_HIP_CHECK(e);
   return 0;
 }
@@ -2796,6 +2837,7 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
   st = ensure_batch(h, n);
   if (st != ORBFE_OK) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+  h->gen++;  // the host pyramid block of the previous call is stale from here on
   return launch_extract(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
                         d_counts, s);
 }
@@ -2939,6 +2981,11 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
   const int nchunks = ngroups * cpg, npieces = small ? 1 : 2 * ngroups;
   st = ensure_pipeline(h, std::max(nchunks, npieces));
   if (st != ORBFE_OK) return st;
+  h->gen++;
+  if (h->host_pyramid) {
+    st = ensure_host_pyramid(h, n);
+    if (st != ORBFE_OK) return st;
+  }
   const hipStream_t s_in = small ? h->stream : h->h2d, s_out = small ? h->stream : h->d2h;
   const int K = h->total_key_slots;
   const size_t img_bytes = (size_t)rows * cols;
@@ -2989,6 +3036,16 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
     st = launch_extract(h, ng, h->d_in + (size_t)g0 * img_bytes, (long long)img_bytes, cols, h->d_kps + (size_t)g0 * K,
                         h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0, h->stream, g0);
     if (st != ORBFE_OK) return st;
+    if (h->host_pyramid) {
+      // mvImagePyramid for a CPU Frame::ComputeStereoMatches: the group's pyramids go down on the
+      // second copy stream as soon as they are built, beside FAST / DistributeOctTree / describe
+      ORBFE_HIP_CHECK(hipStreamWaitEvent(h->d2h, h->ev_pyr, 0));
+      ORBFE_HIP_CHECK(hipMemcpyAsync(h->h_pyr + (size_t)g0 * h->pyr_stride, h->d_pyr + (size_t)g0 * h->pyr_stride,
+                                     (size_t)ng * h->pyr_stride, hipMemcpyDeviceToHost, h->d2h));
+      for (int i = g0; i < g0 + ng; i++) h->h_pyr_gen[i] = h->gen;
+      ORBFE_HIP_CHECK(hipEventRecord(h->ev_hpyr, h->d2h));
+      h->hpyr_pending = true;
+    }
     if (!small) {
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_ext[g], h->stream));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->d2h, h->ev_ext[g], 0));
@@ -3088,15 +3145,41 @@ OrbfeStereoScratch** orbfe_internal_stereo_slot(orbfe_extractor* h) { return &h-
 
 extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const uint8_t** p,
                                int* rows, int* cols, size_t* step) {
+  if (!p) return ORBFE_ERR_ARG;
   const uint8_t* dp = nullptr;
   size_t dstep = 0;
   int st = orbfe_get_level_device(h, image, level, &dp, rows, cols, &dstep);
   if (st != ORBFE_OK) return st;
-  h->level_host.resize((size_t)(*rows) * (*cols));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(h->stream));
-  ORBFE_HIP_CHECK(hipMemcpy2D(h->level_host.data(), *cols, dp, dstep, *cols, *rows, hipMemcpyDeviceToHost));
-  *p = h->level_host.data();
-  *step = (size_t)(*cols);
+  hipSetDevice(h->device);
+  if (h->hpyr_pending) {  // the prefetch copies of the last host-buffer call
+    ORBFE_HIP_CHECK(hipEventSynchronize(h->ev_hpyr));
+    h->hpyr_pending = false;
+  }
+  if ((int)h->h_pyr_gen.size() <= image || h->h_pyr_gen[image] != h->gen) {
+    // first access to this image since the extract call: copy its whole pyramid (every level, one
+    // DMA) once the call's work on its stream is done. The block is sized for all the call's
+    // images up front, so the levels handed out before stay where they are.
+    bool fresh = true;
+    for (int i = 0; i < (int)h->h_pyr_gen.size() && fresh; i++) fresh = h->h_pyr_gen[i] != h->gen;
+    if (fresh) {
+      st = ensure_host_pyramid(h, h->last_n);
+      if (st != ORBFE_OK) return st;
+    }
+    const hipStream_t s = h->last_stream ? h->last_stream : h->stream;
+    ORBFE_HIP_CHECK(hipMemcpyAsync(h->h_pyr + (size_t)image * h->pyr_stride, h->d_pyr + (size_t)image * h->pyr_stride,
+                                   (size_t)h->pyr_stride, hipMemcpyDeviceToHost, s));
+    ORBFE_HIP_CHECK(hipStreamSynchronize(s));
+    h->h_pyr_gen[image] = h->gen;
+  }
+  const LevelDesc& d = h->levels[level];
+  *p = h->h_pyr + (size_t)image * h->pyr_stride + d.pyr_off;
+  *step = (size_t)d.pitch;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_extractor_set_host_pyramid(orbfe_extractor* h, int enable) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extractor_set_host_pyramid: null handle");
+  h->host_pyramid = enable ? 1 : 0;
   return ORBFE_OK;
 }
 

@@ -49,7 +49,13 @@ void retire(State& s, const Pending& p, bool sync) {
 
 // completed launches at the head of the queue (bounded memory over long timed runs)
 void harvest(State& s) {
-  while (!s.pending.empty() && hipEventQuery(s.pending.front().e1) == hipSuccess) {
+  while (!s.pending.empty()) {
+    if (hipEventQuery(s.pending.front().e1) != hipSuccess) {
+      // NotReady may be recorded as the thread's last error: clear that one (not a real error
+      // an earlier launch left), or the library's next hipGetLastError check would fail
+      if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+      break;
+    }
     retire(s, s.pending.front(), false);
     s.pending.pop_front();
   }

@@ -2008,8 +2008,11 @@ static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs&
 // rounds change many owners, work one workgroup would take long over), the rest in k_sbp_settle,
 // then collect / finish: R0 + 3 launches whatever the depth of the claim order.
 static int sbp_settle_from(const orbfe_matcher* m) {
-  static const int r0 = std::getenv("ORBFE_SBP_SETTLE_FROM") ? std::max(2, std::atoi(std::getenv("ORBFE_SBP_SETTLE_FROM")))
-                                                             : SBP_SETTLE_FROM;
+  // the range orbfe_debug_matcher_set_settle_from accepts: k_sbp_round writes state[2 + round]
+  // below SBP_FINAL_SLOT only for rounds < SBP_MAX_ROUNDS
+  static const int r0 = std::getenv("ORBFE_SBP_SETTLE_FROM")
+                            ? std::min(SBP_MAX_ROUNDS, std::max(2, std::atoi(std::getenv("ORBFE_SBP_SETTLE_FROM"))))
+                            : SBP_SETTLE_FROM;
   return m->settle_from >= 2 ? m->settle_from : r0;
 }
 static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
@@ -2050,12 +2053,6 @@ static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_fr
   st.serial_used = m->d_serial;
   st.blocked_scratch = (int32_t*)(A + p.oblk);
   const size_t lds = settle_lds(F->n, nq);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)k_sbp_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)settle_lds(SETTLE_MAX_KEYS, SETTLE_MAX_QUERIES));
-    attr_set = true;
-  }
   ORBFE_LAUNCH("k_sbp_settle", k_sbp_settle, dim3(1), dim3(SETTLE_THREADS), lds, m->stream, a, st);
   sbp_finish_launch(m, p, a, md, res, false, true);
 }
@@ -2098,7 +2095,16 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   sbp_launch_grid(m, p, F, dF);
   // the settle path unless rounds are restricted (orbfe_matcher_set_max_rounds: the serial
   // fallback's tests) or no assignment blocks anything (one round is the result)
-  const bool settle = p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
+  bool settle = p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
+  if (settle && m->settle_attr == 0) {
+    // k_sbp_settle's dynamic LDS (up to ~113 KiB) on this matcher's device, checked once per
+    // matcher (one thread per matcher; the attribute is per device); refused: no settle path here
+    const hipError_t e = hipFuncSetAttribute((const void*)k_sbp_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)settle_lds(SETTLE_MAX_KEYS, SETTLE_MAX_QUERIES));
+    m->settle_attr = e == hipSuccess ? 1 : -1;
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  settle = settle && m->settle_attr > 0;
   sbp_launch_init(m, p, F, settle);
   if (settle) {
     sbp_settle_rounds(m, p, F, dF, md);

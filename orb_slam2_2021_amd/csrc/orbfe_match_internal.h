@@ -58,6 +58,9 @@ struct orbfe_matcher {
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
   int settle_from = 0;            // orbfe_debug_matcher_set_settle_from (0: SBP_SETTLE_FROM)
+  // k_sbp_settle's dynamic-LDS limit on this matcher's device: 0 not set yet, 1 set, -1 refused
+  // (the settle path is then off for this matcher)
+  int settle_attr = 0;
   // orbfe_matcher_set_profiling: HIP events around the device part (first kernel .. last kernel,
   // no H2D / D2H) of each SearchByProjection-family call
   int profile = 0;

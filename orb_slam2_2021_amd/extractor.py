@@ -230,13 +230,23 @@ class ORBextractor:
                 "orbfe_stream_wait_event")
 
     # ---- mvImagePyramid (ORBextractor.h:100) --------------------------------------------
-    def level(self, level: int, image: int = 0) -> np.ndarray:
+    def level_view(self, level: int, image: int = 0) -> np.ndarray:
+        """mvImagePyramid[level] of image `image` of the last call as a view of the handle's host
+        block (no copy): valid until the next extract call, like the reference's cv::Mat headers."""
         p = c_void_p()
         r, c, s = c_int(), c_int(), c_size_t()
         L.check(self._lib.orbfe_get_level(self._h, image, level, byref(p), byref(r), byref(c),
                                           byref(s)), "orbfe_get_level")
-        buf = (ctypes.c_uint8 * (r.value * s.value)).from_address(p.value)
-        return np.frombuffer(buf, np.uint8).reshape(r.value, s.value)[:, :c.value].copy()
+        buf = (ctypes.c_uint8 * ((r.value - 1) * s.value + c.value)).from_address(p.value)
+        return np.lib.stride_tricks.as_strided(np.frombuffer(buf, np.uint8), (r.value, c.value), (s.value, 1))
+
+    def level(self, level: int, image: int = 0) -> np.ndarray:
+        return self.level_view(level, image).copy()
+
+    def set_host_pyramid(self, on: bool = True) -> None:
+        """orbfe_extractor_set_host_pyramid: later host-buffer calls copy each pyramid to the host
+        beside the extraction, so mvImagePyramid costs no copy of its own."""
+        L.check(self._lib.orbfe_extractor_set_host_pyramid(self._h, 1 if on else 0), "set_host_pyramid")
 
     @property
     def mvImagePyramid(self) -> List[np.ndarray]:

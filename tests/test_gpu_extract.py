@@ -183,6 +183,36 @@ def test_host_batch_pipeline(require_gpu):
     assert c == len(kr) and np.array_equal(desc[7 * cap:7 * cap + c], dr)
 
 
+@pytest.mark.parametrize("prefetch", [False, True])
+@pytest.mark.parametrize("n", [1, 3, 9])
+def test_mvimagepyramid_views_held_at_once(require_gpu, prefetch, n):
+    """orbfe_get_level's contract (include/orbfe.h): every level of every image of the last call
+    stays valid together until the next extract call, as the reference's mvImagePyramid[0..7]
+    (ORBextractor.h:100) does for Frame::ComputeStereoMatches (Frame.cc:529,620-640), which reads
+    levels of any octave of both extractors in one pass. All n x 8 views are taken first (no copy)
+    and only then compared with the oracle's levels; the lazy path (one DMA per image on its first
+    access) and the prefetch path (orbfe_extractor_set_host_pyramid, copies beside the extraction);
+    1 image (orbfe_extract's path), 3 (one launch group), 9 (the chunked copy-stream pipeline).
+    After the next call the views show the new call's pyramids."""
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    ext.set_host_pyramid(prefetch)
+    ref = RefExtractor(2000, 1.2, 8, 20, 7)
+    for rnd in range(2):
+        imgs = [synth_frame(70 + 10 * rnd + i, 376, 1241) for i in range(n)]
+        if n == 1:
+            ext(imgs[0])
+        else:
+            ext.extract_batch(imgs)
+        views = [[ext.level_view(l, image=i) for l in range(8)] for i in range(n)]
+        spans = sorted((v.__array_interface__["data"][0], v.__array_interface__["data"][0] +
+                        (v.shape[0] - 1) * v.strides[0] + v.shape[1]) for row in views for v in row)
+        assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])), "two levels share host memory"
+        for i in reversed(range(n)):
+            ref(imgs[i])
+            for l in range(8):
+                assert np.array_equal(views[i][l], ref.level(l)), (rnd, i, l)
+
+
 def test_repeatable(require_gpu):
     img = synth_frame(9, 376, 1241)
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
