@@ -806,7 +806,7 @@ def c2_latency(args, left, right, reps=200):
         call_pair()
         one_call.append(time.perf_counter() - t0)
     out = {"single_image": percentiles(single), "stereo_two_threads": percentiles(pair[10:]),
-           "stereo_pair_one_call": percentiles(one_call),
+           "stereo_pair_one_call": percentiles(one_call), "adapter": adapter_latency(),
            "what": "orbfe_extract wall-clock per call (host buffers in and out), 1241x376, 1 GPU; stereo_two_threads "
                    "= two handles on two threads as Frame.cc:113-116; stereo_pair_one_call = both images in one "
                    "orbfe_extract_batch call on one handle"}
@@ -819,6 +819,29 @@ def c2_latency(args, left, right, reps=200):
                                                             ("x", "y", "size", "response", "octave"))
                                        and np.max(np.abs(k[:m]["angle"] - kr["angle"])) <= 1e-5
                                        and np.array_equal(d[:m], dr))
+    return out
+
+
+def adapter_latency(iters=200):
+    """The reference-side drop-in adapters (adapter/ORBextractor_gpu.cc + adapter/Frame_gpu.cc, built
+    over tests/cpp/cvstub by __graft_entry__.build()) as the reference calls them: ORBextractor::
+    operator() on one image with its cv::Mat outputs and mvImagePyramid, and the stereo Frame
+    constructor's two ExtractORB threads + ComputeStereoMatches (Frame.cc:113-125). Two builds:
+    mvImagePyramid prefetched to the host (the CPU ComputeStereoMatches' input) and
+    ORBFE_ADAPTER_GPU_STEREO=1 (no pyramid copy). Child processes (tests/cpp/adapter_latency.cpp)."""
+    out = {}
+    for name in ("adapter_latency", "adapter_latency_gpustereo"):
+        exe = os.path.join(ROOT, "tests", "cpp", "build", name)
+        if not os.path.exists(exe):
+            out[name] = "not built"
+            continue
+        try:
+            r = subprocess.run([exe, str(iters)], capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            out[name] = "timeout"
+            continue
+        rec = [l for l in r.stdout.splitlines() if l.startswith("ADAPTER ")]
+        out[name] = json.loads(rec[-1][len("ADAPTER "):]) if r.returncode == 0 and rec else f"rc {r.returncode}"
     return out
 
 

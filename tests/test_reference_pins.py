@@ -114,3 +114,35 @@ def test_matcher_thresholds_equal_reference_text():
     from orb_slam2_2021_amd import ORBmatcher
     assert (ORBmatcher.TH_HIGH, ORBmatcher.TH_LOW, ORBmatcher.HISTO_LENGTH) == \
         (ref["TH_HIGH"], ref["TH_LOW"], ref["HISTO_LENGTH"])
+
+
+def _members(text, names):
+    """(type, name) of each data member declaration `T name;` among `names` in declaration order."""
+    out = []
+    for m in re.finditer(r"^\s*([A-Za-z_][\w:<>, \*]*?)\s*\*?\s*([A-Za-z_]\w*)\s*;", _strip_comments(text), re.M):
+        typ, name = re.sub(r"\s+", " ", m.group(1)).strip(), m.group(2)
+        if name in names and typ != "return":
+            out.append((typ, name))
+    return out
+
+
+def test_adapter_test_stub_declares_the_reference_members():
+    """tests/cpp/cvstub/ORBextractor.h (the test-only declaration adapter/ORBextractor_gpu.cc is
+    compiled against in tests/cpp/adapter_e2e.cpp) declares the data members of the reference's
+    include/ORBextractor.h:100-125 the adapter fills, with the same types and in the same order,
+    and the same operator() / constructor parameter lists (ORBextractor.h:56-68)."""
+    names = {"mvImagePyramid", "nfeatures", "scaleFactor", "nlevels", "iniThFAST", "minThFAST",
+             "mnFeaturesPerLevel", "umax", "mvScaleFactor", "mvInvScaleFactor", "mvLevelSigma2",
+             "mvInvLevelSigma2"}
+    with open("/root/reference/include/ORBextractor.h") as f:
+        ref = f.read()
+    with open(os.path.join(ROOT, "tests", "cpp", "cvstub", "ORBextractor.h")) as f:
+        stub = f.read()
+    r, s = _members(ref, names), _members(stub, names)
+    assert len(r) == len(names) and r == s, (r, s)
+
+    def sig(text, pat):
+        m = re.search(pat, _strip_comments(text), re.S)
+        return re.sub(r"\s+", "", m.group(1))
+    for pat in (r"ORBextractor\s*\(([^)]*)\)\s*;", r"void\s+operator\(\)\s*\(([^)]*)\)\s*;"):
+        assert sig(ref, pat) == sig(stub, pat), pat
