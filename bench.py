@@ -121,6 +121,17 @@ def parse(argv=None):
                         "N-1 RCCL self send / receive pairs of the packed worst-case payload (a world-1 "
                         "communicator) as one group on the matching stream, where Gatherer's transfers run, "
                         "with N > 1's hardware-queue setting (DESIGN.md section 7)")
+    p.add_argument("--feed", choices=("device", "host"), default="device",
+                   help="device: the input batches resident in HBM when the timed region starts (the metric); "
+                        "host: every sub-batch's 2B images copied from pinned host memory on a copy stream into "
+                        "one of --input-slots device slots, overlapped with the other sub-batches' extraction and "
+                        "matching (the reference's operator() takes host images, ORBextractor.cc:1041-1048)")
+    p.add_argument("--input-slots", type=int, default=0,
+                   help="--feed host: device input slots (0: one per extractor handle)")
+    p.add_argument("--root-share", type=float, default=-1.0,
+                   help="C4 (and --gather-proxy): the fraction of the per-rank sub-batches rank 0 extracts and "
+                        "matches itself, since it also ingests every peer's payload; on the other slots it only "
+                        "receives (-1: the model of DESIGN.md section 7, 1 - ROOT_INGEST_PER_PEER (N - 1))")
     p.add_argument("--rehearse", action="store_true",
                    help="N ranks on ONE GPU over gloo with host-staged exchanges: exercises the multi-rank "
                         "orchestration on a one-GPU box (not a measurement)")
@@ -141,6 +152,34 @@ def hw_queue_setting(requested: int, world: int) -> int:
     if requested >= 0:
         return requested
     return HW_QUEUES_MULTI_RANK if world > 1 else 0
+
+
+# C4: rank 0's cost of ingesting one peer's packed sub-batch payload, as a fraction of a sub-batch
+# period, from the one-GPU proxy (--gather-proxy N: N - 1 RCCL self send / receive pairs per slot,
+# the send side's HBM traffic included, so an upper bound): round 4 -2.5 / -11.6 / -19.1 % at
+# N = 2 / 4 / 8 (2.7 % per peer); round 5, N = 8: 504.4 vs 387.6 ms per 1,024-sub-batch step, i.e.
+# 116.8 ms for 7,168 payloads = 4.3 % of a period per payload (profiles/r5_c4_proxy.txt). The larger
+# figure: if it overstates the cost, rank 0 finishes first and the whole job still loses only
+# (1 - f) / N.
+ROOT_INGEST_PER_PEER = 0.043
+
+
+def root_share(requested: float, n_gpus: int) -> float:
+    """Fraction of the per-rank sub-batch slots on which rank 0 runs its own sub-batch (it receives
+    the peers' payloads on every slot). With rank 0 slower by c (N - 1) per own sub-batch, the ranks
+    finish together when rank 0 runs 1 - c (N - 1) of the slots: frames = (N - 1 + f) S B in the
+    peers' time S p, a whole-job loss of (1 - f) / N (2.4 % at N = 8) instead of c (N - 1) (19 %)."""
+    if requested >= 0:
+        return min(1.0, max(0.0, requested))
+    if n_gpus <= 1:
+        return 1.0
+    return max(0.5, 1.0 - ROOT_INGEST_PER_PEER * (n_gpus - 1))
+
+
+def own_slots(n: int, share: float):
+    """Which of n slots run the rank's own sub-batch: round(n share) of them, spread evenly."""
+    import math
+    return [math.floor((k + 1) * share + 0.5) > math.floor(k * share + 0.5) for k in range(n)]
 
 
 SEQ_SEED = 0x0C3  # the C3 driving sequence (orbfe_synth_sequence_frame)
@@ -259,6 +298,72 @@ class Gatherer:
         if self.rank == 0:
             self.last = out
 
+    def receive_only(self):
+        """Rank 0 on a slot without its own sub-batch (--root-share): the peers' payloads of that
+        slot, received into the same buffers, on the matching stream (RCCL) or the comm stream."""
+        import torch
+        from orb_slam2_2021_amd.parallel import gather_fixed
+        assert self.rank == 0
+        if self.rccl is not None:
+            recv = [r.data_ptr() for r in self.recv]
+            self.rccl.gather([0], self.cap_bytes, [recv], 0, self.pipe.mstream.cuda_stream)
+        else:
+            buf = next(iter(self.bufs.values()))
+            with torch.cuda.stream(self.comm):
+                gather_fixed(buf.cpu() if self.comm_dev.type == "cpu" else buf, self.cap_bytes, dst=0,
+                             recv=self.recv)
+        self.transfers += 1
+
+
+class HostFeed:
+    """--feed host: each sub-batch's 2B images go from pinned host memory (the NB distinct input
+    batches, page-locked once) into one of R device slots on the pipeline's copy stream, and the
+    extraction waits for that copy. R = the extractor handle count, so slot k mod R is read by the
+    handle that extracts sub-batch k; the copy into it for sub-batch k waits for that handle's
+    pyramid event, which at that point holds sub-batch k - R's record (only k_copy0 reads the input
+    images, before the pyramid completes). Copies run ahead of the extraction as far as the slots
+    allow; the link, not the kernels, bounds the rate when 2B images take longer to copy than to
+    process."""
+
+    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0):
+        import torch
+        self.h = torch.from_numpy(host).pin_memory()
+        self.R = 0
+        self.slots = None
+        self.slots_req = slots
+        self.n_img, self.H, self.W, self.dev = n_img, H, W, dev
+        self.cs = copy_stream
+        self.k = 0
+        self.ready = []
+        self.bytes_per_subbatch = n_img * H * W
+
+    def upload(self, j, pipe):
+        import torch
+        from orb_slam2_2021_amd.pipeline import new_event
+        if self.slots is None:
+            self.R = len(pipe.exts)
+            self.slots = torch.empty((self.R, self.n_img, self.H, self.W), dtype=torch.uint8, device=self.dev)
+            self.ready = [new_event(self.dev.index) for _ in range(self.R)]
+        slot = self.k % self.R
+        ext = pipe.next_handle()
+        assert pipe.exts.index(ext) == slot, "slot k mod R is read by handle k mod R"
+        if self.k >= self.R:  # the slot's last reader: this handle's previous extraction (k - R)
+            L = pipe.lib
+            L.orbfe_stream_wait_event(ctypes.c_void_p(self.cs.cuda_stream),
+                                      ctypes.c_void_p(L.orbfe_extractor_pyramid_event(ext._h)))
+        with torch.cuda.stream(self.cs):
+            self.slots[slot].copy_(self.h[j], non_blocking=True)
+        self.ready[slot].record(self.cs)
+        self.k += 1
+        return self.slots[slot].data_ptr(), self.ready[slot]
+
+    def describe(self, subbatches_per_s):
+        gbs = self.bytes_per_subbatch * subbatches_per_s / 1e9
+        return {"mode": "host", "h2d_bytes_per_subbatch": self.bytes_per_subbatch, "h2d_GBps": round(gbs, 2),
+                "device_slots": self.R,
+                "what": "every sub-batch's images H2D from pinned host memory on a copy stream of its own, "
+                        "overlapped with the other sub-batches' kernels; outputs stay in HBM"}
+
 
 class GatherProxy:
     """--gather-proxy N on one GPU: the cost rank 0 pays for C4's ingestion at N GPUs, without the
@@ -282,6 +387,7 @@ class GatherProxy:
         self.rccl = RcclComm(1, 0, unique_id())
         self.pending = []
         self.transfers = 0
+        self.last_buf = None
 
     def pack(self, o):
         from orb_slam2_2021_amd.parallel import pack_keypoints_device
@@ -290,12 +396,22 @@ class GatherProxy:
         pack_keypoints_device(p.n_img, o.cnt.data_ptr(), o.kps.data_ptr(), o.desc.data_ptr(), p.cap,
                               buf.data_ptr(), self.cap_bytes, self.sizes[id(o)].data_ptr(), m.cuda_stream)
         self.pending.append(buf.data_ptr())
+        self.last_buf = buf.data_ptr()
         if len(self.pending) == self.every:
             # (a set's payload buffer is rewritten only by its next pack, behind this on the stream)
             k = self.n - 1
             recv = [[r.data_ptr() for r in self.recv[j * k:(j + 1) * k]] for j in range(len(self.pending))]
             self.rccl.self_copies(self.pending, self.cap_bytes, recv, m.cuda_stream)
             self.pending = []
+        self.transfers += 1
+
+    def receive_only(self):
+        """A slot without rank 0's own sub-batch: the N - 1 peer payloads only (self pairs of the
+        last packed payload), one group on the matching stream."""
+        m = self.pipe.mstream
+        src = self.last_buf if self.last_buf is not None else next(iter(self.bufs.values())).data_ptr()
+        k = self.n - 1
+        self.rccl.self_copies([src], self.cap_bytes, [[r.data_ptr() for r in self.recv[:k]]], m.cuda_stream)
         self.transfers += 1
 
     def describe(self):
@@ -309,6 +425,8 @@ class GatherProxy:
 def main():
     args = parse()
     hw_queues = hw_queue_setting(args.hw_queues, max(int(os.environ.get("WORLD_SIZE", "1")), args.gather_proxy))
+    if args.feed == "host" and args.hw_queues < 0:
+        hw_queues = HW_QUEUES_MULTI_RANK  # the copy stream on a hardware queue of its own
     if hw_queues > 0:  # read once by the HIP runtime at its start (no HIP call before this)
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(hw_queues, 32))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -328,7 +446,7 @@ def main():
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
     pstreams = PipelineStreams(gpu, n_ext, match_inline=args.match_inline, side_last=args.inline_side,
-                               comm=world > 1)
+                               comm=world > 1, copy=args.feed == "host")
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:
@@ -351,6 +469,9 @@ def main():
     # ---- inputs: NB distinct batches of B stereo frames of this rank, resident in HBM ----
     host = make_inputs(args, world, rank)
     d_img = torch.from_numpy(host).to(dev)
+    feed = None
+    if args.feed == "host":
+        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
@@ -390,11 +511,25 @@ def main():
     if args.gather_proxy > 1 and world == 1:
         g = GatherProxy(pipe, args.gather_proxy, dev, every=args.gather_every)
     counter = [0]
+    # C4: rank 0 extracts on a share of the slots only (it ingests every peer's payload on all of them)
+    n_model = world if isinstance(g, Gatherer) else (args.gather_proxy if isinstance(g, GatherProxy) else 1)
+    share = root_share(args.root_share, n_model) if rank == 0 else 1.0
+    own = own_slots(S_sub, share)
+
+    def slot(k):
+        if own[k]:
+            sub_batch()
+        else:
+            g.receive_only()
 
     def sub_batch():
         j = counter[0] % NB
         counter[0] += 1
-        pipe.run(d_img[j].data_ptr(), after_match=g.pack if g else None)
+        if feed is not None:  # the images go up from pinned host memory first (copy stream)
+            ptr, ready = feed.upload(j, pipe)
+            pipe.run(ptr, after_match=g.pack if g else None, input_ready=ready)
+        else:
+            pipe.run(d_img[j].data_ptr(), after_match=g.pack if g else None)
 
     def barrier():
         if world > 1:
@@ -402,8 +537,9 @@ def main():
 
     # all work goes to the pipeline's two non-default streams, ordered by events
     torch.cuda.set_stream(pipe.stream)
-    for _ in range(args.warmup * S_sub):
-        sub_batch()
+    for _ in range(args.warmup):
+        for k in range(S_sub):
+            slot(k)
     torch.cuda.synchronize()
     # host cost of enqueueing one sub-batch (untimed): 32 sub-batches right after a synchronize,
     # while the device queues are still short enough that no launch blocks
@@ -435,7 +571,7 @@ def main():
             if ev:
                 set_events(True)
                 timed_events += 1
-            sub_batch()
+            slot(k)
             if ev:
                 set_events(False)
     t_enq = time.perf_counter()  # every launch of the timed region enqueued
@@ -459,7 +595,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    frames = world * B * S_sub * args.steps
+    # frames of every rank: the peers' S_sub per step each, rank 0's own share
+    frames = B * args.steps * ((world - 1) * S_sub + sum(own if rank == 0 else own_slots(S_sub, root_share(
+        args.root_share, n_model))))
     value = frames / elapsed
     last = pipe.last
     counts = last.cnt.cpu().numpy()
@@ -502,8 +640,9 @@ def main():
                  if args.pairs == "kf" else "synthetic (seeded KITTI-shaped stereo frames, orbfe_synth_frame")
                 + "; synthetic ORBvoc-shaped "
                 f"vocabulary k=10 L={args.vocab_levels})",
+        **({"feed": feed.describe(value / world / B)} if feed is not None else {}),
         "config": {
-            "workload": "C3: stereo extract + ComputeBoW + "
+            "workload": ("host-fed " if feed is not None else "") + "C3: stereo extract + ComputeBoW + "
                         + ("ComputeStereoMatches + " if args.stereo else "")
                         + (f"SearchForTriangulation(KF t, KF t+1) x{pipe.n_pairs}" if args.pairs == "kf"
                            else f"SearchForTriangulation(left, right) x{pipe.n_pairs}")
@@ -522,6 +661,11 @@ def main():
                          f"{pipe_depth(args)} output sets" if pipe_depth(args) > 1 else "one sub-batch at a time"),
         },
         **({"gather_proxy": g.describe()} if isinstance(g, GatherProxy) else {}),
+        **({"root_share": {"rank0_own_subbatches_per_step": int(sum(own_slots(S_sub, root_share(args.root_share, n_model)))),
+                           "subbatches_per_step": S_sub, "share": round(root_share(args.root_share, n_model), 4),
+                           "model": f"1 - {ROOT_INGEST_PER_PEER} (N - 1), N = {n_model}" if args.root_share < 0 else "given",
+                           "what": "rank 0 runs its own sub-batch on this share of the slots and receives the peers' "
+                                   "payloads on every slot (DESIGN.md section 7)"}} if n_model > 1 else {}),
         "roofline": roof,
         "pipeline_hbm": {
             "algorithmic_bytes_per_stereo_frame": int(algo_frame),
@@ -584,7 +728,8 @@ def main():
         out["host_boundary"] = host_boundary_rate(ext, host[0], others=exts[1:])
         if not args.no_legs:
             out["c2_latency"] = c2_latency(args, host[0][0], host[0][B])
-            out["legs"] = {"tracking_sequence": tracking_leg(args),
+            out["legs"] = {"c3_host_fed": host_fed_leg(args),
+                           "tracking_sequence": tracking_leg(args),
                            "c5_search_local_points": c5_leg(args, 1, 0, dev),
                            "keyframe_searches": keyframe_leg(args),
                            "compute_stereo_matches": stereo_leg(args, ext, d_img[0], host[0], B, H, W,
@@ -600,6 +745,29 @@ def main():
             torch.cuda.synchronize()
             g.rccl.close()
         dist.destroy_process_group()
+
+
+def host_fed_leg(args, steps=3, subbatches=256):
+    """The C3 step fed from host memory (bench.py --feed host as a child process, so that its copy
+    stream gets a hardware queue of its own): the reference's operator() takes host images
+    (ORBextractor.cc:1041-1048, two per stereo Frame, Frame.cc:113-116), so this is the rate a
+    host-resident image stream gets; the headline keeps the inputs in HBM."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--feed", "host", "--steps", str(steps), "--warmup", "1",
+           "--batches-per-step", str(subbatches), "--no-legs", "--no-cpu", "--event-every", "1000000"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return "timeout"
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return f"rc {r.returncode}: {r.stderr[-400:]}"
+    d = json.loads(lines[-1])
+    return {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"], "steps": d["steps"],
+            "subbatches_per_step": d["config"]["subbatches_per_step"], "feed": d.get("feed"),
+            "parity_bit_exact": d.get("parity_bit_exact"), "hw_queues": d["config"]["hw_queues"],
+            "link_bound_stereo_frames_per_s_at_53GBps": round(53e9 / d["feed"]["h2d_bytes_per_subbatch"] * args.batch, 1),
+            "what": "bench.py --feed host (child process): C3 with every sub-batch's images copied H2D from pinned "
+                    "host memory, overlapped with the kernels; not the metric (inputs resident in HBM)"}
 
 
 def dump_gather(d, g, pipe, rank, world):

@@ -106,7 +106,7 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 side_last: bool = False, comm: bool = False):
+                 side_last: bool = False, comm: bool = False, copy: bool = False):
         import torch
         self.device = device
         self._ptrs = []
@@ -135,6 +135,10 @@ class PipelineStreams:
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
         # that stream's kernels: measured 83k -> 52k stereo frames/s on one GPU (--gather-proxy)
         self.comm = make(False) if comm else None
+        # copy: the H2D stream of a host-fed pipeline (bench.py --feed host), created last; with
+        # more hardware queues than busy streams (the caller sets GPU_MAX_HW_QUEUES) it gets a queue
+        # of its own, so that its waits for free input slots never hold an extraction stream
+        self.copy = make(False) if copy else None
 
     def ordered(self):
         """(extraction streams..., matching stream or None) as C3Pipeline takes them."""
@@ -148,7 +152,7 @@ class PipelineStreams:
     def close(self):
         """Wait for the streams, point every attached extractor back at its own side stream, then
         destroy the streams (no handle is left holding a destroyed hipStream_t)."""
-        for s in self.extract + [self.match, self.comm, self.side]:
+        for s in self.extract + [self.match, self.comm, self.copy, self.side]:
             if s is not None:
                 s.synchronize()
         for e in self._attached:
@@ -294,15 +298,22 @@ class C3Pipeline:
         self.stereo_on_match = stereo and stereo_on_match and not self.match_inline
         self.stereo_done = [None] * len(self.exts)
 
-    def run(self, d_img_ptr: int, after_match=None):
+    def next_handle(self):
+        """The extractor handle the next run() extracts with."""
+        return self.exts[self.counter % len(self.exts)]
+
+    def run(self, d_img_ptr: int, after_match=None, input_ready=None):
         """One sub-batch: 2B images of H x W at d_img_ptr (lefts then rights, row pitch W).
         `after_match(o)` runs on the matching stream after SearchForTriangulation (the C4 gather).
-        Returns the output set."""
+        `input_ready`: an event the extraction waits for first (the images' H2D copy of a host-fed
+        pipeline). Returns the output set."""
         o = self.sets[self.counter % len(self.sets)]
         k = self.counter % len(self.exts)
         self.counter += 1
         B, H, W, cap = self.B, self.H, self.W, self.cap
         s, ext = self.streams[k % len(self.streams)], self.exts[k]
+        if input_ready is not None:
+            s.wait_event(input_ready)
         s.wait_event(o.matched)  # the matching that last read this set is done
         if o.released is not None:  # and whatever an after_match hook still runs on it (the gather)
             s.wait_event(o.released)

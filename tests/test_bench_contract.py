@@ -80,3 +80,19 @@ def test_hw_queue_setting():
     assert bench.hw_queue_setting(0, 8) == 0  # the environment's
     assert bench.hw_queue_setting(4, 1) == 4
     assert bench.parse([]).hw_queues == -1 and bench.parse([]).c5_workers >= 1
+
+
+def test_root_share_schedule():
+    """C4's rank-0 share: the model and the slot schedule."""
+    import bench
+    assert bench.root_share(-1, 1) == 1.0
+    assert abs(bench.root_share(-1, 8) - (1 - 7 * bench.ROOT_INGEST_PER_PEER)) < 1e-12
+    assert bench.root_share(0.3, 8) == 0.3 and bench.root_share(2.0, 8) == 1.0
+    for n, f in [(1024, 0.809), (1024, 1.0), (7, 0.5), (3, 0.97), (100, 0.0)]:
+        own = bench.own_slots(n, f)
+        assert len(own) == n and sum(own) == int(n * f + 0.5)
+        if f > 0:
+            assert own[0]  # the first slot runs rank 0's own sub-batch
+    # the whole-job loss the share leaves at N = 8 (rank 0 and the peers finish together)
+    f = bench.root_share(-1, 8)
+    assert (1 - f) / 8 <= 0.05

@@ -107,16 +107,19 @@ def test_k_pack_bench_c3_batch(require_gpu):
     assert cap_bytes <= 1.02 * size
 
 
-def test_bench_gatherer_two_ranks_on_one_gpu(require_gpu, tmp_path):
+@pytest.mark.parametrize("root_share", ["-1", "0.5"])
+def test_bench_gatherer_two_ranks_on_one_gpu(require_gpu, tmp_path, root_share):
     """bench.py --rehearse --gpus 2: two ranks on GPU 0 over gloo run the bench's whole multi-rank
     orchestration (Gatherer: device pack on the matching stream, fixed-count point-to-point
     transfers to rank 0). Rank 0's received payloads must equal each rank's own extraction of its
-    last sub-batch, bit for bit."""
+    last sub-batch, bit for bit. --root-share 0.5: rank 0 extracts on every other slot only and
+    receives the peer's payload on the others (receive-only gathers), so the ranks' exchanges
+    still pair up slot by slot."""
     d = str(tmp_path / "gather")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rehearse", "--gpus", "2", "--steps", "1",
-           "--warmup", "1", "--batches-per-step", "3", "--input-batches", "2", "--probe-subbatches", "2",
-           "--no-cpu", "--no-legs", "--no-parity", "--dump-gather", d]
+           "--warmup", "1", "--batches-per-step", "4", "--input-batches", "2", "--probe-subbatches", "2",
+           "--no-cpu", "--no-legs", "--no-parity", "--dump-gather", d, "--root-share", root_share]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     for rank in range(2):
