@@ -45,14 +45,18 @@ int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
  * deg_bits_begin .. deg_bits_begin + n - 1, into device buffers (NULL stream = default stream;
  * synchronous). Used by the exhaustive glibc check, tests/test_gpu_trig.py. */
 int orbfe_debug_steer_trig(uint32_t deg_bits_begin, uint32_t n, float* d_cos, float* d_sin, void* stream);
-/* The last SearchByProjection's k_sbp_settle statistics: rounds that scanned every query (a
- * keypoint listed by more queries than the inverted index holds), queries re-evaluated, keypoint
- * owners recomputed (all summed over its rounds; zeros when the per-round launches ran), then the
- * kernel's wall-clock ticks (100 MHz) in its prologue and in its steps a-d, summed over rounds. */
-int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out8);
-/* The first SearchByProjection round k_sbp_settle runs for this matcher (2 .. 12; 0 restores the
- * default, round 8): tests drive the settle kernel through most of the fixpoint with 2. */
-int orbfe_debug_matcher_set_settle_from(orbfe_matcher* m, int round0);
+/* The last SearchByProjection's k_sbp_sweep statistics (the claim order after round 0, one
+ * workgroup, chunk by chunk): [0] chunks, [1] Jacobi rounds summed over chunks, [2] live queries
+ * (round 0 pruned the rest), [3] chunks finished by the sequential walk, [4] the most rounds one
+ * chunk took; wall-clock ticks (100 MHz) in [5] the compaction of the live queries, [6] the chunks'
+ * loads, [7] their rounds, [8] their commits; [9] live queries past the cache (grid walk each
+ * round); [10] shader clock cycles / 1000 and [11] 100 MHz ticks over the kernel (its clock rate). */
+int orbfe_debug_matcher_sweep_stats(orbfe_matcher* m, int32_t* out12);
+/* Test knobs of the sweep for this matcher (0: the default): live queries per chunk (1 .. 1024;
+ * small chunks commit claims across many chunks), Jacobi rounds a chunk may take before the
+ * reference's sequential loop over it (1 forces that walk), candidate-cache entries per query (48;
+ * small values send queries past the cache to the grid walk). */
+int orbfe_debug_matcher_set_sweep(orbfe_matcher* m, int chunk, int max_rounds, int cand_cap);
 
 #ifdef __cplusplus
 }

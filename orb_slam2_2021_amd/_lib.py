@@ -124,8 +124,8 @@ _SIGNATURES = {
     "orbfe_event_query": (c_int, [c_void_p]),
     "orbfe_matcher_set_profiling": (c_int, [c_void_p, c_int]),
     "orbfe_matcher_last_device_ms": (c_int, [c_void_p, POINTER(c_float)]),
-    "orbfe_debug_matcher_settle_stats": (c_int, [c_void_p, c_void_p]),
-    "orbfe_debug_matcher_set_settle_from": (c_int, [c_void_p, c_int]),
+    "orbfe_debug_matcher_sweep_stats": (c_int, [c_void_p, c_void_p]),
+    "orbfe_debug_matcher_set_sweep": (c_int, [c_void_p, c_int, c_int, c_int]),
     "orbfe_host_register": (c_int, [c_void_p, c_size_t]),
     "orbfe_host_unregister": (c_int, [c_void_p]),
     "orbfe_stream_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),

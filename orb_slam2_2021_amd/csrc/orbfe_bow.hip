@@ -248,8 +248,7 @@ __global__ __launch_bounds__(256) void k_init_queries(InitQueryArgs a) {
 struct InitFixArgs {
   int n1, n2, cand_cap, round;
   float nnratio;
-  const int16_t* cand_k;
-  const uint8_t* cand_d;
+  const uint32_t* cand;  // SearchByProjection's candidate cache: keypoint | distance << 16 | level << 24
   const int32_t* cand_n;
   const int32_t* dec_prev;
   int32_t* dec_cur;          // accepted i2, or -1
@@ -279,14 +278,14 @@ __global__ __launch_bounds__(256) void k_init_round(InitFixArgs a) {
   const int i1 = blockIdx.x * 16 + row;
   if (i1 >= a.n1) return;  // the 16 lanes of a row leave together
   const int n = a.cand_n[i1];
-  const int16_t* ck = a.cand_k + (size_t)i1 * a.cand_cap;
-  const uint8_t* cd = a.cand_d + (size_t)i1 * a.cand_cap;
+  const uint32_t* ce = a.cand + (size_t)i1 * a.cand_cap;
   const unsigned NONE = 0xffffffffu;
   unsigned k1 = NONE;  // (distance << 16 | position)
   int d2 = INT_MAX;
   for (int c = j; c < n; c += 16) {
-    const int i2 = ck[c];
-    const int dist = cd[c];
+    const uint32_t e = ce[c];
+    const int i2 = cand_key(e);
+    const int dist = cand_dist(e);
     int vmd = INT_MAX;  // vMatchedDistance[i2] before i1, per the previous round's choosers
     const int cc = min(a.cnt_prev[i2], INIT_SLOTS);
     for (int s = 0; s < cc; s++) {
@@ -314,7 +313,7 @@ __global__ __launch_bounds__(256) void k_init_round(InitFixArgs a) {
   int dec = -1;
   if (kmin != NONE) {
     const int bestDist = (int)(kmin >> 16);
-    if (bestDist <= TH_LOW && (float)bestDist < (float)second * a.nnratio) dec = ck[kmin & 0xffffu];  // :473-475
+    if (bestDist <= TH_LOW && (float)bestDist < (float)second * a.nnratio) dec = cand_key(ce[kmin & 0xffffu]);  // :473-475
   }
   bool changed = false;
   if (j == 0) {
@@ -333,8 +332,7 @@ __global__ __launch_bounds__(256) void k_init_round(InitFixArgs a) {
 struct InitSeqArgs {
   int n1, n2, cand_cap, check_ori;
   float nnratio;
-  const int16_t* cand_k;
-  const uint8_t* cand_d;
+  const uint32_t* cand;
   const int32_t* cand_n;
   const orbfe_keypoint* keys1;
   const orbfe_keypoint* keys2;
@@ -390,13 +388,13 @@ __global__ __launch_bounds__(64) void k_init_seq(InitSeqArgs a) {
   for (int i1 = 0; i1 < a.n1 && !settled; i1++) {
     const int n = a.cand_n[i1];
     if (n <= 0) continue;  // not level 0, or vIndices2.empty()
-    const int16_t* ck = a.cand_k + (size_t)i1 * a.cand_cap;
-    const uint8_t* cdd = a.cand_d + (size_t)i1 * a.cand_cap;
+    const uint32_t* ce = a.cand + (size_t)i1 * a.cand_cap;
     unsigned k1 = NONE;  // (distance << 16 | position)
     int d2 = INT_MAX;
     for (int j = lane; j < n; j += 64) {
-      const int i2 = ck[j];
-      const int dist = cdd[j];
+      const uint32_t e = ce[j];
+      const int i2 = cand_key(e);
+      const int dist = cand_dist(e);
       if (mdist[i2] <= dist) continue;  // vMatchedDistance[i2] <= dist (:458-459)
       const unsigned key = ((unsigned)dist << 16) | (unsigned)j;
       if (key < k1) {
@@ -412,7 +410,7 @@ __global__ __launch_bounds__(64) void k_init_seq(InitSeqArgs a) {
     if (kmin == NONE) continue;
     const int bestDist = (int)(kmin >> 16);
     if (bestDist <= TH_LOW && (float)bestDist < (float)bestDist2 * a.nnratio) {  // :473-475
-      const int bestIdx2 = ck[kmin & 0xffffu];
+      const int bestIdx2 = cand_key(ce[kmin & 0xffffu]);
       if (lane == 0) {
         const int prev1 = m21[bestIdx2];
         if (prev1 >= 0) a.match12[prev1] = -1;  // :477-481
@@ -732,8 +730,7 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   fa.n2 = n2;
   fa.cand_cap = cap;
   fa.nnratio = m->nnratio;
-  fa.cand_k = (const int16_t*)(A + p.ocand_k);
-  fa.cand_d = A + p.ocand_d;
+  fa.cand = (const uint32_t*)(A + p.ocand);
   fa.cand_n = (const int32_t*)(A + p.ocand_n);
   fa.state = state;
   const int gx = std::max((n1 + 15) / 16, (n2 + 255) / 256);
@@ -755,8 +752,7 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   sa.cand_cap = cap;
   sa.check_ori = m->check_ori;
   sa.nnratio = m->nnratio;
-  sa.cand_k = fa.cand_k;
-  sa.cand_d = fa.cand_d;
+  sa.cand = fa.cand;
   sa.cand_n = fa.cand_n;
   sa.keys1 = d1.keys_un;
   sa.keys2 = d2.keys_un;

@@ -564,21 +564,23 @@ struct SbpArgs {
   int32_t* state;             // [0] converged flag, [1] rounds run, [2 + r] changed in round r
   int round;
   // per-query candidate cache filled in round 0 (keypoints passing the window, level and stereo
-  // gates, in GetFeaturesInArea order, with their distances); later rounds only re-apply the
-  // claims. cand_n[i] < 0: more than cand_cap candidates, the query re-searches every round.
-  // Candidates at distance 256 are left out: they can be neither best nor second (:106-118).
-  int16_t* cand_k;
-  uint8_t* cand_d;
-  uint8_t* cand_l;
+  // gates, in GetFeaturesInArea order, with their distances; one dword each, cand_pack); later
+  // rounds only re-apply the claims. cand_n[i] < 0: more than cand_cap candidates, the query
+  // re-searches every round. Candidates at distance 256 are left out: they can be neither best
+  // nor second (:106-118).
+  uint32_t* cand;
   int32_t* cand_n;
   // rounds >= 2 with the cache: round r-2's owners (round r compares them with round r-1's and
   // re-evaluates only the queries a changed keypoint can reach); NULL: every query is re-evaluated
   const int32_t* owner_rm2;
-  // round 0 with the settle path: the inverted candidate index, keypoint k -> the queries whose
-  // window holds it as a candidate (inv[k * SBP_INV_CAP + j] = query | claims << 31, claims = the
-  // query's assignment blocks its keypoint; inv_n[k] may exceed the cap); NULL off
-  int32_t* inv;
-  int32_t* inv_n;
+  // round 0 before k_sbp_sweep: a query none of whose candidates (pre-blocked ones aside) is within
+  // dist_th can never match, whatever the claims -- blocking only removes candidates -- so it
+  // leaves the claim order: cand_n = 0 (its round-0 result, -1, is final)
+  int prune;
+  uint32_t* live;  // with prune: bit i set for every query left in the claim order (k_sbp_sweep)
+  // round 0: candidates at a distance >= keep_below are not cached (256: all are). Such a
+  // candidate can never decide a result (sbp_keep_below), so the claim order runs on the rest.
+  int keep_below;
 };
 
 // A keypoint whose owner changed from o1 to o2 between rounds: blocked(k) = owner < q flips exactly
@@ -649,13 +651,12 @@ struct SbpBest {
 template <class Blocked>
 __device__ int sbp_cached(const SbpArgs& a, int i, int n, Blocked blocked) {
   SbpBest b;
-  const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
-  const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
-  const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
+  const uint32_t* ce = a.cand + (size_t)i * a.cand_cap;
   for (int c = 0; c < n; c++) {
-    const int k = ck[c];
+    const uint32_t e = ce[c];
+    const int k = cand_key(e);
     if (blocked(k)) continue;
-    b.add(a.mode, cd[c], cl[c], k);
+    b.add(a.mode, cand_dist(e), cand_level(e), k);
   }
   return b.result(a.mode, a.nnratio, a.dist_th);
 }
@@ -705,11 +706,7 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
         const int dist = hamming256(dq0, dq1, d0, d1);
         if (RECORD) {
           if (dist == 256) continue;
-          if (nc < a.cand_cap) {
-            a.cand_k[(size_t)i * a.cand_cap + nc] = (int16_t)k;
-            a.cand_d[(size_t)i * a.cand_cap + nc] = (uint8_t)dist;
-            a.cand_l[(size_t)i * a.cand_cap + nc] = (uint8_t)kp.octave;
-          }
+          if (nc < a.cand_cap) a.cand[(size_t)i * a.cand_cap + nc] = cand_pack(k, dist, kp.octave);
           nc++;
           if (blocked(k)) continue;
         }
@@ -722,7 +719,8 @@ __device__ int sbp_one(const SbpArgs& a, int i, Blocked blocked) {
 }
 
 struct SbpInit {
-  int32_t *res0, *res1, *own0, *own2, *state, *nmatches, *serial, *inv_n;
+  int32_t *res0, *res1, *own0, *own2, *state, *nmatches, *serial;
+  uint32_t* live;  // the sweep's live-query bitmap (NULL: none)
   int nq, nf;
 };
 // One launch for the per-call initialisation (results "never", owners unclaimed, counters 0).
@@ -732,13 +730,13 @@ __global__ __launch_bounds__(256) void k_sbp_init(SbpInit in) {
     in.res0[i] = (int32_t)0xfefefefe;  // never a result
     in.res1[i] = (int32_t)0xfefefefe;
   }
+  if (in.live && i < (in.nq + 31) / 32) in.live[i] = 0u;
   if (i < in.nf) {
     in.own0[i] = 0x7fffffff;
     in.own2[i] = 0x7fffffff;
-    if (in.inv_n) in.inv_n[i] = 0;
   }
   if (i < SBP_ROUND_CAP + 4) in.state[i] = 0;
-  if (i < 16) in.serial[i] = 0;  // [0] serial walk, [1..9] k_sbp_settle's statistics
+  if (i < 16) in.serial[i] = 0;  // [0] serial walk, [1..9] k_sbp_sweep's statistics
   if (i == 0) *in.nmatches = 0;
 }
 
@@ -851,9 +849,7 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   const bool checkLevels = (q.min_level > 0) || (q.max_level >= 0);
   uint4 dq0 = make_uint4(0, 0, 0, 0), dq1 = dq0;
   if (ncell) load_desc(a.qdesc + (size_t)i * 32, dq0, dq1);
-  int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
-  uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
-  uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
+  uint32_t* ce = a.cand + (size_t)i * a.cand_cap;
   const unsigned long long NONE = ~0ull;
   unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
   int kb1 = -1;                             // keypoint of k1
@@ -902,19 +898,11 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
           load_desc(F.descriptors + (size_t)k * 32, d0, d1);
           dist = hamming256(dq0, dq1, d0, d1);
         }
-        const bool keep = pass && dist < 256;  // a distance of 256 is never best or second
+        const bool keep = pass && dist < a.keep_below;  // 256: never best or second (sbp_keep_below)
         const uint64_t bm = (wave_ballot(keep) >> rowbase) & 0xffffull;
-        if (keep && a.inv) {  // every candidate, cached or not (a query past cand_cap re-walks them all)
-          const int slot = atomicAdd(&a.inv_n[k], 1);
-          if (slot < SBP_INV_CAP) a.inv[(size_t)k * SBP_INV_CAP + slot] = (int32_t)((uint32_t)i | ((q.flags & 2u) << 30));
-        }
         if (keep) {
           const int pos = total + __popcll(bm & ((1ull << j) - 1));
-          if (pos < a.cand_cap) {
-            ck[pos] = (int16_t)k;
-            cd[pos] = (uint8_t)dist;
-            cl[pos] = (uint8_t)oct;
-          }
+          if (pos < a.cand_cap) ce[pos] = cand_pack(k, dist, oct);
           if (!sbp_pre_blocked(a, k)) {  // blocked(k) in round 0
             const unsigned long long key =
                 ((unsigned long long)dist << 40) | ((unsigned long long)pos << 8) | (unsigned)oct;
@@ -944,7 +932,10 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
     }
   }
   if (j != 0) return;
-  a.cand_n[i] = total <= a.cand_cap ? total : -1;
+  // pruned: the smallest unblocked distance exceeds dist_th, so no claim order can make a match
+  const bool dead = a.prune && (k1 == NONE || (int)(k1 >> 40) > a.dist_th);
+  a.cand_n[i] = dead ? 0 : total <= a.cand_cap ? total : -1;
+  if (a.live && !dead) atomicOr(&a.live[i >> 5], 1u << (i & 31));
   int res = -1;
   if (k1 != NONE) {
     SbpBest bb;
@@ -963,149 +954,121 @@ __global__ __launch_bounds__(256) void k_sbp_round0(SbpArgs a) {
   if (changed && lane_id() == __ffsll((long long)wave_ballot(true)) - 1) a.state[2] = 1;
 }
 
-// sbp_cached with a group of L lanes (lane j takes cache entries j, j + L, ...): the sequential
-// best / second-best bookkeeping is the two smallest (dist, position) keys over the unblocked
-// entries (see k_sbp_round0), merged over the group. The first SBP_CAND / L entries of each lane are
-// loaded together with the entry count (one memory latency per query instead of a count -> entries
-// chain); entries past them (a cache larger than SBP_CAND) follow in a loop. Every lane returns the
-// result; n_out is the entry count (< 0: past the cache, the caller walks the grid instead).
-template <int L, class Blocked>
-__device__ __forceinline__ int sbp_cached_group(const SbpArgs& a, int i, int j, Blocked blocked, int& n_out) {
-  constexpr int PRE = SBP_CAND / L;
-  const unsigned long long NONE = ~0ull;
-  unsigned long long k1 = NONE, k2 = NONE;  // (dist << 40 | position << 8 | level)
-  int kb1 = -1;
-  const int16_t* ck = a.cand_k + (size_t)i * a.cand_cap;
-  const uint8_t* cd = a.cand_d + (size_t)i * a.cand_cap;
-  const uint8_t* cl = a.cand_l + (size_t)i * a.cand_cap;
-  int pk[PRE], pd[PRE], pl[PRE];
-#pragma unroll
-  for (int u = 0; u < PRE; u++) {
-    const int c = j + L * u;
-    const bool in = c < a.cand_cap;
-    pk[u] = in ? ck[c] : 0;
-    pd[u] = in ? cd[c] : 0;
-    pl[u] = in ? cl[c] : 0;
-  }
-  const int n = a.cand_n[i];
-  n_out = n;
-  if (n <= 0) return -1;
-  auto add = [&](int c, int k, int d, int l) {
-    if (blocked(k)) return;
-    const unsigned long long key = ((unsigned long long)d << 40) | ((unsigned long long)c << 8) | (unsigned long long)l;
-    if (key < k1) {
-      k2 = k1;
-      k1 = key;
-      kb1 = k;
-    } else if (key < k2) {
-      k2 = key;
-    }
-  };
-#pragma unroll
-  for (int u = 0; u < PRE; u++)
-    if (j + L * u < n) add(j + L * u, pk[u], pd[u], pl[u]);
-  for (int c = j + L * PRE; c < n; c += L) add(c, ck[c], cd[c], cl[c]);
-#pragma unroll
-  for (int s2 = L / 2; s2 > 0; s2 >>= 1) {
-    const unsigned long long o1 = __shfl_xor(k1, s2, L), o2 = __shfl_xor(k2, s2, L);
-    const int ob = __shfl_xor(kb1, s2, L);
-    k2 = min_u64(max_u64(k1, o1), min_u64(k2, o2));
-    if (o1 < k1) {
-      k1 = o1;
-      kb1 = ob;
-    }
-  }
-  if (k1 == NONE) return -1;
-  SbpBest bb;
-  bb.bestDist = (int)(k1 >> 40);
-  bb.bestLevel = (int)(k1 & 0xff);
-  bb.bestIdx = kb1;
-  if (k2 != NONE) {
-    bb.bestDist2 = (int)(k2 >> 40);
-    bb.bestLevel2 = (int)(k2 & 0xff);
-  }
-  return bb.result(a.mode, a.nnratio, a.dist_th);
-}
-
-// ---- the fixpoint's tail in one workgroup ---------------------------------------------------
-// The grid-wide rounds (k_sbp_round, one launch each) settle most searches in 8-12 rounds, but a
-// C5 search needs 8-23 (KITTI-shaped local map: half of them more than 12), and a chain of launches
-// must be sized on the host: too short and the host synchronises to continue it, too long and the
-// empty launches cost ~4 us each. Rounds R0.. therefore run in this one 1024-thread workgroup, with
-// the frame's owners in LDS, touching only what a change can reach. Measured (C5, device time per
-// search, round 4): R0 = 2 / 3 / 4 / 6 / 8 / 10: 691 / 421 / 335 / 296 / 294 / 301 us, the
-// launch chain with host continuation 295-300 us; a settle round costs ~16 us against ~12 us
-// grid-wide (one workgroup's dependent global loads), so it takes over only at R0 = 8 -- equal
-// device time without the host synchronisation. Per round:
-//   a. the keypoints whose owner differs between rounds r-2 and r-1 (owner = the smallest query
-//      index whose result is the keypoint, among queries whose assignment blocks it);
-//   b. their queries from the inverted candidate index (round 0) with lo < i <= hi: only for those
-//      does blocked(k) = owner < i flip -- the k_sbp_round test, exact rather than by window;
-//   c. re-evaluation from the candidate cache: the flagged queries compacted into an LDS list
-//      (they cluster in index ranges: a row of lanes per bitmap word left a few rows doing all
-//      the work) and dealt to groups of SETTLE_L lanes, each query's cache entries, count, result
-//      and flags loaded together; results updated in place (a round reads only the previous
-//      round's owners, never other results);
-//   d. the owners of the keypoints a changed result left or joined, recomputed from their index
-//      lists (every other keypoint keeps its owner).
-// Settled when no owner changed (the next round would reproduce this one). A keypoint listed by
-// more than SBP_INV_CAP queries makes its rounds scan every query instead (exact, slower); past
-// round_cap the reference's sequential loop runs (as k_sbp_finish does).
-struct SbpSettleArgs {
-  int32_t* res;         // round R0-1's results, updated in place to the fixpoint
-  const int32_t* own0;  // round R0-2's owners
-  const int32_t* own1;  // round R0-1's owners
-  int round0;           // R0: the first round run here
-  const int32_t* inv;
-  const int32_t* inv_n;
-  int round_cap;
-  int32_t* serial_used;
-  int32_t* blocked_scratch;
+// ---- the claim order after round 0: one workgroup, query chunk by query chunk ------------------
+// The reference assigns in query order (:51-130 local, :1371-1450 last frame): query i skips a
+// keypoint an earlier query took (mvpMapPoints[k] set, with Observations() > 0 for the local map),
+// so result(i) depends on the results of the queries before it -- a chain the grid-wide rounds
+// resolve one link per launch (8-23 rounds on the C5 scene, ~12 us each). Here round 0 (grid-wide)
+// fills the candidate cache with the candidates that can decide a result (sbp_keep_below) and
+// prunes the queries that can never match (no candidate within dist_th outside the pre-blocked
+// keypoints: cand_n = 0, no bit in the live bitmap), and one 1024-thread workgroup walks the live
+// queries in ascending order, a chunk of up to 1024 at a time:
+//   * a window of the live bitmap (SWEEP_WINDOW_WORDS words) is compacted into an LDS list, order
+//     kept; full chunks of the list are processed, the remainder carried over;
+//   * a chunk's cache entries are staged in an LDS pool (a block scan of the counts; a chunk ends
+//     where the pool is full);
+//   * within the chunk, Jacobi rounds on LDS state: every query re-evaluates from its pooled entries
+//     with blocked(k) = taken[k] (pre-blocked or claimed by an earlier chunk -- every such query
+//     index is smaller) or own[k] < i (own[k] = the smallest chunk query whose current result is k
+//     and whose assignment blocks it), until a round reproduces the previous one. The sequential
+//     results are the unique fixpoint of that map (result(i) depends only on earlier queries), and
+//     after r rounds the chunk's first r queries hold them, so a chunk of C queries settles within
+//     C + 1 rounds; chains inside one chunk are short (a few rounds); the chunk's claims are then
+//     committed to taken[];
+//   * a chunk still moving after max_rounds rounds (a debug knob: orbfe_debug_matcher_set_sweep)
+//     falls back to the reference loop over that chunk, one thread in query order.
+// Results of the live queries are written over round 0's (which are final for the pruned ones).
+struct SbpSweepArgs {
+  int32_t* res;     // round 0's result buffer, the live queries' results written in place
+  int chunk;        // live queries per chunk (1 .. SWEEP_THREADS)
+  int max_rounds;   // Jacobi rounds per chunk before the sequential walk
+  int32_t* stats;   // see orbfe_debug_matcher_sweep_stats
 };
 
-#define SETTLE_QCAP 4096  // flagged queries per pass of step c (LDS list)
-#define SETTLE_L 4        // lanes per re-evaluated query
-__host__ __device__ inline size_t settle_lds(int n, int m) {
-  return sizeof(int) * (5 * (size_t)n + SETTLE_QCAP) + 4 * (size_t)((m + 31) / 32) + 2 * 4 * (size_t)((n + 31) / 32);
+#define SWEEP_WINDOW_WORDS 512  // live-bitmap words compacted per window (16,384 queries)
+#define SWEEP_LIST (SWEEP_WINDOW_WORDS * 32 + SWEEP_THREADS)
+#define SWEEP_E 12              // cache entries a query keeps in registers for its chunk
+__host__ __device__ inline size_t sweep_lds(int n) {
+  // four owner arrays own[4][n] (three rotating, one base: -1 where a keypoint is taken), the live
+  // list (a window plus a chunk's remainder)
+  return sizeof(int) * (4 * (size_t)n + SWEEP_LIST);
 }
-constexpr int SETTLE_INV_PER_LANE = SBP_INV_CAP / 64;  // index entries per lane, loaded together
 
-__global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSettleArgs s) {
-  extern __shared__ int s_lds[];
-  __shared__ int s_cnt, s_dense, s_nq;
-  __shared__ int s_wsum[SETTLE_THREADS / 64];
-  const int n = a.F.n, m = a.m, t = threadIdx.x, wv = t >> 6, ln = t & 63;
-  constexpr int NW = SETTLE_THREADS / 64;
-  const int qw = (m + 31) >> 5, kw = (n + 31) >> 5;
-  if (a.state[0] != 0) return;  // the grid-wide rounds settled already (k_sbp_round's early exit)
-  // phase clock (thread 0, wall clock ticks): [0] prologue, [1] a, [2] b, [3] c, [4] d
-  unsigned long long tck[5] = {0, 0, 0, 0, 0}, tlast = 0;
-  if (t == 0) tlast = wall_clock64();
-  int* rm2 = s_lds;
-  int* prev = rm2 + n;
-  int* cur = prev + n;
-  int* list = cur + n;  // changed / dirty keypoints
-  uint32_t* qbits = reinterpret_cast<uint32_t*>(list + n);
-  uint32_t* dirty = qbits + qw;
-  uint32_t* pre = dirty + kw;  // keypoints taken before the search (sbp_pre_blocked)
-  int* inv_cnt = reinterpret_cast<int*>(pre + kw);  // inv_n, read every round
-  int* qlist = inv_cnt + n;                           // step c's compacted queries
-  for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
-  for (int w = t; w < kw; w += SETTLE_THREADS) {
-    dirty[w] = 0u;
-    pre[w] = 0u;
+// result of query i from its cache (or the grid walk past the cache) under `blocked`
+template <class Blocked>
+__device__ __forceinline__ int sbp_eval(const SbpArgs& a, int i, Blocked blocked) {
+  const int n = a.cand_n[i];
+  return n < 0 ? sbp_one(a, i, blocked) : sbp_cached(a, i, n, blocked);
+}
+
+// inclusive prefix sum over the workgroup (SWEEP_THREADS threads); *total = the sum
+__device__ __forceinline__ int sweep_scan_incl(int v, int* wsum, int* total) {
+  const int ln = lane_id(), wv = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (ln >= o) inc += y;
   }
-  if (t == 0) s_nq = 0;
+  if (ln == 63) wsum[wv] = inc;
   __syncthreads();
-  for (int k = t; k < n; k += SETTLE_THREADS) {  // one thread per keypoint, all loads together
-    const int o0 = s.own0[k], o1 = s.own1[k], c = s.inv_n[k];
-    const bool pb = sbp_pre_blocked(a, k);
-    rm2[k] = o0;
-    prev[k] = o1;
-    inv_cnt[k] = c;
-    if (pb) atomicOr(&pre[k >> 5], 1u << (k & 31));
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < SWEEP_THREADS / 64; q++) {
+    const int x = wsum[q];
+    if (q < wv) off += x;
+    tot += x;
   }
+  __syncthreads();  // wsum is free again
+  *total = tot;
+  return off + inc;
+}
 
+// The reference's best / second-best bookkeeping over cache entries in order (:106-118 / :1417-
+// 1450) is the two smallest (distance, position) keys over the unblocked entries (see
+// k_sbp_round0); as 32-bit keys distance << 17 | position << 5 | octave (position < 4096, octave <
+// 32), kept branch-free by min / max.
+__device__ __forceinline__ uint32_t sweep_key(uint32_t e, int pos) {
+  return ((uint32_t)cand_dist(e) << 17) | ((uint32_t)pos << 5) | (uint32_t)cand_level(e);
+}
+__device__ __forceinline__ int sweep_result(const SbpArgs& a, uint32_t k1, uint32_t k2, int k1_key) {
+  if (k1 == 0xffffffffu) return -1;
+  SbpBest b;
+  b.bestDist = (int)(k1 >> 17);
+  b.bestLevel = (int)(k1 & 31u);
+  b.bestIdx = k1_key;
+  if (k2 != 0xffffffffu) {
+    b.bestDist2 = (int)(k2 >> 17);
+    b.bestLevel2 = (int)(k2 & 31u);
+  }
+  return b.result(a.mode, a.nnratio, a.dist_th);
+}
+
+__global__ __launch_bounds__(SWEEP_THREADS) void k_sbp_sweep(SbpArgs a, SbpSweepArgs s) {
+  extern __shared__ int s_lds[];
+  __shared__ int s_wsum[SWEEP_THREADS / 64];
+  constexpr int T = SWEEP_THREADS;
+  const int n = a.F.n, m = a.m, t = threadIdx.x;
+  // own[0..2][n]: round r reads own[r % 3] (blocked(k) = own < i), claims into own[(r + 1) % 3] and
+  // resets own[(r + 2) % 3] from base[n] = -1 for a taken keypoint (pre-blocked or claimed by an
+  // earlier chunk: every such query index is smaller than the chunk's), INT_MAX otherwise
+  int* ownb = s_lds;
+  int* base = ownb + 3 * n;
+  int* list = base + n;
+  for (int k = t; k < n; k += T) {
+    const int b0 = sbp_pre_blocked(a, k) ? -1 : INT_MAX;
+    base[k] = b0;
+    ownb[k] = b0;
+    ownb[n + k] = b0;
+    ownb[2 * n + k] = b0;
+  }
+  __syncthreads();
+  const int C = s.chunk, mwords = (m + 31) >> 5;
+  int len = 0, n_chunks = 0, n_rounds = 0, n_live = 0, n_seq = 0, max_r = 0, n_over = 0;
+  // phase clock (thread 0, 100 MHz wall clock): [0] compaction, [1] the chunks' loads, [2] their
+  // rounds, [3] their commits
+  unsigned long long tck[4] = {0, 0, 0, 0}, tlast = t == 0 ? wall_clock64() : 0;
+  const unsigned long long wall0 = tlast, cyc0 = t == 0 ? clock64() : 0;  // (the shader clock's rate)
   auto tick = [&](int ph) {
     if (t == 0) {
       const unsigned long long now = wall_clock64();
@@ -1113,172 +1076,134 @@ __global__ __launch_bounds__(SETTLE_THREADS) void k_sbp_settle(SbpArgs a, SbpSet
       tlast = now;
     }
   };
-  __syncthreads();
-  tick(0);
-  int round = s.round0;
-  bool serial = false;
-  for (;; round++) {
-    if (t == 0) {
-      s_cnt = 0;
-      s_dense = 0;
+  for (int w0 = 0; w0 < mwords; w0 += SWEEP_WINDOW_WORDS) {
+    // this window's live queries appended to the list in ascending order (thread t: bitmap word w0 + t)
+    const int wi = w0 + t;
+    uint32_t bits = t < SWEEP_WINDOW_WORDS && wi < mwords ? a.live[wi] : 0u;
+    int total;
+    int pos = len + sweep_scan_incl(__popc(bits), s_wsum, &total) - __popc(bits);
+    while (bits) {
+      list[pos++] = 32 * wi + __builtin_ctz(bits);
+      bits &= bits - 1u;
     }
+    len += total;
+    n_live += total;
     __syncthreads();
-    for (int k = t; k < n; k += SETTLE_THREADS)
-      if (prev[k] != rm2[k]) list[atomicAdd(&s_cnt, 1)] = k;
-    __syncthreads();
-    tick(1);
-    const int nchg = s_cnt;
-    if (nchg == 0) break;  // round r would reproduce round r-1
-    if (round >= s.round_cap) {
-      serial = true;
-      break;
-    }
-    // b. the queries whose blocked state of a changed keypoint flips: one wavefront per keypoint
-    for (int c = wv; c < nchg; c += NW) {
-      const int k = list[c];
-      const int o1 = rm2[k], o2 = prev[k], lo = min(o1, o2), hi = max(o1, o2);
-      const int cnt = inv_cnt[k];
-      if (cnt > SBP_INV_CAP) {
-        if (ln == 0) s_dense = 1;
-        continue;
-      }
-      // every entry's load in flight before the first is used (one memory latency per keypoint)
-      const int32_t* L = s.inv + (size_t)k * SBP_INV_CAP;
-      int e[SETTLE_INV_PER_LANE];
+    tick(0);
+    const bool last = w0 + SWEEP_WINDOW_WORDS >= mwords;
+    int c0 = 0;
+    while (len - c0 >= C || (last && c0 < len)) {
+      // ---- one chunk: thread t <-> live query c0 + t, its count, flags and first SWEEP_E cache
+      //      entries in registers (loaded together) ----
+      const int cn = min(C, len - c0);
+      const int i = t < cn ? list[c0 + t] : -1;
+      int nq = 0, fl = 0;
+      uint32_t e[SWEEP_E];
+      const uint32_t* ce = nullptr;
+      if (i >= 0) {
+        ce = a.cand + (size_t)i * a.cand_cap;
 #pragma unroll
-      for (int u = 0; u < SETTLE_INV_PER_LANE; u++) e[u] = ln + 64 * u < cnt ? L[ln + 64 * u] : -1;
-#pragma unroll
-      for (int u = 0; u < SETTLE_INV_PER_LANE; u++) {
-        const int i = e[u] & 0x7fffffff;
-        if (ln + 64 * u < cnt && lo < i && i <= hi) atomicOr(&qbits[i >> 5], 1u << (i & 31));
+        for (int u = 0; u < SWEEP_E; u++) e[u] = u < a.cand_cap ? ce[u] : 0u;  // (stale past cand_n: unused)
+        nq = a.cand_n[i];
+        fl = a.q[i].flags;
       }
-    }
-    __syncthreads();
-    tick(2);
-    // c. re-evaluate them from the candidate cache with round r-1's owners
-    const bool dense = s_dense != 0;
-    if (t == 0 && dense) s.serial_used[1] += 1;
-    {
-      // compaction: thread t owns words [t per, (t + 1) per); exclusive scan of their popcounts
-      const int per = (qw + SETTLE_THREADS - 1) / SETTLE_THREADS;
-      const int w0 = min(t * per, qw), w1 = min(w0 + per, qw);
-      auto word = [&](int w) -> uint32_t {
-        uint32_t b = dense ? 0xffffffffu : qbits[w];
-        if (32 * w + 32 > m) b &= (1u << (m - 32 * w)) - 1u;  // (m - 32 w) in 1..31 here
-        return b;
-      };
-      int mine = 0;
-      for (int w = w0; w < w1; w++) mine += __popc(word(w));
-      int inc = mine;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o, 64);
-        if (ln >= o) inc += y;
-      }
-      if (ln == 63) s_wsum[wv] = inc;
-      __syncthreads();
-      int off = inc - mine, total = 0;
-      for (int q = 0; q < NW; q++) {
-        if (q < wv) off += s_wsum[q];
-        total += s_wsum[q];
-      }
-      const int g = t / SETTLE_L, j = t % SETTLE_L;
-      for (int base = 0; base < total; base += SETTLE_QCAP) {
-        int pos = off;
-        for (int w = w0; w < w1 && pos < base + SETTLE_QCAP; w++) {
-          uint32_t bits = word(w);
-          while (bits) {
-            const int i = 32 * w + __builtin_ctz(bits);
-            bits &= bits - 1u;
-            if (pos >= base && pos < base + SETTLE_QCAP) qlist[pos - base] = i;
-            pos++;
-          }
+      tick(1);
+      int res = INT_MIN, r = 0;
+      bool seq = false;
+      for (;; r++) {
+        if (r >= s.max_rounds) {
+          seq = true;
+          break;
         }
-        __syncthreads();
-        const int cnt = min(SETTLE_QCAP, total - base);
-        for (int e = g; e < cnt; e += SETTLE_THREADS / SETTLE_L) {
-          const int i = qlist[e];
-          const int old = s.res[i];
-          const int fl = a.q[i].flags;
-          auto blocked = [&](int k) { return ((pre[k >> 5] >> (k & 31)) & 1u) || prev[k] < i; };
-          int nc;
-          int r = sbp_cached_group<SETTLE_L>(a, i, j, blocked, nc);
-          if (nc == 0) continue;  // no candidate: -1 in every round
-          if (nc < 0) r = j == 0 ? sbp_one(a, i, blocked) : 0;  // past the cache: the grid walk
-          if (j == 0) {
-            atomicAdd(&s_nq, 1);
-            if (r != old) {
-              s.res[i] = r;
-              if (fl & 2) {
-                if (old >= 0) atomicOr(&dirty[old >> 5], 1u << (old & 31));
-                if (r >= 0) atomicOr(&dirty[r >> 5], 1u << (r & 31));
-              }
+        const int* own_rd = ownb + (r % 3) * n;
+        int* own_wr = ownb + ((r + 1) % 3) * n;
+        int* own_clr = ownb + ((r + 2) % 3) * n;
+        int nr = -1;
+        if (i >= 0) {
+          if (nq < 0) {  // more candidates than the cache holds: the grid walk
+            nr = sbp_one(a, i, [&](int k) { return own_rd[k] < i; });
+          } else {
+            uint32_t k1 = 0xffffffffu, k2 = 0xffffffffu;
+            int kk1 = -1;
+            int ow[SWEEP_E];
+#pragma unroll
+            for (int u = 0; u < SWEEP_E; u++) ow[u] = u < nq ? own_rd[cand_key(e[u])] : INT_MAX;  // reads in flight together
+#pragma unroll
+            for (int u = 0; u < SWEEP_E; u++) {
+              const uint32_t key = u < nq && ow[u] >= i ? sweep_key(e[u], u) : 0xffffffffu;
+              k2 = min(k2, max(k1, key));
+              kk1 = key < k1 ? cand_key(e[u]) : kk1;
+              k1 = min(k1, key);
             }
+            for (int u = SWEEP_E; u < nq; u++) {  // the rest from the cache (L2)
+              const uint32_t x = ce[u];
+              const uint32_t key = own_rd[cand_key(x)] >= i ? sweep_key(x, u) : 0xffffffffu;
+              k2 = min(k2, max(k1, key));
+              kk1 = key < k1 ? cand_key(x) : kk1;
+              k1 = min(k1, key);
+            }
+            nr = sweep_result(a, k1, k2, kk1);
           }
         }
-        __syncthreads();  // qlist is rewritten by the next pass
+        if (i >= 0 && nr >= 0 && (fl & 2)) atomicMin(&own_wr[nr], i);  // (own_wr was reset last round)
+        for (int k = t; k < n; k += T) own_clr[k] = base[k];  // next round's claim buffer
+        const bool more = __syncthreads_or(i >= 0 && nr != res);
+        if (!more) break;  // this round reproduced the last one
+        res = nr;
       }
-    }
-    tick(3);
-    for (int w = t; w < qw; w += SETTLE_THREADS) qbits[w] = 0u;
-    // d. round r's owners: round r-1's, recomputed where a result left or joined the keypoint
-    for (int k = t; k < n; k += SETTLE_THREADS) cur[k] = prev[k];
-    if (t == 0) s_cnt = 0;
-    __syncthreads();
-    for (int w = t; w < kw; w += SETTLE_THREADS) {
-      uint32_t bits = dirty[w];
-      dirty[w] = 0u;
-      while (bits) {
-        list[atomicAdd(&s_cnt, 1)] = 32 * w + __builtin_ctz(bits);
-        bits &= bits - 1u;
+      tick(2);
+      if (seq) {  // the reference loop over this chunk (debug knob only: C + 1 rounds always settle)
+        __syncthreads();
+        if (t == 0) {
+          for (int c = 0; c < cn; c++) {
+            const int qi = list[c0 + c];
+            const int rr = sbp_eval(a, qi, [&](int k) { return base[k] < 0; });
+            s.res[qi] = rr;
+            if (rr >= 0 && (a.q[qi].flags & 2)) base[rr] = -1;
+          }
+          n_seq++;
+        }
+      } else if (i >= 0) {  // commit the chunk's claims
+        s.res[i] = res;
+        if (res >= 0 && (fl & 2)) base[res] = -1;
       }
-    }
-    __syncthreads();
-    const int nd = s_cnt;
-    if (t == 0) s.serial_used[3] += nd;
-    for (int c = wv; c < nd; c += NW) {
-      const int k = list[c];
-      const int cnt = inv_cnt[k];
-      int best = 0x7fffffff;
-      if (cnt > SBP_INV_CAP) {  // claimants not all indexed: every query
-        for (int i = ln; i < m; i += 64)
-          if (s.res[i] == k && (a.q[i].flags & 2)) best = min(best, i);
-      } else {  // the claiming entries' results, all loads in flight together
-        const int32_t* L = s.inv + (size_t)k * SBP_INV_CAP;
-        int e[SETTLE_INV_PER_LANE], r[SETTLE_INV_PER_LANE];
-#pragma unroll
-        for (int u = 0; u < SETTLE_INV_PER_LANE; u++) e[u] = ln + 64 * u < cnt ? L[ln + 64 * u] : 0;
-#pragma unroll
-        for (int u = 0; u < SETTLE_INV_PER_LANE; u++) r[u] = e[u] < 0 ? s.res[e[u] & 0x7fffffff] : -2;
-#pragma unroll
-        for (int u = 0; u < SETTLE_INV_PER_LANE; u++)
-          if (r[u] == k) best = min(best, e[u] & 0x7fffffff);
+      __syncthreads();
+      // every owner buffer back to the base for the next chunk
+      for (int k = t; k < n; k += T) {
+        const int b0 = base[k];
+        ownb[k] = b0;
+        ownb[n + k] = b0;
+        ownb[2 * n + k] = b0;
       }
-      best = wave_min(best);
-      if (ln == 0) cur[k] = best;
+      const int n_ov = __syncthreads_count(i >= 0 && nq < 0);
+      tick(3);
+      n_chunks++;
+      n_over += n_ov;
+      n_rounds += r;
+      max_r = max(max_r, r);
+      c0 += cn;
     }
+    // the remainder (< C <= T entries) to the front of the list
+    const int rem = len - c0;
+    const int v = t < rem ? list[c0 + t] : 0;
     __syncthreads();
-    tick(4);
-    int* tmp = rm2;
-    rm2 = prev;
-    prev = cur;
-    cur = tmp;
+    if (t < rem) list[t] = v;
+    __syncthreads();
+    len = rem;
   }
-  if (serial && t == 0) {  // the reference loop verbatim (:51-130 / :1371-1450)
-    *s.serial_used = 1;
-    for (int k = 0; k < n; k++) s.blocked_scratch[k] = sbp_pre_blocked(a, k);
-    for (int i = 0; i < m; i++) {
-      const int r = sbp_one(a, i, [&](int k) { return s.blocked_scratch[k] != 0; });
-      s.res[i] = r;
-      if (r >= 0) s.blocked_scratch[r] = (a.q[i].flags & 2) ? 1 : 0;
-    }
-  }
-  if (t == 0) {  // for k_sbp_collect / k_sbp_finish and the round statistics
-    s.serial_used[2] = s_nq;
-    for (int ph = 0; ph < 5; ph++) s.serial_used[4 + ph] = (int32_t)tck[ph];
-    a.state[0] = 1;
-    a.state[1] = round;  // rounds run (the last computed one + 1)
-    a.state[SBP_FINAL_SLOT] = ((s.round0 - 1) & 1) + 1;  // the results stay in round R0-1's buffer
+  if (t == 0) {
+    s.stats[1] = n_chunks;
+    s.stats[2] = n_rounds;
+    s.stats[3] = n_live;
+    s.stats[4] = n_seq;
+    s.stats[5] = max_r;
+    for (int ph = 0; ph < 4; ph++) s.stats[6 + ph] = (int32_t)tck[ph];
+    s.stats[10] = n_over;
+    s.stats[11] = (int32_t)((clock64() - cyc0) / 1000);  // shader cycles / 1000 over the kernel
+    s.stats[12] = (int32_t)(wall_clock64() - wall0);     // 100 MHz ticks over the kernel
+    a.state[0] = 1;          // converged: k_sbp_collect / k_sbp_finish take the results
+    a.state[1] = max_r + 1;  // (round statistics: round 0 + the deepest chunk)
+    a.state[SBP_FINAL_SLOT] = 1;  // in round 0's buffer (res_final[0])
   }
 }
 
@@ -1301,7 +1226,7 @@ __device__ __forceinline__ bool sbp_converged(const SbpArgs& a) {
   return a.state[0] != 0 || (rounds >= 2 && a.state[2 + rounds - 1] == 0);
 }
 
-// The final results: round state[1]-1's buffer, or the one k_sbp_settle updated in place.
+// The final results: round state[1]-1's buffer, or the one k_sbp_sweep updated in place.
 __device__ __forceinline__ const int32_t* sbp_final(const SbpFinishArgs& f) {
   const int slot = f.s.state[SBP_FINAL_SLOT];
   return slot ? f.res_final[slot - 1] : f.res_final[(f.s.state[1] - 1) & 1];
@@ -1867,17 +1792,32 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
   p.oblk = ar.add(4 * f1);
   p.ostate = ar.add(4 * (SBP_ROUND_CAP + 4));
   p.obest = ar.add(4 * q1);
-  p.cache = F->n <= 32767;  // candidate keypoint indices are int16
+  p.cache = F->n <= 65535;  // candidate keypoint indices are 16-bit (cand_pack)
   const size_t cq = p.cache ? (size_t)cand_cap * q1 : 0;
-  p.ocand_k = ar.add(2 * cq);
-  p.ocand_d = ar.add(cq);
-  p.ocand_l = ar.add(cq);
+  p.ocand = ar.add(4 * cq);
   p.ocand_n = ar.add(p.cache ? 4 * q1 : 0);
   p.onm = ar.add(4);
   p.oown3 = ar.add(4 * f1);
-  p.settle = p.cache && F->n <= SETTLE_MAX_KEYS && p.nq <= SETTLE_MAX_QUERIES && p.nq > 0;
-  p.oinv_n = ar.add(p.settle ? 4 * f1 : 0);
-  p.oinv = ar.add(p.settle ? 4 * f1 * SBP_INV_CAP : 0);
+  // k_sbp_sweep keeps own[n] and the taken bits of the frame's keypoints in LDS
+  p.sweep = p.cache && p.nq > 0 && F->n <= SWEEP_MAX_KEYS;
+  p.olive = ar.add(p.sweep ? 4 * ((q1 + 31) / 32) : 0);
+}
+int sbp_cand_cap(const orbfe_matcher* m) { return m->cand_cap > 0 ? m->cand_cap : SBP_CAND; }
+
+// The distance from which a candidate can no longer decide a SearchByProjection result, whatever the
+// claims (the sweep's round 0 leaves such candidates out of the cache). A result needs bestDist <=
+// dist_th, so in first-minimum mode (1) only candidates within dist_th matter: a query whose
+// smallest unblocked distance exceeds it gets -1 with or without the others. In mode 0 the ratio
+// test (:122-129) also reads bestDist2: it rejects only if bestDist > nnratio * bestDist2 with
+// bestDist <= dist_th, so a second-best d2 with nnratio * d2 >= dist_th (float, as the reference
+// computes it) never rejects -- and neither does 256, the value d2 takes when such candidates are
+// left out. The best candidate itself is within dist_th or the result is -1 either way.
+static int sbp_keep_below(const SbpMode& md, float nnratio) {
+  if (md.mode != 0) return std::min(256, md.dist_th + 1);
+  if (!(nnratio > 0.f)) return 256;
+  for (int d = std::max(md.dist_th + 1, 1); d < 256; d++)
+    if (nnratio * (float)d >= (float)md.dist_th) return d;
+  return 256;
 }
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap) {
   SbpPlan p;
@@ -1934,21 +1874,20 @@ static SbpArgs sbp_args(uint8_t* A, const SbpPlan& p, const orbfe_frame_view* F,
   a.block_any = md.block_any;
   a.cand_cap = p.cand_cap;
   a.no_claims = md.no_claims;
+  a.keep_below = 256;
   a.state = (int32_t*)(A + p.ostate);
   if (p.cache) {
-    a.cand_k = (int16_t*)(A + p.ocand_k);
-    a.cand_d = A + p.ocand_d;
-    a.cand_l = A + p.ocand_l;
+    a.cand = (uint32_t*)(A + p.ocand);
     a.cand_n = (int32_t*)(A + p.ocand_n);
   }
   (void)F;
   return a;
 }
 
-static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, bool settle = false) {
+static void sbp_launch_init(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, bool sweep = false) {
   uint8_t* A = m->arena;
   SbpInit in;
-  in.inv_n = settle ? (int32_t*)(A + p.oinv_n) : nullptr;
+  in.live = sweep ? (uint32_t*)(A + p.olive) : nullptr;
   in.res0 = (int32_t*)(A + p.ores0);
   in.res1 = (int32_t*)(A + p.ores1);
   in.own0 = (int32_t*)(A + p.oown0);
@@ -1982,8 +1921,8 @@ void sbp_launch_round0(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
 // Rounds r0 .. r1-1 of the fixpoint, then collect / finish (owner buffers rotate over four:
 // round r claims into own[r % 4], reads own[(r + 3) % 4] (round r-1) and own[(r + 2) % 4]
 // (round r-2), and clears own[(r + 1) % 4] for round r + 1, which nobody reads during round r).
-// `settled`: the settle path ran (the fixpoint is complete on the device, k_sbp_settle ran the
-// serial walk itself if it had to), so without a rotation filter k_sbp_finish has nothing to do.
+// `settled`: the sweep ran (the claim order is complete on the device), so without a rotation
+// filter k_sbp_finish has nothing to do.
 static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs& a, const SbpMode& md,
                               int32_t* const res_final[2], bool defer, bool settled = false) {
   uint8_t* A = m->arena;
@@ -2004,56 +1943,35 @@ static void sbp_finish_launch(orbfe_matcher* m, const SbpPlan& p, const SbpArgs&
     ORBFE_LAUNCH("k_sbp_finish", k_sbp_finish, dim3(1), dim3(256), 0, m->stream, f, (int32_t*)(A + p.oblk));
 }
 
-// Rounds 0 .. R0-1 grid-wide (round 0 fills the candidate cache and the inverted index; the early
-// rounds change many owners, work one workgroup would take long over), the rest in k_sbp_settle,
-// then collect / finish: R0 + 3 launches whatever the depth of the claim order.
-static int sbp_settle_from(const orbfe_matcher* m) {
-  // the range orbfe_debug_matcher_set_settle_from accepts: k_sbp_round writes state[2 + round]
-  // below SBP_FINAL_SLOT only for rounds < SBP_MAX_ROUNDS
-  static const int r0 = std::getenv("ORBFE_SBP_SETTLE_FROM")
-                            ? std::min(SBP_MAX_ROUNDS, std::max(2, std::atoi(std::getenv("ORBFE_SBP_SETTLE_FROM"))))
-                            : SBP_SETTLE_FROM;
-  return m->settle_from >= 2 ? m->settle_from : r0;
-}
-static void sbp_settle_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
-                              const orbfe_frame_view& dF, const SbpMode& md) {
+// Round 0 grid-wide (the candidate cache; queries that can never match pruned), then the claim
+// order in k_sbp_sweep, then collect / finish: 4 launches after the grid whatever the depth of the
+// claim order.
+static void sbp_sweep_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F,
+                             const orbfe_frame_view& dF, const SbpMode& md) {
   uint8_t* A = m->arena;
   const int nq = p.nq;
   SbpArgs a = sbp_args(A, p, F, dF, md, m->nnratio);
   int32_t* res[2] = {(int32_t*)(A + p.ores0), (int32_t*)(A + p.ores1)};
-  int32_t* own[4] = {(int32_t*)(A + p.oown0), (int32_t*)(A + p.oown1), (int32_t*)(A + p.oown2),
-                     (int32_t*)(A + p.oown3)};
-  const int R0 = sbp_settle_from(m);
-  for (int r = 0; r < R0; r++) {
-    a.round = r;
-    a.res_cur = res[r & 1];
-    a.res_prev = res[(r + 1) & 1];
-    a.owner_cur = own[r % 4];
-    a.owner_prev = own[(r + 3) % 4];
-    a.owner_next = own[(r + 1) % 4];
-    a.owner_rm2 = r >= 2 ? own[(r + 2) % 4] : nullptr;
-    if (r == 0) {
-      a.inv = (int32_t*)(A + p.oinv);
-      a.inv_n = (int32_t*)(A + p.oinv_n);
-      ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
-                   m->stream, a);
-      a.inv = a.inv_n = nullptr;
-    } else {
-      ORBFE_LAUNCH("k_sbp_round", k_sbp_round, dim3((std::max(nq, F->n) + 255) / 256), dim3(256), 0, m->stream, a);
-    }
-  }
-  SbpSettleArgs st;
-  st.res = res[(R0 - 1) & 1];  // round R0-1's results and the owners of rounds R0-2, R0-1
-  st.own0 = own[(R0 - 2) % 4];
-  st.own1 = own[(R0 - 1) % 4];
-  st.round0 = R0;
-  st.inv = (const int32_t*)(A + p.oinv);
-  st.inv_n = (const int32_t*)(A + p.oinv_n);
-  st.round_cap = m->round_cap;
-  st.serial_used = m->d_serial;
-  st.blocked_scratch = (int32_t*)(A + p.oblk);
-  const size_t lds = settle_lds(F->n, nq);
-  ORBFE_LAUNCH("k_sbp_settle", k_sbp_settle, dim3(1), dim3(SETTLE_THREADS), lds, m->stream, a, st);
+  a.round = 0;
+  a.res_cur = res[0];
+  a.res_prev = res[1];
+  a.owner_cur = (int32_t*)(A + p.oown0);
+  a.owner_prev = (int32_t*)(A + p.oown3);
+  a.owner_next = (int32_t*)(A + p.oown1);
+  a.owner_rm2 = nullptr;
+  a.prune = 1;
+  a.live = (uint32_t*)(A + p.olive);
+  a.keep_below = sbp_keep_below(md, m->nnratio);
+  ORBFE_LAUNCH("k_sbp_round0", k_sbp_round0, dim3(std::max((nq + 15) / 16, (F->n + 255) / 256)), dim3(256), 0,
+               m->stream, a);
+  a.prune = 0;
+  a.keep_below = 256;
+  SbpSweepArgs sw;
+  sw.res = res[0];
+  sw.chunk = m->sweep_chunk > 0 ? std::min(m->sweep_chunk, SWEEP_THREADS) : SWEEP_THREADS;
+  sw.max_rounds = m->sweep_max_rounds > 0 ? m->sweep_max_rounds : sw.chunk + 2;
+  sw.stats = m->d_serial;
+  ORBFE_LAUNCH("k_sbp_sweep", k_sbp_sweep, dim3(1), dim3(SWEEP_THREADS), sweep_lds(F->n), m->stream, a, sw);
   sbp_finish_launch(m, p, a, md, res, false, true);
 }
 
@@ -2084,30 +2002,31 @@ static void sbp_rounds(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_vie
   if (nq > 0) sbp_finish_launch(m, p, a, md, res, defer);
 }
 
-// ORBFE_SBP_SETTLE=0: the fixpoint as one launch per round (rounds 1-3's engine, for A/B)
-static bool sbp_settle_enabled() {
-  static const bool on = !(std::getenv("ORBFE_SBP_SETTLE") && std::atoi(std::getenv("ORBFE_SBP_SETTLE")) == 0);
+// ORBFE_SBP_SWEEP=0: the claim order as grid-wide Jacobi rounds, one launch each, continued by
+// the host (rounds 1-4's engine, for A/B)
+static bool sbp_sweep_enabled() {
+  static const bool on = !(std::getenv("ORBFE_SBP_SWEEP") && std::atoi(std::getenv("ORBFE_SBP_SWEEP")) == 0);
   return on;
 }
 
 int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const orbfe_frame_view& dF,
                const SbpMode& md, bool defer) {
   sbp_launch_grid(m, p, F, dF);
-  // the settle path unless rounds are restricted (orbfe_matcher_set_max_rounds: the serial
-  // fallback's tests) or no assignment blocks anything (one round is the result)
-  bool settle = p.settle && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_settle_enabled();
-  if (settle && m->settle_attr == 0) {
-    // k_sbp_settle's dynamic LDS (up to ~113 KiB) on this matcher's device, checked once per
-    // matcher (one thread per matcher; the attribute is per device); refused: no settle path here
-    const hipError_t e = hipFuncSetAttribute((const void*)k_sbp_settle, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)settle_lds(SETTLE_MAX_KEYS, SETTLE_MAX_QUERIES));
-    m->settle_attr = e == hipSuccess ? 1 : -1;
+  // the sweep unless rounds are restricted (orbfe_matcher_set_max_rounds: the serial fallback's
+  // tests) or no assignment blocks anything (one round is the result)
+  bool sweep = p.sweep && !md.no_claims && m->round_cap >= SBP_MAX_ROUNDS && sbp_sweep_enabled();
+  if (sweep && m->sweep_attr == 0) {
+    // k_sbp_sweep's dynamic LDS (up to ~70 KiB) on this matcher's device, checked once per matcher
+    // (one thread per matcher; the attribute is per device); refused: the grid-wide rounds instead
+    const hipError_t e = hipFuncSetAttribute((const void*)k_sbp_sweep, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)sweep_lds(SWEEP_MAX_KEYS));
+    m->sweep_attr = e == hipSuccess ? 1 : -1;
     if (e != hipSuccess) (void)hipGetLastError();
   }
-  settle = settle && m->settle_attr > 0;
-  sbp_launch_init(m, p, F, settle);
-  if (settle) {
-    sbp_settle_rounds(m, p, F, dF, md);
+  sweep = sweep && m->sweep_attr > 0;
+  sbp_launch_init(m, p, F, sweep);
+  if (sweep) {
+    sbp_sweep_launch(m, p, F, dF, md);
   } else {
     const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
     sbp_rounds(m, p, F, dF, md, 0, rounds, defer && m->round_cap > rounds);
@@ -2195,7 +2114,7 @@ static int run_sbp(orbfe_matcher* m, const orbfe_frame_view* F, int nq, const Sb
                    int32_t* best_idx, int* nmatches) {
   Arena ar;
   SbpPlan p;
-  sbp_plan_inputs(ar, F, nq, SBP_CAND, p);
+  sbp_plan_inputs(ar, F, nq, sbp_cand_cap(m), p);
   plan_q(ar);
   sbp_plan_scratch(ar, F, p);
   int st = ensure_arena(m, ar.total);
@@ -2334,16 +2253,19 @@ extern "C" int orbfe_matcher_set_max_rounds(orbfe_matcher* m, int rounds) {
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_matcher_set_settle_from(orbfe_matcher* m, int round0) {
-  if (!m || (round0 != 0 && (round0 < 2 || round0 > SBP_MAX_ROUNDS))) return ORBFE_ERR_ARG;
-  m->settle_from = round0;
+extern "C" int orbfe_debug_matcher_set_sweep(orbfe_matcher* m, int chunk, int max_rounds, int cand_cap) {
+  if (!m || chunk < 0 || chunk > SWEEP_THREADS || max_rounds < 0 || cand_cap < 0 || cand_cap > 4096)
+    return ORBFE_ERR_ARG;
+  m->sweep_chunk = chunk;
+  m->sweep_max_rounds = max_rounds;
+  m->cand_cap = cand_cap;
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_matcher_settle_stats(orbfe_matcher* m, int32_t* out8) {
-  if (!m || !out8) return ORBFE_ERR_ARG;
+extern "C" int orbfe_debug_matcher_sweep_stats(orbfe_matcher* m, int32_t* out12) {
+  if (!m || !out12) return ORBFE_ERR_ARG;
   ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
-  ORBFE_HIP_CHECK(hipMemcpy(out8, m->d_serial + 1, 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  ORBFE_HIP_CHECK(hipMemcpy(out12, m->d_serial + 1, 12 * sizeof(int32_t), hipMemcpyDeviceToHost));
   return ORBFE_OK;
 }
 

@@ -27,11 +27,8 @@
 #define GRID_MAX_KEYS 8192   // frame keypoints per matcher call (k_grid sorts them in LDS)
 #define SFT_MAX_KF2 16384    // KF2 keypoints per SearchForTriangulation pair (claim bitmap)
 #define SBP_CAND 48          // default per-query candidate cache of the projection searches
-#define SBP_INV_CAP 1024     // queries per keypoint in the settle path's inverted candidate index
-#define SETTLE_THREADS 1024  // k_sbp_settle: one workgroup for the fixpoint's rounds R0..
-#define SBP_SETTLE_FROM 8    // R0: rounds 0 .. R0-1 grid-wide (ORBFE_SBP_SETTLE_FROM overrides)
-#define SETTLE_MAX_KEYS 4096       // settle path: frame keypoints (owners in LDS) ...
-#define SETTLE_MAX_QUERIES 131072  // ... and queries (a bitmap in LDS)
+#define SWEEP_THREADS 1024   // k_sbp_sweep: one workgroup walks the claim order chunk by chunk
+#define SWEEP_MAX_KEYS 4096  // frame keypoints k_sbp_sweep keeps owners of in LDS (more: grid rounds)
 #define ORBFE_MAX_LEVELS_M 32
 
 struct orbfe_matcher {
@@ -57,10 +54,12 @@ struct orbfe_matcher {
   int last_rounds = 0, last_serial = 0;
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
-  int settle_from = 0;            // orbfe_debug_matcher_set_settle_from (0: SBP_SETTLE_FROM)
-  // k_sbp_settle's dynamic-LDS limit on this matcher's device: 0 not set yet, 1 set, -1 refused
-  // (the settle path is then off for this matcher)
-  int settle_attr = 0;
+  // orbfe_debug_matcher_set_sweep (0: the defaults): queries per k_sbp_sweep chunk, Jacobi rounds a
+  // chunk may take before its sequential walk, cache entries per query (SBP_CAND)
+  int sweep_chunk = 0, sweep_max_rounds = 0, cand_cap = 0;
+  // k_sbp_sweep's dynamic-LDS limit on this matcher's device: 0 not set yet, 1 set, -1 refused
+  // (the sweep is then off for this matcher)
+  int sweep_attr = 0;
   // orbfe_matcher_set_profiling: HIP events around the device part (first kernel .. last kernel,
   // no H2D / D2H) of each SearchByProjection-family call
   int profile = 0;
@@ -82,6 +81,15 @@ inline void prof_end(orbfe_matcher* m) {
     m->prof_done = true;
   }
 }
+
+// SearchByProjection's per-query candidate cache entry: keypoint index | Hamming distance << 16 |
+// octave << 24 (one dword per candidate; a distance of 256 is never cached)
+__host__ __device__ __forceinline__ uint32_t cand_pack(int k, int dist, int level) {
+  return (uint32_t)k | ((uint32_t)dist << 16) | ((uint32_t)level << 24);
+}
+__host__ __device__ __forceinline__ int cand_key(uint32_t e) { return (int)(e & 0xffffu); }
+__host__ __device__ __forceinline__ int cand_dist(uint32_t e) { return (int)((e >> 16) & 0xffu); }
+__host__ __device__ __forceinline__ int cand_level(uint32_t e) { return (int)(e >> 24); }
 
 // ---- device helpers shared by the matcher kernels ---------------------------------------------
 __device__ __forceinline__ int rot_bin_dev(float a1, float a2) {
@@ -185,14 +193,17 @@ bool levels_ok(const orbfe_keypoint* k, int n, int nlevels);
 struct SbpPlan {
   FrameOffsets fo;
   size_t oqd, oqa, og_start, og_items, oq, ores0, ores1, oown0, oown1, oown2, oblk, ostate, obest;
-  size_t ocand_k, ocand_d, ocand_l, ocand_n, onm, oown3, oinv, oinv_n;
+  size_t ocand, ocand_n, onm, oown3, olive;
   bool cache;
-  bool settle;  // the fixpoint's rounds R0.. in k_sbp_settle (cache, frame and query bounds)
+  bool sweep;  // the claim order in k_sbp_sweep after round 0 (the candidate cache exists)
   int nq, cand_cap;
 };
 SbpPlan sbp_plan(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap = SBP_CAND);
 // the two halves of sbp_plan: staged inputs, then device scratch (plan other staged inputs between)
 void sbp_plan_inputs(Arena& ar, const orbfe_frame_view* F, int nq, int cand_cap, SbpPlan& p);
+// the candidate cache entries per query of matcher m's projection searches (SBP_CAND, or the
+// orbfe_debug_matcher_set_sweep override)
+int sbp_cand_cap(const orbfe_matcher* m);
 void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p);
 // stages the frame and the query descriptors / angles (flush before launching)
 int sbp_stage(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, const uint8_t* h_qdesc,

@@ -254,7 +254,7 @@ int run_projection(orbfe_matcher* m, const orbfe_frame_view* target, const orbfe
   hipSetDevice(m->device);
   Arena ar;
   SbpPlan p;
-  sbp_plan_inputs(ar, target, pts->m, SBP_CAND, p);
+  sbp_plan_inputs(ar, target, pts->m, sbp_cand_cap(m), p);
   const GeomOffsets go = plan_geom(ar, pts, need_normal);
   sbp_plan_scratch(ar, target, p);
   int st = ensure_arena(m, ar.total);
@@ -359,8 +359,8 @@ extern "C" int orbfe_search_by_sim3(orbfe_matcher* m, const orbfe_frame_view* kf
   // two searches (KF1's points into KF2, KF2's into KF1) in one arena, then the agreement kernel
   Arena ar;
   SbpPlan p1, p2;
-  sbp_plan_inputs(ar, kf2, mps1->m, SBP_CAND, p1);
-  sbp_plan_inputs(ar, kf1, mps2->m, SBP_CAND, p2);
+  sbp_plan_inputs(ar, kf2, mps1->m, sbp_cand_cap(m), p1);
+  sbp_plan_inputs(ar, kf1, mps2->m, sbp_cand_cap(m), p2);
   const GeomOffsets g1 = plan_geom(ar, mps1, false), g2 = plan_geom(ar, mps2, false);
   sbp_plan_scratch(ar, kf2, p1);
   sbp_plan_scratch(ar, kf1, p2);

@@ -40,13 +40,14 @@ def main():
     dt = (time.perf_counter() - t0) / (reps * len(frames))
     n = reps * len(frames)
     rounds = m.last_stats()[0]
-    st = np.zeros(8, np.int32)
-    L.check(L.lib().orbfe_debug_matcher_settle_stats(m._h, L.ptr(st)), "settle_stats")
+    st = np.zeros(16, np.int32)
+    L.check(L.lib().orbfe_debug_matcher_sweep_stats(m._h, L.ptr(st)), "sweep_stats")
     print(f"c5: {len(G.flags)} MapPoints, {np.mean([F.N for F in frames]):.0f} keypoints per frame, "
-          f"{1e3 * dt:.3f} ms per search (host buffers), device {1e3 * np.mean(dev):.1f} us per search, "
-          f"{reps * len(frames)} searches, {rounds} rounds in the last; settle (last search): dense rounds "
-          f"{st[0]}, queries re-evaluated {st[1]}, owners recomputed {st[2]}; ticks (10 ns) prologue / a / b / c / d "
-          f"{st[3]} / {st[4]} / {st[5]} / {st[6]} / {st[7]}")
+          f"{1e3 * dt:.3f} ms per search (host buffers), device {1e3 * np.mean(dev):.1f} us per search "
+          f"(median {1e3 * np.median(dev):.1f}), {reps * len(frames)} searches; sweep (last search): chunks {st[0]}, "
+          f"rounds {st[1]}, live queries {st[2]}, sequential chunks {st[3]}, deepest chunk {st[4]} rounds; "
+          f"ticks (10 ns) compaction / staging / rounds / commits {st[5]} / {st[6]} / {st[7]} / {st[8]}; "
+          f"past the cache {st[9]}; kernel: {st[10]} k shader cycles in {st[11]} ticks = {st[10] * 1e5 / max(st[11], 1):.0f} MHz")
     print("rounds per search:", dict(sorted(Counter(rounds_all).items())))
     if "--per-kernel" in sys.argv:
         L.ktimer_select(False)

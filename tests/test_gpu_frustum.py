@@ -142,12 +142,23 @@ def test_c5_shape_50k_mappoints(require_gpu):
     assert (nnm, nnv) == (nm, nv) and np.array_equal(nbest, best)
 
 
-@pytest.mark.parametrize("settle_from", [2, 3, 5])
-def test_c5_shape_settle_kernel_through_most_rounds(require_gpu, settle_from):
-    """SearchByProjection's one-workgroup fixpoint (k_sbp_settle) taking over from round 2, 3 or 5
-    instead of 8, so it runs most of the claim order's rounds on the C5 scene (8-23 rounds per
-    search on these frames): the same best_idx as the oracle and as the default schedule, over
-    several frames, and its statistics show it re-evaluated queries."""
+# orbfe_debug_matcher_set_sweep knobs: (chunk, max_rounds, cand_cap); 0 = default
+SWEEP_CASES = {
+    "default": (0, 0, 0),
+    "chunk64": (64, 0, 0),         # claims committed across ~80 chunks
+    "chunk7": (7, 0, 0),           # odd chunks
+    "cap6": (256, 0, 6),           # a 6-entry cache: the queries past it walk the grid
+    "sequential": (128, 1, 0),     # one Jacobi round per chunk: the reference loop per chunk
+}
+
+
+@pytest.mark.parametrize("case", sorted(SWEEP_CASES))
+def test_c5_shape_sweep_kernel(require_gpu, case):
+    """SearchByProjection's claim order in k_sbp_sweep (one workgroup, live queries chunk by chunk
+    after round 0 pruned the ones that can never match) on the C5 scene, with its test knobs: small
+    and odd chunks, a small cache (queries past it walk the grid), and the per-chunk sequential
+    walk. The same best_idx as the oracle and as the
+    default matcher over several frames; the statistics show the pruning and the chunks."""
     from orb_slam2_2021_amd import _lib as L
     ext = ORBextractor(2000, 1.2, 8, 12, 7)
     k0, d0 = ext(synth_frame(7, 480, 640))
@@ -156,20 +167,25 @@ def test_c5_shape_settle_kernel_through_most_rounds(require_gpu, settle_from):
     F0 = S.make_frame(k0, d0, sc, s2, 480, 640, S.ARDUCAM_CAM, rng, mp_frac=0.0, tcw=S.pose(tx=0.1, yaw=0.02))
     G = S.make_local_map(F0, 50000, rng)
     m, ref = ORBmatcher(0.8, True), ORBmatcher(0.8, True)
-    L.check(L.lib().orbfe_debug_matcher_set_settle_from(m._h, settle_from), "set_settle_from")
-    reevaluated = 0
+    chunk, max_rounds, cap = SWEEP_CASES[case]
+    L.check(L.lib().orbfe_debug_matcher_set_sweep(m._h, chunk, max_rounds, cap), "set_sweep")
     for seed, tx in ((103, 0.106), (104, 0.112), (105, 0.094)):
         k, d = ext(synth_frame(seed, 480, 640))
         F = S.Frame(keys_un=k, descriptors=d, u_right=np.full(len(k), -1.0, np.float32),
                     mp_state=np.zeros(len(k), np.uint8), scale_factors=sc, level_sigma2=s2, min_x=0.0, max_x=640.0,
                     min_y=0.0, max_y=480.0, tcw=S.pose(tx=tx, yaw=0.023), **S.ARDUCAM_CAM)
         nm, best, nv, _ = m.SearchLocalPoints(F, G, 3.0)
-        st = np.zeros(8, np.int32)
-        L.check(L.lib().orbfe_debug_matcher_settle_stats(m._h, L.ptr(st)), "settle_stats")
-        reevaluated += int(st[1])
+        st = np.zeros(16, np.int32)
+        L.check(L.lib().orbfe_debug_matcher_sweep_stats(m._h, L.ptr(st)), "sweep_stats")
+        chunks, rounds, live, seq, max_r = (int(x) for x in st[:5])
+        assert 0 < live < nv, "round 0 prunes the queries that cannot match"
+        assert chunks >= (live + (chunk or 1024) - 1) // (chunk or 1024)
+        if case == "sequential":
+            assert seq == chunks and max_r == 1
+        else:
+            assert seq == 0 and rounds >= chunks and max_r >= 1
         rnm, rbest, rnv, _ = ref.SearchLocalPoints(F, G, 3.0)
         assert (nm, nv) == (rnm, rnv) and np.array_equal(best, rbest)
         wnm, wbest, wnv, _ = orbref.search_local_points(F, G, log_scale_factor(1.2), 3.0, 0.8)
         assert (nm, nv) == (wnm, wnv) and np.array_equal(best, wbest), \
             f"best_idx differs at {np.flatnonzero(best != wbest)[:5]}"
-    assert reevaluated > 0

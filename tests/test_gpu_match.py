@@ -213,11 +213,12 @@ def test_search_by_projection_lastframe_kitti(require_gpu, kitti_seq_frame, mono
     assert nm > 100
 
 
+@pytest.mark.parametrize("sweep", [(0, 0, 0), (16, 0, 0), (64, 0, 5), (32, 1, 0)])
 @pytest.mark.parametrize("check_ori", [False, True])
-def test_search_by_projection_lastframe_settle_from_round_2(require_gpu, kitti_seq_frame, check_ori):
-    """The last-frame search with the one-workgroup fixpoint kernel taking over from round 2 (every
-    round after the first two in k_sbp_settle): the oracle's result, with the rotation filter's
-    undo codes."""
+def test_search_by_projection_lastframe_sweep_knobs(require_gpu, kitti_seq_frame, check_ori, sweep):
+    """The last-frame search (first-minimum mode, TH_HIGH, rotation filter) through k_sbp_sweep with
+    its test knobs -- small chunks, a 5-entry cache (queries past it walk the grid), the per-chunk
+    sequential walk: the oracle's result, with the rotation filter's undo codes."""
     from orb_slam2_2021_amd import _lib as L
     k, d, scale, sigma2 = kitti_seq_frame
     rng = np.random.default_rng(211)
@@ -225,7 +226,7 @@ def test_search_by_projection_lastframe_settle_from_round_2(require_gpu, kitti_s
                      tcw=S.pose(tz=-1.0, yaw=0.01))
     last = S.make_lastframe(C, 1800, rng, None)
     m = ORBmatcher(0.9, check_ori)
-    L.check(L.lib().orbfe_debug_matcher_set_settle_from(m._h, 2), "set_settle_from")
+    L.check(L.lib().orbfe_debug_matcher_set_sweep(m._h, *sweep), "set_sweep")
     nm, best = m.SearchByProjection(C, last, 15.0, bMono=True)
     nr, rb = orbref.search_by_projection_lastframe(C, last, 15.0, True, check_ori)
     assert nm == nr and np.array_equal(best, rb)
