@@ -80,6 +80,7 @@ struct LevelDesc {
   int tile_begin, tiles_x;   // k_blur tiles of this level; full-width (BS_W) column strips
   int rgrp_begin, rwin_ok;   // k_resize 4-column group tables; 1 when every group's taps fit 8 bytes
   int ini_thr[8];            // smallest x with (int)(x / hx) >= b, b = 1..7 (initial node of key x)
+  int ftile_begin, nftiles;  // k_fast_map tiles of this level
 };
 
 struct CellDesc {
@@ -122,6 +123,9 @@ struct ExtractArgs {
   int umax[16];
   AtanConsts atan;
   float factor_pi;
+  uint8_t* fmap;          // k_fast_map: per-pixel arc strength, pyramid layout
+  const int4* ftiles;     // k_fast_map tiles {level, first column, first row, end row}
+  int fc_rs, fc_lds;      // k_fast_cells: LDS map row stride and bytes per wavefront
 };
 
 __constant__ int8_t c_pattern[1024];
@@ -981,6 +985,208 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       const uint64_t bal = wave_ballot(keep);
       if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, sc);
       count += __popcll(bal);
+    }
+    if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
+  }
+  if (lane == 0) *cnt_out = count;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same FAST (ORBextractor.cc:792-832) as k_fast in two passes (orbfe_debug_set_fast_mode 1):
+//   k_fast_map    dense: one wavefront per 248-column x FM_RB-row tile of a level streams the rows
+//                 through a 14-row LDS window once (no per-cell ROI halo re-loads), runs the
+//                 antipodal quick test at tlow = min(iniThFAST, minThFAST) on every detection pixel
+//                 and the arc strength on the survivors, and stores the arc strength M (0: no
+//                 corner at tlow) of every detection pixel as one byte in fmap (pyramid layout);
+//   k_fast_cells  per cell: the cell's detection bytes of fmap -> LDS, then per threshold pass
+//                 (iniThFAST, then minThFAST for an empty cell) strict 3x3 NMS inside the cell and
+//                 the row-major compaction, the same keys and order as k_fast.
+// Exact for every threshold pass t >= tlow: a pixel with M >= t + 1 passes the quick test at t,
+// hence at tlow, so fmap holds M for it; a neighbour whose fmap byte is below t + 1 (no corner at
+// t, or a corner only at a lower threshold) is below M too -- the condition k_fast's NMS applies.
+constexpr int FM_COLS = 248;  // output columns of a tile: lanes 1..62, four pixels each
+constexpr int FM_G = 8;       // output rows per LDS window
+constexpr int FM_RB = 32;     // output rows per tile
+constexpr int FM_WAVE_LDS = (FM_G + 6) * 256 + FM_G * 256 + FM_G * FM_COLS * 2;
+
+__global__ __launch_bounds__(256) void k_fast_map(ExtractArgs a, int tile0, int tile1) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int w = wave_id(), lane = lane_id();
+  const int2 blk = xcd_block2d();
+  const int tile = tile0 + blk.x * (int)(blockDim.x >> 6) + w;
+  const int img = blk.y;
+  if (tile >= tile1) return;
+  uint8_t* win = smem + w * FM_WAVE_LDS;  // rows ys - 3 .. ys + FM_G + 2, 256 bytes each
+  uint8_t* mrow = win + (FM_G + 6) * 256;
+  uint16_t* list = reinterpret_cast<uint16_t*>(mrow + FM_G * 256);
+  uint32_t* W32 = reinterpret_cast<uint32_t*>(win);
+  uint32_t* M32 = reinterpret_cast<uint32_t*>(mrow);
+  const int4 td = a.ftiles[tile];
+  const LevelDesc& ld = a.levels[td.x];
+  const int pitch = ld.pitch, lw = ld.w;
+  const long long ioff = (long long)img * a.pyr_stride + ld.pyr_off;
+  const uint8_t* lev = a.pyr + ioff;
+  uint8_t* fm = a.fmap + ioff;
+  // lane's four columns cL .. cL + 3 (x0 = 0 mod 4); lanes 0 and 63 only carry the ring halo
+  const int cL = td.y - 4 + 4 * lane;
+  const int xlo = 19, xhi = lw - 20;  // detection columns (minBorderX + 3 .. maxBorderX - 4)
+  const bool ld_ok = cL <= xhi + 3;
+  uint32_t vmask = 0u;  // 0x80 in byte k for a detection pixel cL + k of a data lane
+  if (lane >= 1 && lane <= 62) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (cL + k >= xlo && cL + k <= xhi) vmask |= 0x80u << (8 * k);
+  }
+  const bool st_ok = vmask != 0u;
+  const int tlow = min(min(max(a.ini_th, 0), 255), min(max(a.min_th, 0), 255));
+  const uint32_t T2 = (uint32_t)tlow * 0x10001u;
+  const int y0 = td.z, y1 = td.w;
+  for (int ys = y0; ys < y1; ys += FM_G) {
+    const int gr = min(FM_G, y1 - ys), nr = gr + 6;
+    // window rows k = image rows ys - 3 + k; after the first window the top six are the previous
+    // window's bottom six (every lane moves its own column: no cross-lane hazard)
+    int k0 = 0;
+    if (ys != y0) {
+      uint32_t v[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) v[k] = W32[(FM_G + k) * 64 + lane];
+#pragma unroll
+      for (int k = 0; k < 6; k++) W32[k * 64 + lane] = v[k];
+      k0 = 6;
+    }
+    {
+      uint32_t v[FM_G + 6];
+      const uint8_t* src = lev + (long long)(ys - 3) * pitch + cL;
+#pragma unroll
+      for (int k = 0; k < FM_G + 6; k++)
+        v[k] = (ld_ok && k >= k0 && k < nr) ? *reinterpret_cast<const uint32_t*>(src + (long long)k * pitch) : 0u;
+#pragma unroll
+      for (int k = 0; k < FM_G + 6; k++)
+        if (k >= k0 && k < nr) W32[k * 64 + lane] = v[k];
+    }
+#pragma unroll
+    for (int r = 0; r < FM_G; r++) M32[r * 64 + lane] = 0u;
+    wave_sync();
+    // quick test at tlow, survivors as (row << 8 | window byte) entries
+    int nlist = 0;
+    for (int r = 0; r < gr; r++) {
+      const uint32_t c = W32[(r + 3) * 64 + lane];
+      const uint32_t u = W32[r * 64 + lane], d = W32[(r + 6) * 64 + lane];
+      const uint32_t cl = W32[(r + 3) * 64 + ((lane + 63) & 63)], cr = W32[(r + 3) * 64 + ((lane + 1) & 63)];
+      const uint32_t l = __builtin_amdgcn_alignbyte(c, cl, 1), rr = __builtin_amdgcn_alignbyte(cr, c, 3);
+      const uint32_t re = quick2(pk_even(c), pk_even(u), pk_even(d), pk_even(l), pk_even(rr), T2);
+      const uint32_t ro = quick2(pk_odd(c), pk_odd(u), pk_odd(d), pk_odd(l), pk_odd(rr), T2);
+      uint32_t m = __builtin_amdgcn_perm(ro, re, 0x07030501u) & vmask;
+      const int n = __popc(m);
+      const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
+      int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
+      const int px = (r << 8) + 4 * lane;
+      while (m) {
+        list[pos++] = (uint16_t)(px + (__builtin_ctz(m) >> 3));
+        m &= m - 1u;
+      }
+      nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    }
+    wave_sync();
+    // arc strength of the survivors, two per lane
+    for (int j0 = 0; j0 < nlist; j0 += 128) {
+      const int ja = j0 + 2 * lane, jb = ja + 1;
+      if (ja < nlist) {
+        const int qa = list[ja], qb = jb < nlist ? list[jb] : qa;
+        const uint8_t* pa = win + ((qa >> 8) + 3) * 256 + (qa & 255);
+        const uint8_t* pb = win + ((qb >> 8) + 3) * 256 + (qb & 255);
+        const uint32_t m = arc_strength_pk(pa, pb, 256, tlow);
+        const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
+        if (ma) mrow[qa] = (uint8_t)ma;
+        if (mb && jb < nlist) mrow[qb] = (uint8_t)mb;
+      }
+    }
+    wave_sync();
+    if (st_ok) {
+      uint8_t* dst = fm + (long long)ys * pitch + cL;
+      for (int r = 0; r < gr; r++) *reinterpret_cast<uint32_t*>(dst + (long long)r * pitch) = M32[r * 64 + lane];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int cell0, int cell1) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int w = wave_id(), lane = lane_id();
+  const int2 blk = xcd_block2d();
+  const int cell = cell0 + blk.x * (int)(blockDim.x >> 6) + w;
+  const int img = blk.y;
+  if (cell >= cell1) return;
+  const CellDesc cd = a.cells[cell];
+  const int dw = cd.rw - 6, dh = cd.rh - 6;
+  int32_t* cnt_out = a.cellcnt + (long long)img * a.ncells + cell;
+  if (dw <= 0 || dh <= 0) {
+    if (lane == 0) *cnt_out = 0;
+    return;
+  }
+  uint8_t* M = smem + w * a.fc_lds;
+  const int RS = a.fc_rs;
+  const int pitch = cd.pitch;
+  const uint8_t* fm = a.fmap + (long long)img * a.pyr_stride + cd.pyr_off;
+  // detection region (gx, gy) .. (gx + dw - 1, gy + dh - 1) of the level -> M, aligned dwords
+  const int gx = cd.x0 + 3, gy = cd.y0 + 3;
+  const int xa = gx & ~3, xo = gx - xa, nw = (xo + dw + 3) >> 2;
+  for (int i0 = 0; i0 < nw * dh; i0 += 4 * 64) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = i0 + lane + 64 * k;
+      if (i < nw * dh) {
+        const int r = i / nw, c = i - r * nw;
+        v[k] = *reinterpret_cast<const uint32_t*>(fm + (long long)(gy + r) * pitch + xa + 4 * c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = i0 + lane + 64 * k;
+      if (i < nw * dh) {
+        const int r = i / nw, c = i - r * nw;
+        *reinterpret_cast<uint32_t*>(M + r * RS + 4 * c) = v[k];
+      }
+    }
+  }
+  wave_sync();
+  const uint8_t* P = M + xo;  // detection pixel (r, c) at P[r * RS + c]
+  uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
+  // lanes: (row parity, column) for cells up to 32 wide, else one row of 64 columns per step
+  const int rpi = dw <= 32 ? 2 : 1, cpi = dw <= 32 ? 32 : 64;
+  const int lr = lane / cpi, lc = lane % cpi;
+  int count = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const int t = min(max(pass == 0 ? a.ini_th : a.min_th, 0), 255);
+    if (pass == 1 && t == min(max(a.ini_th, 0), 255)) break;
+    const int tt = max(t + 1, 2);
+    for (int r0 = 0; r0 < dh; r0 += rpi) {
+      const int rr = r0 + lr;
+      for (int c0 = 0; c0 < dw; c0 += cpi) {
+        const int cc = c0 + lc;
+        bool keep = false;
+        int m = 0;
+        if (rr < dh && cc < dw) {
+          const uint8_t* p = P + rr * RS + cc;
+          m = p[0];
+          if (m >= tt) {
+            const bool up = rr > 0, dn = rr + 1 < dh, lf = cc > 0, rt = cc + 1 < dw;
+            int mn = 0;
+            if (up) mn = max(mn, (int)p[-RS]);
+            if (dn) mn = max(mn, (int)p[RS]);
+            if (lf) mn = max(mn, (int)p[-1]);
+            if (rt) mn = max(mn, (int)p[1]);
+            if (up && lf) mn = max(mn, (int)p[-RS - 1]);
+            if (up && rt) mn = max(mn, (int)p[-RS + 1]);
+            if (dn && lf) mn = max(mn, (int)p[RS - 1]);
+            if (dn && rt) mn = max(mn, (int)p[RS + 1]);
+            keep = m > mn;
+          }
+        }
+        const uint64_t bal = wave_ballot(keep);
+        if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, m - 1);
+        count += __popcll(bal);
+      }
     }
     if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
   }
@@ -2057,6 +2263,7 @@ struct orbfe_extractor {
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
+  int fast_mode = 0;                 // orbfe_debug_set_fast_mode: 0 k_fast, 1 k_fast_map + k_fast_cells
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2075,6 +2282,8 @@ struct orbfe_extractor {
   int2* d_xtab = nullptr;
   int2* d_ytab = nullptr;
   int4* d_ywin = nullptr;
+  int4* d_ftiles = nullptr;
+  int nftiles = 0;
   uint4* d_rgrp = nullptr;
   int* d_rgx0 = nullptr;
   // batch buffers
@@ -2083,6 +2292,7 @@ struct orbfe_extractor {
   size_t in_bytes = 0;
   uint8_t* d_pyr = nullptr;
   uint8_t* d_blur = nullptr;
+  uint8_t* d_fmap = nullptr;  // k_fast_map's arc strengths (fast_mode 1), allocated on first use
   uint32_t* d_cand = nullptr;
   int32_t* d_cellcnt = nullptr;
   uint32_t* d_keys_a = nullptr;
@@ -2133,6 +2343,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   std::vector<int4> yw;  // k_resize_win row table, indexed like yt
   std::vector<uint4> rgrp;
   std::vector<int> rgx0;
+  std::vector<int4> ft;  // k_fast_map tiles
   long long pyr = 0;
   int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0, tiles = 0;
   for (int l = 0; l < L; l++) {
@@ -2205,6 +2416,12 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
+    // k_fast_map tiles over the detection pixels [19, w - 20] x [19, h - 20]: FM_COLS-column
+    // strips from column 16 (x0 = 0 mod 4), FM_RB-row bands from row 19
+    d.ftile_begin = (int)ft.size();
+    for (int y = 19; y <= d.h - 20; y += FM_RB)
+      for (int x = 16; x <= d.w - 20; x += FM_COLS) ft.push_back(make_int4(l, x, y, std::min(y + FM_RB, d.h - 19)));
+    d.nftiles = (int)ft.size() - d.ftile_begin;
     {  // k_blur strips of BS_W x BS_H, the remainder columns in bands of blur_h x BS_H rows
       d.tiles_x = d.w / BS_W;
       const int rem = d.w - d.tiles_x * BS_W;
@@ -2296,6 +2513,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_ywin);
+  hipFree(h->d_ftiles);
+  h->d_ftiles = nullptr;
   h->d_levels = nullptr;
   h->d_cells = nullptr;
   h->d_xtab = h->d_ytab = nullptr;
@@ -2314,6 +2533,10 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice));
   if (!yw.empty())
     ORBFE_HIP_CHECK(hipMemcpy(h->d_ywin, yw.data(), sizeof(int4) * yw.size(), hipMemcpyHostToDevice));
+  ORBFE_HIP_CHECK(hipMalloc(&h->d_ftiles, sizeof(int4) * std::max<size_t>(ft.size(), 1)));
+  if (!ft.empty())
+    ORBFE_HIP_CHECK(hipMemcpy(h->d_ftiles, ft.data(), sizeof(int4) * ft.size(), hipMemcpyHostToDevice));
+  h->nftiles = (int)ft.size();
   h->levels = lv;
   h->cells = cells;
   h->xtab = xt;
@@ -2353,6 +2576,7 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
 static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_pyr);
   hipFree(h->d_blur);
+  hipFree(h->d_fmap);
   hipFree(h->d_cand);
   hipFree(h->d_cellcnt);
   hipFree(h->d_keys_a);
@@ -2361,6 +2585,7 @@ static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_lvlcnt);
   h->d_pyr = nullptr;
   h->d_blur = nullptr;
+  h->d_fmap = nullptr;
   h->d_cand = nullptr;
   h->d_cellcnt = nullptr;
   h->d_keys_a = h->d_keys_b = nullptr;
@@ -2465,7 +2690,31 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.p7 = -0.04432655554792128f * (float)(180 / M_PI);
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
+  if (h->fast_mode == 1) {
+    if (!h->d_fmap)  // (+256: the last strip's dword loads / stores stay inside the block)
+      ORBFE_HIP_CHECK(hipMalloc(&h->d_fmap, (size_t)h->pyr_stride * h->batch_cap + 256));
+    a.fmap = h->d_fmap + (long long)i0 * h->pyr_stride;
+    a.ftiles = h->d_ftiles;
+    a.fc_rs = (h->roi_w_max + 4 + 3) & ~3;
+    a.fc_lds = (a.fc_rs * std::max(h->roi_h_max - 6, 1) + 15) & ~15;
+  }
 
+  // fast_mode 1: levels [l0, l1) as the dense map pass then the per-cell pass
+  auto launch_fast_map = [&](hipStream_t s, int l0, int l1) -> int {
+    const int t0 = h->levels[l0].ftile_begin;
+    const int t1 = l1 < h->nlevels ? h->levels[l1].ftile_begin : h->nftiles;
+    const int c0 = h->levels[l0].cell_begin;
+    const int c1 = l1 < h->nlevels ? h->levels[l1].cell_begin : a.ncells;
+    if (t1 > t0) {
+      dim3 grid((t1 - t0 + 3) / 4, n);
+      ORBFE_LAUNCH("k_fast_map", k_fast_map, grid, dim3(256), 4 * FM_WAVE_LDS, s, a, t0, t1);
+    }
+    if (c1 > c0) {
+      dim3 grid((c1 - c0 + 3) / 4, n);
+      ORBFE_LAUNCH("k_fast_cells", k_fast_cells, grid, dim3(256), 4 * (size_t)a.fc_lds, s, a, c0, c1);
+    }
+    return ORBFE_OK;
+  };
   auto launch_fast = [&](hipStream_t s, int c0, int c1, bool main_launch = false) -> int {
     if (c1 <= c0) return ORBFE_OK;
     // wavefronts (cells) per workgroup: 4 for the side-stream launches of levels 0-2, which run
@@ -2503,6 +2752,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
     ORBFE_HIP_CHECK(hipEventRecord(e, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
+    if (h->fast_mode == 1) return launch_fast_map(side, l, l + 1);
     const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
     return launch_fast(side, h->levels[l].cell_begin, c1);
   };
@@ -2538,7 +2788,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
-  if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
+  if (k_side < h->nlevels) {
+    if (h->fast_mode == 1)
+      launch_fast_map(st, k_side, h->nlevels);
+    else
+      launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
+  }
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
@@ -2691,6 +2946,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_ywin);
+  hipFree(h->d_ftiles);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   hipFree(h->d_in);
@@ -3280,6 +3536,11 @@ extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
   return ORBFE_OK;
 }
 
+extern "C" int orbfe_debug_set_fast_mode(orbfe_extractor* h, int mode) {
+  if (!h || mode < 0 || mode > 1) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_fast_mode: bad argument");
+  h->fast_mode = mode;
+  return ORBFE_OK;
+}
 extern "C" int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k) {
   if (!h) return ORBFE_ERR_ARG;
   h->fast_side_levels = k > 0 ? k : -1;
