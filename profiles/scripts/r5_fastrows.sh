@@ -1,0 +1,13 @@
+#!/bin/bash
+# k_fast_rows (fast mode 2): parity, then interleaved A/B against k_fast (mode 0), then a trace.
+set -o pipefail
+O=gpurun_out/r5fr
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_extract.py -k fast_map > $O/fm_tests.log 2>&1 || exit 1
+for i in 1 2; do
+  for m in 0 2; do
+    timeout -k 10 200 python bench.py --no-legs --no-cpu --fast-mode $m > $O/ab_m${m}_$i.json 2>&1 || exit 1
+  done
+done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof2 -o run -- python bench.py --no-legs --no-cpu --fast-mode 2 --steps 5 > $O/prof2.log 2>&1 || exit 1
+echo done

@@ -137,10 +137,12 @@ FAST_MAP_CASES = [((2000, 1.2, 8, 20, 7), (376, 1241), "synth"), ((2000, 1.2, 8,
                   ((500, 1.2, 2, 20, 7), (377, 643), "noise")]
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("params,shape,kind", FAST_MAP_CASES)
-def test_fast_map_mode(require_gpu, params, shape, kind):
+def test_fast_map_mode(require_gpu, params, shape, kind, mode):
     """orbfe_debug_set_fast_mode(1): the dense arc-strength map (k_fast_map) and the per-cell NMS /
-    compaction (k_fast_cells) give k_fast's candidates, hence the same extraction, on KITTI / TUM /
+    compaction (k_fast_cells), and mode 2 (both fused per run of cells of a cell row, k_fast_rows),
+    give k_fast's candidates, hence the same extraction, on KITTI / TUM /
     wide / tall shapes, iniThFAST > minThFAST, iniThFAST < minThFAST, textured noise and sparse
     images (cells emptied at iniThFAST), and strip widths that are not multiples of 248."""
     if kind == "synth":
@@ -153,15 +155,16 @@ def test_fast_map_mode(require_gpu, params, shape, kind):
         img[250:262, 900:1000] = 10
         img[30:34, 20:1200] = 97
     ext = ORBextractor(*params)
-    ext.debug_set_fast_mode(1)
+    ext.debug_set_fast_mode(mode)
     assert_same_extraction(ext, RefExtractor(*params), img)
 
 
-def test_fast_map_mode_batch(require_gpu):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_fast_map_mode_batch(require_gpu, mode):
     """The map mode over a batch: every image's candidates and outputs equal k_fast's."""
     imgs = np.stack([synth_frame(i, 376, 1241) for i in range(5)])
     a, b = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
-    b.debug_set_fast_mode(1)
+    b.debug_set_fast_mode(mode)
     ra, rb = a.extract_batch(imgs), b.extract_batch(imgs)
     for i in range(len(imgs)):
         for l in range(8):
