@@ -102,9 +102,6 @@ def parse(argv=None):
     p.add_argument("--blur-mode", type=int, default=-1,
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
                         "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
-    p.add_argument("--fast-mode", type=int, default=-1,
-                   help="FAST kernels (orbfe_debug_set_fast_mode): 0 k_fast per cell ROI, 1 k_fast_map dense "
-                        "arc-strength map + k_fast_cells (default: the library's)")
     p.add_argument("--match-inline", action="store_true",
                    help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
     p.add_argument("--stereo-on-extract", action="store_true",
@@ -499,9 +496,6 @@ def main():
             # and the shared side stream is better left to FAST alone: the blur follows the octree
             # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
-    if args.fast_mode >= 0:
-        for e in exts:
-            e.debug_set_fast_mode(args.fast_mode)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)

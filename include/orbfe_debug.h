@@ -38,11 +38,6 @@ int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
 /* Where GaussianBlur runs: 0 (default) on the side stream beside DistributeOctTree, 1 on the
  * launch stream after DistributeOctTree (several handles sharing one side stream). */
 int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode);
-/* FAST kernels: 0 (default) k_fast, one wavefront per cell ROI; 1 k_fast_map, a dense arc-strength
- * map per level, then k_fast_cells, per-cell NMS and compaction; 2 k_fast_rows, one wavefront per
- * run of cells of a cell row (the two passes fused, the band's arc strengths kept in LDS; geometries
- * with a cell wider than 245 columns use 0). The same keys in every mode. */
-int orbfe_debug_set_fast_mode(orbfe_extractor* h, int mode);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

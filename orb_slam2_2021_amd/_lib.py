@@ -160,7 +160,6 @@ _SIGNATURES = {
     "orbfe_debug_set_inline_side": (c_int, [c_void_p, c_int]),
     "orbfe_set_side_stream": (c_int, [c_void_p, c_void_p]),
     "orbfe_debug_set_blur_mode": (c_int, [c_void_p, c_int]),
-    "orbfe_debug_set_fast_mode": (c_int, [c_void_p, c_int]),
     "orbfe_debug_get_umax": (c_int, [c_void_p, c_void_p]),
     "orbfe_debug_steer_trig": (c_int, [c_uint32, c_uint32, c_void_p, c_void_p, c_void_p]),
     "orbfe_vocab_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

@@ -80,8 +80,6 @@ struct LevelDesc {
   int tile_begin, tiles_x;   // k_blur tiles of this level; full-width (BS_W) column strips
   int rgrp_begin, rwin_ok;   // k_resize 4-column group tables; 1 when every group's taps fit 8 bytes
   int ini_thr[8];            // smallest x with (int)(x / hx) >= b, b = 1..7 (initial node of key x)
-  int ftile_begin, nftiles;  // k_fast_map tiles of this level
-  int rtile_begin;           // k_fast_rows tiles of this level
 };
 
 struct CellDesc {
@@ -124,10 +122,6 @@ struct ExtractArgs {
   int umax[16];
   AtanConsts atan;
   float factor_pi;
-  uint8_t* fmap;          // k_fast_map: per-pixel arc strength, pyramid layout
-  const int4* ftiles;     // k_fast_map tiles {level, first column, first row, end row}
-  int fc_rs, fc_lds;      // k_fast_cells: LDS map row stride and bytes per wavefront
-  int fr_dh, fr_list;     // k_fast_rows: band rows and list entries of the LDS plan
 };
 
 __constant__ int8_t c_pattern[1024];
@@ -987,403 +981,6 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
       const uint64_t bal = wave_ballot(keep);
       if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, sc);
       count += __popcll(bal);
-    }
-    if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
-  }
-  if (lane == 0) *cnt_out = count;
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same FAST (ORBextractor.cc:792-832) as k_fast in two passes (orbfe_debug_set_fast_mode 1):
-//   k_fast_map    dense: one wavefront per 248-column x FM_RB-row tile of a level streams the rows
-//                 through a 14-row LDS window once (no per-cell ROI halo re-loads), runs the
-//                 antipodal quick test at tlow = min(iniThFAST, minThFAST) on every detection pixel
-//                 and the arc strength on the survivors, and stores the arc strength M (0: no
-//                 corner at tlow) of every detection pixel as one byte in fmap (pyramid layout);
-//   k_fast_cells  per cell: the cell's detection bytes of fmap -> LDS, then per threshold pass
-//                 (iniThFAST, then minThFAST for an empty cell) strict 3x3 NMS inside the cell and
-//                 the row-major compaction, the same keys and order as k_fast.
-// Exact for every threshold pass t >= tlow: a pixel with M >= t + 1 passes the quick test at t,
-// hence at tlow, so fmap holds M for it; a neighbour whose fmap byte is below t + 1 (no corner at
-// t, or a corner only at a lower threshold) is below M too -- the condition k_fast's NMS applies.
-constexpr int FM_COLS = 248;  // output columns of a tile: lanes 1..62, four pixels each
-constexpr int FM_G = 8;       // output rows per LDS window
-constexpr int FM_RB = 32;     // output rows per tile
-constexpr int FM_WAVE_LDS = (FM_G + 6) * 256 + FM_G * 256 + FM_G * FM_COLS * 2;
-
-__global__ __launch_bounds__(256) void k_fast_map(ExtractArgs a, int tile0, int tile1) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int w = wave_id(), lane = lane_id();
-  const int2 blk = xcd_block2d();
-  const int tile = tile0 + blk.x * (int)(blockDim.x >> 6) + w;
-  const int img = blk.y;
-  if (tile >= tile1) return;
-  uint8_t* win = smem + w * FM_WAVE_LDS;  // rows ys - 3 .. ys + FM_G + 2, 256 bytes each
-  uint8_t* mrow = win + (FM_G + 6) * 256;
-  uint16_t* list = reinterpret_cast<uint16_t*>(mrow + FM_G * 256);
-  uint32_t* W32 = reinterpret_cast<uint32_t*>(win);
-  uint32_t* M32 = reinterpret_cast<uint32_t*>(mrow);
-  const int4 td = a.ftiles[tile];
-  const LevelDesc& ld = a.levels[td.x];
-  const int pitch = ld.pitch, lw = ld.w;
-  const long long ioff = (long long)img * a.pyr_stride + ld.pyr_off;
-  const uint8_t* lev = a.pyr + ioff;
-  uint8_t* fm = a.fmap + ioff;
-  // lane's four columns cL .. cL + 3 (x0 = 0 mod 4); lanes 0 and 63 only carry the ring halo
-  const int cL = td.y - 4 + 4 * lane;
-  const int xlo = 19, xhi = lw - 20;  // detection columns (minBorderX + 3 .. maxBorderX - 4)
-  const bool ld_ok = cL <= xhi + 3;
-  uint32_t vmask = 0u;  // 0x80 in byte k for a detection pixel cL + k of a data lane
-  if (lane >= 1 && lane <= 62) {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (cL + k >= xlo && cL + k <= xhi) vmask |= 0x80u << (8 * k);
-  }
-  const bool st_ok = vmask != 0u;
-  const int tlow = min(min(max(a.ini_th, 0), 255), min(max(a.min_th, 0), 255));
-  const uint32_t T2 = (uint32_t)tlow * 0x10001u;
-  const int y0 = td.z, y1 = td.w;
-  for (int ys = y0; ys < y1; ys += FM_G) {
-    const int gr = min(FM_G, y1 - ys), nr = gr + 6;
-    // window rows k = image rows ys - 3 + k; after the first window the top six are the previous
-    // window's bottom six (every lane moves its own column: no cross-lane hazard)
-    int k0 = 0;
-    if (ys != y0) {
-      uint32_t v[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) v[k] = W32[(FM_G + k) * 64 + lane];
-#pragma unroll
-      for (int k = 0; k < 6; k++) W32[k * 64 + lane] = v[k];
-      k0 = 6;
-    }
-    {
-      uint32_t v[FM_G + 6];
-      const uint8_t* src = lev + (long long)(ys - 3) * pitch + cL;
-#pragma unroll
-      for (int k = 0; k < FM_G + 6; k++)
-        v[k] = (ld_ok && k >= k0 && k < nr) ? *reinterpret_cast<const uint32_t*>(src + (long long)k * pitch) : 0u;
-#pragma unroll
-      for (int k = 0; k < FM_G + 6; k++)
-        if (k >= k0 && k < nr) W32[k * 64 + lane] = v[k];
-    }
-#pragma unroll
-    for (int r = 0; r < FM_G; r++) M32[r * 64 + lane] = 0u;
-    wave_sync();
-    // quick test at tlow, survivors as (row << 8 | window byte) entries
-    int nlist = 0;
-    for (int r = 0; r < gr; r++) {
-      const uint32_t c = W32[(r + 3) * 64 + lane];
-      const uint32_t u = W32[r * 64 + lane], d = W32[(r + 6) * 64 + lane];
-      const uint32_t cl = W32[(r + 3) * 64 + ((lane + 63) & 63)], cr = W32[(r + 3) * 64 + ((lane + 1) & 63)];
-      const uint32_t l = __builtin_amdgcn_alignbyte(c, cl, 1), rr = __builtin_amdgcn_alignbyte(cr, c, 3);
-      const uint32_t re = quick2(pk_even(c), pk_even(u), pk_even(d), pk_even(l), pk_even(rr), T2);
-      const uint32_t ro = quick2(pk_odd(c), pk_odd(u), pk_odd(d), pk_odd(l), pk_odd(rr), T2);
-      uint32_t m = __builtin_amdgcn_perm(ro, re, 0x07030501u) & vmask;
-      const int n = __popc(m);
-      const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
-      int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
-      const int px = (r << 8) + 4 * lane;
-      while (m) {
-        list[pos++] = (uint16_t)(px + (__builtin_ctz(m) >> 3));
-        m &= m - 1u;
-      }
-      nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-    }
-    wave_sync();
-    // arc strength of the survivors, two per lane
-    for (int j0 = 0; j0 < nlist; j0 += 128) {
-      const int ja = j0 + 2 * lane, jb = ja + 1;
-      if (ja < nlist) {
-        const int qa = list[ja], qb = jb < nlist ? list[jb] : qa;
-        const uint8_t* pa = win + ((qa >> 8) + 3) * 256 + (qa & 255);
-        const uint8_t* pb = win + ((qb >> 8) + 3) * 256 + (qb & 255);
-        const uint32_t m = arc_strength_pk(pa, pb, 256, tlow);
-        const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
-        if (ma) mrow[qa] = (uint8_t)ma;
-        if (mb && jb < nlist) mrow[qb] = (uint8_t)mb;
-      }
-    }
-    wave_sync();
-    if (st_ok) {
-      uint8_t* dst = fm + (long long)ys * pitch + cL;
-      for (int r = 0; r < gr; r++) *reinterpret_cast<uint32_t*>(dst + (long long)r * pitch) = M32[r * 64 + lane];
-    }
-  }
-}
-
-// k_fast_rows (orbfe_debug_set_fast_mode 2): the map pass and the cell pass fused. One wavefront
-// per run of J consecutive cells of one cell row (J cells whose detection columns fit the 248 data
-// columns of a strip): it streams the row band's image rows once through the 14-row LDS window
-// (the next window's rows loaded while the current one is scored), keeps the band's arc strengths
-// in LDS, then per cell runs the threshold passes: candidates (M >= max(t + 1, 2)) by packed
-// compares four pixels per lane, compacted row-major, strict 3x3 NMS inside the cell on the list.
-// LDS per wavefront: window | band (rows_max + 1 rows of 256 bytes) | list.
-struct FastRowsLds {
-  int band, list, total;
-};
-__host__ __device__ inline FastRowsLds fast_rows_lds(int dh_max, int list_max) {
-  FastRowsLds f;
-  f.band = (FM_G + 6) * 256;
-  f.list = f.band + (dh_max + 1) * 256;
-  f.total = (f.list + 2 * list_max + 15) & ~15;
-  return f;
-}
-
-__global__ __launch_bounds__(64) void k_fast_rows(ExtractArgs a, int tile0, int tile1) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int lane = lane_id();
-  const int2 blk = xcd_block2d();
-  const int tile = tile0 + blk.x;
-  const int img = blk.y;
-  if (tile >= tile1) return;
-  const FastRowsLds lay = fast_rows_lds(a.fr_dh, a.fr_list);
-  uint8_t* win = smem;
-  uint8_t* band = smem + lay.band;
-  uint16_t* list = reinterpret_cast<uint16_t*>(smem + lay.list);
-  uint32_t* W32 = reinterpret_cast<uint32_t*>(win);
-  uint32_t* B32 = reinterpret_cast<uint32_t*>(band);
-  const int4 td = a.ftiles[tile];  // {J, x0, first cell, last cell}
-  const int J = td.x, x0 = td.y, cell0 = td.z;
-  const CellDesc c0 = a.cells[cell0];
-  const CellDesc cz = a.cells[td.w];
-  const int pitch = c0.pitch;
-  const uint8_t* lev = a.pyr + (long long)img * a.pyr_stride + c0.pyr_off;
-  const int Y = c0.y0 + 3, dh = c0.rh - 6;
-  const int Xa = c0.x0 + 3, Xb = cz.x0 + 3 + (cz.rw - 6);  // detection columns [Xa, Xb)
-  const int cL = x0 - 4 + 4 * lane;
-  const bool ld_ok = cL <= Xb + 2;
-  uint32_t vmask = 0u;
-  if (lane >= 1 && lane <= 62) {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-      if (cL + k >= Xa && cL + k < Xb) vmask |= 0x80u << (8 * k);
-  }
-  int32_t* cnt_out = a.cellcnt + (long long)img * a.ncells;
-  if (dh <= 0) {
-    for (int j = lane; j < J; j += 64) cnt_out[cell0 + j] = 0;
-    return;
-  }
-  const int tini = min(max(a.ini_th, 0), 255), tmin = min(max(a.min_th, 0), 255);
-  const int tlow = min(tini, tmin);
-  const uint32_t T2 = (uint32_t)tlow * 0x10001u;
-  // 1. the band's arc strengths
-  uint32_t pf[FM_G + 6];
-  {
-    const int nr = min(FM_G, dh) + 6;
-    const uint8_t* src = lev + (long long)(Y - 3) * pitch + cL;
-#pragma unroll
-    for (int k = 0; k < FM_G + 6; k++)
-      pf[k] = (ld_ok && k < nr) ? *reinterpret_cast<const uint32_t*>(src + (long long)k * pitch) : 0u;
-  }
-  for (int ys = Y; ys < Y + dh; ys += FM_G) {
-    const int gr = min(FM_G, Y + dh - ys), nr = gr + 6;
-    if (ys != Y) {
-      uint32_t v[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) v[k] = W32[(FM_G + k) * 64 + lane];
-#pragma unroll
-      for (int k = 0; k < 6; k++) W32[k * 64 + lane] = v[k];
-#pragma unroll
-      for (int k = 6; k < FM_G + 6; k++)
-        if (k < nr) W32[k * 64 + lane] = pf[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < FM_G + 6; k++)
-        if (k < nr) W32[k * 64 + lane] = pf[k];
-    }
-    uint8_t* mrow = band + (ys - Y) * 256;
-#pragma unroll
-    for (int r = 0; r < FM_G; r++)
-      if (r < gr) reinterpret_cast<uint32_t*>(mrow)[r * 64 + lane] = 0u;
-    // the next window's new rows (image rows ys + FM_G + 3 ..) in flight during this one
-    if (ys + FM_G < Y + dh) {
-      const int gn = min(FM_G, Y + dh - ys - FM_G);
-      const uint8_t* src = lev + (long long)(ys + FM_G + 3) * pitch + cL;
-#pragma unroll
-      for (int k = 0; k < FM_G; k++)
-        pf[6 + k] = (ld_ok && k < gn) ? *reinterpret_cast<const uint32_t*>(src + (long long)k * pitch) : 0u;
-    }
-    wave_sync();
-    int nlist = 0;
-    for (int r = 0; r < gr; r++) {
-      const uint32_t c = W32[(r + 3) * 64 + lane];
-      const uint32_t u = W32[r * 64 + lane], d = W32[(r + 6) * 64 + lane];
-      const uint32_t cl = W32[(r + 3) * 64 + ((lane + 63) & 63)], cr = W32[(r + 3) * 64 + ((lane + 1) & 63)];
-      const uint32_t l = __builtin_amdgcn_alignbyte(c, cl, 1), rr = __builtin_amdgcn_alignbyte(cr, c, 3);
-      const uint32_t re = quick2(pk_even(c), pk_even(u), pk_even(d), pk_even(l), pk_even(rr), T2);
-      const uint32_t ro = quick2(pk_odd(c), pk_odd(u), pk_odd(d), pk_odd(l), pk_odd(rr), T2);
-      uint32_t m = __builtin_amdgcn_perm(ro, re, 0x07030501u) & vmask;
-      const int n = __popc(m);
-      const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
-      int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
-      const int px = (r << 8) + 4 * lane;
-      while (m) {
-        list[pos++] = (uint16_t)(px + (__builtin_ctz(m) >> 3));
-        m &= m - 1u;
-      }
-      nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-    }
-    wave_sync();
-    for (int j0 = 0; j0 < nlist; j0 += 128) {
-      const int ja = j0 + 2 * lane, jb = ja + 1;
-      if (ja < nlist) {
-        const int qa = list[ja], qb = jb < nlist ? list[jb] : qa;
-        const uint8_t* pa = win + ((qa >> 8) + 3) * 256 + (qa & 255);
-        const uint8_t* pb = win + ((qb >> 8) + 3) * 256 + (qb & 255);
-        const uint32_t m = arc_strength_pk(pa, pb, 256, tlow);
-        const int ma = (int)(m & 0xffffu), mb = (int)(m >> 16);
-        if (ma) mrow[qa] = (uint8_t)ma;
-        if (mb && jb < nlist) mrow[qb] = (uint8_t)mb;
-      }
-    }
-    wave_sync();
-  }
-  // 2. per cell: threshold passes over the band (iniThFAST, then minThFAST for an empty cell)
-  const int bx = x0 - 4;  // band byte b holds column bx + b
-  for (int j = 0; j < J; j++) {
-    const CellDesc cd = a.cells[cell0 + j];
-    const int dw = cd.rw - 6;
-    const int bj = cd.x0 + 3 - bx, sh = bj & 3, bq = bj >> 2;
-    const int G = (dw + 3) >> 2;
-    const int GW = G <= 8 ? 8 : G <= 16 ? 16 : G <= 32 ? 32 : 64, RPI = 64 / GW;
-    const int g = lane & (GW - 1), rs = lane / GW;
-    const int nv = dw - 4 * g;
-    const uint32_t cmask = nv >= 4 ? 0x80808080u : nv <= 0 ? 0u : (0x80808080u >> (8 * (4 - nv)));
-    uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
-    int count = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      const int t = pass == 0 ? tini : tmin;
-      if (pass == 1 && t == tini) break;
-      const int tt = max(t + 1, 2);
-      const uint32_t TT2 = (uint32_t)tt * 0x10001u;
-      int nlist = 0;
-      for (int r0 = 0; r0 < dh; r0 += RPI) {
-        const int r = r0 + rs;
-        uint32_t m = 0u;
-        if (r < dh) {
-          const uint32_t lo = B32[r * 64 + bq + g], hi = B32[r * 64 + bq + g + 1];
-          const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, sh);
-          const uint32_t re = pk_sub16(pk_even(x), TT2), ro = pk_sub16(pk_odd(x), TT2);  // sign: below tt
-          m = ~__builtin_amdgcn_perm(ro, re, 0x07030501u) & cmask;
-        }
-        const int n = __popc(m);
-        const uint64_t b0 = wave_ballot(n & 1), b1 = wave_ballot(n & 2), b2 = wave_ballot(n & 4);
-        int pos = nlist + prefix_in_wave(b0) + 2 * prefix_in_wave(b1) + 4 * prefix_in_wave(b2);
-        const int px = (r << 8) + 4 * g;
-        while (m) {
-          list[pos++] = (uint16_t)(px + (__builtin_ctz(m) >> 3));
-          m &= m - 1u;
-        }
-        nlist += __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-      }
-      wave_sync();
-      for (int q0 = 0; q0 < nlist; q0 += 64) {
-        const int q = q0 + lane;
-        bool keep = false;
-        int rr = 0, cc = 0, m = 0;
-        if (q < nlist) {
-          const int e = list[q];
-          rr = e >> 8;
-          cc = e & 255;
-          const uint8_t* p = band + rr * 256 + bj + cc;
-          m = p[0];
-          const bool up = rr > 0, dn = rr + 1 < dh, lf = cc > 0, rt = cc + 1 < dw;
-          int mn = 0;
-          if (up) mn = max(mn, max(max((int)p[-256], lf ? (int)p[-257] : 0), rt ? (int)p[-255] : 0));
-          if (dn) mn = max(mn, max(max((int)p[256], lf ? (int)p[255] : 0), rt ? (int)p[257] : 0));
-          if (lf) mn = max(mn, (int)p[-1]);
-          if (rt) mn = max(mn, (int)p[1]);
-          keep = m > mn;
-        }
-        const uint64_t bal = wave_ballot(keep);
-        if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, m - 1);
-        count += __popcll(bal);
-      }
-      wave_sync();  // the list is rewritten by the next pass / cell
-      if (count > 0) break;
-    }
-    if (lane == 0) cnt_out[cell0 + j] = count;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_fast_cells(ExtractArgs a, int cell0, int cell1) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int w = wave_id(), lane = lane_id();
-  const int2 blk = xcd_block2d();
-  const int cell = cell0 + blk.x * (int)(blockDim.x >> 6) + w;
-  const int img = blk.y;
-  if (cell >= cell1) return;
-  const CellDesc cd = a.cells[cell];
-  const int dw = cd.rw - 6, dh = cd.rh - 6;
-  int32_t* cnt_out = a.cellcnt + (long long)img * a.ncells + cell;
-  if (dw <= 0 || dh <= 0) {
-    if (lane == 0) *cnt_out = 0;
-    return;
-  }
-  uint8_t* M = smem + w * a.fc_lds;
-  const int RS = a.fc_rs;
-  const int pitch = cd.pitch;
-  const uint8_t* fm = a.fmap + (long long)img * a.pyr_stride + cd.pyr_off;
-  // detection region (gx, gy) .. (gx + dw - 1, gy + dh - 1) of the level -> M, aligned dwords
-  const int gx = cd.x0 + 3, gy = cd.y0 + 3;
-  const int xa = gx & ~3, xo = gx - xa, nw = (xo + dw + 3) >> 2;
-  for (int i0 = 0; i0 < nw * dh; i0 += 4 * 64) {
-    uint32_t v[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = i0 + lane + 64 * k;
-      if (i < nw * dh) {
-        const int r = i / nw, c = i - r * nw;
-        v[k] = *reinterpret_cast<const uint32_t*>(fm + (long long)(gy + r) * pitch + xa + 4 * c);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = i0 + lane + 64 * k;
-      if (i < nw * dh) {
-        const int r = i / nw, c = i - r * nw;
-        *reinterpret_cast<uint32_t*>(M + r * RS + 4 * c) = v[k];
-      }
-    }
-  }
-  wave_sync();
-  const uint8_t* P = M + xo;  // detection pixel (r, c) at P[r * RS + c]
-  uint32_t* out = a.cand + (long long)img * a.cand_stride + cd.slot;
-  // lanes: (row parity, column) for cells up to 32 wide, else one row of 64 columns per step
-  const int rpi = dw <= 32 ? 2 : 1, cpi = dw <= 32 ? 32 : 64;
-  const int lr = lane / cpi, lc = lane % cpi;
-  int count = 0;
-  for (int pass = 0; pass < 2; pass++) {
-    const int t = min(max(pass == 0 ? a.ini_th : a.min_th, 0), 255);
-    if (pass == 1 && t == min(max(a.ini_th, 0), 255)) break;
-    const int tt = max(t + 1, 2);
-    for (int r0 = 0; r0 < dh; r0 += rpi) {
-      const int rr = r0 + lr;
-      for (int c0 = 0; c0 < dw; c0 += cpi) {
-        const int cc = c0 + lc;
-        bool keep = false;
-        int m = 0;
-        if (rr < dh && cc < dw) {
-          const uint8_t* p = P + rr * RS + cc;
-          m = p[0];
-          if (m >= tt) {
-            const bool up = rr > 0, dn = rr + 1 < dh, lf = cc > 0, rt = cc + 1 < dw;
-            int mn = 0;
-            if (up) mn = max(mn, (int)p[-RS]);
-            if (dn) mn = max(mn, (int)p[RS]);
-            if (lf) mn = max(mn, (int)p[-1]);
-            if (rt) mn = max(mn, (int)p[1]);
-            if (up && lf) mn = max(mn, (int)p[-RS - 1]);
-            if (up && rt) mn = max(mn, (int)p[-RS + 1]);
-            if (dn && lf) mn = max(mn, (int)p[RS - 1]);
-            if (dn && rt) mn = max(mn, (int)p[RS + 1]);
-            keep = m > mn;
-          }
-        }
-        const uint64_t bal = wave_ballot(keep);
-        if (keep) out[count + prefix_in_wave(bal)] = pack_key(cc + 3 + cd.ox, rr + 3 + cd.oy, m - 1);
-        count += __popcll(bal);
-      }
     }
     if (count > 0) break;  // ORBextractor.cc:815-819: minThFAST only for an empty cell
   }
@@ -2460,7 +2057,6 @@ struct orbfe_extractor {
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
-  int fast_mode = 0;                 // orbfe_debug_set_fast_mode: 0 k_fast, 1 k_fast_map + k_fast_cells
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2479,11 +2075,6 @@ struct orbfe_extractor {
   int2* d_xtab = nullptr;
   int2* d_ytab = nullptr;
   int4* d_ywin = nullptr;
-  int4* d_ftiles = nullptr;
-  int nftiles = 0;
-  int4* d_rtiles = nullptr;  // k_fast_rows: {J, x0, first cell, last cell}
-  int nrtiles = 0;
-  bool rows_ok = false;      // every cell's detection columns fit one strip
   uint4* d_rgrp = nullptr;
   int* d_rgx0 = nullptr;
   // batch buffers
@@ -2492,7 +2083,6 @@ struct orbfe_extractor {
   size_t in_bytes = 0;
   uint8_t* d_pyr = nullptr;
   uint8_t* d_blur = nullptr;
-  uint8_t* d_fmap = nullptr;  // k_fast_map's arc strengths (fast_mode 1), allocated on first use
   uint32_t* d_cand = nullptr;
   int32_t* d_cellcnt = nullptr;
   uint32_t* d_keys_a = nullptr;
@@ -2543,9 +2133,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   std::vector<int4> yw;  // k_resize_win row table, indexed like yt
   std::vector<uint4> rgrp;
   std::vector<int> rgx0;
-  std::vector<int4> ft;  // k_fast_map tiles
-  std::vector<int4> rt;  // k_fast_rows tiles
-  bool rows_ok = true;
   long long pyr = 0;
   int cand = 0, keys = 0, rwmax = 0, rhmax = 0, ncap = 0, tiles = 0;
   for (int l = 0; l < L; l++) {
@@ -2618,28 +2205,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     }
     d.ncells = (int)cells.size() - d.cell_begin;
     d.cand_cap = cand - d.cand_begin;
-    // k_fast_map tiles over the detection pixels [19, w - 20] x [19, h - 20]: FM_COLS-column
-    // strips from column 16 (x0 = 0 mod 4), FM_RB-row bands from row 19
-    d.ftile_begin = (int)ft.size();
-    for (int y = 19; y <= d.h - 20; y += FM_RB)
-      for (int x = 16; x <= d.w - 20; x += FM_COLS) ft.push_back(make_int4(l, x, y, std::min(y + FM_RB, d.h - 19)));
-    d.nftiles = (int)ft.size() - d.ftile_begin;
-    // k_fast_rows tiles: runs of consecutive cells of one cell row whose detection columns fit the
-    // 248 data columns of a strip starting at the first one's dword
-    d.rtile_begin = (int)rt.size();
-    for (int c = d.cell_begin; c < (int)cells.size();) {
-      const int X = cells[c].x0 + 3, x0 = X & ~3;
-      int e = c;
-      while (e < (int)cells.size() && cells[e].y0 == cells[c].y0 &&
-             cells[e].x0 + 3 + (cells[e].rw - 6) <= x0 + FM_COLS)
-        e++;
-      if (e == c) {  // one cell wider than a strip
-        rows_ok = false;
-        e = c + 1;
-      }
-      rt.push_back(make_int4(e - c, x0, c, e - 1));
-      c = e;
-    }
     {  // k_blur strips of BS_W x BS_H, the remainder columns in bands of blur_h x BS_H rows
       d.tiles_x = d.w / BS_W;
       const int rem = d.w - d.tiles_x * BS_W;
@@ -2731,10 +2296,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_ywin);
-  hipFree(h->d_ftiles);
-  hipFree(h->d_rtiles);
-  h->d_ftiles = nullptr;
-  h->d_rtiles = nullptr;
   h->d_levels = nullptr;
   h->d_cells = nullptr;
   h->d_xtab = h->d_ytab = nullptr;
@@ -2753,15 +2314,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     ORBFE_HIP_CHECK(hipMemcpy(h->d_ytab, yt.data(), sizeof(int2) * yt.size(), hipMemcpyHostToDevice));
   if (!yw.empty())
     ORBFE_HIP_CHECK(hipMemcpy(h->d_ywin, yw.data(), sizeof(int4) * yw.size(), hipMemcpyHostToDevice));
-  ORBFE_HIP_CHECK(hipMalloc(&h->d_ftiles, sizeof(int4) * std::max<size_t>(ft.size(), 1)));
-  if (!ft.empty())
-    ORBFE_HIP_CHECK(hipMemcpy(h->d_ftiles, ft.data(), sizeof(int4) * ft.size(), hipMemcpyHostToDevice));
-  h->nftiles = (int)ft.size();
-  ORBFE_HIP_CHECK(hipMalloc(&h->d_rtiles, sizeof(int4) * std::max<size_t>(rt.size(), 1)));
-  if (!rt.empty())
-    ORBFE_HIP_CHECK(hipMemcpy(h->d_rtiles, rt.data(), sizeof(int4) * rt.size(), hipMemcpyHostToDevice));
-  h->nrtiles = (int)rt.size();
-  h->rows_ok = rows_ok;
   h->levels = lv;
   h->cells = cells;
   h->xtab = xt;
@@ -2801,7 +2353,6 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
 static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_pyr);
   hipFree(h->d_blur);
-  hipFree(h->d_fmap);
   hipFree(h->d_cand);
   hipFree(h->d_cellcnt);
   hipFree(h->d_keys_a);
@@ -2810,7 +2361,6 @@ static void free_batch(orbfe_extractor* h) {
   hipFree(h->d_lvlcnt);
   h->d_pyr = nullptr;
   h->d_blur = nullptr;
-  h->d_fmap = nullptr;
   h->d_cand = nullptr;
   h->d_cellcnt = nullptr;
   h->d_keys_a = h->d_keys_b = nullptr;
@@ -2915,47 +2465,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   a.atan.p7 = -0.04432655554792128f * (float)(180 / M_PI);
   a.atan.eps = (float)DBL_EPSILON;
   a.factor_pi = (float)(M_PI / 180.f);
-  const int fast_mode = h->fast_mode == 2 && !h->rows_ok ? 0 : h->fast_mode;
-  if (fast_mode == 2) {
-    a.ftiles = h->d_rtiles;
-    a.fr_dh = std::max(h->roi_h_max - 6, 1);
-    a.fr_list = std::max(FM_G * FM_COLS, a.fr_dh * std::max(h->roi_w_max - 6, 1));
-  }
-  if (fast_mode == 1) {
-    if (!h->d_fmap)  // (+256: the last strip's dword loads / stores stay inside the block)
-      ORBFE_HIP_CHECK(hipMalloc(&h->d_fmap, (size_t)h->pyr_stride * h->batch_cap + 256));
-    a.fmap = h->d_fmap + (long long)i0 * h->pyr_stride;
-    a.ftiles = h->d_ftiles;
-    a.fc_rs = (h->roi_w_max + 4 + 3) & ~3;
-    a.fc_lds = (a.fc_rs * std::max(h->roi_h_max - 6, 1) + 15) & ~15;
-  }
 
-  // fast_mode 1: levels [l0, l1) as the dense map pass then the per-cell pass
-  auto launch_fast_map = [&](hipStream_t s, int l0, int l1) -> int {
-    const int t0 = h->levels[l0].ftile_begin;
-    const int t1 = l1 < h->nlevels ? h->levels[l1].ftile_begin : h->nftiles;
-    const int c0 = h->levels[l0].cell_begin;
-    const int c1 = l1 < h->nlevels ? h->levels[l1].cell_begin : a.ncells;
-    if (t1 > t0) {
-      dim3 grid((t1 - t0 + 3) / 4, n);
-      ORBFE_LAUNCH("k_fast_map", k_fast_map, grid, dim3(256), 4 * FM_WAVE_LDS, s, a, t0, t1);
-    }
-    if (c1 > c0) {
-      dim3 grid((c1 - c0 + 3) / 4, n);
-      ORBFE_LAUNCH("k_fast_cells", k_fast_cells, grid, dim3(256), 4 * (size_t)a.fc_lds, s, a, c0, c1);
-    }
-    return ORBFE_OK;
-  };
-  // fast_mode 2: levels [l0, l1) as row-band runs of cells, one wavefront each
-  auto launch_fast_rows = [&](hipStream_t s, int l0, int l1) -> int {
-    const int t0 = h->levels[l0].rtile_begin;
-    const int t1 = l1 < h->nlevels ? h->levels[l1].rtile_begin : h->nrtiles;
-    if (t1 > t0) {
-      dim3 grid(t1 - t0, n);
-      ORBFE_LAUNCH("k_fast_rows", k_fast_rows, grid, dim3(64), fast_rows_lds(a.fr_dh, a.fr_list).total, s, a, t0, t1);
-    }
-    return ORBFE_OK;
-  };
   auto launch_fast = [&](hipStream_t s, int c0, int c1, bool main_launch = false) -> int {
     if (c1 <= c0) return ORBFE_OK;
     // wavefronts (cells) per workgroup: 4 for the side-stream launches of levels 0-2, which run
@@ -2993,8 +2503,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     const hipEvent_t e = l == 0 ? h->ev_l0 : h->ev_lvl[l];
     ORBFE_HIP_CHECK(hipEventRecord(e, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
-    if (fast_mode == 1) return launch_fast_map(side, l, l + 1);
-    if (fast_mode == 2) return launch_fast_rows(side, l, l + 1);
     const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
     return launch_fast(side, h->levels[l].cell_begin, c1);
   };
@@ -3030,14 +2538,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
-  if (k_side < h->nlevels) {
-    if (fast_mode == 1)
-      launch_fast_map(st, k_side, h->nlevels);
-    else if (fast_mode == 2)
-      launch_fast_rows(st, k_side, h->nlevels);
-    else
-      launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
-  }
+  if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
   ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
@@ -3190,8 +2691,6 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_xtab);
   hipFree(h->d_ytab);
   hipFree(h->d_ywin);
-  hipFree(h->d_ftiles);
-  hipFree(h->d_rtiles);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   hipFree(h->d_in);
@@ -3781,11 +3280,6 @@ extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_set_fast_mode(orbfe_extractor* h, int mode) {
-  if (!h || mode < 0 || mode > 2) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_fast_mode: bad argument");
-  h->fast_mode = mode;
-  return ORBFE_OK;
-}
 extern "C" int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k) {
   if (!h) return ORBFE_ERR_ARG;
   h->fast_side_levels = k > 0 ? k : -1;

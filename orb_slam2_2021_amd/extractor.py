@@ -297,12 +297,6 @@ class ORBextractor:
         after it (several handles sharing one side stream)."""
         L.check(self._lib.orbfe_debug_set_blur_mode(self._h, int(mode)), "set_blur_mode")
 
-    def debug_set_fast_mode(self, mode: int) -> None:
-        """FAST kernels: 0 k_fast (one wavefront per cell ROI, default), 1 k_fast_map (dense per-level
-        arc-strength map) + k_fast_cells (per-cell NMS / compaction), 2 k_fast_rows (both fused, one
-        wavefront per run of cells of a cell row). Same keys in every mode."""
-        L.check(self._lib.orbfe_debug_set_fast_mode(self._h, int(mode)), "set_fast_mode")
-
     def set_side_stream(self, stream: int) -> None:
         """Run the side-stream work on `stream` (a hipStream_t address; 0 restores the handle's own)."""
         L.check(self._lib.orbfe_set_side_stream(self._h, c_void_p(stream or 0)), "set_side_stream")

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ran at commit f55e8c0; the fast modes were removed after the A/B: DESIGN.md section 5)
 # k_fast_map + k_fast_cells (fast mode 1): parity, then the full -m gpu suite, then interleaved A/B.
 set -o pipefail
 O=gpurun_out/r5fm

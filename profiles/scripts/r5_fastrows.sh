@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ran at commit f55e8c0; the fast modes were removed after the A/B: DESIGN.md section 5)
 # k_fast_rows (fast mode 2): parity, then interleaved A/B against k_fast (mode 0), then a trace.
 set -o pipefail
 O=gpurun_out/r5fr

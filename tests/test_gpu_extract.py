@@ -130,48 +130,6 @@ def test_large_scale_factors(require_gpu, params):
     assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
 
-FAST_MAP_CASES = [((2000, 1.2, 8, 20, 7), (376, 1241), "synth"), ((2000, 1.2, 8, 20, 7), (376, 1241), "noise"),
-                  ((2000, 1.2, 8, 20, 7), (376, 1241), "sparse"), ((1000, 1.2, 8, 12, 7), (480, 640), "synth"),
-                  ((2000, 1.2, 8, 7, 20), (400, 700), "synth"), ((800, 1.1, 12, 20, 7), (480, 640), "noise"),
-                  ((1000, 2.5, 3, 20, 7), (600, 1241), "synth"), ((1000, 1.2, 8, 20, 7), (260, 1500), "synth"),
-                  ((500, 1.2, 2, 20, 7), (377, 643), "noise")]
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("params,shape,kind", FAST_MAP_CASES)
-def test_fast_map_mode(require_gpu, params, shape, kind, mode):
-    """orbfe_debug_set_fast_mode(1): the dense arc-strength map (k_fast_map) and the per-cell NMS /
-    compaction (k_fast_cells), and mode 2 (both fused per run of cells of a cell row, k_fast_rows),
-    give k_fast's candidates, hence the same extraction, on KITTI / TUM /
-    wide / tall shapes, iniThFAST > minThFAST, iniThFAST < minThFAST, textured noise and sparse
-    images (cells emptied at iniThFAST), and strip widths that are not multiples of 248."""
-    if kind == "synth":
-        img = synth_frame(23, *shape)
-    elif kind == "noise":
-        img = np.random.default_rng(7).integers(0, 256, shape, dtype=np.uint8)
-    else:
-        img = np.full(shape, 90, np.uint8)
-        img[100:140, 300:330] = 200
-        img[250:262, 900:1000] = 10
-        img[30:34, 20:1200] = 97
-    ext = ORBextractor(*params)
-    ext.debug_set_fast_mode(mode)
-    assert_same_extraction(ext, RefExtractor(*params), img)
-
-
-@pytest.mark.parametrize("mode", [1, 2])
-def test_fast_map_mode_batch(require_gpu, mode):
-    """The map mode over a batch: every image's candidates and outputs equal k_fast's."""
-    imgs = np.stack([synth_frame(i, 376, 1241) for i in range(5)])
-    a, b = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
-    b.debug_set_fast_mode(mode)
-    ra, rb = a.extract_batch(imgs), b.extract_batch(imgs)
-    for i in range(len(imgs)):
-        for l in range(8):
-            assert np.array_equal(a.debug_candidates(l, image=i), b.debug_candidates(l, image=i))
-        assert np.array_equal(ra[i][0], rb[i][0]) and np.array_equal(ra[i][1], rb[i][1])
-
-
 def test_empty_image(require_gpu):
     k, d = ORBextractor(2000, 1.2, 8, 20, 7)(np.zeros((0, 0), np.uint8))
     assert len(k) == 0 and d is None
