@@ -102,6 +102,9 @@ def parse(argv=None):
     p.add_argument("--blur-mode", type=int, default=-1,
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
                         "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
+    p.add_argument("--no-graphs", action="store_true",
+                   help="launch every extraction kernel directly instead of replaying the handle's captured "
+                        "launch graphs (orbfe_extractor_set_graphs)")
     p.add_argument("--match-inline", action="store_true",
                    help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
     p.add_argument("--stereo-on-extract", action="store_true",
@@ -127,7 +130,7 @@ def parse(argv=None):
                         "one of --input-slots device slots, overlapped with the other sub-batches' extraction and "
                         "matching (the reference's operator() takes host images, ORBextractor.cc:1041-1048)")
     p.add_argument("--input-slots", type=int, default=0,
-                   help="--feed host: device input slots (0: one per extractor handle)")
+                   help="--feed host: device input slots (0: two per extractor handle)")
     p.add_argument("--root-share", type=float, default=-1.0,
                    help="C4 (and --gather-proxy): the fraction of the per-rank sub-batches rank 0 extracts and "
                         "matches itself, since it also ingests every peer's payload; on the other slots it only "
@@ -318,12 +321,12 @@ class Gatherer:
 class HostFeed:
     """--feed host: each sub-batch's 2B images go from pinned host memory (the NB distinct input
     batches, page-locked once) into one of R device slots on the pipeline's copy stream, and the
-    extraction waits for that copy. R = the extractor handle count, so slot k mod R is read by the
-    handle that extracts sub-batch k; the copy into it for sub-batch k waits for that handle's
-    pyramid event, which at that point holds sub-batch k - R's record (only k_copy0 reads the input
-    images, before the pyramid completes). Copies run ahead of the extraction as far as the slots
-    allow; the link, not the kernels, bounds the rate when 2B images take longer to copy than to
-    process."""
+    extraction waits for that copy. After each extraction is enqueued, an event on its stream marks
+    the slot consumed (only k_copy0 reads the input images, and the whole extraction is behind the
+    event); the copy into slot k mod R for sub-batch k waits for sub-batch k - R's event. R defaults
+    to two per extractor handle, so the copies run up to R sub-batches ahead of the extraction and
+    the link, not slot reuse, bounds the rate when 2B images take longer to copy than to process
+    (round 4 tied the slots to the handles' pyramid events, R = 4: 45.8k stereo frames/s)."""
 
     def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0):
         import torch
@@ -335,27 +338,29 @@ class HostFeed:
         self.cs = copy_stream
         self.k = 0
         self.ready = []
+        self.consumed = []
         self.bytes_per_subbatch = n_img * H * W
 
     def upload(self, j, pipe):
         import torch
         from orb_slam2_2021_amd.pipeline import new_event
         if self.slots is None:
-            self.R = len(pipe.exts)
+            self.R = self.slots_req if self.slots_req > 0 else 2 * len(pipe.exts)
             self.slots = torch.empty((self.R, self.n_img, self.H, self.W), dtype=torch.uint8, device=self.dev)
             self.ready = [new_event(self.dev.index) for _ in range(self.R)]
+            self.consumed = [new_event(self.dev.index) for _ in range(self.R)]
         slot = self.k % self.R
-        ext = pipe.next_handle()
-        assert pipe.exts.index(ext) == slot, "slot k mod R is read by handle k mod R"
-        if self.k >= self.R:  # the slot's last reader: this handle's previous extraction (k - R)
-            L = pipe.lib
-            L.orbfe_stream_wait_event(ctypes.c_void_p(self.cs.cuda_stream),
-                                      ctypes.c_void_p(L.orbfe_extractor_pyramid_event(ext._h)))
+        if self.k >= self.R:  # sub-batch k - R's extraction read this slot
+            self.consumed[slot].wait(self.cs)
         with torch.cuda.stream(self.cs):
             self.slots[slot].copy_(self.h[j], non_blocking=True)
         self.ready[slot].record(self.cs)
         self.k += 1
         return self.slots[slot].data_ptr(), self.ready[slot]
+
+    def extracted(self, pipe):
+        """After pipe.run() of the last uploaded sub-batch: its slot is free once that extraction is."""
+        self.consumed[(self.k - 1) % self.R].record(pipe.last_stream)
 
     def describe(self, subbatches_per_s):
         gbs = self.bytes_per_subbatch * subbatches_per_s / 1e9
@@ -471,7 +476,7 @@ def main():
     d_img = torch.from_numpy(host).to(dev)
     feed = None
     if args.feed == "host":
-        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy)
+        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
@@ -496,6 +501,9 @@ def main():
             # and the shared side stream is better left to FAST alone: the blur follows the octree
             # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
+    if args.no_graphs:
+        for e in exts:
+            e.set_graphs(False)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)
@@ -528,6 +536,7 @@ def main():
         if feed is not None:  # the images go up from pinned host memory first (copy stream)
             ptr, ready = feed.upload(j, pipe)
             pipe.run(ptr, after_match=g.pack if g else None, input_ready=ready)
+            feed.extracted(pipe)
         else:
             pipe.run(d_img[j].data_ptr(), after_match=g.pack if g else None)
 
@@ -631,6 +640,7 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / args.steps, 4),
         "host_us_per_subbatch_unblocked": round(host_us, 1),
+        "launch_graphs": dict(zip(("captures", "replays", "held"), ext.debug_graph_stats())),
         **({"diagnostic": "matching skipped: extraction only, not the C3 metric"} if args.diag_skip_matching else {}),
         "higher_is_better": True,
         "scaling": "weak",
@@ -924,6 +934,16 @@ def c2_latency(args, left, right, reps=200):
         t0 = time.perf_counter()
         call(0)
         single.append(time.perf_counter() - t0)
+    # the same call with every kernel launched directly (orbfe_extractor_set_graphs(0))
+    exts[0].set_graphs(False)
+    for _ in range(10):
+        call(0)
+    direct = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        call(0)
+        direct.append(time.perf_counter() - t0)
+    exts[0].set_graphs(True)
     pair = []
     go = [threading.Event(), threading.Event()]
     done = [threading.Event(), threading.Event()]
@@ -973,11 +993,13 @@ def c2_latency(args, left, right, reps=200):
         t0 = time.perf_counter()
         call_pair()
         one_call.append(time.perf_counter() - t0)
-    out = {"single_image": percentiles(single), "stereo_two_threads": percentiles(pair[10:]),
+    out = {"single_image": percentiles(single), "single_image_direct_launches": percentiles(direct),
+           "stereo_two_threads": percentiles(pair[10:]),
            "stereo_pair_one_call": percentiles(one_call), "adapter": adapter_latency(),
            "what": "orbfe_extract wall-clock per call (host buffers in and out), 1241x376, 1 GPU; stereo_two_threads "
                    "= two handles on two threads as Frame.cc:113-116; stereo_pair_one_call = both images in one "
-                   "orbfe_extract_batch call on one handle"}
+                   "orbfe_extract_batch call on one handle; the launch sequence replayed from a captured hipGraph "
+                   "(the default), single_image_direct_launches = the same call with every kernel launched directly"}
     if not args.no_cpu:
         from oracle.orbref import RefExtractor
         k, d, n = bufs[0]

@@ -38,6 +38,8 @@ int orbfe_set_side_stream(orbfe_extractor* h, void* stream);
 /* Where GaussianBlur runs: 0 (default) on the side stream beside DistributeOctTree, 1 on the
  * launch stream after DistributeOctTree (several handles sharing one side stream). */
 int orbfe_debug_set_blur_mode(orbfe_extractor* h, int mode);
+/* Launch-graph counters of the handle: captures, replays, graphs held (3 values). */
+int orbfe_debug_graph_stats(const orbfe_extractor* h, long long* out3);
 /* The IC_Angle circle's row extents umax[0..15] the handle computed (ORBextractor.cc:457-472). */
 int orbfe_debug_get_umax(const orbfe_extractor* h, int32_t* umax16);
 /* computeOrbDescriptor's steering cos / sin (ORBextractor.cc:109-110) exactly as k_describe

@@ -111,6 +111,8 @@ _SIGNATURES = {
     "orbfe_get_level_device": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int),
                                        POINTER(c_int), POINTER(c_size_t)]),
     "orbfe_extractor_set_host_pyramid": (c_int, [c_void_p, c_int]),
+    "orbfe_extractor_set_graphs": (c_int, [c_void_p, c_int]),
+    "orbfe_debug_graph_stats": (c_int, [c_void_p, c_void_p]),
     "orbfe_ktimer_select": (c_int, [ctypes.c_char_p]),
     "orbfe_ktimer_read": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, POINTER(c_int)]),
     "orbfe_ktimer_reset": (c_int, []),

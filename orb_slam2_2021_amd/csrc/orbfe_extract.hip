@@ -1210,6 +1210,18 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
   return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
 }
 
+// Phase clocks of k_octree (profiling builds only, -DORBFE_OCT_PROF=1, read by
+// profiles/scripts/r5_octree_prof.py through orbfe_debug_octree_prof): per (image < 64, level < 16)
+// wall_clock64 at the kernel start, after the cell-count scan, the gather, the initial nodes, the
+// first refinement round, the loop end and the end, then n | passes << 24 | rounds << 32 | S << 48.
+#ifdef ORBFE_OCT_PROF
+__device__ unsigned long long g_oct_prof[64 * 16 * 8];
+#define OCT_MARK(k, v) \
+  do { if (threadIdx.x == 0 && blockIdx.y < 64 && l < 16) g_oct_prof[(blockIdx.y * 16 + l) * 8 + (k)] = (v); } while (0)
+#else
+#define OCT_MARK(k, v) do { } while (0)
+#endif
+
 template <bool LDSK>
 __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, int l, int n, uint32_t* ka,
                                            uint32_t* kb) {
@@ -1238,6 +1250,17 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     const int b0 = sa[c], cnt = (c + 1 < ncells ? sa[c + 1] : n) - b0;
     const uint32_t* src = cand + sx[c];
     int k = 0;
+#ifdef ORBFE_OCT_GATHER16
+    {  // the first 16 keys of the cell in flight together (a 30x30 cell holds ~10-20 at level 0)
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; q++) v[q] = q < cnt ? src[q] : 0u;
+#pragma unroll
+      for (int q = 0; q < 16; q++)
+        if (q < cnt) ka[b0 + q] = v[q];
+      k = min(cnt, 16);
+    }
+#endif
     for (; k + 4 <= cnt; k += 4) {
       const uint32_t v0 = src[k], v1 = src[k + 1], v2 = src[k + 2], v3 = src[k + 3];
       ka[b0 + k] = v0;
@@ -1248,6 +1271,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     for (; k < cnt; k++) ka[b0 + k] = src[k];
   }
   __syncthreads();
+  OCT_MARK(2, wall_clock64());
 
   // 2. initial nodes (:555-588): key -> vpIniNodes[(size_t)(x / hX)], stable, all 4 waves:
   //    wave w counts then places the keys of its quarter; bucket offsets in between
@@ -1357,11 +1381,14 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   int S = misc[8];
   int cur = 0;
   bool refine = false;
+  OCT_MARK(3, wall_clock64());
+  int n_passes = 0, n_rounds = 0;
   for (int iter = 0; iter < 4 * NC + 64; iter++) {
     ONode* Lc = cur ? nodes1 : nodes0;
     ONode* Ln = cur ? nodes0 : nodes1;
     const int prevS = S;
     if (!refine) {
+      n_passes++;
       // ---- full pass (:603-668) ----
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
@@ -1411,6 +1438,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       if (S >= N || S == prevS) break;
       if (S + nexp * 3 > N) refine = true;
     } else {
+      if (n_rounds++ == 0) OCT_MARK(4, wall_clock64());
       // ---- refinement round (:679-740) ----
       for (int i = t; i < S; i += 256) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
       __syncthreads();
@@ -1550,6 +1578,8 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     }
   }
 
+  OCT_MARK(5, wall_clock64());
+  if (n_rounds == 0) OCT_MARK(4, wall_clock64());
   // 3. retain the best key of every node, in list order (:744-763; strict '>' keeps the first)
   ONode* Lf = cur ? nodes1 : nodes0;
   for (int i = t; i < S; i += 256) {
@@ -1564,6 +1594,12 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     out[i] = pack_key(key_x(best) + 16, key_y(best) + 16, key_s(best));
   }
   if (t == 0) *out_n = S;
+#ifdef ORBFE_OCT_PROF
+  __syncthreads();
+  OCT_MARK(6, wall_clock64());
+  OCT_MARK(7, (unsigned long long)n | ((unsigned long long)n_passes << 24) | ((unsigned long long)n_rounds << 32) |
+                  ((unsigned long long)S << 48));
+#endif
 }
 
 
@@ -1575,6 +1611,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a, int l0) {
   int* sx = sa + 2 * SA;
   int* misc = reinterpret_cast<int*>(reinterpret_cast<unsigned long long*>(sx + SA) + SC);
   uint32_t* lds_keys = reinterpret_cast<uint32_t*>(misc + 16);
+  OCT_MARK(0, wall_clock64());
   const LevelDesc ld = a.levels[l];
   const int32_t* ccount = a.cellcnt + (long long)img * a.ncells + ld.cell_begin;
   for (int c = t; c < ld.ncells; c += 256) {
@@ -1583,6 +1620,7 @@ __global__ __launch_bounds__(256) void k_octree(ExtractArgs a, int l0) {
   }
   __syncthreads();
   const int n = block_scan_excl(sa, ld.ncells, misc);
+  OCT_MARK(1, wall_clock64());
   if (n == 0) {
     if (t == 0) a.lvlcnt[(long long)img * a.nlevels + l] = 0;
     return;
@@ -2121,9 +2159,22 @@ struct orbfe_extractor {
   bool hpyr_pending = false;
   // Frame::ComputeStereoMatches scratch (orbfe_stereo.hip)
   OrbfeStereoScratch* stereo = nullptr;
+  // launch_extract's enqueue sequence captured once per distinct set of arguments and replayed as
+  // a hipGraph (orbfe_extractor_set_graphs; `graphs` keyed by everything the sequence depends on)
+  int use_graphs = 1;
+  struct GraphEntry {
+    std::vector<uintptr_t> key;
+    hipGraphExec_t exec;
+    unsigned long long used;
+  };
+  std::vector<GraphEntry> graphs;
+  unsigned long long graph_clock = 0;
+  unsigned long long graph_hits = 0, graph_captures = 0;
 };
 
 constexpr int OCT_LDS_KB = 80;  // k_octree's LDS per workgroup (two per CU)
+static size_t octree_lds(const orbfe_extractor* h);
+static void drop_graphs(orbfe_extractor* h);
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   if (h->rows == rows && h->cols == cols && h->geom_mode == h->resize_mode) return ORBFE_OK;
   const int L = h->nlevels;
@@ -2279,8 +2330,9 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
       d.simd_end = se;
     }
   }
-  // release old geometry buffers and upload new ones
+  // release old geometry buffers and upload new ones (and the launch graphs that point at them)
   hipSetDevice(h->device);
+  drop_graphs(h);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   h->d_rgrp = nullptr;
@@ -2347,10 +2399,24 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->cols = cols;
   h->geom_mode = h->resize_mode;
   h->batch_cap = 0;  // strides changed: reallocate batch buffers on the next call
+  // k_octree's dynamic LDS limit, set here rather than per launch (a host call a captured launch
+  // sequence cannot replay); the attribute is per function, so the largest plan any handle of the
+  // process asked for stays in force
+  static std::mutex attr_mu;
+  static int attr_lds = 0;
+  {
+    std::lock_guard<std::mutex> lk(attr_mu);
+    const int need = (int)octree_lds(h);
+    if (need <= 160 * 1024 && need > attr_lds) {
+      ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      attr_lds = need;
+    }
+  }
   return ORBFE_OK;
 }
 
 static void free_batch(orbfe_extractor* h) {
+  drop_graphs(h);
   hipFree(h->d_pyr);
   hipFree(h->d_blur);
   hipFree(h->d_cand);
@@ -2521,8 +2587,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     if (l < k_side) side_fast(l);
   }
   if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
-  ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)octree_lds(h)));
   auto launch_octree = [&](hipStream_t s, int l0, int nl) {
     if (nl <= 0) return;
     dim3 grid(nl, n);
@@ -2534,7 +2598,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // DistributeOctTree of the side's levels on the side stream right after their FAST, beside the
   // main stream's FAST -- bench 63.7k vs 67.0k stereo frames/s, it competes with that FAST; the
   // blur on the side stream as soon as the pyramid is complete -- 65.1k vs 69.3-70.0k.)
-  ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));  // the pyramid is complete on st
+  // the pyramid is complete on st (under capture this record is only a graph-internal dependency:
+  // launch_extract_graphed records the event again after the graph launch)
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));
   const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
@@ -2562,6 +2628,90 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   h->last_n = i0 + n;
   h->last_stream = st;
   return ORBFE_OK;
+}
+
+// launch_extract through a hipGraph: the enqueue sequence (about 20 kernel launches and the side
+// stream's fork / join events) is captured from the launch stream the first time a set of
+// arguments is seen, instantiated, and replayed with one hipGraphLaunch afterwards. The key holds
+// every input the sequence depends on: the caller's pointers, strides and stream, the handle's
+// scratch (reallocated buffers change it), streams and placement switches. Launches stay direct
+// while the kernel timer is on (its per-dispatch events cannot be captured), while the stream is
+// already being captured by the caller, or after a capture failed on this handle.
+constexpr size_t kMaxGraphs = 8;
+static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_imgs, long long img_stride,
+                                  int pitch, orbfe_keypoint* d_kps, uint8_t* d_desc, int cap,
+                                  int32_t* d_counts, hipStream_t st, int i0 = 0) {
+  // the per-level fork events exist before any capture
+  while ((int)h->ev_lvl.size() < h->nlevels) {
+    hipEvent_t e = nullptr;
+    ORBFE_HIP_CHECK(hipEventCreateWithFlags(&e, kForkJoinEvent));
+    h->ev_lvl.push_back(e);
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (!h->use_graphs || !st || orbfe_kt::g_on.load(std::memory_order_relaxed) ||
+      hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return launch_extract(h, n, d_imgs, img_stride, pitch, d_kps, d_desc, cap, d_counts, st, i0);
+  const hipStream_t side = h->inline_side ? st : (h->side_ext ? h->side_ext : h->side);
+  const std::vector<uintptr_t> key = {
+      (uintptr_t)n, (uintptr_t)d_imgs, (uintptr_t)img_stride, (uintptr_t)pitch, (uintptr_t)d_kps,
+      (uintptr_t)d_desc, (uintptr_t)cap, (uintptr_t)d_counts, (uintptr_t)st, (uintptr_t)i0, (uintptr_t)side,
+      (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
+      (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
+      (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->blur_mode};
+  h->graph_clock++;
+  hipGraphExec_t exec = nullptr;
+  for (auto& e : h->graphs)
+    if (e.key == key) {
+      exec = e.exec;
+      e.used = h->graph_clock;
+      h->graph_hits++;
+      break;
+    }
+  if (!exec) {
+    hipGraph_t g = nullptr;
+    ORBFE_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int r = launch_extract(h, n, d_imgs, img_stride, pitch, d_kps, d_desc, cap, d_counts, st, i0);
+    const hipError_t ee = hipStreamEndCapture(st, &g);
+    hipError_t ie = hipErrorUnknown;
+    if (r == ORBFE_OK && ee == hipSuccess && g) ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (g) hipGraphDestroy(g);
+    if (r != ORBFE_OK) return r;
+    if (ee != hipSuccess || ie != hipSuccess) {  // this handle launches directly from now on
+      (void)hipGetLastError();
+      h->use_graphs = 0;
+      return launch_extract(h, n, d_imgs, img_stride, pitch, d_kps, d_desc, cap, d_counts, st, i0);
+    }
+    if (h->graphs.size() >= kMaxGraphs) {
+      auto lru = std::min_element(h->graphs.begin(), h->graphs.end(),
+                                  [](const orbfe_extractor::GraphEntry& a, const orbfe_extractor::GraphEntry& b) {
+                                    return a.used < b.used;
+                                  });
+      hipGraphExecDestroy(lru->exec);
+      h->graphs.erase(lru);
+    }
+    h->graphs.push_back({key, exec, h->graph_clock});
+    h->graph_captures++;
+  }
+  ORBFE_HIP_CHECK(hipGraphLaunch(exec, st));
+  // for the callers that wait on the pyramid event (the host pyramid prefetch, other streams'
+  // consumers of orbfe_extractor_pyramid_event): recorded after the whole replayed extraction, a
+  // later point than the direct launches' record after the resize chain. (Capturing the record as
+  // an external event node, hipEventRecordWithFlags(..., hipEventRecordExternal), failed with
+  // "invalid argument" in the host-fed pipeline on ROCm 7.2.)
+  ORBFE_HIP_CHECK(hipEventRecord(h->ev_pyr, st));
+  h->last_img0 = d_imgs - (long long)i0 * img_stride;
+  h->last_img_stride = img_stride;
+  h->last_img_pitch = pitch;
+  h->last_n = i0 + n;
+  h->last_stream = st;
+  return ORBFE_OK;
+}
+
+static void drop_graphs(orbfe_extractor* h) {
+  for (auto& e : h->graphs) hipGraphExecDestroy(e.exec);
+  h->graphs.clear();
 }
 
 // The host block of orbfe_get_level, sized for n images of the current geometry. Called once per
@@ -2685,6 +2835,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   orbfe_internal_stereo_free(h->stereo);
+  drop_graphs(h);
   free_batch(h);
   hipFree(h->d_levels);
   hipFree(h->d_cells);
@@ -2838,8 +2989,8 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
   if (st != ORBFE_OK) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   h->gen++;  // the host pyramid block of the previous call is stale from here on
-  return launch_extract(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
-                        d_counts, s);
+  return launch_extract_graphed(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
+                                d_counts, s);
 }
 
 static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
@@ -3033,8 +3184,9 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_in[g], h->h2d));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->stream, h->ev_in[g], 0));
     }
-    st = launch_extract(h, ng, h->d_in + (size_t)g0 * img_bytes, (long long)img_bytes, cols, h->d_kps + (size_t)g0 * K,
-                        h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0, h->stream, g0);
+    st = launch_extract_graphed(h, ng, h->d_in + (size_t)g0 * img_bytes, (long long)img_bytes, cols,
+                                h->d_kps + (size_t)g0 * K, h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0,
+                                h->stream, g0);
     if (st != ORBFE_OK) return st;
     if (h->host_pyramid) {
       // mvImagePyramid for a CPU Frame::ComputeStereoMatches: the group's pyramids go down on the
@@ -3174,6 +3326,35 @@ extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const u
   const LevelDesc& d = h->levels[level];
   *p = h->h_pyr + (size_t)image * h->pyr_stride + d.pyr_off;
   *step = (size_t)d.pitch;
+  return ORBFE_OK;
+}
+
+// profiling builds only (not declared in a header): the k_octree phase clocks, 64 * 16 * 8 values
+extern "C" int orbfe_debug_octree_prof(unsigned long long* out, int cap) {
+#ifdef ORBFE_OCT_PROF
+  if (!out || cap < 64 * 16 * 8) return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_prof), sizeof(unsigned long long) * 64 * 16 * 8));
+  return ORBFE_OK;
+#else
+  (void)out;
+  (void)cap;
+  return orbfe_set_error(ORBFE_ERR_STATE, "built without ORBFE_OCT_PROF");
+#endif
+}
+
+extern "C" int orbfe_extractor_set_graphs(orbfe_extractor* h, int enable) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extractor_set_graphs: null handle");
+  hipSetDevice(h->device);
+  if (!enable) drop_graphs(h);
+  h->use_graphs = enable ? 1 : 0;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_graph_stats(const orbfe_extractor* h, long long* out3) {
+  if (!h || !out3) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_graph_stats: bad argument");
+  out3[0] = (long long)h->graph_captures;
+  out3[1] = (long long)h->graph_hits;
+  out3[2] = (long long)h->graphs.size();
   return ORBFE_OK;
 }
 

@@ -248,6 +248,18 @@ class ORBextractor:
         beside the extraction, so mvImagePyramid costs no copy of its own."""
         L.check(self._lib.orbfe_extractor_set_host_pyramid(self._h, 1 if on else 0), "set_host_pyramid")
 
+    def set_graphs(self, on: bool) -> None:
+        """orbfe_extractor_set_graphs: replay each extract call's launch sequence as a hipGraph
+        captured per argument set (default on); off launches every kernel directly."""
+        L.check(self._lib.orbfe_extractor_set_graphs(self._h, 1 if on else 0), "set_graphs")
+
+    def debug_graph_stats(self) -> tuple:
+        """(graph captures, graph replays, graphs held) of this handle."""
+        import numpy as np
+        out = np.zeros(3, np.int64)
+        L.check(self._lib.orbfe_debug_graph_stats(self._h, out.ctypes.data), "graph_stats")
+        return tuple(int(x) for x in out)
+
     @property
     def mvImagePyramid(self) -> List[np.ndarray]:
         return [self.level(l) for l in range(self.nlevels)]
@@ -261,7 +273,6 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_get_candidates(self._h, image, level, L.ptr(out), len(out),
                                                      byref(n)), "debug_candidates")
         return out[:n.value]
-
     def debug_candidate_total(self) -> int:
         """FAST candidates over every image and level of the last call."""
         t = ctypes.c_longlong()

@@ -287,6 +287,7 @@ class C3Pipeline:
         self.mstream = self.stream if self.match_inline else streams[-1]
         self.counter = 0
         self.last = None
+        self.last_stream = None
         self._torch = torch
         # stereo_on_match: ComputeStereoMatches on the matching stream (it needs only the extracted
         # pyramids and keypoints) instead of right after the extraction; the handle's next
@@ -325,6 +326,7 @@ class C3Pipeline:
                                  o.desc.data_ptr(), cap, o.cnt.data_ptr(), stream=s.cuda_stream)
         o.ext = ext
         o.k = k
+        self.last_stream = s  # the extraction stream of this sub-batch
         if self.stereo and not self.stereo_on_match:  # Frame.cc:125, on the extraction stream
             self._stereo(o, ext, s)
         o.extracted.record(s)

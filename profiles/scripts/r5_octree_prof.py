@@ -1,0 +1,61 @@
+"""k_octree phase clocks (DistributeOctTree, ORBextractor.cc:542-766) of a profiling build of
+liborbfe (-DORBFE_OCT_PROF=1, ORBFE_LIB pointing at it): one 64-image KITTI-shaped extraction at a
+time, the handle alone on the GPU (inline side work, so the octree launch runs by itself), then per
+level the mean and max over images of each phase in microseconds (wall_clock64, 100 MHz), the key
+count, the full passes and refinement rounds, and the launch's span.
+usage: ORBFE_LIB=... python profiles/scripts/r5_octree_prof.py [reps]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from orb_slam2_2021_amd import ORBextractor, synth_frame  # noqa: E402
+from orb_slam2_2021_amd import _lib as L  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    n, H, W = 64, 376, 1241
+    dev = torch.device("cuda", 0)
+    imgs = torch.from_numpy(np.stack([synth_frame(i, H, W) for i in range(n)])).to(dev)
+    ext = ORBextractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_inline_side(True)
+    cap = ext.max_keypoints(H, W)
+    kps = torch.empty(n * cap * 28, dtype=torch.uint8, device=dev)
+    desc = torch.empty(n * cap * 32, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    lib = L.lib()
+    fn = lib.orbfe_debug_octree_prof
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = np.zeros(64 * 16 * 8, np.uint64)
+    names = ["scan", "gather", "initial", "passes", "refine", "retain"]
+    acc = []
+    for r in range(reps + 1):
+        ext.extract_batch_device(n, imgs.data_ptr(), H * W, H, W, W, kps.data_ptr(), desc.data_ptr(), cap,
+                                 cnt.data_ptr())
+        torch.cuda.synchronize()
+        L.check(fn(buf.ctypes.data, buf.size), "octree_prof")
+        if r:
+            acc.append(buf.reshape(64, 16, 8).astype(np.int64).copy())
+    a = np.stack(acc)  # reps x img x level x 8
+    t = a[..., :7].astype(np.float64) / 100.0  # us
+    start = t[..., 0]
+    print(f"launch span (first block start .. last block end): "
+          f"{np.mean([(t[i, :, :8, 6].max() - start[i, :, :8].min()) for i in range(len(acc))]):.1f} us")
+    print("level  n_keys passes rounds  S   " + "  ".join(f"{x:>13s}" for x in names) + "   total(mean/max)")
+    for l in range(8):
+        c = a[..., l, 7]
+        nk, passes, rounds, S = c & 0xffffff, (c >> 24) & 0xff, (c >> 32) & 0xffff, (c >> 48) & 0xffff
+        ph = [t[..., l, k + 1] - t[..., l, k] for k in range(6)]
+        tot = t[..., l, 6] - t[..., l, 0]
+        print(f"{l:5d} {nk.mean():7.0f} {passes.mean():6.1f} {rounds.mean():6.1f} {S.mean():5.0f}  " +
+              "  ".join(f"{p.mean():6.1f}/{p.max():6.1f}" for p in ph) + f"   {tot.mean():6.1f}/{tot.max():6.1f}")
+
+
+if __name__ == "__main__":
+    main()

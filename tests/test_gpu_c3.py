@@ -101,3 +101,24 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
                      st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"], pairs=pairs)
         assert r["all"], (j, r)
     streams.close()
+
+
+@pytest.mark.parametrize("slots", ["0", "4", "5"])
+def test_bench_host_fed_parity(require_gpu, slots):
+    """bench.py --feed host: every sub-batch's images copied from pinned host memory into a ring of
+    device slots on the copy stream, a slot reused only after the extraction that read it (its
+    consumed event). Default ring (2 per handle: 8), one slot per handle (4) and a ring that is not a
+    multiple of the handle count (5): the timed line's last sub-batch is bit-exact against the oracle
+    chain, and the line reports the ring it used."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--feed", "host", "--input-slots", slots, "--steps", "1",
+           "--warmup", "1", "--batches-per-step", "24", "--no-cpu", "--no-legs", "--event-every", "1000000"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["parity_bit_exact"] is True
+    assert line["feed"]["device_slots"] == (8 if slots == "0" else int(slots))

@@ -279,3 +279,63 @@ def test_device_input_odd_pitch_and_alignment(require_gpu):
     for i in reversed(range(n)):
         c = int(C[i])
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=(K[i, :c], D[i, :c]))
+
+
+def test_launch_graph_replay(require_gpu):
+    """The launch sequence replayed from hipGraphs (the default) equals direct launches: host path
+    (orbfe_extract, captured once then replayed), device batches into alternating output sets on a
+    caller's stream (one graph per argument set), a new output pointer (a new capture), the kernel
+    timer on (direct launches inside a graphed handle), and graphs off."""
+    import torch
+    from orb_slam2_2021_amd import _lib as L
+    imgs = [synth_frame(60 + i, 376, 1241) for i in range(3)]
+    a, b = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
+    b.set_graphs(False)
+    for img in imgs + imgs:
+        ka, da = a(img)
+        kb, db = b(img)
+        for f in ("x", "y", "size", "response", "octave", "angle"):
+            assert np.array_equal(ka[f], kb[f]), f
+        assert np.array_equal(da, db)
+    cap_, hits, held = a.debug_graph_stats()
+    assert cap_ == 1 and hits == 5 and held == 1, (cap_, hits, held)
+    assert b.debug_graph_stats() == (0, 0, 0)
+    # device batches: 2 images per call, two output sets, a caller stream
+    dev = torch.device("cuda", 0)
+    n, H, W = 2, 376, 1241
+    cap = a.max_keypoints(H, W)
+    d_in = torch.from_numpy(np.stack(imgs[:n])).to(dev)
+    outs = [(torch.empty(n * cap * 28, dtype=torch.uint8, device=dev), torch.empty(n * cap * 32, dtype=torch.uint8, device=dev),
+             torch.zeros(n, dtype=torch.int32, device=dev)) for _ in range(3)]
+    s = torch.cuda.Stream(dev)
+
+    def run(e, o):
+        e.extract_batch_device(n, d_in.data_ptr(), H * W, H, W, W, o[0].data_ptr(), o[1].data_ptr(), cap,
+                               o[2].data_ptr(), stream=s.cuda_stream)
+
+    for k in range(6):
+        run(a, outs[k % 2])
+    run(b, outs[2])
+    torch.cuda.synchronize()
+    for o in outs[:2]:
+        assert torch.equal(o[2], outs[2][2])
+        for i in range(n):
+            c = int(outs[2][2][i])
+            assert torch.equal(o[0][i * cap * 28:(i * cap + c) * 28], outs[2][0][i * cap * 28:(i * cap + c) * 28])
+            assert torch.equal(o[1][i * cap * 32:(i * cap + c) * 32], outs[2][1][i * cap * 32:(i * cap + c) * 32])
+    cap2, hits2, held2 = a.debug_graph_stats()
+    # (the 2-image batch reallocated the handle's scratch, which drops the 1-image host-path graph)
+    assert cap2 == 3 and hits2 == 5 + 4 and held2 == 2, (cap2, hits2, held2)
+    # the kernel timer on: launches go direct (no capture, no replay)
+    L.ktimer_select(True)
+    try:
+        run(a, outs[0])
+        torch.cuda.synchronize()
+    finally:
+        L.ktimer_select(False)
+        L.ktimer_read()
+    assert a.debug_graph_stats() == (cap2, hits2, held2)
+    assert torch.equal(outs[0][2], outs[2][2])
+    # graphs off drops them
+    a.set_graphs(False)
+    assert a.debug_graph_stats()[2] == 0
