@@ -102,9 +102,12 @@ def parse(argv=None):
     p.add_argument("--blur-mode", type=int, default=-1,
                    help="GaussianBlur placement (orbfe_debug_set_blur_mode): 0 beside DistributeOctTree on the "
                         "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
-    p.add_argument("--no-graphs", action="store_true",
-                   help="launch every extraction kernel directly instead of replaying the handle's captured "
-                        "launch graphs (orbfe_extractor_set_graphs)")
+    p.add_argument("--octree-split", type=int, default=-1,
+                   help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
+                        "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, one launch)")
+    p.add_argument("--graphs", action="store_true",
+                   help="replay each extraction's launch sequence from the handle's captured hipGraphs "
+                        "(orbfe_extractor_set_graphs; off by default: 38.6k vs 83.7k stereo frames/s, round 5)")
     p.add_argument("--match-inline", action="store_true",
                    help="vocabulary + matching on each sub-batch's extraction stream (no matching stream)")
     p.add_argument("--stereo-on-extract", action="store_true",
@@ -501,9 +504,12 @@ def main():
             # and the shared side stream is better left to FAST alone: the blur follows the octree
             # on the handle's own stream (82.0k vs 80.8k stereo frames/s, interleaved runs)
             e.debug_set_blur_mode(args.blur_mode if args.blur_mode >= 0 else 1)
-    if args.no_graphs:
+    if args.graphs:
         for e in exts:
-            e.set_graphs(False)
+            e.set_graphs(True)
+    if args.octree_split >= 0:
+        for e in exts:
+            e.debug_set_octree_split(args.octree_split)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)
@@ -934,16 +940,16 @@ def c2_latency(args, left, right, reps=200):
         t0 = time.perf_counter()
         call(0)
         single.append(time.perf_counter() - t0)
-    # the same call with every kernel launched directly (orbfe_extractor_set_graphs(0))
-    exts[0].set_graphs(False)
+    # the same call replayed from a captured hipGraph (orbfe_extractor_set_graphs(1))
+    exts[0].set_graphs(True)
     for _ in range(10):
         call(0)
-    direct = []
+    graphed = []
     for _ in range(reps):
         t0 = time.perf_counter()
         call(0)
-        direct.append(time.perf_counter() - t0)
-    exts[0].set_graphs(True)
+        graphed.append(time.perf_counter() - t0)
+    exts[0].set_graphs(False)
     pair = []
     go = [threading.Event(), threading.Event()]
     done = [threading.Event(), threading.Event()]
@@ -993,13 +999,13 @@ def c2_latency(args, left, right, reps=200):
         t0 = time.perf_counter()
         call_pair()
         one_call.append(time.perf_counter() - t0)
-    out = {"single_image": percentiles(single), "single_image_direct_launches": percentiles(direct),
+    out = {"single_image": percentiles(single), "single_image_graph_replay": percentiles(graphed),
            "stereo_two_threads": percentiles(pair[10:]),
            "stereo_pair_one_call": percentiles(one_call), "adapter": adapter_latency(),
            "what": "orbfe_extract wall-clock per call (host buffers in and out), 1241x376, 1 GPU; stereo_two_threads "
                    "= two handles on two threads as Frame.cc:113-116; stereo_pair_one_call = both images in one "
-                   "orbfe_extract_batch call on one handle; the launch sequence replayed from a captured hipGraph "
-                   "(the default), single_image_direct_launches = the same call with every kernel launched directly"}
+                   "orbfe_extract_batch call on one handle; single_image_graph_replay = the same call with the launch "
+                   "sequence replayed from a captured hipGraph (orbfe_extractor_set_graphs, off by default)"}
     if not args.no_cpu:
         from oracle.orbref import RefExtractor
         k, d, n = bufs[0]

@@ -103,7 +103,7 @@ class Extractor {
   }
   // Copy each call's pyramid to the host beside the extraction (orbfe_extractor_set_host_pyramid).
   void SetHostPyramid(bool on) { check(orbfe_extractor_set_host_pyramid(h_, on ? 1 : 0), "set_host_pyramid"); }
-  // Replay the launch sequence as a hipGraph per argument set (default on; orbfe_extractor_set_graphs).
+  // Replay the launch sequence as a hipGraph per argument set (default off; orbfe_extractor_set_graphs).
   void SetGraphs(bool on) { check(orbfe_extractor_set_graphs(h_, on ? 1 : 0), "set_graphs"); }
 
   // getters (ORBextractor.h:70-98)

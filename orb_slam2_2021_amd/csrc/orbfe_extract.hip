@@ -1210,14 +1210,38 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
   return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
 }
 
+// The nodes of list positions [0, m) (position p -> node index idx(p)) holding more than OCT_SMALL
+// keys, dealt round-robin over the block's 4 wavefronts in position order: each wavefront reads the
+// counts of 64 positions at a time (one LDS read per lane) and walks the ballot of the big ones, so
+// no wavefront steps through the small nodes one dependent read at a time.
+template <typename Idx, typename F>
+__device__ __forceinline__ void for_big_nodes(const ONode* L, int m, Idx idx, F f) {
+  const int w = wave_id(), lane = lane_id();
+  int ord = 0;
+  for (int c0 = 0; c0 < m; c0 += 64) {
+    const int p = c0 + lane;
+    const bool big = p < m && L[idx(p)].count > OCT_SMALL;
+    uint64_t bal = wave_ballot(big);
+    while (bal) {
+      const int b = __builtin_ctzll(bal);
+      bal &= bal - 1;
+      if ((ord & 3) == w) f(c0 + b);
+      ord++;
+    }
+  }
+}
+
 // Phase clocks of k_octree (profiling builds only, -DORBFE_OCT_PROF=1, read by
 // profiles/scripts/r5_octree_prof.py through orbfe_debug_octree_prof): per (image < 64, level < 16)
 // wall_clock64 at the kernel start, after the cell-count scan, the gather, the initial nodes, the
-// first refinement round, the loop end and the end, then n | passes << 24 | rounds << 32 | S << 48.
+// first refinement round, the loop end and the end, then n | passes << 24 | rounds << 32 | S << 48;
+// slots 8-13 inside the first refinement round (after the flag scan, the sort, the child counts,
+// the stop scan, the partition, the round), 14-15 inside the first full pass (after the splits,
+// after the scan).
 #ifdef ORBFE_OCT_PROF
-__device__ unsigned long long g_oct_prof[64 * 16 * 8];
+__device__ unsigned long long g_oct_prof[64 * 16 * 16];
 #define OCT_MARK(k, v) \
-  do { if (threadIdx.x == 0 && blockIdx.y < 64 && l < 16) g_oct_prof[(blockIdx.y * 16 + l) * 8 + (k)] = (v); } while (0)
+  do { if (threadIdx.x == 0 && blockIdx.y < 64 && l < 16) g_oct_prof[(blockIdx.y * 16 + l) * 16 + (k)] = (v); } while (0)
 #else
 #define OCT_MARK(k, v) do { } while (0)
 #endif
@@ -1295,19 +1319,42 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   const bool cached = wend - wbeg <= 64 * INI_J;
   uint32_t kr[INI_J];
   int br[INI_J];
+  const int nj = (wend - wbeg + 63) >> 6;  // register rows this wave uses (wave-uniform)
   if (cached) {
+    // only the rows the wave's keys fill, the bucket by compares against the host thresholds
+    // (the division form only for nIni > 8), so the unrolled loop carries no dead rows
 #pragma unroll
-    for (int j = 0; j < INI_J; j++) {
-      const int i = wbeg + 64 * j + lane;
-      kr[j] = i < wend ? ka[i] : 0u;
-      br[j] = i < wend ? ini_node(kr[j]) : -1;
+    for (int j = 0; j < INI_J; j++) br[j] = -1;
+    if (nini <= 8) {
+#pragma unroll
+      for (int j = 0; j < INI_J; j++) {
+        if (j >= nj) break;
+        const int i = wbeg + 64 * j + lane;
+        kr[j] = i < wend ? ka[i] : 0u;
+        const int x = key_x(kr[j]);
+        int b = 0;
+#pragma unroll
+        for (int k = 1; k < 8; k++) b += (k < nini && x >= ld.ini_thr[k]) ? 1 : 0;
+        br[j] = i < wend ? b : -1;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < INI_J; j++) {
+        if (j >= nj) break;
+        const int i = wbeg + 64 * j + lane;
+        kr[j] = i < wend ? ka[i] : 0u;
+        br[j] = i < wend ? (int)((float)key_x(kr[j]) / hx) : -1;
+      }
     }
   }
   for (int bkt = 0; bkt < nini; bkt++) {
     int cnt = 0;
     if (cached) {
 #pragma unroll
-      for (int j = 0; j < INI_J; j++) cnt += __popcll(wave_ballot(br[j] == bkt));
+      for (int j = 0; j < INI_J; j++) {
+        if (j >= nj) break;
+        cnt += __popcll(wave_ballot(br[j] == bkt));
+      }
     } else {
       for (int i0 = wbeg; i0 < wend; i0 += 64) {
         const int i = i0 + lane;
@@ -1335,6 +1382,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     if (cached) {
 #pragma unroll
       for (int j = 0; j < INI_J; j++) {
+        if (j >= nj) break;
         const bool in = br[j] == bkt;
         const uint64_t bal = wave_ballot(in);
         if (in) kb[run + prefix_in_wave(bal)] = kr[j];
@@ -1394,14 +1442,12 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         const ONode nd = Lc[i];
         if (nd.count > 1 && nd.count <= OCT_SMALL) cc[i] = serial_child_split(nd, ka, kb);
       }
-      for (int i = w; i < S; i += 4) {
-        const ONode nd = Lc[i];
-        if (nd.count > OCT_SMALL) {
-          const int4 c4 = wave_child_split(nd, ka, kb);
-          if (lane == 0) cc[i] = c4;
-        }
-      }
+      for_big_nodes(Lc, S, [](int p) { return p; }, [&](int i) {
+        const int4 c4 = wave_child_split(Lc[i], ka, kb);
+        if (lane == 0) cc[i] = c4;
+      });
       __syncthreads();
+      if (n_passes == 1) OCT_MARK(14, wall_clock64());
       for (int i = t; i < S; i += 256) {
         const bool par = Lc[i].count > 1;
         const int4 c4 = par ? cc[i] : make_int4(0, 0, 0, 0);
@@ -1412,6 +1458,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       __syncthreads();
       // (sk is free during full passes: its first 12 ints hold the scan's wave sums)
       const int3 tot3 = block_scan_excl3(sa, sb, sx, S, reinterpret_cast<int*>(sk));
+      if (n_passes == 1) OCT_MARK(15, wall_clock64());
       const int T = tot3.x, NP = tot3.y, nexp = tot3.z;
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
@@ -1443,6 +1490,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       for (int i = t; i < S; i += 256) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
       __syncthreads();
       const int nR = block_scan_excl(sa, S, misc);
+      if (n_rounds == 1) OCT_MARK(8, wall_clock64());
       int P2 = 1;
       while (P2 < nR) P2 <<= 1;
       if (nR > 1024) {
@@ -1470,15 +1518,15 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         }
         const int per = (nR + 255) >> 8;
         int j = 0;
-        for (; j + 8 <= nR; j += 8) {  // eight broadcast reads in flight
-          unsigned long long y[8];
+        for (; j + 16 <= nR; j += 16) {  // sixteen broadcast reads in flight
+          unsigned long long y[16];
 #pragma unroll
-          for (int q = 0; q < 8; q++) y[q] = sk[j + q];
+          for (int q = 0; q < 16; q++) y[q] = sk[j + q];
 #pragma unroll
           for (int r = 0; r < 4; r++)
             if (r == 0 || per > r) {
 #pragma unroll
-              for (int q = 0; q < 8; q++) rk[r] += y[q] > kk[r];
+              for (int q = 0; q < 16; q++) rk[r] += y[q] > kk[r];
             }
         }
         for (; j < nR; j++) {
@@ -1509,19 +1557,18 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
           }
         }
       }
+      if (n_rounds == 1) OCT_MARK(9, wall_clock64());
       // child counts of every candidate, in processing order
       for (int k = t; k < nR; k += 256) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
         if (nd.count <= OCT_SMALL) cc[k] = serial_child_counts(nd, ka, kb);
       }
-      for (int k = w; k < nR; k += 4) {
-        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
-        if (nd.count > OCT_SMALL) {
-          const int4 c4 = wave_child_counts(nd, ka, kb);
-          if (lane == 0) cc[k] = c4;
-        }
-      }
+      for_big_nodes(Lc, nR, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+        const int4 c4 = wave_child_counts(Lc[(int)(sk[k] & 0xfffffull)], ka, kb);
+        if (lane == 0) cc[k] = c4;
+      });
       __syncthreads();
+      if (n_rounds == 1) OCT_MARK(10, wall_clock64());
       for (int k = t; k < nR; k += 256) sa[k] = nonempty4(cc[k]) - 1;
       if (t == 0) misc[9] = nR;
       __syncthreads();
@@ -1532,6 +1579,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       }
       __syncthreads();
       const int nproc = misc[9];
+      if (n_rounds == 1) OCT_MARK(11, wall_clock64());
       for (int i = t; i < S; i += 256) sb[i] = -1;
       __syncthreads();
       for (int k = t; k < nproc; k += 256) sb[(int)(sk[k] & 0xfffffull)] = k;
@@ -1541,12 +1589,12 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
         if (nd.count <= OCT_SMALL) serial_child_partition(nd, cc[k], ka, kb);
       }
-      for (int k = w; k < nproc; k += 4) {
-        const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
-        if (nd.count > OCT_SMALL) wave_child_partition(nd, cc[k], ka, kb);
-      }
+      for_big_nodes(Lc, nproc, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+        wave_child_partition(Lc[(int)(sk[k] & 0xfffffull)], cc[k], ka, kb);
+      });
       for (int k = t; k < nR; k += 256) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
       __syncthreads();
+      if (n_rounds == 1) OCT_MARK(12, wall_clock64());
       const int T = block_scan_excl(sx, nR, misc);
       for (int i = t; i < S; i += 256) sa[i] = sb[i] < 0 ? 1 : 0;
       __syncthreads();
@@ -1574,6 +1622,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       S = T + NK;
       cur ^= 1;
       __syncthreads();
+      if (n_rounds == 1) OCT_MARK(13, wall_clock64());
       if (S >= N || S == prevS) break;
     }
   }
@@ -2082,6 +2131,13 @@ class HostPool {
   bool stop_ = false;
 };
 
+// k_octree's LDS plan for a range of levels: node arena, scan and sort capacities from those levels'
+// budgets and cell counts, and as many keys (two ping-pong halves) as the budget leaves
+struct OctPlan {
+  int node_cap = 0, sort_cap = 0, scan_cap = 0, key_lds_cap = 0;
+  size_t lds = 0;
+};
+
 struct orbfe_extractor {
   int device = 0;
   int nfeatures, nlevels, ini_th, min_th;
@@ -2095,6 +2151,7 @@ struct orbfe_extractor {
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
+  int octree_split = 0;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2108,6 +2165,7 @@ struct orbfe_extractor {
   long long pyr_stride = 0, cand_stride = 0, keyscr_stride = 0, lvlkey_stride = 0;
   int total_key_slots = 0, roi_w_max = 0, roi_h_max = 0, node_cap = 0, sort_cap = 0, blur_tiles = 0;
   int scan_cap = 0, key_lds_cap = 0;
+  OctPlan oct_all, oct_hi, oct_lo;  // k_octree LDS plans: one launch, or levels [0, split) / [split, L)
   LevelDesc* d_levels = nullptr;
   CellDesc* d_cells = nullptr;
   int2* d_xtab = nullptr;
@@ -2160,8 +2218,9 @@ struct orbfe_extractor {
   // Frame::ComputeStereoMatches scratch (orbfe_stereo.hip)
   OrbfeStereoScratch* stereo = nullptr;
   // launch_extract's enqueue sequence captured once per distinct set of arguments and replayed as
-  // a hipGraph (orbfe_extractor_set_graphs; `graphs` keyed by everything the sequence depends on)
-  int use_graphs = 1;
+  // a hipGraph (orbfe_extractor_set_graphs; `graphs` keyed by everything the sequence depends on).
+  // Off by default: measured slower on MI355X / ROCm 7.2
+  int use_graphs = 0;
   struct GraphEntry {
     std::vector<uintptr_t> key;
     hipGraphExec_t exec;
@@ -2173,6 +2232,7 @@ struct orbfe_extractor {
 };
 
 constexpr int OCT_LDS_KB = 80;  // k_octree's LDS per workgroup (two per CU)
+static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int budget_kb, int key_cap_override);
 static size_t octree_lds(const orbfe_extractor* h);
 static void drop_graphs(orbfe_extractor* h);
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
@@ -2378,23 +2438,17 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->blur_tiles = tiles;
   h->roi_w_max = rwmax;
   h->roi_h_max = rhmax;
-  h->node_cap = ncap;
-  int mc = 0, mini = 0;
-  for (const LevelDesc& d : lv) {
-    mc = std::max(mc, d.ncells);
-    mini = std::max(mini, d.nini);
-  }
-  int sc = 1;
-  while (sc < std::max(ncap, 4 * mini)) sc <<= 1;  // sk doubles as the [4][nini] bucket tables
-  h->sort_cap = sc;
-  h->scan_cap = (std::max(ncap, mc) + 3) & ~3;
-  // octree keys stay in LDS up to this many per level (ping-pong) within an 80 KiB block, so two
-  // blocks share a CU; larger levels use the global scratch path
-  const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * h->scan_cap +
-                       sizeof(unsigned long long) * sc + sizeof(int) * 16;
-  const size_t oct_lds = (size_t)OCT_LDS_KB * 1024;
-  h->key_lds_cap = fixed < oct_lds ? (int)((oct_lds - fixed) / 8) & ~63 : 0;
-  if (h->octree_key_cap_override >= 0) h->key_lds_cap = std::min(h->key_lds_cap, h->octree_key_cap_override);
+  h->oct_all = octree_plan(lv, 0, L, OCT_LDS_KB, h->octree_key_cap_override);
+  // two launches: the large levels at the full budget (two blocks per CU), the small ones at half
+  // of it (four per CU), so the short blocks of levels >= split hold half the LDS
+  const int ks = std::min(std::max(h->octree_split, 0), L);
+  h->oct_hi = octree_plan(lv, 0, ks, OCT_LDS_KB, h->octree_key_cap_override);
+  h->oct_lo = octree_plan(lv, ks, L, OCT_LDS_KB / 2, h->octree_key_cap_override);
+  h->node_cap = h->oct_all.node_cap;
+  h->sort_cap = h->oct_all.sort_cap;
+  h->scan_cap = h->oct_all.scan_cap;
+  h->key_lds_cap = h->oct_all.key_lds_cap;
+  (void)ncap;
   h->rows = rows;
   h->cols = cols;
   h->geom_mode = h->resize_mode;
@@ -2406,13 +2460,36 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   static int attr_lds = 0;
   {
     std::lock_guard<std::mutex> lk(attr_mu);
-    const int need = (int)octree_lds(h);
+    const int need = (int)std::max(h->oct_all.lds, std::max(h->oct_hi.lds, h->oct_lo.lds));
     if (need <= 160 * 1024 && need > attr_lds) {
       ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       attr_lds = need;
     }
   }
   return ORBFE_OK;
+}
+
+static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int budget_kb, int key_cap_override) {
+  OctPlan p;
+  if (l1 <= l0) return p;
+  int ncap = 0, mc = 0, mini = 0;
+  for (int l = l0; l < l1; l++) {
+    ncap = std::max(ncap, lv[l].key_cap + 4);
+    mc = std::max(mc, lv[l].ncells);
+    mini = std::max(mini, lv[l].nini);
+  }
+  int sc = 1;
+  while (sc < std::max(ncap, 4 * mini)) sc <<= 1;  // sk doubles as the [4][nini] bucket tables
+  p.node_cap = ncap;
+  p.sort_cap = sc;
+  p.scan_cap = (std::max(ncap, mc) + 3) & ~3;
+  const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * p.scan_cap +
+                       sizeof(unsigned long long) * sc + sizeof(int) * 16;
+  const size_t budget = (size_t)budget_kb * 1024;
+  p.key_lds_cap = fixed < budget ? (int)((budget - fixed) / 8) & ~63 : 0;
+  if (key_cap_override >= 0) p.key_lds_cap = std::min(p.key_lds_cap, key_cap_override);
+  p.lds = fixed + sizeof(uint32_t) * 2 * (size_t)p.key_lds_cap;
+  return p;
 }
 
 static void free_batch(orbfe_extractor* h) {
@@ -2453,8 +2530,7 @@ static int ensure_batch(orbfe_extractor* h, int n) {
 }
 
 static size_t octree_lds(const orbfe_extractor* h) {
-  return sizeof(ONode) * 2 * h->node_cap + sizeof(int4) * h->node_cap + sizeof(int) * 3 * h->scan_cap +
-         sizeof(unsigned long long) * h->sort_cap + sizeof(int) * 16 + sizeof(uint32_t) * 2 * h->key_lds_cap;
+  return h->oct_all.lds;
 }
 // constant 68-byte ROI rows when every cell ROI fits (xo <= 3 alignment bytes + rw <= 61) and the
 // multiply-shift row split stays exact (dw^2 * dh < 2^20)
@@ -2586,11 +2662,17 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     }
     if (l < k_side) side_fast(l);
   }
-  if (octree_lds(h) > 160 * 1024) return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
-  auto launch_octree = [&](hipStream_t s, int l0, int nl) {
+  if (std::max(h->oct_all.lds, std::max(h->oct_hi.lds, h->oct_lo.lds)) > 160 * 1024)
+    return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
+  auto launch_octree = [&](hipStream_t s, int l0, int nl, const OctPlan& P) {
     if (nl <= 0) return;
+    ExtractArgs ao = a;
+    ao.node_cap = P.node_cap;
+    ao.sort_cap = P.sort_cap;
+    ao.scan_cap = P.scan_cap;
+    ao.key_lds_cap = P.key_lds_cap;
     dim3 grid(nl, n);
-    ORBFE_LAUNCH("k_octree", k_octree, grid, dim3(256), octree_lds(h), s, a, l0);
+    ORBFE_LAUNCH("k_octree", k_octree, grid, dim3(256), P.lds, s, ao, l0);
   };
   // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
   // only the pyramid, so it runs on the side stream beside k_octree (a small, latency-bound grid
@@ -2612,7 +2694,15 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
-  launch_octree(st, 0, h->nlevels);
+  {
+    const int ks = std::min(std::max(h->octree_split, 0), h->nlevels);
+    if (ks > 0 && ks < h->nlevels) {
+      launch_octree(st, 0, ks, h->oct_hi);
+      launch_octree(st, ks, h->nlevels - ks, h->oct_lo);
+    } else {
+      launch_octree(st, 0, h->nlevels, h->oct_all);
+    }
+  }
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a);
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
@@ -2658,7 +2748,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3329,11 +3419,11 @@ extern "C" int orbfe_get_level(orbfe_extractor* h, int image, int level, const u
   return ORBFE_OK;
 }
 
-// profiling builds only (not declared in a header): the k_octree phase clocks, 64 * 16 * 8 values
+// profiling builds only (not declared in a header): the k_octree phase clocks, 64 * 16 * 16 values
 extern "C" int orbfe_debug_octree_prof(unsigned long long* out, int cap) {
 #ifdef ORBFE_OCT_PROF
-  if (!out || cap < 64 * 16 * 8) return ORBFE_ERR_ARG;
-  ORBFE_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_prof), sizeof(unsigned long long) * 64 * 16 * 8));
+  if (!out || cap < 64 * 16 * 16) return ORBFE_ERR_ARG;
+  ORBFE_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_oct_prof), sizeof(unsigned long long) * 64 * 16 * 16));
   return ORBFE_OK;
 #else
   (void)out;
@@ -3458,6 +3548,13 @@ extern "C" int orbfe_set_side_stream(orbfe_extractor* h, void* stream) {
 extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
   if (!h) return ORBFE_ERR_ARG;
   h->inline_side = on ? 1 : 0;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
+  h->octree_split = k > 0 ? k : 0;
+  h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
   return ORBFE_OK;
 }
 

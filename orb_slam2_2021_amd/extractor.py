@@ -250,7 +250,7 @@ class ORBextractor:
 
     def set_graphs(self, on: bool) -> None:
         """orbfe_extractor_set_graphs: replay each extract call's launch sequence as a hipGraph
-        captured per argument set (default on); off launches every kernel directly."""
+        captured per argument set; off (the default) launches every kernel directly."""
         L.check(self._lib.orbfe_extractor_set_graphs(self._h, 1 if on else 0), "set_graphs")
 
     def debug_graph_stats(self) -> tuple:
@@ -302,6 +302,11 @@ class ORBextractor:
     def debug_set_fast_side_levels(self, k: int) -> None:
         """FAST of levels 0..k-1 on the side stream as each level is built (k <= 0: the default, 3)."""
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
+
+    def debug_set_octree_split(self, k: int) -> None:
+        """DistributeOctTree in two launches, levels 0..k-1 at 80 KiB of LDS per block and k.. at 40 KiB
+        (k <= 0, the default: one launch of every level at 80 KiB)."""
+        L.check(self._lib.orbfe_debug_set_octree_split(self._h, int(k)), "set_octree_split")
 
     def debug_set_blur_mode(self, mode: int) -> None:
         """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (ran at commit 18192e4, when replay was the library default; replay is opt-in since: --graphs)
 # Launch-graph replay: parity (the new test + the extraction / C3 / stereo / C++ facade suites run
 # with graphs on), interleaved bench A/B against direct launches, the k_octree phase clocks of the
 # profiling builds (-DORBFE_OCT_PROF=1; lib_prof_g16 adds -DORBFE_OCT_GATHER16=1), the gather

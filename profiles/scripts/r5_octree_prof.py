@@ -24,6 +24,8 @@ def main():
     imgs = torch.from_numpy(np.stack([synth_frame(i, H, W) for i in range(n)])).to(dev)
     ext = ORBextractor(2000, 1.2, 8, 20, 7)
     ext.debug_set_inline_side(True)
+    if os.environ.get("ORBFE_OCT_SPLIT"):  # the octree launch split (orbfe_debug_set_octree_split)
+        ext.debug_set_octree_split(int(os.environ["ORBFE_OCT_SPLIT"]))
     cap = ext.max_keypoints(H, W)
     kps = torch.empty(n * cap * 28, dtype=torch.uint8, device=dev)
     desc = torch.empty(n * cap * 32, dtype=torch.uint8, device=dev)
@@ -32,7 +34,7 @@ def main():
     fn = lib.orbfe_debug_octree_prof
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    buf = np.zeros(64 * 16 * 8, np.uint64)
+    buf = np.zeros(64 * 16 * 16, np.uint64)
     names = ["scan", "gather", "initial", "passes", "refine", "retain"]
     acc = []
     for r in range(reps + 1):
@@ -41,9 +43,9 @@ def main():
         torch.cuda.synchronize()
         L.check(fn(buf.ctypes.data, buf.size), "octree_prof")
         if r:
-            acc.append(buf.reshape(64, 16, 8).astype(np.int64).copy())
-    a = np.stack(acc)  # reps x img x level x 8
-    t = a[..., :7].astype(np.float64) / 100.0  # us
+            acc.append(buf.reshape(64, 16, 16).astype(np.int64).copy())
+    a = np.stack(acc)  # reps x img x level x 16
+    t = a.astype(np.float64) / 100.0  # us
     start = t[..., 0]
     print(f"launch span (first block start .. last block end): "
           f"{np.mean([(t[i, :, :8, 6].max() - start[i, :, :8].min()) for i in range(len(acc))]):.1f} us")
@@ -55,6 +57,14 @@ def main():
         tot = t[..., l, 6] - t[..., l, 0]
         print(f"{l:5d} {nk.mean():7.0f} {passes.mean():6.1f} {rounds.mean():6.1f} {S.mean():5.0f}  " +
               "  ".join(f"{p.mean():6.1f}/{p.max():6.1f}" for p in ph) + f"   {tot.mean():6.1f}/{tot.max():6.1f}")
+    sub = ["flag scan", "sort", "child counts", "stop scan", "partition", "build"]
+    print("first refinement round (us):  " + "  ".join(f"{x:>12s}" for x in sub) +
+          "     first pass: splits   scan   rest")
+    for l in range(8):
+        r = [t[..., l, 8] - t[..., l, 4]] + [t[..., l, k + 1] - t[..., l, k] for k in range(8, 13)]
+        p1 = [t[..., l, 14] - t[..., l, 3], t[..., l, 15] - t[..., l, 14]]
+        print(f"{l:5d}                         " + "  ".join(f"{x.mean():12.1f}" for x in r) +
+              f"     {p1[0].mean():12.1f} {p1[1].mean():6.1f}")
 
 
 if __name__ == "__main__":

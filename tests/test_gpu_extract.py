@@ -122,6 +122,18 @@ def test_octree_global_key_path(require_gpu, cap):
     assert_same_extraction(ext, ref, noise)
 
 
+@pytest.mark.parametrize("split", [0, 1, 3, 7, 8])
+def test_octree_launch_split(require_gpu, split):
+    """DistributeOctTree as one launch (0, 8) or two (levels 0..k-1 at the 80 KiB LDS plan, k.. at
+    the 40 KiB one): the same survivors, on textured and noise images (noise pushes the small
+    levels' key counts past the half plan's LDS capacity, onto the global path)."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_octree_split(split)
+    assert_same_extraction(ext, ref, synth_frame(4, 376, 1241))
+    noise = np.random.default_rng(9).integers(0, 256, (376, 1241), dtype=np.uint8)
+    assert_same_extraction(ext, ref, noise)
+
+
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_large_scale_factors(require_gpu, params):
     """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
@@ -282,7 +294,8 @@ def test_device_input_odd_pitch_and_alignment(require_gpu):
 
 
 def test_launch_graph_replay(require_gpu):
-    """The launch sequence replayed from hipGraphs (the default) equals direct launches: host path
+    """The launch sequence replayed from hipGraphs (orbfe_extractor_set_graphs(1)) equals direct
+    launches (the default): host path
     (orbfe_extract, captured once then replayed), device batches into alternating output sets on a
     caller's stream (one graph per argument set), a new output pointer (a new capture), the kernel
     timer on (direct launches inside a graphed handle), and graphs off."""
@@ -290,7 +303,7 @@ def test_launch_graph_replay(require_gpu):
     from orb_slam2_2021_amd import _lib as L
     imgs = [synth_frame(60 + i, 376, 1241) for i in range(3)]
     a, b = ORBextractor(2000, 1.2, 8, 20, 7), ORBextractor(2000, 1.2, 8, 20, 7)
-    b.set_graphs(False)
+    a.set_graphs(True)
     for img in imgs + imgs:
         ka, da = a(img)
         kb, db = b(img)
