@@ -104,7 +104,11 @@ def parse(argv=None):
                         "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
     p.add_argument("--octree-split", type=int, default=-1,
                    help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
-                        "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, one launch)")
+                        "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 4: 85.4-85.5k vs 84.0-84.1k "
+                        "stereo frames/s at 0, round 5)")
+    p.add_argument("--octree-lds", default="",
+                   help="HI,LO: LDS KiB per block of the two octree launches (orbfe_debug_set_octree_lds; "
+                        "default: the library's 80,40)")
     p.add_argument("--graphs", action="store_true",
                    help="replay each extraction's launch sequence from the handle's captured hipGraphs "
                         "(orbfe_extractor_set_graphs; off by default: 38.6k vs 83.7k stereo frames/s, round 5)")
@@ -132,6 +136,8 @@ def parse(argv=None):
                         "host: every sub-batch's 2B images copied from pinned host memory on a copy stream into "
                         "one of --input-slots device slots, overlapped with the other sub-batches' extraction and "
                         "matching (the reference's operator() takes host images, ORBextractor.cc:1041-1048)")
+    p.add_argument("--copy-streams", type=int, default=1, choices=(1, 2),
+                   help="--feed host: copy streams per sub-batch's H2D (2: two halves on two streams)")
     p.add_argument("--input-slots", type=int, default=0,
                    help="--feed host: device input slots (0: two per extractor handle)")
     p.add_argument("--root-share", type=float, default=-1.0,
@@ -331,9 +337,13 @@ class HostFeed:
     the link, not slot reuse, bounds the rate when 2B images take longer to copy than to process
     (round 4 tied the slots to the handles' pyramid events, R = 4: 45.8k stereo frames/s)."""
 
-    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0):
+    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0, copy_streams=1):
         import torch
         self.h = torch.from_numpy(host).pin_memory()
+        # --copy-streams 2: each sub-batch's images as two halves on two copy streams (the second
+        # created here, after the pipeline's), joined by an event before the extraction's
+        self.cs2 = [torch.cuda.Stream(dev) for _ in range(max(0, copy_streams - 1))]
+        self.joined = []
         self.R = 0
         self.slots = None
         self.slots_req = slots
@@ -352,11 +362,23 @@ class HostFeed:
             self.slots = torch.empty((self.R, self.n_img, self.H, self.W), dtype=torch.uint8, device=self.dev)
             self.ready = [new_event(self.dev.index) for _ in range(self.R)]
             self.consumed = [new_event(self.dev.index) for _ in range(self.R)]
+            self.joined = [new_event(self.dev.index) for _ in range(self.R)] if self.cs2 else []
         slot = self.k % self.R
         if self.k >= self.R:  # sub-batch k - R's extraction read this slot
             self.consumed[slot].wait(self.cs)
-        with torch.cuda.stream(self.cs):
-            self.slots[slot].copy_(self.h[j], non_blocking=True)
+            for c in self.cs2:
+                self.consumed[slot].wait(c)
+        if self.cs2:
+            half = self.n_img // 2
+            with torch.cuda.stream(self.cs):
+                self.slots[slot][:half].copy_(self.h[j][:half], non_blocking=True)
+            with torch.cuda.stream(self.cs2[0]):
+                self.slots[slot][half:].copy_(self.h[j][half:], non_blocking=True)
+            self.joined[slot].record(self.cs2[0])
+            self.joined[slot].wait(self.cs)
+        else:
+            with torch.cuda.stream(self.cs):
+                self.slots[slot].copy_(self.h[j], non_blocking=True)
         self.ready[slot].record(self.cs)
         self.k += 1
         return self.slots[slot].data_ptr(), self.ready[slot]
@@ -368,7 +390,7 @@ class HostFeed:
     def describe(self, subbatches_per_s):
         gbs = self.bytes_per_subbatch * subbatches_per_s / 1e9
         return {"mode": "host", "h2d_bytes_per_subbatch": self.bytes_per_subbatch, "h2d_GBps": round(gbs, 2),
-                "device_slots": self.R,
+                "device_slots": self.R, "copy_streams": 1 + len(self.cs2),
                 "what": "every sub-batch's images H2D from pinned host memory on a copy stream of its own, "
                         "overlapped with the other sub-batches' kernels; outputs stay in HBM"}
 
@@ -479,7 +501,8 @@ def main():
     d_img = torch.from_numpy(host).to(dev)
     feed = None
     if args.feed == "host":
-        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots)
+        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots,
+                        copy_streams=args.copy_streams)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
     voc = ORBVocabulary.from_tree(tree, device=dev.index)
@@ -510,6 +533,10 @@ def main():
     if args.octree_split >= 0:
         for e in exts:
             e.debug_set_octree_split(args.octree_split)
+    if args.octree_lds:
+        hi, lo = (int(x) for x in args.octree_lds.split(","))
+        for e in exts:
+            e.debug_set_octree_lds(hi, lo)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)

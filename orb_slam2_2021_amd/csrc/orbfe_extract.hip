@@ -2138,6 +2138,8 @@ struct OctPlan {
   size_t lds = 0;
 };
 
+constexpr int OCT_LDS_KB = 80;  // k_octree's LDS per workgroup (two per CU)
+
 struct orbfe_extractor {
   int device = 0;
   int nfeatures, nlevels, ini_th, min_th;
@@ -2151,7 +2153,8 @@ struct orbfe_extractor {
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
-  int octree_split = 0;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
+  int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
+  int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2231,7 +2234,6 @@ struct orbfe_extractor {
   unsigned long long graph_hits = 0, graph_captures = 0;
 };
 
-constexpr int OCT_LDS_KB = 80;  // k_octree's LDS per workgroup (two per CU)
 static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int budget_kb, int key_cap_override);
 static size_t octree_lds(const orbfe_extractor* h);
 static void drop_graphs(orbfe_extractor* h);
@@ -2442,8 +2444,8 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   // two launches: the large levels at the full budget (two blocks per CU), the small ones at half
   // of it (four per CU), so the short blocks of levels >= split hold half the LDS
   const int ks = std::min(std::max(h->octree_split, 0), L);
-  h->oct_hi = octree_plan(lv, 0, ks, OCT_LDS_KB, h->octree_key_cap_override);
-  h->oct_lo = octree_plan(lv, ks, L, OCT_LDS_KB / 2, h->octree_key_cap_override);
+  h->oct_hi = octree_plan(lv, 0, ks, h->oct_hi_kb, h->octree_key_cap_override);
+  h->oct_lo = octree_plan(lv, ks, L, h->oct_lo_kb, h->octree_key_cap_override);
   h->node_cap = h->oct_all.node_cap;
   h->sort_cap = h->oct_all.sort_cap;
   h->scan_cap = h->oct_all.scan_cap;
@@ -2695,7 +2697,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   {
-    const int ks = std::min(std::max(h->octree_split, 0), h->nlevels);
+    // two launches only for batches: they cut the LDS the short small-level blocks hold (the C3
+    // bench: 85.4-85.5k vs 84.0-84.1k stereo frames/s, interleaved, round 5), but one image's octree
+    // then runs as two dependent launches instead of one (the launch span 116 vs 69 us alone)
+    const int ks = n >= 8 ? std::min(std::max(h->octree_split, 0), h->nlevels) : 0;
     if (ks > 0 && ks < h->nlevels) {
       launch_octree(st, 0, ks, h->oct_hi);
       launch_octree(st, ks, h->nlevels - ks, h->oct_lo);
@@ -2748,7 +2753,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3548,6 +3553,15 @@ extern "C" int orbfe_set_side_stream(orbfe_extractor* h, void* stream) {
 extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
   if (!h) return ORBFE_ERR_ARG;
   h->inline_side = on ? 1 : 0;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_lds(orbfe_extractor* h, int hi_kb, int lo_kb) {
+  if (!h || hi_kb < 16 || hi_kb > 160 || lo_kb < 16 || lo_kb > 160)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_lds: budgets must be 16-160 KiB");
+  h->oct_hi_kb = hi_kb;
+  h->oct_lo_kb = lo_kb;
+  h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
   return ORBFE_OK;
 }
 

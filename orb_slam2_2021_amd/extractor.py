@@ -304,9 +304,13 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_fast_side_levels(self._h, int(k)), "set_fast_side_levels")
 
     def debug_set_octree_split(self, k: int) -> None:
-        """DistributeOctTree in two launches, levels 0..k-1 at 80 KiB of LDS per block and k.. at 40 KiB
-        (k <= 0, the default: one launch of every level at 80 KiB)."""
+        """DistributeOctTree in two launches for batches of 8+ images, levels 0..k-1 at 80 KiB of LDS
+        per block and k.. at 40 KiB (default 4; k <= 0: one launch of every level at 80 KiB)."""
         L.check(self._lib.orbfe_debug_set_octree_split(self._h, int(k)), "set_octree_split")
+
+    def debug_set_octree_lds(self, hi_kb: int, lo_kb: int) -> None:
+        """LDS budgets (KiB per block) of the octree launches below / from the split (80 / 40)."""
+        L.check(self._lib.orbfe_debug_set_octree_lds(self._h, int(hi_kb), int(lo_kb)), "set_octree_lds")
 
     def debug_set_blur_mode(self, mode: int) -> None:
         """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream

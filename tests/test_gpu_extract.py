@@ -122,16 +122,22 @@ def test_octree_global_key_path(require_gpu, cap):
     assert_same_extraction(ext, ref, noise)
 
 
-@pytest.mark.parametrize("split", [0, 1, 3, 7, 8])
-def test_octree_launch_split(require_gpu, split):
+@pytest.mark.parametrize("split,lds", [(0, None), (1, None), (3, None), (4, None), (7, None), (8, None),
+                                       (4, (64, 32)), (4, (48, 24))])
+def test_octree_launch_split(require_gpu, split, lds):
     """DistributeOctTree as one launch (0, 8) or two (levels 0..k-1 at the 80 KiB LDS plan, k.. at
-    the 40 KiB one): the same survivors, on textured and noise images (noise pushes the small
-    levels' key counts past the half plan's LDS capacity, onto the global path)."""
+    the 40 KiB one) over an 8-image batch: the same survivors, on textured and noise images (noise
+    pushes the small levels' key counts past the half plan's LDS capacity, onto the global path)."""
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
     ext.debug_set_octree_split(split)
-    assert_same_extraction(ext, ref, synth_frame(4, 376, 1241))
+    if lds:  # smaller plans: more keys through the global path
+        ext.debug_set_octree_lds(*lds)
+    # (the split applies to batches of 8+ images: a batch, every image checked)
     noise = np.random.default_rng(9).integers(0, 256, (376, 1241), dtype=np.uint8)
-    assert_same_extraction(ext, ref, noise)
+    imgs = [synth_frame(4 + i, 376, 1241) for i in range(7)] + [noise]
+    outs = ext.extract_batch(imgs)
+    for i in reversed(range(len(imgs))):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
