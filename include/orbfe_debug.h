@@ -25,10 +25,11 @@ int orbfe_debug_geometry(orbfe_extractor* h, int rows, int cols, int32_t* info, 
 /* Cap the per-level key count DistributeOctTree keeps in LDS (rounded down to 64; 0 forces the
  * global-memory path for every level; < 0 restores the automatic size). */
 int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
-/* DistributeOctTree in two launches for batches of 8 or more images: levels 0..k-1 with the full LDS
+/* DistributeOctTree in two launches for device-resident batches (orbfe_extract_batch_device) of 8 or
+ * more images: levels 0..k-1 with the full LDS
  * plan (80 KiB per block), levels k..L-1 with half of it (their smaller node arenas and key counts
  * fit 40 KiB: four blocks per CU); k <= 0 or k >= L: one launch of every level at 80 KiB. Default 4;
- * smaller batches always take one launch (lower latency). */
+ * smaller batches and the host-buffer calls always take one launch (lower latency alone). */
 int orbfe_debug_set_octree_split(orbfe_extractor* h, int k);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */

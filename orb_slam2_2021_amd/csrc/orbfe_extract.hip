@@ -1274,17 +1274,6 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     const int b0 = sa[c], cnt = (c + 1 < ncells ? sa[c + 1] : n) - b0;
     const uint32_t* src = cand + sx[c];
     int k = 0;
-#ifdef ORBFE_OCT_GATHER16
-    {  // the first 16 keys of the cell in flight together (a 30x30 cell holds ~10-20 at level 0)
-      uint32_t v[16];
-#pragma unroll
-      for (int q = 0; q < 16; q++) v[q] = q < cnt ? src[q] : 0u;
-#pragma unroll
-      for (int q = 0; q < 16; q++)
-        if (q < cnt) ka[b0 + q] = v[q];
-      k = min(cnt, 16);
-    }
-#endif
     for (; k + 4 <= cnt; k += 4) {
       const uint32_t v0 = src[k], v1 = src[k + 1], v2 = src[k + 2], v3 = src[k + 3];
       ka[b0 + k] = v0;
@@ -2155,6 +2144,7 @@ struct orbfe_extractor {
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
+  bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2697,10 +2687,13 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
   }
   {
-    // two launches only for batches: they cut the LDS the short small-level blocks hold (the C3
-    // bench: 85.4-85.5k vs 84.0-84.1k stereo frames/s, interleaved, round 5), but one image's octree
-    // then runs as two dependent launches instead of one (the launch span 116 vs 69 us alone)
-    const int ks = n >= 8 ? std::min(std::max(h->octree_split, 0), h->nlevels) : 0;
+    // two launches only for device-resident batches (the entry point of callers that overlap
+    // extractions): they cut the LDS the short small-level blocks hold, which pays when other
+    // kernels run beside the octree (the C3 bench: 85.4-85.5k vs 84.0-84.1k stereo frames/s,
+    // interleaved, round 5); alone, one extraction's octree then runs as two dependent launches
+    // (the launch span 116 vs 69 us), so single images and the synchronous host-buffer calls
+    // keep one launch
+    const int ks = (h->device_call && n >= 8) ? std::min(std::max(h->octree_split, 0), h->nlevels) : 0;
     if (ks > 0 && ks < h->nlevels) {
       launch_octree(st, 0, ks, h->oct_hi);
       launch_octree(st, ks, h->nlevels - ks, h->oct_lo);
@@ -2753,7 +2746,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3084,8 +3077,11 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
   if (st != ORBFE_OK) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   h->gen++;  // the host pyramid block of the previous call is stale from here on
-  return launch_extract_graphed(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
-                                d_counts, s);
+  h->device_call = true;
+  st = launch_extract_graphed(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
+                              d_counts, s);
+  h->device_call = false;
+  return st;
 }
 
 static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
