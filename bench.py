@@ -109,6 +109,9 @@ def parse(argv=None):
     p.add_argument("--octree-lds", default="",
                    help="HI,LO: LDS KiB per block of the two octree launches (orbfe_debug_set_octree_lds; "
                         "default: the library's 80,40)")
+    p.add_argument("--fast-wpb", default="",
+                   help="SIDE,MAIN: k_fast cells per workgroup of the side-stream / remaining launches "
+                        "(orbfe_debug_set_fast_wpb; default: the library's 4,1)")
     p.add_argument("--graphs", action="store_true",
                    help="replay each extraction's launch sequence from the handle's captured hipGraphs "
                         "(orbfe_extractor_set_graphs; off by default: 38.6k vs 83.7k stereo frames/s, round 5)")
@@ -533,6 +536,10 @@ def main():
     if args.octree_split >= 0:
         for e in exts:
             e.debug_set_octree_split(args.octree_split)
+    if args.fast_wpb:
+        sw, mw = (int(x) for x in args.fast_wpb.split(","))
+        for e in exts:
+            e.debug_set_fast_wpb(sw, mw)
     if args.octree_lds:
         hi, lo = (int(x) for x in args.octree_lds.split(","))
         for e in exts:

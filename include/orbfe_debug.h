@@ -34,6 +34,9 @@ int orbfe_debug_set_octree_split(orbfe_extractor* h, int k);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */
 int orbfe_debug_set_octree_lds(orbfe_extractor* h, int hi_kb, int lo_kb);
+/* k_fast cells (wavefronts) per workgroup: the side-stream launches of the early levels (default 4)
+ * and the launch of the remaining levels (default 1); 1, 2, 4 or 8. */
+int orbfe_debug_set_fast_wpb(orbfe_extractor* h, int side_wpb, int main_wpb);
 /* FAST of levels 0..k-1 on the side stream, each launched as soon as its level is built, the rest
  * in one launch after the resize chain (k <= 0: the default, levels 0..2). */
 int orbfe_debug_set_fast_side_levels(orbfe_extractor* h, int k);

@@ -2145,6 +2145,7 @@ struct orbfe_extractor {
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
+  int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2607,7 +2608,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     // k_fast 176 -> 161 us alone but k_resize 146 -> 177 us); 1 for the levels-3..7 launch after
     // the chain (bench 77.4 / 77.6k vs 76.5 / 76.8k stereo frames/s, interleaved; 8 per workgroup
     // everywhere: 71.3k). profiles/scripts/r3_fast_wpb.sh
-    const int wpb = main_launch ? 1 : 4;
+    const int wpb = main_launch ? h->fast_wpb_main : h->fast_wpb_side;
     dim3 grid((c1 - c0 + wpb - 1) / wpb, n);
     const size_t lds = fast_lds(h) / 4 * wpb;
     if (fast_rs(h) == 68)
@@ -2746,7 +2747,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3549,6 +3550,16 @@ extern "C" int orbfe_set_side_stream(orbfe_extractor* h, void* stream) {
 extern "C" int orbfe_debug_set_inline_side(orbfe_extractor* h, int on) {
   if (!h) return ORBFE_ERR_ARG;
   h->inline_side = on ? 1 : 0;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_fast_wpb(orbfe_extractor* h, int side_wpb, int main_wpb) {
+  auto ok = [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; };
+  if (!h || !ok(side_wpb) || !ok(main_wpb))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_fast_wpb: 1, 2, 4 or 8 cells per workgroup");
+  h->fast_wpb_side = side_wpb;
+  h->fast_wpb_main = main_wpb;
+  drop_graphs(h);
   return ORBFE_OK;
 }
 

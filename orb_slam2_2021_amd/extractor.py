@@ -312,6 +312,10 @@ class ORBextractor:
         """LDS budgets (KiB per block) of the octree launches below / from the split (80 / 40)."""
         L.check(self._lib.orbfe_debug_set_octree_lds(self._h, int(hi_kb), int(lo_kb)), "set_octree_lds")
 
+    def debug_set_fast_wpb(self, side_wpb: int, main_wpb: int) -> None:
+        """k_fast cells per workgroup: side-stream launches (default 4), the rest (default 1)."""
+        L.check(self._lib.orbfe_debug_set_fast_wpb(self._h, int(side_wpb), int(main_wpb)), "set_fast_wpb")
+
     def debug_set_blur_mode(self, mode: int) -> None:
         """GaussianBlur placement: 0 side stream beside DistributeOctTree (default), 1 launch stream
         after it (several handles sharing one side stream)."""
