@@ -112,6 +112,8 @@ def parse(argv=None):
     p.add_argument("--fast-wpb", default="",
                    help="SIDE,MAIN: k_fast cells per workgroup of the side-stream / remaining launches "
                         "(orbfe_debug_set_fast_wpb; default: the library's 4,1)")
+    p.add_argument("--high-prio", default="side,match",
+                   help="pipeline streams created at high priority: any of extract, side, match (default side,match)")
     p.add_argument("--graphs", action="store_true",
                    help="replay each extraction's launch sequence from the handle's captured hipGraphs "
                         "(orbfe_extractor_set_graphs; off by default: 38.6k vs 83.7k stereo frames/s, round 5)")
@@ -479,7 +481,7 @@ def main():
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     n_ext = max(1, args.extractors)
     pstreams = PipelineStreams(gpu, n_ext, match_inline=args.match_inline, side_last=args.inline_side,
-                               comm=world > 1, copy=args.feed == "host")
+                               comm=world > 1, copy=args.feed == "host", high=tuple(args.high_prio.split(",")))
     if world > 1 and args.rehearse:  # every rank on GPU 0, gloo between the processes
         dist.init_process_group("gloo")
     elif world > 1:

@@ -106,7 +106,8 @@ class PipelineStreams:
     process, the busy streams each open a queue of their own."""
 
     def __init__(self, device: int, n_extractors: int = 1, match_inline: bool = False,
-                 side_last: bool = False, comm: bool = False, copy: bool = False):
+                 side_last: bool = False, comm: bool = False, copy: bool = False,
+                 high=("side", "match")):
         import torch
         self.device = device
         self._ptrs = []
@@ -119,17 +120,19 @@ class PipelineStreams:
             return torch.cuda.ExternalStream(p.value, device=torch.device("cuda", device))
 
         n = max(1, n_extractors)
-        self.extract = [make(False) for _ in range(n)]
+        # `high`: the streams created at high priority (the runtime serves each priority from its own
+        # hardware queues); default the shared side stream and the matching stream
+        self.extract = [make("extract" in high) for _ in range(n)]
         # the matching stream at high priority, beside the shared side stream, so that the
         # latency-bound vocabulary + SFT chain keeps up with the extraction handles (normal priority
         # and the other placements measured slower: DESIGN.md section 5); match_inline: each
         # sub-batch's vocabulary + matching follow its extraction on the same stream instead
         self.match = None
         if not match_inline and side_last:
-            self.match = make(True)
-        self.side = make(True)
+            self.match = make("match" in high)
+        self.side = make("side" in high)
         if not match_inline and not side_last:
-            self.match = make(True)
+            self.match = make("match" in high)
         # comm: a stream for the C4 gather's transfers, created here with the others so that it gets
         # a hardware queue of its own. A stream from torch's pool shares a queue with a pipeline
         # stream, and its barrier packets (waiting for the pack on the matching stream) then hold
