@@ -132,6 +132,33 @@ __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
 // Three exclusive scans at once (one pair of barriers instead of three); wsum holds 12 ints.
 __device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum) {
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  if (n <= 64) {  // (n is block-uniform) one wavefront scans, one barrier publishes
+    if (w == 0) {
+      const int va = lane < n ? a[lane] : 0, vb = lane < n ? b[lane] : 0, vc = lane < n ? c[lane] : 0;
+      int ia = va, ib = vb, ic = vc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int ya = __shfl_up(ia, o, 64), yb = __shfl_up(ib, o, 64), yc = __shfl_up(ic, o, 64);
+        if (lane >= o) {
+          ia += ya;
+          ib += yb;
+          ic += yc;
+        }
+      }
+      if (lane < n) {
+        a[lane] = ia - va;
+        b[lane] = ib - vb;
+        c[lane] = ic - vc;
+      }
+      if (lane == 63) {
+        wsum[0] = ia;
+        wsum[1] = ib;
+        wsum[2] = ic;
+      }
+    }
+    __syncthreads();
+    return make_int3(wsum[0], wsum[1], wsum[2]);
+  }
   const int per = (n + 255) / 256;
   const int beg = min(t * per, n), end = min(beg + per, n);
   int sa = 0, sb = 0, sc = 0;

@@ -1010,7 +1010,7 @@ __device__ __forceinline__ int child_of(uint32_t key, int mx, int my) {
 }
 
 // Count the keys of `nd` falling in each of its 4 DivideNode children (wave-level).
-__device__ int4 wave_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
+__device__ __forceinline__ int4 wave_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
   const uint32_t* src = (nd.flags & 1) ? kb : ka;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
   int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
@@ -1026,7 +1026,7 @@ __device__ int4 wave_child_counts(const ONode& nd, const uint32_t* ka, const uin
 }
 
 // Stable 4-way partition of the node's keys into the other buffer (children contiguous, n1..n4).
-__device__ void wave_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, uint32_t* kb) {
+__device__ __forceinline__ void wave_child_partition(const ONode& nd, int4 cnt, uint32_t* ka, uint32_t* kb) {
   const uint32_t* src = (nd.flags & 1) ? kb : ka;
   uint32_t* dst = (nd.flags & 1) ? ka : kb;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
@@ -1113,7 +1113,7 @@ __device__ __forceinline__ void serial_child_partition(const ONode& nd, int4 cnt
 // a wavefront for a large node (up to 64 * OCT_WJ keys), a thread for a small one (up to OCT_SJ).
 #define OCT_WJ 16
 #define OCT_SJ 16
-__device__ int4 wave_child_split(const ONode& nd, uint32_t* ka, uint32_t* kb) {
+__device__ __forceinline__ int4 wave_child_split(const ONode& nd, uint32_t* ka, uint32_t* kb) {
   if (nd.count > 64 * OCT_WJ) {
     const int4 c4 = wave_child_counts(nd, ka, kb);
     wave_child_partition(nd, c4, ka, kb);
@@ -1244,6 +1244,13 @@ __device__ unsigned long long g_oct_prof[64 * 16 * 16];
   do { if (threadIdx.x == 0 && blockIdx.y < 64 && l < 16) g_oct_prof[(blockIdx.y * 16 + l) * 16 + (k)] = (v); } while (0)
 #else
 #define OCT_MARK(k, v) do { } while (0)
+#endif
+#ifdef ORBFE_OCT_PROF_PASS  // slots 8-11 then time the sub-steps of that full pass instead
+#define OCT_RMARK(k, v) do { } while (0)
+#define OCT_PMARK(k, v) do { if (n_passes == ORBFE_OCT_PROF_PASS) OCT_MARK(k, v); } while (0)
+#else
+#define OCT_RMARK(k, v) OCT_MARK(k, v)
+#define OCT_PMARK(k, v) do { } while (0)
 #endif
 
 template <bool LDSK>
@@ -1426,28 +1433,58 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     const int prevS = S;
     if (!refine) {
       n_passes++;
+#ifdef ORBFE_OCT_PROF_PASS  // (profiling builds: marks 14/15 bracket full pass ORBFE_OCT_PROF_PASS)
+      if (n_passes == ORBFE_OCT_PROF_PASS) OCT_MARK(14, wall_clock64());
+#endif
       // ---- full pass (:603-668) ----
+      // each node's split and its scan inputs by whoever splits it (a thread for <= OCT_SMALL
+      // keys, a wavefront above): children (sa), kept single-key nodes (sb), multi-key children (sx)
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
-        if (nd.count > 1 && nd.count <= OCT_SMALL) cc[i] = serial_child_split(nd, ka, kb);
-      }
-      for_big_nodes(Lc, S, [](int p) { return p; }, [&](int i) {
-        const int4 c4 = wave_child_split(Lc[i], ka, kb);
-        if (lane == 0) cc[i] = c4;
-      });
-      __syncthreads();
-      if (n_passes == 1) OCT_MARK(14, wall_clock64());
-      for (int i = t; i < S; i += 256) {
-        const bool par = Lc[i].count > 1;
-        const int4 c4 = par ? cc[i] : make_int4(0, 0, 0, 0);
+        if (nd.count > OCT_SMALL) continue;
+        const bool par = nd.count > 1;
+        const int4 c4 = par ? serial_child_split(nd, ka, kb) : make_int4(0, 0, 0, 0);
+        if (par) cc[i] = c4;
         sa[i] = par ? nonempty4(c4) : 0;
         sb[i] = par ? 0 : 1;
         sx[i] = par ? multi4(c4) : 0;
       }
+      OCT_PMARK(8, wall_clock64());
+#ifdef ORBFE_OCT_PROF_PASS
+      unsigned long long split_cyc = 0, split_n = 0;
+#endif
+      for_big_nodes(Lc, S, [](int p) { return p; }, [&](int i) {
+#ifdef ORBFE_OCT_PROF_PASS
+        const unsigned long long c0 = clock64();
+        const int4 c4 = wave_child_split(Lc[i], ka, kb);
+        split_cyc += clock64() - c0;
+        split_n += (unsigned long long)Lc[i].count << 16 | 1ull;
+#else
+        const int4 c4 = wave_child_split(Lc[i], ka, kb);
+#endif
+        if (lane == 0) {
+          cc[i] = c4;
+          sa[i] = nonempty4(c4);
+          sb[i] = 0;
+          sx[i] = multi4(c4);
+        }
+      });
+      OCT_PMARK(9, wall_clock64());
+#ifdef ORBFE_OCT_PROF_PASS  // wave 0's shader clocks inside its wave splits, its keys << 16 | splits
+      OCT_PMARK(12, split_cyc);
+      OCT_PMARK(13, split_n);
+#endif
       __syncthreads();
+      OCT_PMARK(10, wall_clock64());
+#ifndef ORBFE_OCT_PROF_PASS
+      if (n_passes == 1) OCT_MARK(14, wall_clock64());
+#endif
       // (sk is free during full passes: its first 12 ints hold the scan's wave sums)
       const int3 tot3 = block_scan_excl3(sa, sb, sx, S, reinterpret_cast<int*>(sk));
+#ifndef ORBFE_OCT_PROF_PASS
       if (n_passes == 1) OCT_MARK(15, wall_clock64());
+#endif
+      OCT_PMARK(11, wall_clock64());
       const int T = tot3.x, NP = tot3.y, nexp = tot3.z;
       for (int i = t; i < S; i += 256) {
         const ONode nd = Lc[i];
@@ -1471,6 +1508,9 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       S = T + NP;
       cur ^= 1;
       __syncthreads();
+#ifdef ORBFE_OCT_PROF_PASS
+      if (n_passes == ORBFE_OCT_PROF_PASS) OCT_MARK(15, wall_clock64());
+#endif
       if (S >= N || S == prevS) break;
       if (S + nexp * 3 > N) refine = true;
     } else {
@@ -1479,7 +1519,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       for (int i = t; i < S; i += 256) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
       __syncthreads();
       const int nR = block_scan_excl(sa, S, misc);
-      if (n_rounds == 1) OCT_MARK(8, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(8, wall_clock64());
       int P2 = 1;
       while (P2 < nR) P2 <<= 1;
       if (nR > 1024) {
@@ -1546,7 +1586,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
           }
         }
       }
-      if (n_rounds == 1) OCT_MARK(9, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(9, wall_clock64());
       // child counts of every candidate, in processing order
       for (int k = t; k < nR; k += 256) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
@@ -1557,7 +1597,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         if (lane == 0) cc[k] = c4;
       });
       __syncthreads();
-      if (n_rounds == 1) OCT_MARK(10, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(10, wall_clock64());
       for (int k = t; k < nR; k += 256) sa[k] = nonempty4(cc[k]) - 1;
       if (t == 0) misc[9] = nR;
       __syncthreads();
@@ -1568,7 +1608,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       }
       __syncthreads();
       const int nproc = misc[9];
-      if (n_rounds == 1) OCT_MARK(11, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(11, wall_clock64());
       for (int i = t; i < S; i += 256) sb[i] = -1;
       __syncthreads();
       for (int k = t; k < nproc; k += 256) sb[(int)(sk[k] & 0xfffffull)] = k;
@@ -1583,7 +1623,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       });
       for (int k = t; k < nR; k += 256) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
       __syncthreads();
-      if (n_rounds == 1) OCT_MARK(12, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(12, wall_clock64());
       const int T = block_scan_excl(sx, nR, misc);
       for (int i = t; i < S; i += 256) sa[i] = sb[i] < 0 ? 1 : 0;
       __syncthreads();
@@ -1611,7 +1651,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       S = T + NK;
       cur ^= 1;
       __syncthreads();
-      if (n_rounds == 1) OCT_MARK(13, wall_clock64());
+      if (n_rounds == 1) OCT_RMARK(13, wall_clock64());
       if (S >= N || S == prevS) break;
     }
   }

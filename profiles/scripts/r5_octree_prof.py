@@ -65,6 +65,22 @@ def main():
         p1 = [t[..., l, 14] - t[..., l, 3], t[..., l, 15] - t[..., l, 14]]
         print(f"{l:5d}                         " + "  ".join(f"{x.mean():12.1f}" for x in r) +
               f"     {p1[0].mean():12.1f} {p1[1].mean():6.1f}")
+    if os.environ.get("ORBFE_OCT_PROF_PASS"):  # a build with -DORBFE_OCT_PROF_PASS=k: marks 14/15
+        k = os.environ["ORBFE_OCT_PROF_PASS"]  # bracket full pass k (zero when a level has fewer)
+        d = t[..., :8, 15] - t[..., :8, 14]
+        print(f"full pass {k} (us, mean/max per level): " +
+              "  ".join(f"{d[..., l].mean():5.1f}/{d[..., l].max():5.1f}" for l in range(8)))
+        cyc, sn = a[..., :8, 12].astype(np.float64), a[..., :8, 13]
+        ns, nk = (sn & 0xffff).astype(np.float64), (sn >> 16).astype(np.float64)
+        print("  wave 0's wave splits (shader clocks per split / keys per split / splits, per level): " +
+              "  ".join(f"{(cyc[..., l] / np.maximum(ns[..., l], 1)).mean():6.0f}/"
+                        f"{(nk[..., l] / np.maximum(ns[..., l], 1)).mean():4.0f}/{ns[..., l].mean():3.1f}"
+                        for l in range(8)))
+        print("  sub-steps (us, thread 0's wavefront): thread-split  wave-split  barrier  scan  build")
+        for l in range(8):
+            m = [14, 8, 9, 10, 11, 15]
+            print(f"  {l:5d}  " + "  ".join(f"{(t[..., l, m[i + 1]] - t[..., l, m[i]]).mean():10.1f}"
+                                         for i in range(5)))
 
 
 if __name__ == "__main__":
