@@ -2183,6 +2183,7 @@ struct orbfe_extractor {
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
+  int lat_sched = 2;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -2666,7 +2667,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main stream
   // has built it, beside the chain of small dependent resize launches that leaves most CUs idle;
   // levels k..L-1 follow the chain on the main stream
-  const int k_side = fast_side_split(h);
+  // latency schedule (orbfe_debug_set_latency_schedule, calls of fewer than 8 images): FAST of
+  // levels 0..k-1 and then their DistributeOctTree on the side stream, beside the main stream's
+  // resize chain, FAST and octree of levels k..L-1 (both octree launches at the full LDS plan);
+  // joined before k_describe. Level 0's octree block, the longest, starts right after its FAST
+  // instead of after the whole pyramid's: one KITTI image 0.181-0.183 vs 0.191-0.201 ms per
+  // orbfe_extract at k = 2 (k = 1 the same, k = 3 0.185-0.194; profiles/r5_c2_sched.txt)
+  const bool lat = h->lat_sched > 0 && h->lat_sched < h->nlevels && n < 8;
+  const int k_side = lat ? h->lat_sched : fast_side_split(h);
   if ((int)h->ev_lvl.size() < h->nlevels) {
     for (int l = (int)h->ev_lvl.size(); l < h->nlevels; l++) {
       hipEvent_t e = nullptr;
@@ -2681,20 +2689,6 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
     return launch_fast(side, h->levels[l].cell_begin, c1);
   };
-  side_fast(0);
-  for (int l = 1; l < h->nlevels; l++) {
-    const LevelDesc& d = h->levels[l];
-    if (d.rwin_ok) {
-      const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
-      const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
-      dim3 grid((items + 255) / 256, n);
-      ORBFE_LAUNCH("k_resize_win", k_resize_win, grid, dim3(256), 0, st, a, l, G, gm);
-    } else {
-      dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
-      ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
-    }
-    if (l < k_side) side_fast(l);
-  }
   if (std::max(h->oct_all.lds, std::max(h->oct_hi.lds, h->oct_lo.lds)) > 160 * 1024)
     return orbfe_set_error(ORBFE_ERR_ARG, "image too large for the octree LDS plan");
   auto launch_octree = [&](hipStream_t s, int l0, int nl, const OctPlan& P) {
@@ -2707,6 +2701,22 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     dim3 grid(nl, n);
     ORBFE_LAUNCH("k_octree", k_octree, grid, dim3(256), P.lds, s, ao, l0);
   };
+  side_fast(0);
+  if (lat && k_side == 1) launch_octree(side, 0, 1, h->oct_all);
+  for (int l = 1; l < h->nlevels; l++) {
+    const LevelDesc& d = h->levels[l];
+    if (d.rwin_ok) {
+      const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
+      const uint32_t gm = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / G) : 0u;  // exact: items * G < 2^32
+      dim3 grid((items + 255) / 256, n);
+      ORBFE_LAUNCH("k_resize_win", k_resize_win, grid, dim3(256), 0, st, a, l, G, gm);
+    } else {
+      dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
+      ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
+    }
+    if (l < k_side) side_fast(l);
+    if (lat && l == k_side - 1) launch_octree(side, 0, k_side, h->oct_all);
+  }
   // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
   // only the pyramid, so it runs on the side stream beside k_octree (a small, latency-bound grid
   // that leaves most CUs idle); joined before k_describe. (Measured on MI355X and not kept:
@@ -2719,10 +2729,12 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   const int blur_wpb = 4;  // 1 or 2 strips per workgroup: no difference (76.4-77.0k vs 77.2k)
   const dim3 blur_grid((h->blur_tiles + blur_wpb - 1) / blur_wpb, n);
   ORBFE_HIP_CHECK(hipEventRecord(h->ev_f0, side));
+  // (latency schedule: the blur follows the side's octree as soon as the pyramid is complete)
+  if (lat && h->blur_mode == 0) ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
   if (k_side < h->nlevels) launch_fast(st, h->levels[k_side].cell_begin, a.ncells, true);
-  ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
+  if (!lat) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));
   if (h->blur_mode == 0) {  // the blur on the side stream beside DistributeOctTree
-    ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
+    if (!lat) ORBFE_HIP_CHECK(hipEventRecord(h->ev_fork, st));
     ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork, 0));
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, side, a);
     ORBFE_HIP_CHECK(hipEventRecord(h->ev_join, side));
@@ -2735,7 +2747,9 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     // (the launch span 116 vs 69 us), so single images and the synchronous host-buffer calls
     // keep one launch
     const int ks = (h->device_call && n >= 8) ? std::min(std::max(h->octree_split, 0), h->nlevels) : 0;
-    if (ks > 0 && ks < h->nlevels) {
+    if (lat) {
+      launch_octree(st, k_side, h->nlevels - k_side, h->oct_all);
+    } else if (ks > 0 && ks < h->nlevels) {
       launch_octree(st, 0, ks, h->oct_hi);
       launch_octree(st, ks, h->nlevels - ks, h->oct_lo);
     } else {
@@ -2745,6 +2759,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   if (h->blur_mode == 1)  // the blur after DistributeOctTree on the launch stream
     ORBFE_LAUNCH("k_blur", k_blur, blur_grid, dim3(64 * blur_wpb), 0, st, a);
   if (h->blur_mode == 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
+  if (lat && h->blur_mode != 0) ORBFE_HIP_CHECK(hipStreamWaitEvent(st, h->ev_f0, 0));  // the side's octree
   {
     constexpr int per_block = 4 * DESC_WPB;  // keypoints per workgroup
     dim3 grid((h->total_key_slots + per_block - 1) / per_block, n);
@@ -3616,6 +3631,13 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_latency_schedule: null handle");
+  h->lat_sched = k > 0 ? k : 0;
+  drop_graphs(h);  // a captured sequence follows the old schedule
   return ORBFE_OK;
 }
 

@@ -308,6 +308,11 @@ class ORBextractor:
         per block and k.. at 40 KiB (default 4; k <= 0: one launch of every level at 80 KiB)."""
         L.check(self._lib.orbfe_debug_set_octree_split(self._h, int(k)), "set_octree_split")
 
+    def debug_set_latency_schedule(self, k: int) -> None:
+        """Calls of fewer than 8 images: FAST and DistributeOctTree of levels 0..k-1 on the side stream
+        beside the main stream's levels k.. (default 2; k <= 0: the throughput schedule)."""
+        L.check(self._lib.orbfe_debug_set_latency_schedule(self._h, int(k)), "set_latency_schedule")
+
     def debug_set_octree_lds(self, hi_kb: int, lo_kb: int) -> None:
         """LDS budgets (KiB per block) of the octree launches below / from the split (80 / 40)."""
         L.check(self._lib.orbfe_debug_set_octree_lds(self._h, int(hi_kb), int(lo_kb)), "set_octree_lds")

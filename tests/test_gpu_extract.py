@@ -155,6 +155,23 @@ def test_octree_launch_split(require_gpu, split, lds):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=got)
 
 
+@pytest.mark.parametrize("blur_mode,k,n", [(0, 2, 1), (1, 2, 1), (0, 3, 2), (0, 1, 1), (0, 7, 4), (0, 0, 1)])
+def test_latency_schedule(require_gpu, blur_mode, k, n):
+    """The latency schedule (FAST and DistributeOctTree of levels 0..k-1 on the side stream beside the
+    main stream's levels k..; calls of fewer than 8 images; k = 0 the throughput schedule): every
+    stage equals the oracle, for both blur placements, several k and 1-4 images, on textured and
+    noise images."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_latency_schedule(k)
+    ext.debug_set_blur_mode(blur_mode)
+    noise = np.random.default_rng(11).integers(0, 256, (376, 1241), dtype=np.uint8)
+    imgs = [synth_frame(21 + i, 376, 1241) for i in range(n - 1)] + [noise]
+    for _ in range(2):  # the second round through the same handle (its streams and events reused)
+        outs = ext.extract_batch(imgs) if n > 1 else [ext(imgs[0])]
+    for i in reversed(range(n)):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_large_scale_factors(require_gpu, params):
     """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
