@@ -33,7 +33,7 @@ int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
 int orbfe_debug_set_octree_split(orbfe_extractor* h, int k);
 /* Latency schedule for calls of fewer than 8 images: FAST of levels 0..k-1 and their
  * DistributeOctTree on the handle's side stream while the main stream builds and processes levels
- * k..L-1; joined before the descriptors. Default k = 2; k <= 0 or k >= L: the throughput schedule
+ * k..L-1; joined before the descriptors. Default k = 1; k <= 0 or k >= L: the throughput schedule
  * (FAST of the first levels on the side stream, one octree launch after every level's FAST). */
 int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)

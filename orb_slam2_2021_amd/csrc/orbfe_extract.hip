@@ -2183,7 +2183,7 @@ struct orbfe_extractor {
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
-  int lat_sched = 2;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
+  int lat_sched = 1;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -2220,10 +2220,15 @@ struct orbfe_extractor {
   uint32_t* d_keys_b = nullptr;
   uint32_t* d_lvlkeys = nullptr;
   int32_t* d_lvlcnt = nullptr;
+  // host-buffer entry points' results: one block [slots x keypoint][slots x 32 B][images x count],
+  // laid out like its pinned host mirror h_out, so a small call's results go down in one copy
+  uint8_t* d_out = nullptr;
   orbfe_keypoint* d_kps = nullptr;
   uint8_t* d_desc = nullptr;
   int32_t* d_counts = nullptr;
-  size_t out_cap_alloc = 0;
+  size_t out_cap_alloc = 0;  // keypoint slots (a multiple of 64)
+  int out_n_alloc = 0;       // image counts
+  size_t out_bytes = 0;
   // host-buffer entry points: worker pool for the staging copies, copy streams and per-chunk
   // events of the H2D / extract / D2H pipeline
   HostPool* pool = nullptr;
@@ -2671,8 +2676,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // levels 0..k-1 and then their DistributeOctTree on the side stream, beside the main stream's
   // resize chain, FAST and octree of levels k..L-1 (both octree launches at the full LDS plan);
   // joined before k_describe. Level 0's octree block, the longest, starts right after its FAST
-  // instead of after the whole pyramid's: one KITTI image 0.181-0.183 vs 0.191-0.201 ms per
-  // orbfe_extract at k = 2 (k = 1 the same, k = 3 0.185-0.194; profiles/r5_c2_sched.txt)
+  // instead of after the whole pyramid's: one KITTI image 0.169-0.181 vs 0.189-0.201 ms per
+  // orbfe_extract at k = 1 (k = 2 1-3 us slower in 3 of 4 A/B runs, k = 3 0.185-0.194; enqueueing
+  // the side's work after the main chain's: no gain at k = 2, far slower at 1 and 3;
+  // profiles/r5_c2_sched.txt)
   const bool lat = h->lat_sched > 0 && h->lat_sched < h->nlevels && n < 8;
   const int k_side = lat ? h->lat_sched : fast_side_split(h);
   if ((int)h->ev_lvl.size() < h->nlevels) {
@@ -2989,9 +2996,7 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
   hipFree(h->d_in);
-  hipFree(h->d_kps);
-  hipFree(h->d_desc);
-  hipFree(h->d_counts);
+  hipFree(h->d_out);
   if (h->h_in) hipHostFree(h->h_in);
   if (h->h_out) hipHostFree(h->h_out);
   if (h->h2d) hipStreamSynchronize(h->h2d);
@@ -3149,30 +3154,35 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
     h->in_bytes = need_in;
   }
   const size_t need_out = (size_t)n * h->total_key_slots;
-  if (need_out > h->out_cap_alloc) {
-    hipFree(h->d_kps);
-    hipFree(h->d_desc);
-    hipFree(h->d_counts);
+  if (need_out > h->out_cap_alloc || n > h->out_n_alloc) {
+    // (64-slot multiples keep the descriptor and count regions 256-byte aligned)
+    const size_t cap = (std::max(need_out, h->out_cap_alloc) + 63) & ~(size_t)63;
+    const int nn = std::max(n, h->out_n_alloc);
+    const size_t bytes = cap * (sizeof(orbfe_keypoint) + 32) + sizeof(int32_t) * (size_t)nn;
+    hipFree(h->d_out);
+    h->d_out = nullptr;
     h->d_kps = nullptr;
     h->d_desc = nullptr;
     h->d_counts = nullptr;
-    ORBFE_HIP_CHECK(hipMalloc(&h->d_kps, need_out * sizeof(orbfe_keypoint)));
-    ORBFE_HIP_CHECK(hipMalloc(&h->d_desc, need_out * 32));
-    ORBFE_HIP_CHECK(hipMalloc(&h->d_counts, sizeof(int32_t) * n));
-    h->out_cap_alloc = need_out;
+    h->out_cap_alloc = 0;
+    h->out_n_alloc = 0;
+    if (h->h_out) hipHostFree(h->h_out);
+    h->h_out = nullptr;
+    h->h_out_bytes = 0;
+    ORBFE_HIP_CHECK(hipMalloc(&h->d_out, bytes));
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_out, bytes, hipHostMallocDefault));
+    h->d_kps = reinterpret_cast<orbfe_keypoint*>(h->d_out);
+    h->d_desc = h->d_out + cap * sizeof(orbfe_keypoint);
+    h->d_counts = reinterpret_cast<int32_t*>(h->d_desc + cap * 32);
+    h->out_cap_alloc = cap;
+    h->out_n_alloc = nn;
+    h->out_bytes = h->h_out_bytes = bytes;
   }
   if (need_in > h->h_in_bytes) {
     if (h->h_in) hipHostFree(h->h_in);
     h->h_in = nullptr;
     ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_in, hipHostMallocDefault));
     h->h_in_bytes = need_in;
-  }
-  const size_t need_hout = need_out * (sizeof(orbfe_keypoint) + 32) + sizeof(int32_t) * n;
-  if (need_hout > h->h_out_bytes) {
-    if (h->h_out) hipHostFree(h->h_out);
-    h->h_out = nullptr;
-    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_out, need_hout, hipHostMallocDefault));
-    h->h_out_bytes = need_hout;
   }
   return ORBFE_OK;
 }
@@ -3242,7 +3252,14 @@ static int ensure_pipeline(orbfe_extractor* h, int nchunks) {
 extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* const* imgs,
                                    int rows, int cols, size_t step, orbfe_keypoint* kps,
                                    uint8_t* desc, int cap, int32_t* counts) {
+  return orbfe_internal_extract_batch(h, n, imgs, rows, cols, step, kps, desc, cap, counts, {});
+}
+
+int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const* imgs, int rows, int cols,
+                                 size_t step, orbfe_keypoint* kps, uint8_t* desc, int cap, int32_t* counts,
+                                 const std::function<int()>& after_launch) {
   if (!h || n < 0 || !imgs || !counts) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extract_batch: bad argument");
+  if (after_launch && n >= 8) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_internal_extract_batch: hook on a large batch");
   if (n == 0) return ORBFE_OK;
   if (rows == 0 || cols == 0) {  // empty image: operator() returns without output (:1044-1045)
     for (int i = 0; i < n; i++) counts[i] = 0;
@@ -3289,9 +3306,14 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
   const size_t img_bytes = (size_t)rows * cols;
   const int band = 64;  // staging rows per task
   const int bands = (rows + band - 1) / band;
+  // (h_out mirrors the device block d_out: the same offsets)
   orbfe_keypoint* hk = reinterpret_cast<orbfe_keypoint*>(h->h_out);
-  uint8_t* hd = h->h_out + (size_t)n * K * sizeof(orbfe_keypoint);
-  int32_t* hc = reinterpret_cast<int32_t*>(hd + (size_t)n * K * 32);
+  uint8_t* hd = h->h_out + (h->d_desc - h->d_out);
+  int32_t* hc = reinterpret_cast<int32_t*>(h->h_out + (reinterpret_cast<uint8_t*>(h->d_counts) - h->d_out));
+  // a small call through the staging mirror takes its results down in one copy of the block's
+  // prefix when the block is not much larger than the call (one copy engine transfer instead of
+  // three, the counts' through a blit kernel among them: one image 0.17-0.18 vs 0.18-0.20 ms)
+  const bool one_copy = small && !direct_out && h->out_cap_alloc <= 2 * (size_t)n * K + 64;
   static const bool trace = std::getenv("ORBFE_HOST_TRACE") != nullptr;  // phase times to stderr
   auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = trace ? now() : 0.0;
@@ -3335,6 +3357,10 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
                                 h->d_kps + (size_t)g0 * K, h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0,
                                 h->stream, g0);
     if (st != ORBFE_OK) return st;
+    if (after_launch) {  // (small: one group on the handle's stream, before the results' copies)
+      st = after_launch();
+      if (st != ORBFE_OK) return st;
+    }
     if (h->host_pyramid) {
       // mvImagePyramid for a CPU Frame::ComputeStereoMatches: the group's pyramids go down on the
       // second copy stream as soon as they are built, beside FAST / DistributeOctTree / describe
@@ -3348,6 +3374,12 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
     if (!small) {
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_ext[g], h->stream));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->d2h, h->ev_ext[g], 0));
+    }
+    if (one_copy) {  // (small: one group, one piece)
+      const size_t span = (reinterpret_cast<uint8_t*>(h->d_counts) - h->d_out) + sizeof(int32_t) * (size_t)n;
+      ORBFE_HIP_CHECK(hipMemcpyAsync(h->h_out, h->d_out, span, hipMemcpyDeviceToHost, s_out));
+      ORBFE_HIP_CHECK(hipEventRecord(h->ev_out[0], s_out));
+      continue;
     }
     ORBFE_HIP_CHECK(hipMemcpyAsync(hc + g0, h->d_counts + g0, sizeof(int32_t) * ng, hipMemcpyDeviceToHost, s_out));
     const int ppg = npieces / ngroups;

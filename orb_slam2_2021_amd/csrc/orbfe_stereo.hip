@@ -611,12 +611,29 @@ extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const
   if (cap < K) return orbfe_set_error(ORBFE_ERR_CAPACITY, "cap < orbfe_max_keypoints");
   if (!kps_l || !desc_l || !kps_r || !desc_r || !u_right || !depth)
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_stereo_frame: null output buffer");
-  // ExtractORB(0) and ExtractORB(1) as one batch (:113-116); the results stay on the device
+  // ExtractORB(0) and ExtractORB(1) as one batch (:113-116); ComputeStereoMatches enqueued right
+  // behind the extraction on the handle's stream, its uRight / depth copied down with the keypoints
+  // (one wait for the whole Frame; the kernels see the keypoint counts on the device)
   const uint8_t* imgs[2] = {left, right};
   std::vector<orbfe_keypoint> k2(2 * (size_t)K);
   std::vector<uint8_t> d2(2 * (size_t)K * 32);
   int32_t counts[2] = {0, 0};
-  int st = orbfe_extract_batch(h, 2, imgs, rows, cols, step, k2.data(), d2.data(), K, counts);
+  float* ho = nullptr;
+  auto stereo = [&]() -> int {
+    OrbfePyramid P;
+    int r = orbfe_internal_pyramid(h, &P);
+    if (r != ORBFE_OK) return r;
+    OrbfeStereoScratch* S = scratch_of(h);
+    r = ensure_io(S, (size_t)K);
+    if (r != ORBFE_OK) return r;
+    r = launch_stereo(S, P, 0, P, 1, 1, 0, 1, P.io_kps, P.io_desc, P.io_counts, K, mbf, mb, S->d_out, S->d_out + K,
+                      P.stream);
+    if (r != ORBFE_OK) return r;
+    ho = reinterpret_cast<float*>(S->h_stage);
+    ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * 2 * (size_t)K, hipMemcpyDeviceToHost, P.stream));
+    return ORBFE_OK;
+  };
+  const int st = orbfe_internal_extract_batch(h, 2, imgs, rows, cols, step, k2.data(), d2.data(), K, counts, stereo);
   if (st != ORBFE_OK) return st;
   *n_l = counts[0];
   *n_r = counts[1];
@@ -625,21 +642,7 @@ extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const
   std::memcpy(kps_r, k2.data() + K, sizeof(orbfe_keypoint) * counts[1]);
   std::memcpy(desc_r, d2.data() + (size_t)K * 32, (size_t)counts[1] * 32);
   if (counts[0] == 0) return ORBFE_OK;
-  OrbfePyramid P;
-  st = orbfe_internal_pyramid(h, &P);
-  if (st != ORBFE_OK) return st;
-  OrbfeStereoScratch* S = scratch_of(h);
-  st = ensure_io(S, (size_t)K);
-  if (st != ORBFE_OK) return st;
-  st = launch_stereo(S, P, 0, P, 1, 1, 0, 1, P.io_kps, P.io_desc, P.io_counts, K, mbf, mb, S->d_out,
-                     S->d_out + K, P.stream);
-  if (st != ORBFE_OK) return st;
-  float* ho = reinterpret_cast<float*>(S->h_stage);
-  ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * counts[0], hipMemcpyDeviceToHost, P.stream));
-  ORBFE_HIP_CHECK(hipMemcpyAsync(ho + counts[0], S->d_out + K, sizeof(float) * counts[0], hipMemcpyDeviceToHost,
-                                 P.stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(P.stream));
   std::memcpy(u_right, ho, sizeof(float) * counts[0]);
-  std::memcpy(depth, ho + counts[0], sizeof(float) * counts[0]);
+  std::memcpy(depth, ho + K, sizeof(float) * counts[0]);
   return ORBFE_OK;
 }

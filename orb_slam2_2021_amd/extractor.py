@@ -310,7 +310,7 @@ class ORBextractor:
 
     def debug_set_latency_schedule(self, k: int) -> None:
         """Calls of fewer than 8 images: FAST and DistributeOctTree of levels 0..k-1 on the side stream
-        beside the main stream's levels k.. (default 2; k <= 0: the throughput schedule)."""
+        beside the main stream's levels k.. (default 1; k <= 0: the throughput schedule)."""
         L.check(self._lib.orbfe_debug_set_latency_schedule(self._h, int(k)), "set_latency_schedule")
 
     def debug_set_octree_lds(self, hi_kb: int, lo_kb: int) -> None:

@@ -21,7 +21,9 @@ def main():
     rows, cols = 376, 1241
     img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
-    modes = {"thru": 0, "lat_k1": 1, "lat_k2": 2, "lat_k3": 3}  # latency schedule k (0: off)
+    # latency schedule k (0: off). (Round 5 also measured a build that enqueued the side's work
+    # after the main chain's, "d" in profiles/r5_c2_sched.txt: removed.)
+    modes = {"thru": 0, "lat_k1": 1, "lat_k2": 2, "lat_k3": 3}
     exts = {}
     for m, k in modes.items():
         e = ORBextractor(2000, 1.2, 8, 20, 7)

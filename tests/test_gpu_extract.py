@@ -155,7 +155,8 @@ def test_octree_launch_split(require_gpu, split, lds):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=got)
 
 
-@pytest.mark.parametrize("blur_mode,k,n", [(0, 2, 1), (1, 2, 1), (0, 3, 2), (0, 1, 1), (0, 7, 4), (0, 0, 1)])
+@pytest.mark.parametrize("blur_mode,k,n", [(0, 1, 1), (1, 1, 1), (0, 2, 1), (1, 2, 2), (0, 3, 2), (0, 7, 4),
+                                            (0, 0, 1)])
 def test_latency_schedule(require_gpu, blur_mode, k, n):
     """The latency schedule (FAST and DistributeOctTree of levels 0..k-1 on the side stream beside the
     main stream's levels k..; calls of fewer than 8 images; k = 0 the throughput schedule): every
