@@ -3349,6 +3349,7 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
                                      (size_t)nc * img_bytes, hipMemcpyHostToDevice, s_in));
     }
     const int g0 = part(g, ngroups), ng = part(g + 1, ngroups) - g0;
+    if (trace) std::fprintf(stderr, "[host] group %d staged + H2D enqueued %.1f\n", g, now() - t_start);
     if (!small) {
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_in[g], h->h2d));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->stream, h->ev_in[g], 0));
@@ -3357,6 +3358,7 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
                                 h->d_kps + (size_t)g0 * K, h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0,
                                 h->stream, g0);
     if (st != ORBFE_OK) return st;
+    if (trace) std::fprintf(stderr, "[host] group %d launched %.1f\n", g, now() - t_start);
     if (after_launch) {  // (small: one group on the handle's stream, before the results' copies)
       st = after_launch();
       if (st != ORBFE_OK) return st;
@@ -3379,6 +3381,7 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       const size_t span = (reinterpret_cast<uint8_t*>(h->d_counts) - h->d_out) + sizeof(int32_t) * (size_t)n;
       ORBFE_HIP_CHECK(hipMemcpyAsync(h->h_out, h->d_out, span, hipMemcpyDeviceToHost, s_out));
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_out[0], s_out));
+      if (trace) std::fprintf(stderr, "[host] group %d D2H enqueued %.1f\n", g, now() - t_start);
       continue;
     }
     ORBFE_HIP_CHECK(hipMemcpyAsync(hc + g0, h->d_counts + g0, sizeof(int32_t) * ng, hipMemcpyDeviceToHost, s_out));

@@ -1,5 +1,5 @@
-"""One 1241x376 image through orbfe_extract, 60 calls per schedule (latency k = 2, then the
-throughput schedule), for a rocprofv3 kernel / memory-copy trace of the C2 call's timeline.
+"""One 1241x376 image through orbfe_extract, 60 calls per schedule (latency k = 1, then the
+throughput schedule; latency k = 1), for a rocprofv3 kernel / memory-copy trace of the C2 call's timeline.
 usage: rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -- python3 profiles/scripts/r5_c2_trace.py"""
 import os
 import sys
@@ -18,7 +18,7 @@ def main():
     rows, cols = 376, 1241
     img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
-    for k in (2, 0):
+    for k in (1, 0):
         e = ORBextractor(2000, 1.2, 8, 20, 7)
         e.debug_set_latency_schedule(k)
         cap = e.max_keypoints(rows, cols)
