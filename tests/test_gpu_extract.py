@@ -234,6 +234,28 @@ def test_host_batch_pipeline(require_gpu):
     assert c == len(kr) and np.array_equal(desc[7 * cap:7 * cap + c], dr)
 
 
+def test_small_calls_after_large_on_one_handle(require_gpu):
+    """A small host call's results come down in one copy of the output block's prefix only while the
+    block is not much larger than the call; after a 9-image call on the same handle, single images
+    and pairs take the separate copies, and a later larger call regrows the block: every result
+    equals a fresh handle's (and one image the oracle's)."""
+    rows, cols = 240, 333
+    ext, fresh = ORBextractor(1000, 1.2, 8, 20, 7), ORBextractor(1000, 1.2, 8, 20, 7)
+    seq = [1, 9, 1, 2, 1, 12, 1]
+    for j, n in enumerate(seq):
+        imgs = [synth_frame(70 + 13 * j + i, rows, cols) for i in range(n)]
+        outs = ext.extract_batch(imgs) if n > 1 else [ext(imgs[0])]
+        for i in range(n):
+            k1, d1 = fresh(imgs[i])
+            kb, db = outs[i]
+            assert len(kb) == len(k1), (j, i)
+            for f in ("x", "y", "size", "response", "octave", "angle"):
+                assert np.array_equal(kb[f], k1[f]), (j, i, f)
+            assert np.array_equal(db, d1), (j, i)
+    kr, dr = RefExtractor(1000, 1.2, 8, 20, 7)(imgs[0])
+    assert np.array_equal(outs[0][1], dr)
+
+
 @pytest.mark.parametrize("prefetch", [False, True])
 @pytest.mark.parametrize("n", [1, 3, 9])
 def test_mvimagepyramid_views_held_at_once(require_gpu, prefetch, n):
