@@ -1053,7 +1053,9 @@ __device__ __forceinline__ void wave_child_partition(const ONode& nd, int4 cnt, 
 }
 
 // Thread-serial forms for small nodes (count <= OCT_SMALL): one lane walks the whole segment.
+#ifndef OCT_SMALL  // (a build option for the threshold's sweep: profiles/r5_octree_passes.txt)
 #define OCT_SMALL 48
+#endif
 // Four keys per step (four independent loads in flight); the four counts / offsets are packed in
 // the bytes of one register (count <= OCT_SMALL < 256), not a dynamically indexed array.
 __device__ __forceinline__ int4 serial_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
