@@ -234,6 +234,31 @@ def test_host_batch_pipeline(require_gpu):
     assert c == len(kr) and np.array_equal(desc[7 * cap:7 * cap + c], dr)
 
 
+@pytest.mark.parametrize("k", [1, 2, 0])
+def test_small_device_batch_latency_schedule(require_gpu, k):
+    """orbfe_extract_batch_device with fewer than 8 images takes the latency schedule too (k side
+    levels; 0 = the throughput schedule): every image equals the oracle."""
+    import torch
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_latency_schedule(k)
+    imgs = np.stack([synth_frame(90 + i, 376, 1241) for i in range(3)])
+    n, H, W = imgs.shape
+    cap = ext.max_keypoints(H, W)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(imgs).to(dev)
+    kps = torch.empty(n * cap * 28, dtype=torch.uint8, device=dev)
+    desc = torch.empty(n * cap * 32, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    ext.extract_batch_device(n, d_in.data_ptr(), H * W, H, W, W, kps.data_ptr(), desc.data_ptr(), cap,
+                             cnt.data_ptr())
+    torch.cuda.synchronize()
+    C = cnt.cpu().numpy()
+    K = kps.cpu().numpy().view(KEYPOINT_DTYPE).reshape(n, cap)
+    D = desc.cpu().numpy().reshape(n, cap, 32)
+    for i in reversed(range(n)):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=(K[i, :C[i]], D[i, :C[i]] if C[i] else None))
+
+
 def test_small_calls_after_large_on_one_handle(require_gpu):
     """A small host call's results come down in one copy of the output block's prefix only while the
     block is not much larger than the call; after a 9-image call on the same handle, single images
