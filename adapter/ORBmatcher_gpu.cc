@@ -7,7 +7,9 @@
 //
 // One line changes in the reference's include/MapPoint.h: `friend class ORBmatcher;` beside the
 // protected mfMinDistance / mfMaxDistance (MapPoint.h:151-152), which the keyframe searches pass
-// to the GPU as they are (MapPoint exposes only 0.8f / 1.2f times them). The protected helpers
+// to the GPU as they are (MapPoint exposes only 0.8f / 1.2f times them). They are read under the
+// MapPoint's mMutexPos, the mutex UpdateNormalAndDepth writes them under (MapPoint.cc:396-398) on
+// the LocalMapping thread while Tracking / LoopClosing run these searches. The protected helpers
 // CheckDistEpipolarLine, RadiusByViewingCos and ComputeThreeMaxima have no caller left outside
 // the searches and are not defined.
 //
@@ -17,6 +19,7 @@
 
 #include <map>
 #include <memory>
+#include <mutex>
 #include <utility>
 
 #include <opencv2/core.hpp>
@@ -31,13 +34,19 @@ const int ORBmatcher::TH_HIGH = 100;  // ORBmatcher.cc:37-39
 const int ORBmatcher::TH_LOW = 50;
 const int ORBmatcher::HISTO_LENGTH = 30;
 
+// The matcher behind the methods: liborbfe's facade. tests/cpp/matcher_tsan.cpp builds this file
+// with a recording matcher in its place (no GPU) to run the packers under ThreadSanitizer.
+#ifndef ORBFE_ADAPTER_MATCHER
+#define ORBFE_ADAPTER_MATCHER orbfe::Matcher
+#endif
+
 namespace {
 // one GPU matcher per (thread, nnratio, checkOri): the reference constructs ORBmatchers on the stack
 // per call (Tracking.cc:889,1207, LocalMapping.cc:219), and the handles are thread-compatible only
-orbfe::Matcher& gpu_matcher(float nnratio, bool checkOri) {
-  thread_local std::map<std::pair<float, bool>, std::unique_ptr<orbfe::Matcher>> pool;
-  std::unique_ptr<orbfe::Matcher>& m = pool[{nnratio, checkOri}];
-  if (!m) m.reset(new orbfe::Matcher(nnratio, checkOri));
+ORBFE_ADAPTER_MATCHER& gpu_matcher(float nnratio, bool checkOri) {
+  thread_local std::map<std::pair<float, bool>, std::unique_ptr<ORBFE_ADAPTER_MATCHER>> pool;
+  std::unique_ptr<ORBFE_ADAPTER_MATCHER>& m = pool[{nnratio, checkOri}];
+  if (!m) m.reset(new ORBFE_ADAPTER_MATCHER(nnratio, checkOri));
   return *m;
 }
 cv::Mat continuous(const cv::Mat& m) { return m.isContinuous() ? m : m.clone(); }
@@ -65,7 +74,11 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const std
   CurrentFrame.mTcw = continuous(CurrentFrame.mTcw);
   return orbfe_adapter::search_by_projection_keyframe(
       gpu_matcher(mfNNratio, mbCheckOrientation), CurrentFrame, pKF, sAlreadyFound, th, ORBdist,
-      [](MapPoint* p, float& dmin, float& dmax) { dmin = p->mfMinDistance; dmax = p->mfMaxDistance; });
+      [](MapPoint* p, float& dmin, float& dmax) {  // under mMutexPos, as MapPoint.cc:403-447 reads them
+        std::unique_lock<std::mutex> lock(p->mMutexPos);
+        dmin = p->mfMinDistance;
+        dmax = p->mfMaxDistance;
+      });
 }
 
 int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& vpPoints,
@@ -73,7 +86,11 @@ int ORBmatcher::SearchByProjection(KeyFrame* pKF, cv::Mat Scw, const std::vector
   const cv::Mat S = continuous(Scw);
   return orbfe_adapter::search_by_projection_sim3(
       gpu_matcher(mfNNratio, mbCheckOrientation), pKF, S.ptr<float>(), vpPoints, vpMatched, th,
-      [](MapPoint* p, float& dmin, float& dmax) { dmin = p->mfMinDistance; dmax = p->mfMaxDistance; },
+      [](MapPoint* p, float& dmin, float& dmax) {  // under mMutexPos, as MapPoint.cc:403-447 reads them
+        std::unique_lock<std::mutex> lock(p->mMutexPos);
+        dmin = p->mfMinDistance;
+        dmax = p->mfMaxDistance;
+      },
       Frame::mnMinX, Frame::mnMinY);
 }
 
@@ -113,14 +130,22 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoin
   const cv::Mat R = continuous(R12), t = continuous(t12);
   return orbfe_adapter::search_by_sim3(
       gpu_matcher(mfNNratio, mbCheckOrientation), pKF1, pKF2, vpMatches12, s12, R.ptr<float>(), t.ptr<float>(), th,
-      [](MapPoint* p, float& dmin, float& dmax) { dmin = p->mfMinDistance; dmax = p->mfMaxDistance; },
+      [](MapPoint* p, float& dmin, float& dmax) {  // under mMutexPos, as MapPoint.cc:403-447 reads them
+        std::unique_lock<std::mutex> lock(p->mMutexPos);
+        dmin = p->mfMinDistance;
+        dmax = p->mfMaxDistance;
+      },
       Frame::mnMinX, Frame::mnMinY);
 }
 
 int ORBmatcher::Fuse(KeyFrame* pKF, const std::vector<MapPoint*>& vpMapPoints, const float th) {
   return orbfe_adapter::fuse(
       gpu_matcher(mfNNratio, mbCheckOrientation), pKF, vpMapPoints, th,
-      [](MapPoint* p, float& dmin, float& dmax) { dmin = p->mfMinDistance; dmax = p->mfMaxDistance; },
+      [](MapPoint* p, float& dmin, float& dmax) {  // under mMutexPos, as MapPoint.cc:403-447 reads them
+        std::unique_lock<std::mutex> lock(p->mMutexPos);
+        dmin = p->mfMinDistance;
+        dmax = p->mfMaxDistance;
+      },
       Frame::mnMinX, Frame::mnMinY);
 }
 
@@ -129,7 +154,11 @@ int ORBmatcher::Fuse(KeyFrame* pKF, cv::Mat Scw, const std::vector<MapPoint*>& v
   const cv::Mat S = continuous(Scw);
   return orbfe_adapter::fuse_sim3(
       gpu_matcher(mfNNratio, mbCheckOrientation), pKF, S.ptr<float>(), vpPoints, th, vpReplacePoint,
-      [](MapPoint* p, float& dmin, float& dmax) { dmin = p->mfMinDistance; dmax = p->mfMaxDistance; },
+      [](MapPoint* p, float& dmin, float& dmax) {  // under mMutexPos, as MapPoint.cc:403-447 reads them
+        std::unique_lock<std::mutex> lock(p->mMutexPos);
+        dmin = p->mfMinDistance;
+        dmax = p->mfMaxDistance;
+      },
       Frame::mnMinX, Frame::mnMinY);
 }
 

@@ -95,6 +95,26 @@ class Mat {
   const T& at(int r, int c) const {
     return ptr<T>(r)[c];
   }
+  // element i of a continuous single-row or single-column matrix
+  template <typename T>
+  T& at(int i) {
+    return reinterpret_cast<T*>(data)[i];
+  }
+  template <typename T>
+  const T& at(int i) const {
+    return reinterpret_cast<const T*>(data)[i];
+  }
+  bool isContinuous() const { return rows <= 1 || step == (size_t)cols * elem_size(type_); }
+  static Mat zeros(int r, int c, int type) {
+    Mat m(r, c, type);
+    std::memset(m.data, 0, (size_t)r * m.step);
+    return m;
+  }
+  static Mat eye(int r, int c, int type) {
+    Mat m = zeros(r, c, type);
+    for (int i = 0; i < r && i < c; i++) m.at<float>(i, i) = 1.f;
+    return m;
+  }
 
  private:
   int type_ = CV_8U;
@@ -123,6 +143,28 @@ class _OutputArray {
   Mat* m_;
 };
 typedef const _OutputArray& OutputArray;
+
+// CV_32F matrix product and sum (the adapter's epipole, ORBmatcher.cc:678-681): each product
+// element accumulated in double and rounded once, as OpenCV's small-matrix gemm does
+inline Mat operator*(const Mat& a, const Mat& b) {
+  if (a.type() != CV_32F || b.type() != CV_32F || a.cols != b.rows) throw std::invalid_argument("cvstub: gemm");
+  Mat c(a.rows, b.cols, CV_32F);
+  for (int i = 0; i < a.rows; i++)
+    for (int j = 0; j < b.cols; j++) {
+      double s = 0.0;
+      for (int k = 0; k < a.cols; k++) s += (double)a.at<float>(i, k) * (double)b.at<float>(k, j);
+      c.at<float>(i, j) = (float)s;
+    }
+  return c;
+}
+inline Mat operator+(const Mat& a, const Mat& b) {
+  if (a.type() != CV_32F || b.type() != CV_32F || a.rows != b.rows || a.cols != b.cols)
+    throw std::invalid_argument("cvstub: add");
+  Mat c(a.rows, a.cols, CV_32F);
+  for (int i = 0; i < a.rows; i++)
+    for (int j = 0; j < a.cols; j++) c.at<float>(i, j) = a.at<float>(i, j) + b.at<float>(i, j);
+  return c;
+}
 
 }  // namespace cv
 

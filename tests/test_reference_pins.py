@@ -146,3 +146,62 @@ def test_adapter_test_stub_declares_the_reference_members():
         return re.sub(r"\s+", "", m.group(1))
     for pat in (r"ORBextractor\s*\(([^)]*)\)\s*;", r"void\s+operator\(\)\s*\(([^)]*)\)\s*;"):
         assert sig(ref, pat) == sig(stub, pat), pat
+
+
+def _signatures(text, cls):
+    """Public method declarations `Ret Name(params);` of class `cls`, whitespace-normalised."""
+    body = _strip_comments(text)
+    start = re.search(r"class\s+" + cls + r"\s*\{", body).end()
+    depth, i = 1, start
+    while depth:
+        depth += {"{": 1, "}": -1}.get(body[i], 0)
+        i += 1
+    body = body[start:i - 1]
+    out = set()
+    for m in re.finditer(r"([\w:<>,\s\*&]+?)\b(\w+)\s*\(([^;{)]*(?:\([^)]*\)[^;{)]*)*)\)\s*;", body):
+        out.add((m.group(2), re.sub(r"\s+", "", m.group(3))))
+    return out
+
+
+def test_matcher_stub_declares_the_reference_interface():
+    """tests/cpp/cvstub/ORBmatcher.h (what adapter/ORBmatcher_gpu.cc is compiled over in
+    tests/cpp/matcher_e2e.cpp / matcher_tsan.cpp) declares every public method of the reference's
+    include/ORBmatcher.h:41-105 with the same parameter lists, default arguments included."""
+    with open("/root/reference/include/ORBmatcher.h") as f:
+        ref = _signatures(f.read(), "ORBmatcher")
+    with open(os.path.join(ROOT, "tests", "cpp", "cvstub", "ORBmatcher.h")) as f:
+        stub = _signatures(f.read(), "ORBmatcher")
+    public = {s for s in ref if s[0] not in ("CheckDistEpipolarLine", "RadiusByViewingCos", "ComputeThreeMaxima")}
+    assert len(public) == 13, public  # the constructor and the 12 searches
+    assert public <= stub, public - stub
+
+
+@pytest.mark.parametrize("header,names", [
+    ("MapPoint.h", ["GetWorldPos", "GetNormal", "Observations", "AddObservation", "GetIndexInKeyFrame",
+                    "IsInKeyFrame", "isBad", "Replace", "GetDescriptor", "UpdateNormalAndDepth", "mTrackProjX",
+                    "mTrackProjY", "mTrackProjXR", "mbTrackInView", "mnTrackScaleLevel", "mTrackViewCos",
+                    "mfMinDistance", "mfMaxDistance", "mMutexPos", "mMutexFeatures"]),
+    ("KeyFrame.h", ["GetPose", "GetCameraCenter", "GetRotation", "GetTranslation", "AddMapPoint", "GetMapPoints",
+                    "GetMapPointMatches", "GetMapPoint", "mfGridElementWidthInv", "mvKeysUn", "mvuRight",
+                    "mDescriptors", "mFeatVec", "mnScaleLevels", "mfLogScaleFactor", "mvScaleFactors",
+                    "mvLevelSigma2", "mnMinX", "mnMaxY", "mvpMapPoints", "mMutexFeatures"]),
+    ("Frame.h", ["fx", "cx", "mb", "mvKeysUn", "mFeatVec", "mvpMapPoints", "mvbOutlier", "mfGridElementWidthInv",
+                 "mTcw", "mnScaleLevels", "mfLogScaleFactor", "mvScaleFactors", "mvLevelSigma2", "mnMinX",
+                 "mnMaxY"]),
+])
+def test_object_stubs_use_the_reference_names(header, names):
+    """The cvstub Frame / KeyFrame / MapPoint declare, under the reference's own names, what the matcher
+    adapter's packers read (adapter/orbfe_pack.hpp, orbfe_adapter.hpp): each name appears in both the
+    reference header and the stub, MapPoint's distances as protected members beside mMutexPos."""
+    with open(os.path.join("/root/reference/include", header)) as f:
+        ref = _strip_comments(f.read())
+    with open(os.path.join(ROOT, "tests", "cpp", "cvstub", header)) as f:
+        stub = _strip_comments(f.read())
+    for n in names:
+        pat = r"\b" + n + r"\b"
+        assert re.search(pat, ref), (header, n)
+        assert re.search(pat, stub), (header, n)
+    if header == "MapPoint.h":
+        for text in (ref, stub):
+            prot = text[text.index("protected:"):]
+            assert "mfMinDistance" in prot and "mMutexPos" in prot
