@@ -17,6 +17,7 @@
 #if __has_include(<opencv2/core.hpp>) && __has_include("ORBextractor.h")
 
 #include <cassert>
+#include <cstddef>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -73,6 +74,15 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray /*_mask: ign
   // cv::KeyPoint is orbfe_keypoint's layout (pt.x, pt.y, size, angle, response, octave, class_id):
   // the keypoints land in the caller's vector directly
   static_assert(sizeof(cv::KeyPoint) == sizeof(orbfe_keypoint), "cv::KeyPoint is 28 bytes");
+  static_assert(offsetof(cv::KeyPoint, pt) == offsetof(orbfe_keypoint, x) &&
+                    offsetof(cv::KeyPoint, pt) + sizeof(float) == offsetof(orbfe_keypoint, y) &&
+                    sizeof(cv::KeyPoint::pt) == 2 * sizeof(float) &&
+                    offsetof(cv::KeyPoint, size) == offsetof(orbfe_keypoint, size) &&
+                    offsetof(cv::KeyPoint, angle) == offsetof(orbfe_keypoint, angle) &&
+                    offsetof(cv::KeyPoint, response) == offsetof(orbfe_keypoint, response) &&
+                    offsetof(cv::KeyPoint, octave) == offsetof(orbfe_keypoint, octave) &&
+                    offsetof(cv::KeyPoint, class_id) == offsetof(orbfe_keypoint, class_id),
+                "cv::KeyPoint's fields sit where orbfe_keypoint's do");
   const int cap = orbfe::check(orbfe_max_keypoints(g.handle(), image.rows, image.cols), "orbfe_max_keypoints");
   thread_local std::vector<uint8_t> desc;  // one operator() per thread at a time (Frame.cc:113-116)
   desc.resize((size_t)cap * 32);

@@ -128,7 +128,9 @@ int orbfe_extractor_set_host_pyramid(orbfe_extractor* h, int enable);
  * replayed with one graph launch afterwards (up to 8 argument sets per handle, least recently used
  * dropped); 0 (the default) launches every kernel directly. Same results either way. Measured on
  * MI355X / ROCm 7.2 the replay is slower: one 1241x376 image 0.33 vs 0.22 ms,
- * the C3 pipeline 38.6k vs 83.7k stereo frames/s. */
+ * the C3 pipeline 38.6k vs 83.7k stereo frames/s. A handle whose side stream is a caller's shared
+ * stream (orbfe_set_side_stream) always launches directly: a capture would pull that stream, which
+ * other handles launch onto from their own threads, into the graph. */
 int orbfe_extractor_set_graphs(orbfe_extractor* h, int enable);
 
 /* Device pointer of the same level (no copy), for device-side consumers. */

@@ -2495,16 +2495,18 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->geom_mode = h->resize_mode;
   h->batch_cap = 0;  // strides changed: reallocate batch buffers on the next call
   // k_octree's dynamic LDS limit, set here rather than per launch (a host call a captured launch
-  // sequence cannot replay); the attribute is per function, so the largest plan any handle of the
-  // process asked for stays in force
+  // sequence cannot replay); the attribute is per function and device, so the largest plan any
+  // handle of the process asked for on this device stays in force there
+  constexpr int kMaxDevices = 64;
   static std::mutex attr_mu;
-  static int attr_lds = 0;
+  static int attr_lds[kMaxDevices] = {};
   {
     std::lock_guard<std::mutex> lk(attr_mu);
     const int need = (int)std::max(h->oct_all.lds, std::max(h->oct_hi.lds, h->oct_lo.lds));
-    if (need <= 160 * 1024 && need > attr_lds) {
+    int* have = h->device >= 0 && h->device < kMaxDevices ? &attr_lds[h->device] : nullptr;
+    if (need <= 160 * 1024 && (!have || need > *have)) {
       ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, need));
-      attr_lds = need;
+      if (have) *have = need;
     }
   }
   return ORBFE_OK;
@@ -2534,6 +2536,10 @@ static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int
 }
 
 static void free_batch(orbfe_extractor* h) {
+  if (h->hpyr_pending) {  // the host-pyramid prefetch still reads d_pyr
+    hipEventSynchronize(h->ev_hpyr);
+    h->hpyr_pending = false;
+  }
   drop_graphs(h);
   hipFree(h->d_pyr);
   hipFree(h->d_blur);
@@ -2801,7 +2807,10 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
     h->ev_lvl.push_back(e);
   }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (!h->use_graphs || !st || orbfe_kt::g_on.load(std::memory_order_relaxed) ||
+  // direct launches when the side stream is a caller's shared one (orbfe_set_side_stream): a
+  // capture pulls the side stream in through the fork / join events, and the other handles'
+  // launches onto it from their threads would collide with the capture
+  if (!h->use_graphs || !st || h->side_ext || orbfe_kt::g_on.load(std::memory_order_relaxed) ||
       hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
     return launch_extract(h, n, d_imgs, img_stride, pitch, d_kps, d_desc, cap, d_counts, st, i0);
   const hipStream_t side = h->inline_side ? st : (h->side_ext ? h->side_ext : h->side);
@@ -2859,6 +2868,13 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
   h->last_img_pitch = pitch;
   h->last_n = i0 + n;
   h->last_stream = st;
+  return ORBFE_OK;
+}
+
+// A new call rewrites d_pyr: its launches on `s` wait for the previous call's host-pyramid
+// prefetch copies (h->d2h), which only orbfe_get_level otherwise waits for.
+static int wait_host_pyramid(orbfe_extractor* h, hipStream_t s) {
+  if (h->hpyr_pending) ORBFE_HIP_CHECK(hipStreamWaitEvent(s, h->ev_hpyr, 0));
   return ORBFE_OK;
 }
 
@@ -2987,6 +3003,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   if (!h) return ORBFE_OK;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->h2d) hipStreamSynchronize(h->h2d);
+  if (h->d2h) hipStreamSynchronize(h->d2h);  // (the host-pyramid prefetch reads d_pyr)
   orbfe_internal_stereo_free(h->stereo);
   drop_graphs(h);
   free_batch(h);
@@ -3001,8 +3019,6 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_out);
   if (h->h_in) hipHostFree(h->h_in);
   if (h->h_out) hipHostFree(h->h_out);
-  if (h->h2d) hipStreamSynchronize(h->h2d);
-  if (h->d2h) hipStreamSynchronize(h->d2h);
   if (h->h_pyr) hipHostFree(h->h_pyr);
   if (h->ev_hpyr) hipEventDestroy(h->ev_hpyr);
   delete h->pool;
@@ -3140,6 +3156,8 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
   if (st != ORBFE_OK) return st;
   hipStream_t s = stream ? (hipStream_t)stream : h->stream;
   h->gen++;  // the host pyramid block of the previous call is stale from here on
+  st = wait_host_pyramid(h, s);
+  if (st != ORBFE_OK) return st;
   h->device_call = true;
   st = launch_extract_graphed(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
                               d_counts, s);
@@ -3299,6 +3317,8 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   st = ensure_pipeline(h, std::max(nchunks, npieces));
   if (st != ORBFE_OK) return st;
   h->gen++;
+  st = wait_host_pyramid(h, h->stream);
+  if (st != ORBFE_OK) return st;
   if (h->host_pyramid) {
     st = ensure_host_pyramid(h, n);
     if (st != ORBFE_OK) return st;

@@ -66,19 +66,20 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
             assert abs(st["epipole"][0] - st["cam"]["cx"]) < 1e-3 and abs(st["epipole"][1] - st["cam"]["cy"]) < 1e-3
 
 
-@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match,handles",
-                         [(False, False, 1, "stereo", True, 2), (True, False, 0, "stereo", True, 2),
-                          (False, True, 0, "stereo", False, 2), (False, True, 1, "kf", True, 2),
-                          (True, True, 1, "kf", True, 2), (False, True, 1, "kf", False, 2),
-                          (False, True, 1, "kf", True, 4)])
+@pytest.mark.parametrize("match_inline,stereo,blur_mode,pairs,stereo_on_match,handles,fast_side",
+                         [(False, False, 1, "stereo", True, 2, 0), (True, False, 0, "stereo", True, 2, 0),
+                          (False, True, 0, "stereo", False, 2, 0), (False, True, 1, "kf", True, 2, 0),
+                          (True, True, 1, "kf", True, 2, 0), (False, True, 1, "kf", False, 2, 0),
+                          (False, True, 1, "kf", True, 4, 0), (False, True, 1, "kf", True, 4, 4)])
 def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match,
-                                     handles):
+                                     handles, fast_side):
     """bench.py's schedules: extractor handles extract consecutive sub-batches on two extraction
     streams (handle k on stream k mod 2; side-stream work on one shared high-priority stream),
     matching on its own stream or inline after each extraction (then two vocabulary transforms run
     concurrently on the one handle: per-stream scratch), 4+ output sets; ComputeStereoMatches on the
     matching stream (with 2 handles the handle's next extraction waits for it; with 4 -- bench.py's
-    default -- nothing waits) or right after the extraction."""
+    default -- nothing waits) or right after the extraction. fast_side 4: FAST of levels 0-3 on the
+    shared side stream, bench.py's setting (0 keeps the library default, 3)."""
     import torch
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     tree, voc, ref = vocab
@@ -86,6 +87,8 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
     exts = [ORBextractor(2000, 1.2, 8, 20, 7) for _ in range(handles)]
     for e in exts:
         e.debug_set_blur_mode(blur_mode)
+        if fast_side > 0:
+            e.debug_set_fast_side_levels(fast_side)
     streams = PipelineStreams(0, 2, match_inline=match_inline)
     pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs,
                         stereo_on_match=stereo_on_match)
