@@ -114,6 +114,9 @@ def parse(argv=None):
                         "(orbfe_debug_set_fast_wpb; default: the library's 4,1)")
     p.add_argument("--high-prio", default="side,match",
                    help="pipeline streams created at high priority: any of extract, side, match (default side,match)")
+    p.add_argument("--stage-calls", action="store_true",
+                   help="enqueue each sub-batch stage by stage from Python (~25 library calls) instead of "
+                        "one orbfe_c3_run call (include/orbfe_c3.h)")
     p.add_argument("--graphs", action="store_true",
                    help="replay each extraction's launch sequence from the handle's captured hipGraphs "
                         "(orbfe_extractor_set_graphs; off by default: 38.6k vs 83.7k stereo frames/s, round 5)")
@@ -145,6 +148,9 @@ def parse(argv=None):
                    help="--feed host: copy streams per sub-batch's H2D (2: two halves on two streams)")
     p.add_argument("--input-slots", type=int, default=0,
                    help="--feed host: device input slots (0: two per extractor handle)")
+    p.add_argument("--host-pin", choices=("torch", "register"), default="torch",
+                   help="--feed host: page-lock the host images with torch's pin_memory (hipHostMalloc) or "
+                        "register the numpy buffer in place (orbfe_host_register, hipHostRegister)")
     p.add_argument("--root-share", type=float, default=-1.0,
                    help="C4 (and --gather-proxy): the fraction of the per-rank sub-batches rank 0 extracts and "
                         "matches itself, since it also ingests every peer's payload; on the other slots it only "
@@ -342,9 +348,20 @@ class HostFeed:
     the link, not slot reuse, bounds the rate when 2B images take longer to copy than to process
     (round 4 tied the slots to the handles' pyramid events, R = 4: 45.8k stereo frames/s)."""
 
-    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0, copy_streams=1):
+    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0, copy_streams=1, pin="torch"):
         import torch
-        self.h = torch.from_numpy(host).pin_memory()
+        self.pin = pin
+        if pin == "register":  # the numpy buffer itself, page-aligned, registered with the runtime
+            from orb_slam2_2021_amd import _lib as L
+            raw = np.empty(host.nbytes + 4096, np.uint8)
+            off = (-raw.ctypes.data) % 4096
+            buf = raw[off:off + host.nbytes].view(host.dtype).reshape(host.shape)
+            buf[...] = host
+            L.check(L.lib().orbfe_host_register(ctypes.c_void_p(buf.ctypes.data), host.nbytes), "host_register")
+            self._raw = raw
+            self.h = torch.from_numpy(buf)
+        else:
+            self.h = torch.from_numpy(host).pin_memory()
         # --copy-streams 2: each sub-batch's images as two halves on two copy streams (the second
         # created here, after the pipeline's), joined by an event before the extraction's
         self.cs2 = [torch.cuda.Stream(dev) for _ in range(max(0, copy_streams - 1))]
@@ -395,7 +412,8 @@ class HostFeed:
     def describe(self, subbatches_per_s):
         gbs = self.bytes_per_subbatch * subbatches_per_s / 1e9
         return {"mode": "host", "h2d_bytes_per_subbatch": self.bytes_per_subbatch, "h2d_GBps": round(gbs, 2),
-                "device_slots": self.R, "copy_streams": 1 + len(self.cs2),
+                "device_slots": self.R, "copy_streams": 1 + len(self.cs2), "host_pin": self.pin,
+                "source_pinned": bool(self.h.is_pinned()),
                 "what": "every sub-batch's images H2D from pinned host memory on a copy stream of its own, "
                         "overlapped with the other sub-batches' kernels; outputs stay in HBM"}
 
@@ -506,7 +524,7 @@ def main():
     d_img = torch.from_numpy(host).to(dev)
     feed = None
     if args.feed == "host":
-        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots,
+        feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots, pin=args.host_pin,
                         copy_streams=args.copy_streams)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
@@ -548,7 +566,8 @@ def main():
             e.debug_set_octree_lds(hi, lo)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
-                           pairs=args.pairs, stereo_on_match=not args.stereo_on_extract)
+                           pairs=args.pairs, stereo_on_match=not args.stereo_on_extract,
+                           native=not (args.stage_calls or args.diag_skip_matching))
     if args.diag_skip_matching:  # diagnostic only: the extraction alone (not the metric's workload)
         def extract_only(o, after_match):
             m = o.mstream = pipe.mstream
@@ -592,12 +611,17 @@ def main():
         for k in range(S_sub):
             slot(k)
     torch.cuda.synchronize()
-    # host cost of enqueueing one sub-batch (untimed): 32 sub-batches right after a synchronize,
-    # while the device queues are still short enough that no launch blocks
-    th0 = time.perf_counter()
-    for _ in range(32):
+    # host cost of enqueueing one sub-batch (untimed): two sub-batches right after a synchronize,
+    # 24 times, the median -- the device queues stay short, so no launch blocks on a full queue (32
+    # back to back, rounds 3-5, could fill them: 88-197 us for the same code)
+    host_samples = []
+    for _ in range(24):
+        torch.cuda.synchronize()
+        th0 = time.perf_counter()
         sub_batch()
-    host_us = (time.perf_counter() - th0) / 32 * 1e6
+        sub_batch()
+        host_samples.append((time.perf_counter() - th0) / 2)
+    host_us = float(np.median(host_samples)) * 1e6
     torch.cuda.synchronize()
     # timed region: every kernel's launches on every n-th group of sub-batches timed by their own
     # dispatch interval (orbfe_ktimer: start / stop events bound to the dispatch, the interval
@@ -666,6 +690,9 @@ def main():
         if r["traffic"] is not None:  # per launch, like `achieved`: the sub-batch figure / its launches
             r["traffic_per_subbatch"] = r["traffic"]
             r["traffic"] = int(r["traffic"] / r["launches_per_subbatch"])
+        issue = pmc_issue(kname, r.get("avg_launch_us"), W, H, B, args)
+        if issue is not None:
+            r["issue"] = issue
         rooflines.append(r)
     roof = rooflines[0]
     roof["dominant_by"] = "device time per sub-batch, every kernel timed on the same sub-batches"
@@ -683,6 +710,8 @@ def main():
         "host_enqueue_ms_per_step": round(1e3 * (t_enq - t0) / args.steps, 4),
         "host_us_per_subbatch_unblocked": round(host_us, 1),
         "launch_graphs": dict(zip(("captures", "replays", "held"), ext.debug_graph_stats())),
+        "enqueue": ("one orbfe_c3_run call per sub-batch (include/orbfe_c3.h)" if pipe._c3 is not None
+                    else "per-stage library calls from Python (--stage-calls)"),
         **({"diagnostic": "matching skipped: extraction only, not the C3 metric"} if args.diag_skip_matching else {}),
         "higher_is_better": True,
         "scaling": "weak",
@@ -930,6 +959,38 @@ def pmc_traffic(kernel, W, H, B, args):
     if not k:
         return None, None
     return int(k["traffic_bytes_per_step"]), doc.get("source")
+
+
+SIMDS = 1024             # 256 CUs x 4 SIMD-32 (MI355X_MICROARCH.md)
+ISSUE_CLOCK_GHZ = 2.4    # max engine clock
+VALU_CYCLES_WAVE64 = 2   # a wave64 VALU instruction on a SIMD-32 with two or more waves resident
+
+
+def pmc_issue(kernel, avg_launch_us, W, H, B, args):
+    """The VALU-issue roof of `kernel` beside its HBM roof: SQ_INSTS_VALU per launch (committed
+    rocprofv3 PMC summary of this workload, profiles/pmc_waits.json from profiles/pmc_waits.py)
+    x 2 cycles / (1,024 SIMDs x 2.4 GHz x the launch time this run measured), with the PMC run's
+    wave-time split (issuing / ready but not issued / parked on waitcnt or barriers) and resident
+    waves per SIMD. None when no summary for this kernel and workload is committed."""
+    path = os.path.join(ROOT, "profiles", "pmc_waits.json")
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if doc.get("workload") != pmc_workload(W, H, B, args) or not avg_launch_us:
+        return None
+    k = doc.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    issue_us = k["insts_valu_per_launch"] * VALU_CYCLES_WAVE64 / (SIMDS * ISSUE_CLOCK_GHZ * 1e3)
+    return {"bound": "valu_issue", "valu_insts_per_launch": int(k["insts_valu_per_launch"]),
+            "issue_us_per_launch": round(issue_us, 2), "frac": round(issue_us / avg_launch_us, 4),
+            "wave_split": {"issuing": round(k["active"], 3), "ready_not_issued": round(k["wait_inst"], 3),
+                           "parked": round(k["wait_any"], 3)},
+            "waves_per_simd": round(k["waves_per_simd"], 2),
+            "formula": "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x avg_launch_us)",
+            "source": doc.get("source")}
 
 
 def pipeline_bytes_per_stereo_frame(geo, counts, B, n_pairs):

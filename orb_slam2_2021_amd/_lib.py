@@ -1,5 +1,5 @@
 """ctypes binding of liborbfe.so (include/orbfe.h, orbfe_match_batch.h, orbfe_debug.h, orbfe_synth.h,
-orbfe_vocab.h, orbfe_stereo.h, orbfe_frustum.h).
+orbfe_vocab.h, orbfe_stereo.h, orbfe_frustum.h, orbfe_keyframe.h, orbfe_pack.h, orbfe_c3.h).
 
 The shared library is the product: every compute call below runs the HIP kernels in it. There is
 no CPU fallback -- if the library is missing, or no HIP device is present when a compute handle is
@@ -89,6 +89,19 @@ class sft_pair(Structure):
                 ("fv2", feature_vector), ("f12", c_float * 9), ("ex", c_float), ("ey", c_float),
                 ("match12", c_void_p), ("nmatches", c_void_p), ("kf1_n_dev", c_void_p),
                 ("kf2_n_dev", c_void_p), ("fv1_nodes_dev", c_void_p), ("fv2_nodes_dev", c_void_p)]
+
+
+class c3_set(Structure):  # orbfe_c3.h
+    _fields_ = [("kps", c_void_p), ("desc", c_void_p), ("counts", c_void_p), ("fv_node_ids", c_void_p),
+                ("fv_offsets", c_void_p), ("fv_indices", c_void_p), ("fv_n_nodes", c_void_p),
+                ("bow_words", c_void_p), ("bow_weights", c_void_p), ("bow_n", c_void_p),
+                ("u_right", c_void_p), ("depth", c_void_p), ("matcher", c_void_p), ("pairs", c_void_p)]
+
+
+class c3_config(Structure):
+    _fields_ = [("n_images", c_int), ("rows", c_int), ("cols", c_int), ("cap", c_int), ("n_vocab", c_int),
+                ("levelsup", c_int), ("n_stereo", c_int), ("mbf", c_float), ("mb", c_float),
+                ("stereo_on_match", c_int), ("n_pairs", c_int)]
 
 
 # name -> (restype, argtypes)
@@ -233,6 +246,13 @@ _SIGNATURES = {
     "orbfe_compute_distinctive_descriptors_device": (c_int, [c_void_p, c_int, c_void_p, c_void_p,
                                                              c_void_p, c_void_p]),
     "orbfe_predict_scale_thresholds": (c_int, [c_float, c_int, c_void_p]),
+    # orbfe_c3.h
+    "orbfe_c3_create": (c_int, [POINTER(c3_config), c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                c_void_p, c_int, POINTER(c_void_p)]),
+    "orbfe_c3_run": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int]),
+    "orbfe_c3_finish": (c_int, [c_void_p, c_int, c_void_p]),
+    "orbfe_c3_match_stream": (c_void_p, [c_void_p, c_int]),
+    "orbfe_c3_destroy": (c_int, [c_void_p]),
 }
 
 # symbols declared in include/*.h (checked by tests/test_library.py)
@@ -250,7 +270,10 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
                 f"g.build()'` (or make -C orb_slam2_2021_amd/csrc)")
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        ab_build = "ORBFE_LIB" in os.environ  # an A/B build may predate newer entry points
         for name, (res, args) in _SIGNATURES.items():
+            if ab_build and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

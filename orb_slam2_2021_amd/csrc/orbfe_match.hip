@@ -273,18 +273,185 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
 }
 
+// Nodes past the fixpoint path's 128 features on either side but within SFT_BIG_MAX on both are
+// solved by a whole workgroup instead of one wavefront's sequential walk (which was the kernel's
+// critical path: ~130 dependent claim steps, each a wave-wide min). SFT_BIG_WG extra workgroups per
+// pair find the pair's big nodes (a thread per node, the same common-node lookup the wavefronts
+// do) and take every SFT_BIG_WG-th in node order. Per node: thread p stages KF2 candidate p in
+// LDS; thread i takes KF1 feature i, walks all candidates once (LDS broadcast reads) for its passing
+// set S_i (a bit mask) and its round-0 choice; then the claim order (:772-777) as the same fixpoint
+// as sft_node_fixpoint -- choice(i) = best of S_i minus the choices of the features before i --
+// with claim[p] = atomicMin over the choosers and a workgroup vote per round. The node's LDS
+// (15.3 KiB) aliases the wavefronts' 18 KiB, so the kernel's LDS does not grow.
+constexpr int SFT_BIG_MAX = 256;
+constexpr int SFT_BIG_WG = 2;
+constexpr int SFT_LDS_BYTES = 4 * (SFT_FP_MAX * 8 * 4 + SFT_FP_MAX * 4);  // 18 KiB
+__device__ __forceinline__ bool sft_big_node(int n1, int n2) {
+  return (n1 > SFT_FP_MAX || n2 > SFT_FP_MAX) && n1 <= SFT_BIG_MAX && n2 <= SFT_BIG_MAX;
+}
+struct SftBigLds {
+  uint4 desc[SFT_BIG_MAX][2];  // candidate descriptors (8 KiB)
+  float4 xye[SFT_BIG_MAX];     // x, y, 100 * scale[octave] (4 KiB)
+  double sig[SFT_BIG_MAX];     // 3.84 * sigma2[octave] (2 KiB)
+  int claim[SFT_BIG_MAX];      // first chooser per candidate (1 KiB)
+  uint8_t flags[SFT_BIG_MAX];  // 1 usable, 2 stereo
+  int list[2 * (256 / SFT_BIG_WG + 1)];  // this workgroup's big nodes of a 256-node chunk: (node, KF2 node)
+  int nlist;
+  int wave_cnt[4];
+};
+static_assert(sizeof(SftBigLds) <= SFT_LDS_BYTES, "the big-node LDS aliases the wavefronts' 18 KiB");
+
+// index of node id `id` among fv2's ascending node ids, -1 if absent
+__device__ __forceinline__ int sft_find_node(const orbfe_sft_pair& P, uint32_t id) {
+  int lo = 0, hi = P.fv2.n_nodes - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) >> 1;
+    const uint32_t v = P.fv2.node_ids[mid];
+    if (v == id) return mid;
+    if (v < id) lo = mid + 1;
+    else hi = mid - 1;
+  }
+  return -1;
+}
+
+__device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, SftBigLds& L) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const SftOctTab tab = sft_oct_tab(P);
+  const float* F = P.f12;
+  int base = 0;
+  for (int a0 = 0; a0 < P.fv1.n_nodes; a0 += 256) {
+  // 1. this workgroup's share of the chunk's big nodes, in node order
+    if (t == 0) L.nlist = 0;
+    const int a = a0 + t;
+    int pairv = -1;
+    if (a < P.fv1.n_nodes) {
+      const int n1 = P.fv1.offsets[a + 1] - P.fv1.offsets[a];
+      if (n1 > 0 && n1 <= SFT_BIG_MAX) {
+        const int q = sft_find_node(P, P.fv1.node_ids[a]);
+        if (q >= 0 && sft_big_node(n1, P.fv2.offsets[q + 1] - P.fv2.offsets[q])) pairv = q;
+      }
+    }
+    const uint64_t m = wave_ballot(pairv >= 0);
+    if (lane == 0) L.wave_cnt[w] = __popcll(m);
+    __syncthreads();
+    int rank = base + prefix_in_wave(m);
+    for (int k = 0; k < w; k++) rank += L.wave_cnt[k];
+    if (pairv >= 0 && rank % SFT_BIG_WG == b) {
+      const int slot = rank / SFT_BIG_WG - base / SFT_BIG_WG;  // < 256 / SFT_BIG_WG within the chunk
+      L.list[2 * slot] = a;
+      L.list[2 * slot + 1] = pairv;
+      atomicMax(&L.nlist, slot + 1);
+    }
+    base += L.wave_cnt[0] + L.wave_cnt[1] + L.wave_cnt[2] + L.wave_cnt[3];
+    __syncthreads();
+    const int nlist = L.nlist;
+  for (int e = 0; e < nlist; e++) {
+    const int a = L.list[2 * e], q = L.list[2 * e + 1];
+    const int o1 = P.fv1.offsets[a], n1 = P.fv1.offsets[a + 1] - o1;
+    const int o2 = P.fv2.offsets[q], n2 = P.fv2.offsets[q + 1] - o2;
+    // 2. candidates to LDS
+    {
+      SftCand c;
+      sft_load_cand(P, o2, n2, t, only_stereo, tab, c);
+      if (t < n2) {
+        L.desc[t][0] = c.d0;
+        L.desc[t][1] = c.d1;
+        L.xye[t] = make_float4(c.x, c.y, c.epi_thr, 0.f);
+        L.sig[t] = c.sig_thr;
+        L.flags[t] = (c.usable ? 1 : 0) | (c.stereo ? 2 : 0);
+      }
+    }
+    // 3. KF1 feature t
+    int idx1 = -1;
+    bool ok1 = false, st1 = false;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    float la = 0.f, lb = 0.f, lc = 0.f, den = 0.f;
+    if (t < n1) {
+      idx1 = P.fv1.indices[o1 + t];
+      st1 = P.kf1.u_right[idx1] >= 0;
+      ok1 = P.kf1.mp_state[idx1] == ORBFE_MP_NONE && !(only_stereo && !st1);
+      const orbfe_keypoint kp = P.kf1.keys_un[idx1];
+      load_desc(P.kf1.descriptors + (size_t)idx1 * 32, a0, a1);
+      la = kp.x * F[0] + kp.y * F[3] + F[6];  // CheckDistEpipolarLine :149-151
+      lb = kp.x * F[1] + kp.y * F[4] + F[7];
+      lc = kp.x * F[2] + kp.y * F[5] + F[8];
+      den = la * la + lb * lb;
+    }
+    __syncthreads();
+    // 4. passing set and round-0 choice: one pass over the candidates (uniform LDS reads)
+    uint64_t pm[SFT_BIG_MAX / 64] = {0, 0, 0, 0};
+    unsigned long long best = ~0ull;
+    if (ok1 && den != 0) {
+      for (int p = 0; p < n2; p++) {
+        if (!(L.flags[p] & 1)) continue;
+        const int dist = hamming256(a0, a1, L.desc[p][0], L.desc[p][1]);
+        if (dist > TH_LOW) continue;
+        const float4 c = L.xye[p];
+        if (!st1 && !(L.flags[p] & 2)) {
+          const float dex = P.ex - c.x, dey = P.ey - c.y;
+          if (dex * dex + dey * dey < c.z) continue;
+        }
+        const float num = la * c.x + lb * c.y + lc;
+        const float dsqr = num * num / den;
+        if (!((double)dsqr < L.sig[p])) continue;
+        pm[p >> 6] |= 1ull << (p & 63);
+        const unsigned long long key = ((unsigned long long)dist << 32) | (unsigned long long)(0x7fffffff - p);
+        best = key < best ? key : best;
+      }
+    }
+    int ch = best == ~0ull ? -1 : 0x7fffffff - (int)(best & 0xffffffffull);
+    // 5. the claim order as a fixpoint over the node's features (feature i final after i rounds)
+    for (int round = 0; round <= n1; round++) {
+      if (t < n2) L.claim[t] = 0x7fffffff;
+      __syncthreads();
+      if (ch >= 0) atomicMin(&L.claim[ch], t);
+      __syncthreads();
+      unsigned long long bk = ~0ull;
+#pragma unroll
+      for (int h = 0; h < SFT_BIG_MAX / 64; h++) {
+        uint64_t m = pm[h];
+        while (m) {
+          const int p = 64 * h + __builtin_ctzll(m);
+          m &= m - 1;
+          if (L.claim[p] < t) continue;  // vbMatched2: taken by an earlier feature of the node
+          const unsigned long long key = ((unsigned long long)hamming256(a0, a1, L.desc[p][0], L.desc[p][1]) << 32) |
+                                         (unsigned long long)(0x7fffffff - p);
+          bk = key < bk ? key : bk;
+        }
+      }
+      const int nk = bk == ~0ull ? -1 : 0x7fffffff - (int)(bk & 0xffffffffull);
+      const bool changed = nk != ch;
+      ch = nk;
+      if (!__syncthreads_or(changed)) break;
+    }
+    // 6. every feature of the node gets its final value (-1: no match)
+    if (t < n1) P.match12[idx1] = ch >= 0 ? P.fv2.indices[o2 + ch] : -1;
+    __syncthreads();  // the next node's candidates overwrite this one's
+  }
+  }
+}
+
 __global__ __launch_bounds__(256, 4) void k_sft_nodes(const orbfe_sft_pair* pairs, int only_stereo) {
   // per wave: the fixpoint path's node candidates, or the large-node path's claim bits beyond the
-  // register chunks (a wave takes one path; 18 KiB per workgroup in all)
+  // register chunks (a wave takes one path); a big-node workgroup's staging (SftBigLds) aliases
+  // the same 18 KiB
   static_assert(SFT_MAX_NODE / 32 <= SFT_FP_MAX * 8, "claim bits fit the candidate area");
-  __shared__ uint32_t s_fp_desc[4][SFT_FP_MAX * 8];
-  __shared__ int s_fp_claim[4][SFT_FP_MAX];
+  __shared__ uint4 s_lds[SFT_LDS_BYTES / 16];
+  uint32_t (*s_fp_desc)[SFT_FP_MAX * 8] = reinterpret_cast<uint32_t (*)[SFT_FP_MAX * 8]>(s_lds);
+  int (*s_fp_claim)[SFT_FP_MAX] = reinterpret_cast<int (*)[SFT_FP_MAX]>(
+      reinterpret_cast<uint8_t*>(s_lds) + 4 * SFT_FP_MAX * 8 * 4);
   // XCD-aware order: the workgroups of one pair run on one XCD, so its KeyFrames' keypoints,
   // descriptors and FeatureVectors are fetched into one L2 rather than eight
   const int2 blk = xcd_block2d();
   orbfe_sft_pair P = pairs[blk.y];
   sft_resolve_sizes(P);
-  if (blk.x == gridDim.x - 1) {
+  const int node_wgs = (int)gridDim.x - 1 - SFT_BIG_WG;
+  if (blk.x > node_wgs) {  // the big-node workgroups of the pair
+    if (P.kf2.n > SFT_MAX_KF2) return;
+    sft_big_nodes(P, only_stereo, blk.x - node_wgs - 1, *reinterpret_cast<SftBigLds*>(s_lds));
+    return;
+  }
+  if (blk.x == node_wgs) {
     // the last workgroup of a pair: KF1 features that no FeatureVector node lists -- a stopped
     // word (weight 0) is not added (TemplatedVocabulary.h:1198-1201) -- never match: -1. Disjoint
     // from the features the node wavefronts write, so no ordering is needed between them.
@@ -330,6 +497,7 @@ __global__ __launch_bounds__(256, 4) void k_sft_nodes(const orbfe_sft_pair* pair
     return;
   }
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
+  if (sft_big_node(e1 - o1, n2)) return;  // a big-node workgroup of the pair writes this node
   if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
     sft_node_fixpoint<2>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
@@ -1694,8 +1862,10 @@ extern "C" int orbfe_search_for_triangulation_batch_device(orbfe_matcher* m, int
   // fv1.n_nodes bounds the node grid (with fv1_nodes_dev set it must be an upper bound)
   int max_nodes = 1;
   for (int p = 0; p < n_pairs; p++) max_nodes = std::max(max_nodes, pairs[p].fv1.n_nodes);
-  // (max_nodes + 3) / 4 workgroups of node wavefronts + one for the features no node lists
-  ORBFE_LAUNCH("k_sft_nodes", k_sft_nodes, dim3((max_nodes + 3) / 4 + 1, n_pairs), dim3(256), 0, s, m->d_pairs,
+  // (max_nodes + 3) / 4 workgroups of node wavefronts + one for the features no node lists +
+  // SFT_BIG_WG for the nodes past the wavefront fixpoint
+  ORBFE_LAUNCH("k_sft_nodes", k_sft_nodes, dim3((max_nodes + 3) / 4 + 1 + SFT_BIG_WG, n_pairs), dim3(256), 0, s,
+               m->d_pairs,
                      only_stereo ? 1 : 0);
   ORBFE_LAUNCH("k_sft_finish", k_sft_finish, dim3(n_pairs), dim3(256), 0, s, m->d_pairs, m->check_ori);
   ORBFE_HIP_CHECK(hipGetLastError());

@@ -171,7 +171,7 @@ class C3Pipeline:
                  epipole: tuple, grid_inv: tuple, mb: float, u_right, mp_state, device,
                  depth: int = 2, levelsup: int = 4, stereo: bool = False, bow: bool = True,
                  nnratio: float = 0.6, check_ori: bool = False, streams=None, pairs: str = "stereo",
-                 stereo_on_match: bool = False):
+                 stereo_on_match: bool = False, native: bool = True):
         import torch
         from .matcher import ORBmatcher
         # one extractor, or several whose extractions of consecutive sub-batches overlap on their
@@ -301,6 +301,51 @@ class C3Pipeline:
         # the class default stays off for single-handle callers
         self.stereo_on_match = stereo and stereo_on_match and not self.match_inline
         self.stereo_done = [None] * len(self.exts)
+        # native: each sub-batch enqueued by one orbfe_c3_run call (include/orbfe_c3.h: the waits,
+        # the extraction, ComputeStereoMatches, the vocabulary transform, SearchForTriangulation and
+        # the ordering events from C++); otherwise the per-stage calls of run_stages() below.
+        # Same work, same streams, same order.
+        self._c3 = None
+        if native:
+            self._c3 = self._create_native()
+
+    def _create_native(self):
+        L_ = self.lib
+        cfg = L.c3_config(n_images=self.n_img, rows=self.H, cols=self.W, cap=self.cap, n_vocab=self.n_vocab,
+                          levelsup=self.levelsup, n_stereo=self.B if self.stereo else 0, mbf=float(self.cam["bf"]),
+                          mb=self.mb, stereo_on_match=1 if self.stereo_on_match else 0, n_pairs=self.n_pairs)
+        sets = (L.c3_set * len(self.sets))()
+        for i, o in enumerate(self.sets):
+            c = sets[i]
+            c.kps, c.desc, c.counts = o.kps.data_ptr(), o.desc.data_ptr(), o.cnt.data_ptr()
+            c.fv_node_ids, c.fv_offsets = o.ids.data_ptr(), o.offs.data_ptr()
+            c.fv_indices, c.fv_n_nodes = o.idx.data_ptr(), o.nodes.data_ptr()
+            if self.bow:
+                c.bow_words, c.bow_weights, c.bow_n = (o.bow_words.data_ptr(), o.bow_weights.data_ptr(),
+                                                       o.bow_n.data_ptr())
+            if self.stereo:
+                c.u_right, c.depth = o.ur.data_ptr(), o.dep.data_ptr()
+            c.matcher = o.matcher._h
+            c.pairs = ctypes.cast(o.pairs, ctypes.c_void_p)
+        exts = (ctypes.c_void_p * len(self.exts))(*[e._h for e in self.exts])
+        strs = (ctypes.c_void_p * len(self.streams))(*[st.cuda_stream for st in self.streams])
+        h = ctypes.c_void_p()
+        L.check(L_.orbfe_c3_create(ctypes.byref(cfg), exts, len(self.exts), strs, len(self.streams),
+                                   None if self.match_inline else ctypes.c_void_p(self.mstream.cuda_stream),
+                                   self.voc._h, sets, len(self.sets), ctypes.byref(h)), "orbfe_c3_create")
+        return h
+
+    def close(self):
+        """Destroy the native plan (waits for its events); the buffers stay the caller's."""
+        if getattr(self, "_c3", None):
+            self.lib.orbfe_c3_destroy(self._c3)
+            self._c3 = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     def next_handle(self):
         """The extractor handle the next run() extracts with."""
@@ -311,6 +356,34 @@ class C3Pipeline:
         `after_match(o)` runs on the matching stream after SearchForTriangulation (the C4 gather).
         `input_ready`: an event the extraction waits for first (the images' H2D copy of a host-fed
         pipeline). Returns the output set."""
+        if self._c3 is not None:
+            return self._run_native(d_img_ptr, after_match, input_ready)
+        return self.run_stages(d_img_ptr, after_match, input_ready)
+
+    def _run_native(self, d_img_ptr: int, after_match=None, input_ready=None):
+        si = self.counter % len(self.sets)
+        o = self.sets[si]
+        k = self.counter % len(self.exts)
+        self.counter += 1
+        s = self.streams[k % len(self.streams)]
+        L.check(self.lib.orbfe_c3_run(self._c3, si, k, ctypes.c_void_p(d_img_ptr),
+                                      input_ready._e if input_ready is not None else None,
+                                      1 if after_match is not None else 0), "orbfe_c3_run")
+        o.ext, o.k = self.exts[k], k
+        o.mstream = s if self.match_inline else self.mstream
+        self.last_stream = s
+        self.last = o
+        if self.match_inline:
+            self.mstream = s
+        if after_match is not None:  # the C4 pack + gather on the matching stream, then the set's event
+            o.released = None
+            after_match(o)
+            L.check(self.lib.orbfe_c3_finish(self._c3, si, o.released._e if o.released is not None else None),
+                    "orbfe_c3_finish")
+        return o
+
+    def run_stages(self, d_img_ptr: int, after_match=None, input_ready=None):
+        """run() as separate library calls per stage (the native plan's sequence, from Python)."""
         o = self.sets[self.counter % len(self.sets)]
         k = self.counter % len(self.exts)
         self.counter += 1
@@ -419,7 +492,7 @@ STEP_Z = 1.0  # metres between consecutive frames of the C3 driving sequence (SU
 
 def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, depth: int = 2,
              stereo: bool = False, levelsup: int = 4, streams=None, pairs: str = "stereo",
-             stereo_on_match: bool = False):
+             stereo_on_match: bool = False, native: bool = True):
     """The C3 scene of bench.py: KITTI intrinsics, seeded KeyFrame state per keypoint slot (half
     the keypoints stereo unless ComputeStereoMatches provides mvuRight, 30 % with a MapPoint), and
     the KeyFrame pair geometry with F12 and epipole from LocalMapping::ComputeF12
@@ -450,7 +523,7 @@ def build_c3(ext, tree, voc, B: int, H: int, W: int, device, seed: int = 1234, d
                       (float(dummy.grid_inv_w), float(dummy.grid_inv_h)), float(dummy.mb),
                       torch.from_numpy(ur).to(dev), torch.from_numpy(mp).to(dev), dev, depth=depth,
                       levelsup=levelsup, stereo=stereo, streams=streams, pairs=pairs,
-                      stereo_on_match=stereo_on_match)
+                      stereo_on_match=stereo_on_match, native=native)
     state = dict(u_right=ur, mp_state=mp, scale=scale, sigma2=sigma2, cam=cam, F12=F12,
                  epipole=(ex, ey), mb=float(dummy.mb), levelsup=levelsup, stereo=stereo, pairs=pairs)
     return pipe, state

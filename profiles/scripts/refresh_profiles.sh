@@ -24,6 +24,7 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/c5F -o run --output
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/c5W -o run --output-format csv -- python3 profiles/scripts/c5_only.py 5 > gpurun_out/c5W.log 2>&1 &&
 python3 profiles/pmc_c5_summary.py gpurun_out/c5F/run_counter_collection.csv gpurun_out/c5W/run_counter_collection.csv 81 gpurun_out/pmc_traffic_c5.json > /dev/null && cp gpurun_out/pmc_traffic_c5.json profiles/ &&
 timeout -s KILL 120 rocprofv3 --pmc $W -d gpurun_out/pmcWait -o run --output-format csv -- python3 bench.py $SMALL > gpurun_out/pmcWait.log 2>&1 &&
+python3 profiles/pmc_waits.py gpurun_out/pmcWait/run_counter_collection.csv --json gpurun_out/pmc_waits.json --workload '{"cols": 1241, "rows": 376, "batch": 32, "pairs": "kf", "stereo": true}' > gpurun_out/pmc_waits_contended.txt && cp gpurun_out/pmc_waits.json profiles/ &&
 timeout -s KILL 90 rocprofv3 --pmc $W --kernel-include-regex 'k_' -d gpurun_out/pmcAlone -o run --output-format csv -- python3 profiles/scripts/extract_only.py 5 --seq > gpurun_out/pmcAlone.log 2>&1
 ;;
 *) echo "usage: refresh_profiles.sh bench|pmc"; exit 2;;

@@ -71,15 +71,17 @@ def test_c3_batch32_bit_exact(require_gpu, vocab, pairs, stereo):
                           (False, True, 0, "stereo", False, 2, 0), (False, True, 1, "kf", True, 2, 0),
                           (True, True, 1, "kf", True, 2, 0), (False, True, 1, "kf", False, 2, 0),
                           (False, True, 1, "kf", True, 4, 0), (False, True, 1, "kf", True, 4, 4)])
+@pytest.mark.parametrize("native", [True, False])
 def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, blur_mode, pairs, stereo_on_match,
-                                     handles, fast_side):
+                                     handles, fast_side, native):
     """bench.py's schedules: extractor handles extract consecutive sub-batches on two extraction
     streams (handle k on stream k mod 2; side-stream work on one shared high-priority stream),
     matching on its own stream or inline after each extraction (then two vocabulary transforms run
     concurrently on the one handle: per-stream scratch), 4+ output sets; ComputeStereoMatches on the
     matching stream (with 2 handles the handle's next extraction waits for it; with 4 -- bench.py's
     default -- nothing waits) or right after the extraction. fast_side 4: FAST of levels 0-3 on the
-    shared side stream, bench.py's setting (0 keeps the library default, 3)."""
+    shared side stream, bench.py's setting (0 keeps the library default, 3). native: each sub-batch
+    enqueued by one orbfe_c3_run call (include/orbfe_c3.h), or stage by stage from Python."""
     import torch
     from orb_slam2_2021_amd.pipeline import PipelineStreams
     tree, voc, ref = vocab
@@ -91,7 +93,8 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
             e.debug_set_fast_side_levels(fast_side)
     streams = PipelineStreams(0, 2, match_inline=match_inline)
     pipe, st = build_c3(exts, tree, voc, B, H, W, 0, stereo=stereo, depth=4, streams=streams, pairs=pairs,
-                        stereo_on_match=stereo_on_match)
+                        stereo_on_match=stereo_on_match, native=native)
+    assert (pipe._c3 is not None) == native
     batches = [frames(B, 0, pairs), frames(B, 1000, pairs), frames(B, 2000, pairs)]
     d = [torch.from_numpy(b).to("cuda") for b in batches]
     nsets = len(pipe.sets)
@@ -103,6 +106,7 @@ def test_c3_two_extractors_bit_exact(require_gpu, vocab, match_inline, stereo, b
         r = check_c3(batches[j % 3], out, ref, st["u_right"], st["mp_state"], st["scale"], st["sigma2"],
                      st["cam"], st["F12"], st["epipole"], levelsup=4, stereo=stereo, mb=st["mb"], pairs=pairs)
         assert r["all"], (j, r)
+    pipe.close()
     streams.close()
 
 

@@ -95,6 +95,12 @@ def test_bad_arguments_rejected_without_device():
     assert lib.orbfe_pack_keypoints_device(1 << 16, one, one, one, 1 << 15, one, c_size_t(1 << 62), one,
                                            None) == L.ORBFE_ERR_ARG
     assert b"2^31" in lib.orbfe_last_error()
+    # the one-call C3 plan (orbfe_c3.h) checks its configuration before touching a device
+    cfg = L.c3_config(n_images=64, rows=376, cols=1241, cap=2048, n_vocab=32, levelsup=4, n_stereo=32)
+    assert lib.orbfe_c3_create(byref(cfg), None, 0, None, 0, None, None, None, 0, byref(h)) == L.ORBFE_ERR_ARG
+    assert lib.orbfe_c3_run(None, 0, 0, one, None, 0) == L.ORBFE_ERR_ARG
+    assert lib.orbfe_c3_finish(None, 0, None) == L.ORBFE_ERR_ARG
+    assert lib.orbfe_c3_destroy(None) == L.ORBFE_OK
 
 
 def test_product_never_imports_the_oracle():
