@@ -273,21 +273,23 @@ __device__ __forceinline__ void sft_node_fixpoint(const orbfe_sft_pair& P, int o
     if (64 * k + lane < n1) P.match12[idx1[k]] = ch[k] >= 0 ? P.fv2.indices[o2 + ch[k]] : -1;
 }
 
-// Nodes past the fixpoint path's 128 features on either side but within SFT_BIG_MAX on both are
-// solved by a whole workgroup instead of one wavefront's sequential walk (which was the kernel's
-// critical path: ~130 dependent claim steps, each a wave-wide min). SFT_BIG_WG extra workgroups per
+// Nodes past 64 features on either side but within SFT_BIG_MAX on both are solved by a whole
+// workgroup instead of one wavefront (whose sequential walk of a 133-feature node, ~130 dependent
+// claim steps each a wave-wide min, was the kernel's critical path, and whose 2-per-lane fixpoint
+// walks a 100-feature node's candidates with two keys per step). SFT_BIG_WG extra workgroups per
 // pair find the pair's big nodes (a thread per node, the same common-node lookup the wavefronts
 // do) and take every SFT_BIG_WG-th in node order. Per node: thread p stages KF2 candidate p in
-// LDS; thread i takes KF1 feature i, walks all candidates once (LDS broadcast reads) for its passing
-// set S_i (a bit mask) and its round-0 choice; then the claim order (:772-777) as the same fixpoint
-// as sft_node_fixpoint -- choice(i) = best of S_i minus the choices of the features before i --
-// with claim[p] = atomicMin over the choosers and a workgroup vote per round. The node's LDS
-// (15.3 KiB) aliases the wavefronts' 18 KiB, so the kernel's LDS does not grow.
+// LDS; KF1 feature i is taken by lane i % 64 of one wavefront, or of two when n1 <= 128 (each then
+// walks every other candidate, and the halves' passing bits and best keys are merged through LDS),
+// for its passing set S_i (a bit mask) and its round-0 choice; then the claim order (:772-777) as
+// the same fixpoint as sft_node_fixpoint -- choice(i) = best of S_i minus the choices of the
+// features before i -- with claim[p] = atomicMin over the choosers and a workgroup vote per round.
+// The node's LDS (15.9 KiB) aliases the wavefronts' 18 KiB, so the kernel's LDS does not grow.
 constexpr int SFT_BIG_MAX = 256;
 constexpr int SFT_BIG_WG = 2;
 constexpr int SFT_LDS_BYTES = 4 * (SFT_FP_MAX * 8 * 4 + SFT_FP_MAX * 4);  // 18 KiB
 __device__ __forceinline__ bool sft_big_node(int n1, int n2) {
-  return (n1 > SFT_FP_MAX || n2 > SFT_FP_MAX) && n1 <= SFT_BIG_MAX && n2 <= SFT_BIG_MAX;
+  return (n1 > 64 || n2 > 64) && n1 <= SFT_BIG_MAX && n2 <= SFT_BIG_MAX;
 }
 struct SftBigLds {
   uint4 desc[SFT_BIG_MAX][2];  // candidate descriptors (8 KiB)
@@ -300,6 +302,12 @@ struct SftBigLds {
   int wave_cnt[4];
 };
 static_assert(sizeof(SftBigLds) <= SFT_LDS_BYTES, "the big-node LDS aliases the wavefronts' 18 KiB");
+struct SftMerge {  // one feature's passing bits and best key from its second wavefront
+  uint64_t pm[SFT_BIG_MAX / 64];
+  unsigned long long best;
+};
+static_assert(128 * sizeof(SftMerge) <= sizeof(float4) * SFT_BIG_MAX + sizeof(double) * SFT_BIG_MAX,
+              "the merge slots of 128 features fit the candidates' xye + sig");
 
 // index of node id `id` among fv2's ascending node ids, -1 if absent
 __device__ __forceinline__ int sft_find_node(const orbfe_sft_pair& P, uint32_t id) {
@@ -361,13 +369,16 @@ __device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, S
         L.flags[t] = (c.usable ? 1 : 0) | (c.stereo ? 2 : 0);
       }
     }
-    // 3. KF1 feature t
+    // 3. KF1 feature i of this thread: features in 64-lane chunks; with n1 <= 128 two wavefronts
+    //    share a chunk (g = 0 / 1), each walking every other candidate, so all four wavefronts work
+    const int G = n1 <= 128 ? 2 : 1, nchunk = 4 / G;
+    const int chunk = w % nchunk, g = w / nchunk, i = 64 * chunk + lane;
     int idx1 = -1;
     bool ok1 = false, st1 = false;
     uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
     float la = 0.f, lb = 0.f, lc = 0.f, den = 0.f;
-    if (t < n1) {
-      idx1 = P.fv1.indices[o1 + t];
+    if (i < n1) {
+      idx1 = P.fv1.indices[o1 + i];
       st1 = P.kf1.u_right[idx1] >= 0;
       ok1 = P.kf1.mp_state[idx1] == ORBFE_MP_NONE && !(only_stereo && !st1);
       const orbfe_keypoint kp = P.kf1.keys_un[idx1];
@@ -378,11 +389,12 @@ __device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, S
       den = la * la + lb * lb;
     }
     __syncthreads();
-    // 4. passing set and round-0 choice: one pass over the candidates (uniform LDS reads)
+    // 4. passing set and round-0 choice: one pass over this thread's candidates p = g, g + G, ...
+    //    (uniform LDS reads)
     uint64_t pm[SFT_BIG_MAX / 64] = {0, 0, 0, 0};
     unsigned long long best = ~0ull;
     if (ok1 && den != 0) {
-      for (int p = 0; p < n2; p++) {
+      for (int p = g; p < n2; p += G) {
         if (!(L.flags[p] & 1)) continue;
         const int dist = hamming256(a0, a1, L.desc[p][0], L.desc[p][1]);
         if (dist > TH_LOW) continue;
@@ -399,24 +411,40 @@ __device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, S
         best = key < best ? key : best;
       }
     }
-    int ch = best == ~0ull ? -1 : 0x7fffffff - (int)(best & 0xffffffffull);
+    if (G == 2) {  // the g = 1 half's passing bits and best key join the g = 0 thread of the feature
+      __syncthreads();  // (the merge slots alias the candidates' xye / sig, read until here)
+      SftMerge* mg = reinterpret_cast<SftMerge*>(&L.xye[0]);
+      if (g == 1) mg[i] = SftMerge{{pm[0], pm[1], pm[2], pm[3]}, best};
+      __syncthreads();
+      if (g == 0) {
+        const SftMerge o = mg[i];
+#pragma unroll
+        for (int h = 0; h < SFT_BIG_MAX / 64; h++) pm[h] |= o.pm[h];
+        best = o.best < best ? o.best : best;
+      }
+    }
+    const bool owner = g == 0 && i < n1;  // the thread that carries feature i from here on
+    int ch = !owner || best == ~0ull ? -1 : 0x7fffffff - (int)(best & 0xffffffffull);
     // 5. the claim order as a fixpoint over the node's features (feature i final after i rounds)
     for (int round = 0; round <= n1; round++) {
       if (t < n2) L.claim[t] = 0x7fffffff;
       __syncthreads();
-      if (ch >= 0) atomicMin(&L.claim[ch], t);
+      if (ch >= 0) atomicMin(&L.claim[ch], i);
       __syncthreads();
       unsigned long long bk = ~0ull;
+      if (owner) {
 #pragma unroll
-      for (int h = 0; h < SFT_BIG_MAX / 64; h++) {
-        uint64_t m = pm[h];
-        while (m) {
-          const int p = 64 * h + __builtin_ctzll(m);
-          m &= m - 1;
-          if (L.claim[p] < t) continue;  // vbMatched2: taken by an earlier feature of the node
-          const unsigned long long key = ((unsigned long long)hamming256(a0, a1, L.desc[p][0], L.desc[p][1]) << 32) |
-                                         (unsigned long long)(0x7fffffff - p);
-          bk = key < bk ? key : bk;
+        for (int h = 0; h < SFT_BIG_MAX / 64; h++) {
+          uint64_t m = pm[h];
+          while (m) {
+            const int p = 64 * h + __builtin_ctzll(m);
+            m &= m - 1;
+            if (L.claim[p] < i) continue;  // vbMatched2: taken by an earlier feature of the node
+            const unsigned long long key =
+                ((unsigned long long)hamming256(a0, a1, L.desc[p][0], L.desc[p][1]) << 32) |
+                (unsigned long long)(0x7fffffff - p);
+            bk = key < bk ? key : bk;
+          }
         }
       }
       const int nk = bk == ~0ull ? -1 : 0x7fffffff - (int)(bk & 0xffffffffull);
@@ -425,7 +453,7 @@ __device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, S
       if (!__syncthreads_or(changed)) break;
     }
     // 6. every feature of the node gets its final value (-1: no match)
-    if (t < n1) P.match12[idx1] = ch >= 0 ? P.fv2.indices[o2 + ch] : -1;
+    if (owner) P.match12[idx1] = ch >= 0 ? P.fv2.indices[o2 + ch] : -1;
     __syncthreads();  // the next node's candidates overwrite this one's
   }
   }
@@ -498,8 +526,8 @@ __global__ __launch_bounds__(256, 4) void k_sft_nodes(const orbfe_sft_pair* pair
   }
   const int o2 = P.fv2.offsets[lo], n2 = P.fv2.offsets[lo + 1] - o2;
   if (sft_big_node(e1 - o1, n2)) return;  // a big-node workgroup of the pair writes this node
-  if (e1 - o1 <= SFT_FP_MAX && n2 <= SFT_FP_MAX) {
-    sft_node_fixpoint<2>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
+  if (e1 - o1 <= 64 && n2 <= 64) {
+    sft_node_fixpoint<1>(P, o1, e1 - o1, o2, n2, only_stereo, s_fp_desc[w], s_fp_claim[w]);
     return;
   }
   // large nodes: -1 first, stored before the walk's matches overwrite some of them (the wait
