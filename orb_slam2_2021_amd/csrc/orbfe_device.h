@@ -102,9 +102,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__device__ inline int block_scan_excl(int* data, int n, int* wsum) {
+// Exclusive scan of data[0..n) in LDS by the NT threads of the block (wsum: NT / 64 ints).
+template <int NT>
+__device__ inline int block_scan_excl_n(int* data, int n, int* wsum) {
+  constexpr int NW = NT / 64;
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int per = (n + 255) / 256;
+  const int per = (n + NT - 1) / NT;
   const int beg = min(t * per, n), end = min(beg + per, n);
   int s = 0;
   for (int i = beg; i < end; i++) s += data[i];
@@ -116,9 +119,12 @@ __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
   }
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  int woff = 0;
-  for (int k = 0; k < w; k++) woff += wsum[k];
-  const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int woff = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    woff += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
   int run = woff + inc - s;
   for (int i = beg; i < end; i++) {
     const int v = data[i];
@@ -128,9 +134,12 @@ __device__ inline int block_scan_excl(int* data, int n, int* wsum) {
   __syncthreads();
   return total;
 }
+__device__ inline int block_scan_excl(int* data, int n, int* wsum) { return block_scan_excl_n<256>(data, n, wsum); }
 
-// Three exclusive scans at once (one pair of barriers instead of three); wsum holds 12 ints.
-__device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum) {
+// Three exclusive scans at once (one pair of barriers instead of three); wsum holds 3 x NT / 64 ints.
+template <int NT>
+__device__ inline int3 block_scan_excl3_n(int* a, int* b, int* c, int n, int* wsum) {
+  constexpr int NW = NT / 64;
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
   if (n <= 64) {  // (n is block-uniform) one wavefront scans, one barrier publishes
     if (w == 0) {
@@ -159,7 +168,7 @@ __device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum
     __syncthreads();
     return make_int3(wsum[0], wsum[1], wsum[2]);
   }
-  const int per = (n + 255) / 256;
+  const int per = (n + NT - 1) / NT;
   const int beg = min(t * per, n), end = min(beg + per, n);
   int sa = 0, sb = 0, sc = 0;
   for (int i = beg; i < end; i++) {
@@ -179,18 +188,23 @@ __device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum
   }
   if (lane == 63) {
     wsum[w] = ia;
-    wsum[4 + w] = ib;
-    wsum[8 + w] = ic;
+    wsum[NW + w] = ib;
+    wsum[2 * NW + w] = ic;
   }
   __syncthreads();
-  int oa = 0, ob = 0, oc = 0;
-  for (int k = 0; k < w; k++) {
-    oa += wsum[k];
-    ob += wsum[4 + k];
-    oc += wsum[8 + k];
+  int oa = 0, ob = 0, oc = 0, ta = 0, tb = 0, tc = 0;
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    const int xa = wsum[k], xb = wsum[NW + k], xc = wsum[2 * NW + k];
+    if (k < w) {
+      oa += xa;
+      ob += xb;
+      oc += xc;
+    }
+    ta += xa;
+    tb += xb;
+    tc += xc;
   }
-  const int3 tot = make_int3(wsum[0] + wsum[1] + wsum[2] + wsum[3], wsum[4] + wsum[5] + wsum[6] + wsum[7],
-                             wsum[8] + wsum[9] + wsum[10] + wsum[11]);
   int ra = oa + ia - sa, rb = ob + ib - sb, rc = oc + ic - sc;
   for (int i = beg; i < end; i++) {
     const int va = a[i], vb = b[i], vc = c[i];
@@ -202,7 +216,10 @@ __device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum
     rc += vc;
   }
   __syncthreads();
-  return tot;
+  return make_int3(ta, tb, tc);
+}
+__device__ inline int3 block_scan_excl3(int* a, int* b, int* c, int n, int* wsum) {
+  return block_scan_excl3_n<256>(a, b, c, n, wsum);
 }
 
 // Exclusive scan of data[0..n) in LDS by the 1024 threads of the block (wsum: 16 ints).

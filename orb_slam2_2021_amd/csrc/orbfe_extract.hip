@@ -999,6 +999,10 @@ __global__ __launch_bounds__(512) void k_fast(ExtractArgs a, int cell0, int cell
 //   reverse(children of the divided nodes, in processing order) ++ (old list minus divided).
 // Both are computed with block scans; each node's keys stay one contiguous segment, partitioned
 // stably by one wavefront per divided node (ballot + popcount).
+// k_octree's LDS scalars: wave sums of the block scans in misc[0 .. NW), scalars from
+// misc[OCT_MISC_SCALAR]; OCT_MISC_INTS ints in all (up to 16 wavefronts: 1024 threads)
+#define OCT_MISC_SCALAR 16
+#define OCT_MISC_INTS 32
 struct ONode {
   int16_t x0, y0, x1, y1;
   int32_t begin, count, seq, flags;  // flags: bit0 = key buffer (0: A, 1: B), bit1 = in R set
@@ -1213,10 +1217,10 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
 }
 
 // The nodes of list positions [0, m) (position p -> node index idx(p)) holding more than OCT_SMALL
-// keys, dealt round-robin over the block's 4 wavefronts in position order: each wavefront reads the
+// keys, dealt round-robin over the block's NW wavefronts in position order: each wavefront reads the
 // counts of 64 positions at a time (one LDS read per lane) and walks the ballot of the big ones, so
 // no wavefront steps through the small nodes one dependent read at a time.
-template <typename Idx, typename F>
+template <int NW, typename Idx, typename F>
 __device__ __forceinline__ void for_big_nodes(const ONode* L, int m, Idx idx, F f) {
   const int w = wave_id(), lane = lane_id();
   int ord = 0;
@@ -1227,7 +1231,7 @@ __device__ __forceinline__ void for_big_nodes(const ONode* L, int m, Idx idx, F 
     while (bal) {
       const int b = __builtin_ctzll(bal);
       bal &= bal - 1;
-      if ((ord & 3) == w) f(c0 + b);
+      if (ord % NW == w) f(c0 + b);
       ord++;
     }
   }
@@ -1255,9 +1259,10 @@ __device__ unsigned long long g_oct_prof[64 * 16 * 16];
 #define OCT_PMARK(k, v) do { } while (0)
 #endif
 
-template <bool LDSK>
+template <bool LDSK, int NT>
 __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, int l, int n, uint32_t* ka,
                                            uint32_t* kb) {
+  constexpr int NW = NT / 64;
   const int img = blockIdx.y;
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
   const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
@@ -1268,7 +1273,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   int* sb = sa + SA;
   int* sx = sb + SA;
   unsigned long long* sk = reinterpret_cast<unsigned long long*>(sx + SA);
-  int* misc = reinterpret_cast<int*>(sk + SC);  // [0..3] scan wave sums, [8..] scalars
+  int* misc = reinterpret_cast<int*>(sk + SC);  // [0..NW) scan wave sums, [OCT_MISC_SCALAR..] scalars
   const LevelDesc ld = a.levels[l];
   const int N = ld.budget;
   const uint32_t* cand = a.cand + (long long)img * a.cand_stride;
@@ -1279,7 +1284,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   //    sa = exclusive prefix of the cell counts, sx = cell slots (filled by the caller); a thread
   //    per cell copies the cell's keys, four loads in flight
   const int ncells = ld.ncells;
-  for (int c = t; c < ncells; c += 256) {
+  for (int c = t; c < ncells; c += NT) {
     const int b0 = sa[c], cnt = (c + 1 < ncells ? sa[c + 1] : n) - b0;
     const uint32_t* src = cand + sx[c];
     int k = 0;
@@ -1307,13 +1312,13 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     for (int k = 1; k < 8; k++) b += (k < nini && x >= ld.ini_thr[k]) ? 1 : 0;
     return b;
   };
-  int* bcnt = reinterpret_cast<int*>(sk);  // [4][nini] counts, then [4][nini] offsets
-  int* boff = bcnt + 4 * nini;
-  const int R = ((n + 3) / 4 + 63) & ~63;
+  int* bcnt = reinterpret_cast<int*>(sk);  // [NW][nini] counts, then [NW][nini] offsets
+  int* boff = bcnt + NW * nini;
+  const int R = ((n + NW - 1) / NW + 63) & ~63;
   const int wbeg = min(w * R, n), wend = min(wbeg + R, n);
   // the wave's keys and their initial nodes stay in registers for both walks (one LDS read and one
   // bucket per key) when the quarter has at most 64 * INI_J keys
-  constexpr int INI_J = 24;
+  constexpr int INI_J = NT >= 1024 ? 8 : 24;  // (16 wavefronts: 8 rows cache 8,192 keys)
   const bool cached = wend - wbeg <= 64 * INI_J;
   uint32_t kr[INI_J];
   int br[INI_J];
@@ -1367,7 +1372,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     int run = 0;
     for (int bkt = 0; bkt < nini; bkt++) {
       sb[bkt] = 0;
-      for (int ww = 0; ww < 4; ww++) {
+      for (int ww = 0; ww < NW; ww++) {
         boff[ww * nini + bkt] = run;
         run += bcnt[ww * nini + bkt];
         sb[bkt] += bcnt[ww * nini + bkt];
@@ -1420,11 +1425,11 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       }
       run += cnt;
     }
-    misc[8] = S;
+    misc[OCT_MISC_SCALAR] = S;
   }
   __syncthreads();
 
-  int S = misc[8];
+  int S = misc[OCT_MISC_SCALAR];
   int cur = 0;
   bool refine = false;
   OCT_MARK(3, wall_clock64());
@@ -1441,7 +1446,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       // ---- full pass (:603-668) ----
       // each node's split and its scan inputs by whoever splits it (a thread for <= OCT_SMALL
       // keys, a wavefront above): children (sa), kept single-key nodes (sb), multi-key children (sx)
-      for (int i = t; i < S; i += 256) {
+      for (int i = t; i < S; i += NT) {
         const ONode nd = Lc[i];
         if (nd.count > OCT_SMALL) continue;
         const bool par = nd.count > 1;
@@ -1455,7 +1460,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
 #ifdef ORBFE_OCT_PROF_PASS
       unsigned long long split_cyc = 0, split_n = 0;
 #endif
-      for_big_nodes(Lc, S, [](int p) { return p; }, [&](int i) {
+      for_big_nodes<NW>(Lc, S, [](int p) { return p; }, [&](int i) {
 #ifdef ORBFE_OCT_PROF_PASS
         const unsigned long long c0 = clock64();
         const int4 c4 = wave_child_split(Lc[i], ka, kb);
@@ -1482,13 +1487,13 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       if (n_passes == 1) OCT_MARK(14, wall_clock64());
 #endif
       // (sk is free during full passes: its first 12 ints hold the scan's wave sums)
-      const int3 tot3 = block_scan_excl3(sa, sb, sx, S, reinterpret_cast<int*>(sk));
+      const int3 tot3 = block_scan_excl3_n<NT>(sa, sb, sx, S, reinterpret_cast<int*>(sk));
 #ifndef ORBFE_OCT_PROF_PASS
       if (n_passes == 1) OCT_MARK(15, wall_clock64());
 #endif
       OCT_PMARK(11, wall_clock64());
       const int T = tot3.x, NP = tot3.y, nexp = tot3.z;
-      for (int i = t; i < S; i += 256) {
+      for (int i = t; i < S; i += NT) {
         const ONode nd = Lc[i];
         if (nd.count > 1) {
           const int4 c4 = cc[i];
@@ -1518,17 +1523,17 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     } else {
       if (n_rounds++ == 0) OCT_MARK(4, wall_clock64());
       // ---- refinement round (:679-740) ----
-      for (int i = t; i < S; i += 256) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
+      for (int i = t; i < S; i += NT) sa[i] = (Lc[i].flags & 2) ? 1 : 0;
       __syncthreads();
-      const int nR = block_scan_excl(sa, S, misc);
+      const int nR = block_scan_excl_n<NT>(sa, S, misc);
       if (n_rounds == 1) OCT_RMARK(8, wall_clock64());
       int P2 = 1;
       while (P2 < nR) P2 <<= 1;
       if (nR > 1024) {
-        for (int i = t; i < P2; i += 256) sk[i] = 0ull;
+        for (int i = t; i < P2; i += NT) sk[i] = 0ull;
         __syncthreads();
       }
-      for (int i = t; i < S; i += 256) {
+      for (int i = t; i < S; i += NT) {
         const ONode nd = Lc[i];
         if (nd.flags & 2)
           sk[sa[i]] = ((unsigned long long)nd.count << 40) | ((unsigned long long)nd.seq << 20) |
@@ -1539,22 +1544,23 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         // rank sort, descending (largest (size, creation) first; the keys are distinct): every
         // key counts the larger ones with broadcast LDS reads -- two barriers instead of a
         // bitonic network's log^2
-        unsigned long long kk[4];
-        int rk[4];
+        constexpr int RP = (1024 + NT - 1) / NT;  // keys per thread
+        unsigned long long kk[RP];
+        int rk[RP];
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int k = t + 256 * r;
+        for (int r = 0; r < RP; r++) {
+          const int k = t + NT * r;
           kk[r] = k < nR ? sk[k] : 0ull;
           rk[r] = 0;
         }
-        const int per = (nR + 255) >> 8;
+        const int per = (nR + NT - 1) / NT;
         int j = 0;
         for (; j + 16 <= nR; j += 16) {  // sixteen broadcast reads in flight
           unsigned long long y[16];
 #pragma unroll
           for (int q = 0; q < 16; q++) y[q] = sk[j + q];
 #pragma unroll
-          for (int r = 0; r < 4; r++)
+          for (int r = 0; r < RP; r++)
             if (r == 0 || per > r) {
 #pragma unroll
               for (int q = 0; q < 16; q++) rk[r] += y[q] > kk[r];
@@ -1562,21 +1568,20 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
         }
         for (; j < nR; j++) {
           const unsigned long long y = sk[j];
-          rk[0] += y > kk[0];
-          if (per > 1) rk[1] += y > kk[1];
-          if (per > 2) rk[2] += y > kk[2];
-          if (per > 3) rk[3] += y > kk[3];
+#pragma unroll
+          for (int r = 0; r < RP; r++)
+            if (r == 0 || per > r) rk[r] += y > kk[r];
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-          if (t + 256 * r < nR) sk[rk[r]] = kk[r];
+        for (int r = 0; r < RP; r++)
+          if (t + NT * r < nR) sk[rk[r]] = kk[r];
         __syncthreads();
       } else {
         // bitonic sort, descending: largest (size, creation) first
         for (int k = 2; k <= P2; k <<= 1) {
           for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int pidx = t; pidx < (P2 >> 1); pidx += 256) {
+            for (int pidx = t; pidx < (P2 >> 1); pidx += NT) {
               const int i = ((pidx & ~(j - 1)) << 1) | (pidx & (j - 1)), ixj = i + j;  // j is a power of 2
               const unsigned long long x = sk[i], y = sk[ixj];
               if ((i & k) == 0 ? (x < y) : (x > y)) {
@@ -1590,47 +1595,47 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       }
       if (n_rounds == 1) OCT_RMARK(9, wall_clock64());
       // child counts of every candidate, in processing order
-      for (int k = t; k < nR; k += 256) {
+      for (int k = t; k < nR; k += NT) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
         if (nd.count <= OCT_SMALL) cc[k] = serial_child_counts(nd, ka, kb);
       }
-      for_big_nodes(Lc, nR, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+      for_big_nodes<NW>(Lc, nR, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
         const int4 c4 = wave_child_counts(Lc[(int)(sk[k] & 0xfffffull)], ka, kb);
         if (lane == 0) cc[k] = c4;
       });
       __syncthreads();
       if (n_rounds == 1) OCT_RMARK(10, wall_clock64());
-      for (int k = t; k < nR; k += 256) sa[k] = nonempty4(cc[k]) - 1;
-      if (t == 0) misc[9] = nR;
+      for (int k = t; k < nR; k += NT) sa[k] = nonempty4(cc[k]) - 1;
+      if (t == 0) misc[OCT_MISC_SCALAR + 1] = nR;
       __syncthreads();
-      block_scan_excl(sa, nR, misc);
-      for (int k = t; k < nR; k += 256) {
+      block_scan_excl_n<NT>(sa, nR, misc);
+      for (int k = t; k < nR; k += NT) {
         const int incl = sa[k] + nonempty4(cc[k]) - 1;
-        if (prevS + incl >= N) atomicMin(&misc[9], k + 1);  // break at the first k reaching N
+        if (prevS + incl >= N) atomicMin(&misc[OCT_MISC_SCALAR + 1], k + 1);  // break at the first k reaching N
       }
       __syncthreads();
-      const int nproc = misc[9];
+      const int nproc = misc[OCT_MISC_SCALAR + 1];
       if (n_rounds == 1) OCT_RMARK(11, wall_clock64());
-      for (int i = t; i < S; i += 256) sb[i] = -1;
+      for (int i = t; i < S; i += NT) sb[i] = -1;
       __syncthreads();
-      for (int k = t; k < nproc; k += 256) sb[(int)(sk[k] & 0xfffffull)] = k;
+      for (int k = t; k < nproc; k += NT) sb[(int)(sk[k] & 0xfffffull)] = k;
       __syncthreads();
       // partition the divided nodes' keys
-      for (int k = t; k < nproc; k += 256) {
+      for (int k = t; k < nproc; k += NT) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
         if (nd.count <= OCT_SMALL) serial_child_partition(nd, cc[k], ka, kb);
       }
-      for_big_nodes(Lc, nproc, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+      for_big_nodes<NW>(Lc, nproc, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
         wave_child_partition(Lc[(int)(sk[k] & 0xfffffull)], cc[k], ka, kb);
       });
-      for (int k = t; k < nR; k += 256) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
+      for (int k = t; k < nR; k += NT) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
       __syncthreads();
       if (n_rounds == 1) OCT_RMARK(12, wall_clock64());
-      const int T = block_scan_excl(sx, nR, misc);
-      for (int i = t; i < S; i += 256) sa[i] = sb[i] < 0 ? 1 : 0;
+      const int T = block_scan_excl_n<NT>(sx, nR, misc);
+      for (int i = t; i < S; i += NT) sa[i] = sb[i] < 0 ? 1 : 0;
       __syncthreads();
-      const int NK = block_scan_excl(sa, S, misc);
-      for (int i = t; i < S; i += 256) {
+      const int NK = block_scan_excl_n<NT>(sa, S, misc);
+      for (int i = t; i < S; i += NT) {
         const ONode nd = Lc[i];
         const int k = sb[i];
         if (k >= 0) {
@@ -1662,7 +1667,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   if (n_rounds == 0) OCT_MARK(4, wall_clock64());
   // 3. retain the best key of every node, in list order (:744-763; strict '>' keeps the first)
   ONode* Lf = cur ? nodes1 : nodes0;
-  for (int i = t; i < S; i += 256) {
+  for (int i = t; i < S; i += NT) {
     const ONode nd = Lf[i];
     const uint32_t* src = (nd.flags & 1) ? kb : ka;
     uint32_t best = src[nd.begin];
@@ -1683,32 +1688,33 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
 }
 
 
-__global__ __launch_bounds__(256) void k_octree(ExtractArgs a, int l0) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_octree(ExtractArgs a, int l0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int l = l0 + blockIdx.x, img = blockIdx.y, t = threadIdx.x;  // levels l0 .. l0 + gridDim.x - 1
   const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
   int* sa = reinterpret_cast<int*>(smem + (sizeof(ONode) * 2 + sizeof(int4)) * NC);
   int* sx = sa + 2 * SA;
   int* misc = reinterpret_cast<int*>(reinterpret_cast<unsigned long long*>(sx + SA) + SC);
-  uint32_t* lds_keys = reinterpret_cast<uint32_t*>(misc + 16);
+  uint32_t* lds_keys = reinterpret_cast<uint32_t*>(misc + OCT_MISC_INTS);
   OCT_MARK(0, wall_clock64());
   const LevelDesc ld = a.levels[l];
   const int32_t* ccount = a.cellcnt + (long long)img * a.ncells + ld.cell_begin;
-  for (int c = t; c < ld.ncells; c += 256) {
+  for (int c = t; c < ld.ncells; c += NT) {
     sa[c] = ccount[c];
     sx[c] = a.cells[ld.cell_begin + c].slot;
   }
   __syncthreads();
-  const int n = block_scan_excl(sa, ld.ncells, misc);
+  const int n = block_scan_excl_n<NT>(sa, ld.ncells, misc);
   OCT_MARK(1, wall_clock64());
   if (n == 0) {
     if (t == 0) a.lvlcnt[(long long)img * a.nlevels + l] = 0;
     return;
   }
   if (n <= a.key_lds_cap) {  // keys in LDS (two ping-pong halves)
-    octree_run<true>(a, smem, l, n, lds_keys, lds_keys + a.key_lds_cap);
+    octree_run<true, NT>(a, smem, l, n, lds_keys, lds_keys + a.key_lds_cap);
   } else {  // very large levels: keys in the global scratch buffers
-    octree_run<false>(a, smem, l, n, a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin,
+    octree_run<false, NT>(a, smem, l, n, a.keys_a + (long long)img * a.keyscr_stride + ld.cand_begin,
                       a.keys_b + (long long)img * a.keyscr_stride + ld.cand_begin);
   }
 }
@@ -2186,6 +2192,7 @@ struct orbfe_extractor {
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
   int lat_sched = 1;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
+  int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -2505,7 +2512,12 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
     const int need = (int)std::max(h->oct_all.lds, std::max(h->oct_hi.lds, h->oct_lo.lds));
     int* have = h->device >= 0 && h->device < kMaxDevices ? &attr_lds[h->device] : nullptr;
     if (need <= 160 * 1024 && (!have || need > *have)) {
-      ORBFE_HIP_CHECK(hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      ORBFE_HIP_CHECK(
+          hipFuncSetAttribute((const void*)k_octree<256>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      ORBFE_HIP_CHECK(
+          hipFuncSetAttribute((const void*)k_octree<512>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
+      ORBFE_HIP_CHECK(
+          hipFuncSetAttribute((const void*)k_octree<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, need));
       if (have) *have = need;
     }
   }
@@ -2522,12 +2534,12 @@ static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int
     mini = std::max(mini, lv[l].nini);
   }
   int sc = 1;
-  while (sc < std::max(ncap, 4 * mini)) sc <<= 1;  // sk doubles as the [4][nini] bucket tables
+  while (sc < std::max(std::max(ncap, 16 * mini), 24)) sc <<= 1;  // sk doubles as the [NW][nini] bucket tables and 3 x NW scan sums
   p.node_cap = ncap;
   p.sort_cap = sc;
   p.scan_cap = (std::max(ncap, mc) + 3) & ~3;
   const size_t fixed = sizeof(ONode) * 2 * ncap + sizeof(int4) * ncap + sizeof(int) * 3 * p.scan_cap +
-                       sizeof(unsigned long long) * sc + sizeof(int) * 16;
+                       sizeof(unsigned long long) * sc + sizeof(int) * OCT_MISC_INTS;
   const size_t budget = (size_t)budget_kb * 1024;
   p.key_lds_cap = fixed < budget ? (int)((budget - fixed) / 8) & ~63 : 0;
   if (key_cap_override >= 0) p.key_lds_cap = std::min(p.key_lds_cap, key_cap_override);
@@ -2714,7 +2726,18 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ao.scan_cap = P.scan_cap;
     ao.key_lds_cap = P.key_lds_cap;
     dim3 grid(nl, n);
-    ORBFE_LAUNCH("k_octree", k_octree, grid, dim3(256), P.lds, s, ao, l0);
+    // calls of fewer than 8 images leave the chip nearly idle: one 512-thread block per level (8
+    // wavefronts share each pass's node splits and the refinement's child counts, partitions and
+    // rank sort), against 256 threads for batches, where the blocks run beside other kernels. One
+    // KITTI image: the octree's two launches 84.6 us summed at 512 vs 95.4 at 256 and 92.9 at 1024
+    // threads (16 wavefronts pay more per barrier and spill 2 VGPRs); orbfe_extract p50 0.196 vs
+    // 0.198 / 0.202 ms (profiles/r6_c2_octree.txt)
+    if (n < 8 && h->oct_threads_small == 1024)
+      ORBFE_LAUNCH("k_octree", k_octree<1024>, grid, dim3(1024), P.lds, s, ao, l0);
+    else if (n < 8 && h->oct_threads_small == 512)
+      ORBFE_LAUNCH("k_octree", k_octree<512>, grid, dim3(512), P.lds, s, ao, l0);
+    else
+      ORBFE_LAUNCH("k_octree", k_octree<256>, grid, dim3(256), P.lds, s, ao, l0);
   };
   side_fast(0);
   if (lat && k_side == 1) launch_octree(side, 0, 1, h->oct_all);
@@ -2820,7 +2843,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)h->oct_threads_small,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3688,6 +3711,13 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_threads(orbfe_extractor* h, int threads) {
+  if (!h || (threads != 256 && threads != 512 && threads != 1024))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_threads: 256, 512 or 1024");
+  h->oct_threads_small = threads;
   return ORBFE_OK;
 }
 

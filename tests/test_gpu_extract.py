@@ -173,6 +173,25 @@ def test_latency_schedule(require_gpu, blur_mode, k, n):
         assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
+@pytest.mark.parametrize("threads,cap", [(256, -1), (512, -1), (1024, -1), (1024, 0), (1024, 1024), (512, 0)])
+def test_octree_block_sizes(require_gpu, threads, cap):
+    """DistributeOctTree's block of a call of fewer than 8 images: 512 threads (the default), 1024,
+    or the batches' 256 -- the same survivors on KITTI-, TUM- and odd-shaped images, textured and
+    noise, one image and three per call, with the keys in LDS or forced to the global path (cap 0:
+    every level, 1024: the large ones)."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_octree_threads(threads)
+    if cap >= 0:
+        ext.debug_set_octree_key_cap(cap)
+    rng = np.random.default_rng(17)
+    for shape in ((376, 1241), (480, 640), (301, 517)):
+        imgs = [synth_frame(31, *shape), rng.integers(0, 256, shape, dtype=np.uint8), synth_frame(32, *shape)]
+        assert_same_extraction(ext, ref, imgs[0])
+        outs = ext.extract_batch(imgs)
+        for i in reversed(range(len(imgs))):
+            assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_large_scale_factors(require_gpu, params):
     """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
