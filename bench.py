@@ -106,6 +106,9 @@ def parse(argv=None):
                    help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
                         "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 4: 85.4-85.5k vs 84.0-84.1k "
                         "stereo frames/s at 0, round 5)")
+    p.add_argument("--octree-threads", default="",
+                   help="SMALL,BATCH: DistributeOctTree's block size for calls of < 8 images and for batches "
+                        "(orbfe_debug_set_octree_threads; default 512,256)")
     p.add_argument("--octree-lds", default="",
                    help="HI,LO: LDS KiB per block of the two octree launches (orbfe_debug_set_octree_lds; "
                         "default: the library's 80,40)")
@@ -564,6 +567,10 @@ def main():
         hi, lo = (int(x) for x in args.octree_lds.split(","))
         for e in exts:
             e.debug_set_octree_lds(hi, lo)
+    if args.octree_threads:
+        small, batch = (int(x) for x in args.octree_threads.split(","))
+        for e in exts:
+            e.debug_set_octree_threads(small, batch)
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract,

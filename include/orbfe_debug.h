@@ -36,9 +36,9 @@ int orbfe_debug_set_octree_split(orbfe_extractor* h, int k);
  * k..L-1; joined before the descriptors. Default k = 1; k <= 0 or k >= L: the throughput schedule
  * (FAST of the first levels on the side stream, one octree launch after every level's FAST). */
 int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k);
-/* DistributeOctTree's block size for calls of fewer than 8 images: 512 threads (default), 1024, or
- * 256, the batches' size (same results). */
-int orbfe_debug_set_octree_threads(orbfe_extractor* h, int threads);
+/* DistributeOctTree's block size (256, 512 or 1024 threads; same results) for calls of fewer than 8
+ * images (default 512) and for batches of 8+ (default 256). */
+int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batches);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */
 int orbfe_debug_set_octree_lds(orbfe_extractor* h, int hi_kb, int lo_kb);

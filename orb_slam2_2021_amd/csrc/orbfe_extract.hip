@@ -2193,6 +2193,7 @@ struct orbfe_extractor {
   int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
   int lat_sched = 1;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
   int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
+  int oct_threads_batch = 256;       // ... and for batches of 8+
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -2732,9 +2733,10 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     // KITTI image: the octree's two launches 84.6 us summed at 512 vs 95.4 at 256 and 92.9 at 1024
     // threads (16 wavefronts pay more per barrier and spill 2 VGPRs); orbfe_extract p50 0.196 vs
     // 0.198 / 0.202 ms (profiles/r6_c2_octree.txt)
-    if (n < 8 && h->oct_threads_small == 1024)
+    const int nt = n < 8 ? h->oct_threads_small : h->oct_threads_batch;
+    if (nt == 1024)
       ORBFE_LAUNCH("k_octree", k_octree<1024>, grid, dim3(1024), P.lds, s, ao, l0);
-    else if (n < 8 && h->oct_threads_small == 512)
+    else if (nt == 512)
       ORBFE_LAUNCH("k_octree", k_octree<512>, grid, dim3(512), P.lds, s, ao, l0);
     else
       ORBFE_LAUNCH("k_octree", k_octree<256>, grid, dim3(256), P.lds, s, ao, l0);
@@ -2843,7 +2845,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)h->oct_threads_small,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch),
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3714,10 +3716,12 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   return ORBFE_OK;
 }
 
-extern "C" int orbfe_debug_set_octree_threads(orbfe_extractor* h, int threads) {
-  if (!h || (threads != 256 && threads != 512 && threads != 1024))
+extern "C" int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batches) {
+  auto ok = [](int t) { return t == 256 || t == 512 || t == 1024; };
+  if (!h || !ok(small_calls) || !ok(batches))
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_threads: 256, 512 or 1024");
-  h->oct_threads_small = threads;
+  h->oct_threads_small = small_calls;
+  h->oct_threads_batch = batches;
   return ORBFE_OK;
 }
 

@@ -308,9 +308,11 @@ class ORBextractor:
         per block and k.. at 40 KiB (default 4; k <= 0: one launch of every level at 80 KiB)."""
         L.check(self._lib.orbfe_debug_set_octree_split(self._h, int(k)), "set_octree_split")
 
-    def debug_set_octree_threads(self, threads: int) -> None:
-        """DistributeOctTree's block size for calls of fewer than 8 images (512 default, 1024 or 256)."""
-        L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(threads)), "set_octree_threads")
+    def debug_set_octree_threads(self, small_calls: int, batches: int = 256) -> None:
+        """DistributeOctTree's block size (256 / 512 / 1024) for calls of fewer than 8 images (512
+        default) and for batches of 8+ (256 default)."""
+        L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
+                "set_octree_threads")
 
     def debug_set_latency_schedule(self, k: int) -> None:
         """Calls of fewer than 8 images: FAST and DistributeOctTree of levels 0..k-1 on the side stream

@@ -23,7 +23,7 @@ def main():
     exts = {}
     for t in settings:
         e = ORBextractor(2000, 1.2, 8, 20, 7)
-        e.debug_set_octree_threads(t)
+        e.debug_set_octree_threads(t, 256)
         for _ in range(20):
             e(img)
         exts[t] = e

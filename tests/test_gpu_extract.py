@@ -123,14 +123,17 @@ def test_octree_global_key_path(require_gpu, cap):
     assert_same_extraction(ext, ref, noise)
 
 
-@pytest.mark.parametrize("split,lds", [(0, None), (1, None), (3, None), (4, None), (7, None), (8, None),
-                                       (4, (64, 32)), (4, (48, 24))])
-def test_octree_launch_split(require_gpu, split, lds):
+@pytest.mark.parametrize("split,lds,threads", [(0, None, 256), (1, None, 256), (3, None, 256), (4, None, 256),
+                                               (7, None, 256), (8, None, 256), (4, (64, 32), 256),
+                                               (4, (48, 24), 256), (4, None, 512), (0, None, 1024),
+                                               (4, (48, 24), 512)])
+def test_octree_launch_split(require_gpu, split, lds, threads):
     """DistributeOctTree as one launch (0, 8) or two (levels 0..k-1 at the 80 KiB LDS plan, k.. at
     the 40 KiB one) over an 8-image batch: the same survivors, on textured and noise images (noise
     pushes the small levels' key counts past the half plan's LDS capacity, onto the global path)."""
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
     ext.debug_set_octree_split(split)
+    ext.debug_set_octree_threads(512, threads)  # the batch's block size
     if lds:  # smaller plans: more keys through the global path
         ext.debug_set_octree_lds(*lds)
     # (the split applies to device-resident batches of 8+ images: one such batch, every image checked)
@@ -180,7 +183,7 @@ def test_octree_block_sizes(require_gpu, threads, cap):
     noise, one image and three per call, with the keys in LDS or forced to the global path (cap 0:
     every level, 1024: the large ones)."""
     ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
-    ext.debug_set_octree_threads(threads)
+    ext.debug_set_octree_threads(threads, 256)
     if cap >= 0:
         ext.debug_set_octree_key_cap(cap)
     rng = np.random.default_rng(17)
