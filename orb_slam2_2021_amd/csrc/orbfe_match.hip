@@ -345,7 +345,9 @@ __device__ void sft_big_nodes(const orbfe_sft_pair& P, int only_stereo, int b, S
     int rank = base + prefix_in_wave(m);
     for (int k = 0; k < w; k++) rank += L.wave_cnt[k];
     if (pairv >= 0 && rank % SFT_BIG_WG == b) {
-      const int slot = rank / SFT_BIG_WG - base / SFT_BIG_WG;  // < 256 / SFT_BIG_WG within the chunk
+      // this workgroup's ranks in the chunk are first, first + SFT_BIG_WG, ...: slots 0, 1, ...
+      const int first = base + ((b - base % SFT_BIG_WG) + SFT_BIG_WG) % SFT_BIG_WG;
+      const int slot = (rank - first) / SFT_BIG_WG;  // <= 256 / SFT_BIG_WG within the chunk
       L.list[2 * slot] = a;
       L.list[2 * slot + 1] = pairv;
       atomicMax(&L.nlist, slot + 1);

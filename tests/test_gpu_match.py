@@ -87,6 +87,41 @@ def test_search_for_triangulation_node_sizes(require_gpu, kitti_pair, k, levels,
     assert nm > 0
 
 
+@pytest.mark.parametrize("big_at", [(3, 259, 262, 300, 511), (0, 1, 2, 257, 258, 259, 260), (300, 301)])
+def test_search_for_triangulation_big_nodes_across_chunks(require_gpu, kitti_pair, big_at):
+    """FeatureVectors of 520 nodes whose 65-256-feature nodes sit at the given node positions, in and
+    past the first 256-node chunk the big-node workgroups scan at a time, so that the workgroups'
+    shares of a chunk start at odd and even ranks; KF2 = KF1 shuffled (every feature has a twin)."""
+    from orb_slam2_2021_amd.frames import FeatureVector
+    k1, d1, _, _, scale, sigma2 = kitti_pair
+    n = len(k1)
+    rng = np.random.default_rng(23)
+    perm = rng.permutation(n)
+    k2, d2 = k1[perm], d1[perm]
+    node = np.empty(n, np.int64)
+    sizes = [70 + 40 * (j % 4) for j in range(len(big_at))]  # 70, 110, 150, 190
+    pos = 0
+    for j, b in enumerate(big_at):
+        node[pos:pos + sizes[j]] = b
+        pos += sizes[j]
+    small = np.array([b for b in range(520) if b not in big_at])
+    node[pos:] = small[np.arange(n - pos) % len(small)]  # every id present: CSR position = node id
+    rng.shuffle(node)
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    t1, t2 = S.pose(), S.pose(tx=-0.537, tz=0.05)
+    F1 = S.make_frame(k1, d1, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.4, tcw=t1)
+    F2 = S.make_frame(k2, d2, scale, sigma2, 376, 1241, S.KITTI_CAM, rng, stereo_frac=0.4, tcw=t2)
+    F1.feat_vec = FeatureVector.from_assignment(node)
+    F2.feat_vec = FeatureVector.from_assignment(node[perm])  # feature q of KF2 is KF1's perm[q]
+    F12 = S.compute_f12(t1, t2, S.intrinsics(S.KITTI_CAM))
+    ex, ey = -1.0e7, 185.0
+    nm, _, m12 = ORBmatcher(0.6, False).SearchForTriangulation(F1, F2, F12, False, epipole_xy=(ex, ey))
+    nr, r12 = orbref.search_for_triangulation(F1, F2, F12, ex, ey, False, False)
+    assert nm == nr and np.array_equal(m12, r12)
+    assert nm > 0
+
+
 def test_search_for_triangulation_unlisted_features(require_gpu, kitti_pair):
     """Features a FeatureVector does not list -- DBoW2 leaves out stopped words (weight 0,
     TemplatedVocabulary.h:1198-1201) -- are never matched: match12 = -1 for them even when the
