@@ -104,8 +104,8 @@ def parse(argv=None):
                         "side stream, 1 after it on the launch stream (default: 0 with one handle, 1 with several)")
     p.add_argument("--octree-split", type=int, default=-1,
                    help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
-                        "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 4: 85.4-85.5k vs 84.0-84.1k "
-                        "stereo frames/s at 0, round 5)")
+                        "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 5: 86.7-86.9k vs 85.7-85.9k "
+                        "at 4 and 84.0-84.1k at 0, rounds 5-6)")
     p.add_argument("--octree-threads", default="",
                    help="SMALL,BATCH: DistributeOctTree's block size for calls of < 8 images and for batches "
                         "(orbfe_debug_set_octree_threads; default 512,256)")

@@ -28,7 +28,7 @@ int orbfe_debug_set_octree_key_cap(orbfe_extractor* h, int cap);
 /* DistributeOctTree in two launches for device-resident batches (orbfe_extract_batch_device) of 8 or
  * more images: levels 0..k-1 with the full LDS
  * plan (80 KiB per block), levels k..L-1 with half of it (their smaller node arenas and key counts
- * fit 40 KiB: four blocks per CU); k <= 0 or k >= L: one launch of every level at 80 KiB. Default 4;
+ * fit 40 KiB: four blocks per CU); k <= 0 or k >= L: one launch of every level at 80 KiB. Default 5;
  * smaller batches and the host-buffer calls always take one launch (lower latency alone). */
 int orbfe_debug_set_octree_split(orbfe_extractor* h, int k);
 /* Latency schedule for calls of fewer than 8 images: FAST of levels 0..k-1 and their

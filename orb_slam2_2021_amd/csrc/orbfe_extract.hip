@@ -2190,7 +2190,8 @@ struct orbfe_extractor {
   int inline_side = 0;               // orbfe_debug_set_inline_side: side-stream work on the launch stream
   hipStream_t side_ext = nullptr;    // orbfe_set_side_stream: a caller's stream instead of h->side
   int blur_mode = 0;                 // orbfe_debug_set_blur_mode
-  int octree_split = 4;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
+  int octree_split = 5;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
+                                     // (k = 5 86.7-86.9k vs 4 85.7-85.9k stereo frames/s, round 6)
   int lat_sched = 1;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
   int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
   int oct_threads_batch = 256;       // ... and for batches of 8+

@@ -305,7 +305,7 @@ class ORBextractor:
 
     def debug_set_octree_split(self, k: int) -> None:
         """DistributeOctTree in two launches for batches of 8+ images, levels 0..k-1 at 80 KiB of LDS
-        per block and k.. at 40 KiB (default 4; k <= 0: one launch of every level at 80 KiB)."""
+        per block and k.. at 40 KiB (default 5; k <= 0: one launch of every level at 80 KiB)."""
         L.check(self._lib.orbfe_debug_set_octree_split(self._h, int(k)), "set_octree_split")
 
     def debug_set_octree_threads(self, small_calls: int, batches: int = 256) -> None:
