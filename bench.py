@@ -106,6 +106,9 @@ def parse(argv=None):
                    help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
                         "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 5: 86.7-86.9k vs 85.7-85.9k "
                         "at 4 and 84.0-84.1k at 0, rounds 5-6)")
+    p.add_argument("--pyramid-tiles", default="",
+                   help="k_pyramid tiles per image sx,sy,bx,by for calls of < 8 images / batches "
+                        "(orbfe_debug_set_pyramid_tiles; 0,0: the per-level resize chain)")
     p.add_argument("--octree-threads", default="",
                    help="SMALL,BATCH: DistributeOctTree's block size for calls of < 8 images and for batches "
                         "(orbfe_debug_set_octree_threads; default 512,256)")
@@ -571,6 +574,10 @@ def main():
         small, batch = (int(x) for x in args.octree_threads.split(","))
         for e in exts:
             e.debug_set_octree_threads(small, batch)
+    if args.pyramid_tiles:
+        t = [int(x) for x in args.pyramid_tiles.split(",")]
+        for e in exts:
+            e.debug_set_pyramid_tiles((t[0], t[1]), (t[2], t[3]))
     pipe, state = build_c3(exts if len(exts) > 1 else ext, tree, voc, B, H, W, dev, seed=1234 + rank,
                            depth=pipe_depth(args), stereo=args.stereo, levelsup=args.levelsup, streams=pstreams,
                            pairs=args.pairs, stereo_on_match=not args.stereo_on_extract,

@@ -39,6 +39,11 @@ int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k);
 /* DistributeOctTree's block size (256, 512 or 1024 threads; same results) for calls of fewer than 8
  * images (default 512) and for batches of 8+ (default 256). */
 int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batches);
+/* ComputePyramid's levels 1..L-1 in one k_pyramid launch of tx x ty tiles per image (each
+ * workgroup builds its tile of every level, the previous level in LDS, the halo recomputed) for
+ * calls of fewer than 8 images / batches of 8+; 0, 0: one k_resize_win launch per level. Same
+ * bytes either way; a tiling whose tile needs more than 64 KiB of LDS falls back to the chain. */
+int orbfe_debug_set_pyramid_tiles(orbfe_extractor* h, int small_tx, int small_ty, int batch_tx, int batch_ty);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */
 int orbfe_debug_set_octree_lds(orbfe_extractor* h, int hi_kb, int lo_kb);

@@ -380,6 +380,206 @@ __global__ __launch_bounds__(256) void k_resize_win(ExtractArgs a, int l, int G,
   if (y0 + 1 < ld.h) store_row4(out + __umul24((uint32_t)(y0 + 1), (uint32_t)ld.pitch), x, ld.w, pb);
 }
 
+// k_pyramid: levels 1..L-1 of ComputePyramid (ORBextractor.cc:1105-1135) in ONE launch, the chain
+// of dependent per-level resizes kept inside each workgroup. The image is cut into tx x ty tiles
+// per level (PyrTileLevel, host-planned by pyramid_plan); a workgroup owns one tile of every level
+// and computes, level after level, its owned 4-column groups and rows plus the halo the next
+// level's computed region reads (the dependency cone, at most a few rows / groups per side), with
+// level l-1 held in LDS while level l is built (two LDS buffers, one barrier per level); level 1
+// reads level 0 from the pyramid block. Owned pixels (and their REFLECT_101 padding columns) go to
+// the pyramid block; halo pixels are recomputed by the neighbouring tiles from the same source
+// bytes with the same arithmetic as k_resize_win, so the result is the per-level chain's byte for
+// byte. Replaces L-1 launches (each a latency-bound grid that leaves most CUs idle, plus a kernel
+// boundary) by one, and level l-1's bytes are read from LDS instead of L2 / HBM.
+struct PyrTileLevel {
+  int16_t ng_a, ng_b, ny_a, ny_b;  // computed groups [ng_a, ng_b) and rows [ny_a, ny_b)
+  int16_t og_a, og_b, oy_a, oy_b;  // owned (stored): a subset of the computed region
+  uint32_t gmagic;                 // item / (4 (ng_b - ng_a)) as __umulhi(item, gmagic)
+  int32_t tab_off;                 // this level's staged tables in LDS (dwords; entries 9 per group, 2 per row)
+};
+constexpr int PYR_MAX_LEVELS = 32;
+constexpr int PYR_LV_DW = 8;  // staged LevelDesc fields per level
+
+// The tables one tile reads (per computed 4-column group its first source column and byte
+// selectors / alphas, per computed row the source row and betas) and the level fields are staged in
+// LDS first, all loads in flight together, so the level loop touches global memory only for level
+// 0's bytes and the owned stores (one dependent table fetch per level measured ~3 us per level).
+// A workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding
+// global store (s_waitcnt vmcnt(0)), ~2-3 us per level here for pyramid bytes no workgroup of this
+// launch reads back.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+constexpr int PYR_NT = 1024;  // k_pyramid's workgroup
+__global__ __launch_bounds__(PYR_NT) void k_pyramid(ExtractArgs a, const PyrTileLevel* __restrict__ tiles,
+                                                 int half_dw, int dbg) {
+#ifdef ORBFE_PYR_CLOCKS  // phase clocks of two workgroups (printf; a timing build only)
+  unsigned long long tclk[40];
+  int nclk = 0;
+#define PYR_CLK() if (dbg) tclk[nclk++] = __builtin_amdgcn_s_memrealtime();
+#else
+#define PYR_CLK()
+#endif
+  PYR_CLK();
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_pyr[];
+  __shared__ PyrTileLevel s_t[PYR_MAX_LEVELS];
+  __shared__ int s_lv[PYR_MAX_LEVELS][PYR_LV_DW];  // w, h, pitch, pyr_off, simd_end, rgrp_begin, tab_y
+  const int L = a.nlevels, tid = threadIdx.x;
+  const int img = blockIdx.y;
+  {
+    const PyrTileLevel* T = tiles + (size_t)blockIdx.x * L;
+    const int nT = L * (int)(sizeof(PyrTileLevel) / 4);
+    if (tid < nT) reinterpret_cast<int*>(s_t)[tid] = reinterpret_cast<const int*>(T)[tid];
+    const int u = tid - 128;
+    if (u >= 0 && u < L * 7) {
+      const int l = u / 7, f = u - 7 * l;
+      const LevelDesc* d = a.levels + l;
+      const int v = f == 0 ? d->w : f == 1 ? d->h : f == 2 ? d->pitch : f == 3 ? (int)d->pyr_off
+                  : f == 4 ? d->simd_end : f == 5 ? d->rgrp_begin : d->tab_y;
+      s_lv[l][f] = v;
+    }
+  }
+  __syncthreads();
+  PYR_CLK();
+  uint32_t* s_tab = s_pyr + 2 * half_dw;
+  {
+    const int last = L - 1;
+    const int total = s_t[last].tab_off + 9 * (s_t[last].ng_b - s_t[last].ng_a) + 2 * (s_t[last].ny_b - s_t[last].ny_a);
+    const uint32_t* rg = reinterpret_cast<const uint32_t*>(a.rgrp);
+    const uint32_t* yt = reinterpret_cast<const uint32_t*>(a.ytab);
+    for (int e0 = tid; e0 < total; e0 += 4 * PYR_NT) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int e = e0 + PYR_NT * k;
+        v[k] = 0;
+        if (e < total) {
+          int l = 1;
+          while (l < last && e >= s_t[l + 1].tab_off) l++;
+          const PyrTileLevel& t = s_t[l];
+          const int j = e - t.tab_off, G9 = 9 * (t.ng_b - t.ng_a);
+          if (j < G9) {
+            const int g = j / 9, w = j - 9 * g;
+            const uint32_t gi = (uint32_t)(s_lv[l][5] + t.ng_a + g);
+            v[k] = w == 0 ? (uint32_t)a.rgx0[gi] : rg[8 * gi + (w - 1)];
+          } else {
+            const int r = j - G9;
+            v[k] = yt[2 * (s_lv[l][6] + t.ny_a + (r >> 1)) + (r & 1)];
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (e0 + PYR_NT * k < total) s_tab[e0 + PYR_NT * k] = v[k];
+    }
+  }
+  __syncthreads();
+  PYR_CLK();
+  // (uniform values read from LDS go through readfirstlane: scalar registers, and the level-0
+  // buffer descriptor stays scalar instead of a per-load waterfall loop)
+  auto uni = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+  uint8_t* base = a.pyr + (long long)img * a.pyr_stride;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + uni(s_lv[0][3]), 0, 0x7fffffff, 0x00020000);
+  const uint32_t pdw0 = (uint32_t)uni(s_lv[0][2]) >> 2;
+  for (int l = 1; l < L; l++) {
+    PyrTileLevel t = s_t[l], tp = s_t[l - 1];
+    t.ng_a = (int16_t)uni(t.ng_a), t.ng_b = (int16_t)uni(t.ng_b), t.ny_a = (int16_t)uni(t.ny_a);
+    t.ny_b = (int16_t)uni(t.ny_b), t.og_a = (int16_t)uni(t.og_a), t.og_b = (int16_t)uni(t.og_b);
+    t.oy_a = (int16_t)uni(t.oy_a), t.oy_b = (int16_t)uni(t.oy_b), t.gmagic = (uint32_t)uni((int)t.gmagic);
+    t.tab_off = uni(t.tab_off);
+    tp.ng_a = (int16_t)uni(tp.ng_a), tp.ng_b = (int16_t)uni(tp.ng_b), tp.ny_a = (int16_t)uni(tp.ny_a);
+    const int w = uni(s_lv[l][0]), pitch = uni(s_lv[l][2]), simd_end = uni(s_lv[l][4]), hs = uni(s_lv[l - 1][1]);
+    const int ng = t.ng_b - t.ng_a, nc = 4 * ng;
+    const int items = ng > 0 ? nc * ((t.ny_b - t.ny_a + 1) >> 1) : 0;
+    uint8_t* dst = reinterpret_cast<uint8_t*>(s_pyr + (l & 1) * half_dw);
+    const uint32_t* srcl = s_pyr + ((l - 1) & 1) * half_dw;
+    const uint32_t* tg = s_tab + t.tab_off;
+    const uint32_t* ty = tg + 9 * ng;
+    const int dpitch = 4 * (ng + 3), spitch = tp.ng_b - tp.ng_a + 3;
+    const bool keep = l + 1 < L;
+    uint8_t* out = base + uni(s_lv[l][3]);
+    // one output pixel (column x, rows y0 and y0 + 1) per thread: the group's window and tables
+    // are read by its 4 lanes (LDS broadcast), each lane its own selector / alpha pair
+    for (int item = tid; item < items; item += PYR_NT) {
+      const int pr = t.gmagic ? (int)__umulhi((uint32_t)item, t.gmagic) : item;
+      const int xo = item - pr * nc, gl = xo >> 2, k = xo & 3;
+      const int g = t.ng_a + gl, x = 4 * t.ng_a + xo;
+      const int y0 = t.ny_a + 2 * pr;
+      const bool two = y0 + 1 < t.ny_b;
+      const uint32_t* q = tg + 9 * gl;
+      const uint32_t sx0 = q[0], sel = q[1 + k], alp16 = q[5 + k];
+      const int ra = 2 * (y0 - t.ny_a), rb = two ? ra + 2 : ra;
+      const int2 ya = make_int2((int)ty[ra], (int)ty[ra + 1]), yb = make_int2((int)ty[rb], (int)ty[rb + 1]);
+      const int rr[4] = {min(max(ya.x, 0), hs - 1), min(max(ya.x + 1, 0), hs - 1), min(max(yb.x, 0), hs - 1),
+                         min(max(yb.x + 1, 0), hs - 1)};
+      uint32_t wv[4][3];
+      if (l == 1) {  // level 0 from the pyramid block: 3 aligned dwords per source row
+        const uint32_t cx = sx0 >> 2;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+#pragma unroll
+          for (int kk = 0; kk < 3; kk++)
+            wv[r][kk] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * ((uint32_t)rr[r] * pdw0 + cx)) + 4 * kk, 0, 0);
+        }
+      } else {  // level l-1 from this tile's LDS copy
+        const int c = (int)(sx0 >> 2) - tp.ng_a;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const uint32_t* p = srcl + (rr[r] - tp.ny_a) * spitch + c;
+#pragma unroll
+          for (int kk = 0; kk < 3; kk++) wv[r][kk] = p[kk];
+        }
+      }
+      const int sh = (int)(sx0 & 3u);
+      uint32_t H[4];  // 16 h of the 4 source rows (resize_win_row's horizontal pass, one column)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t W0 = __builtin_amdgcn_alignbyte(wv[r][1], wv[r][0], sh);
+        const uint32_t W1 = __builtin_amdgcn_alignbyte(wv[r][2], wv[r][1], sh);
+        H[r] = (uint32_t)dot2_u16(__builtin_amdgcn_perm(W1, W0, sel), alp16);
+      }
+      uint32_t va, vb;
+      const uint32_t ba0 = (uint32_t)ya.y & 0xffffu, ba1 = (uint32_t)ya.y >> 16;
+      const uint32_t bb0 = (uint32_t)yb.y & 0xffffu, bb1 = (uint32_t)yb.y >> 16;
+      if (x < simd_end) {  // OpenCV's SIMD128 vertical rounding (resize_win_row)
+        va = (mulhi_u24(H[0] & 0xffff00u, ba0 << 8) + mulhi_u24(H[1] & 0xffff00u, ba1 << 8) + 2u) >> 2;
+        vb = (mulhi_u24(H[2] & 0xffff00u, bb0 << 8) + mulhi_u24(H[3] & 0xffff00u, bb1 << 8) + 2u) >> 2;
+      } else {  // FixedPtCast<int, uchar, 22>
+        const int h0 = (int)(H[0] >> 4), h1 = (int)(H[1] >> 4), h2 = (int)(H[2] >> 4), h3 = (int)(H[3] >> 4);
+        va = (uint32_t)min(max((h0 * (int)ba0 + h1 * (int)ba1 + (1 << 21)) >> 22, 0), 255);
+        vb = (uint32_t)min(max((h2 * (int)bb0 + h3 * (int)bb1 + (1 << 21)) >> 22, 0), 255);
+      }
+      if (keep) {
+        uint8_t* d = dst + (y0 - t.ny_a) * dpitch + xo;
+        d[0] = (uint8_t)va;
+        if (two) d[dpitch] = (uint8_t)vb;
+      }
+      if (g >= t.og_a && g < t.og_b && x < w) {  // owned: the byte and its REFLECT_101 copies (store_row4)
+        const int xr = x >= 1 && x <= 3 ? -x : x >= w - 4 && x <= w - 2 ? 2 * w - 2 - x : INT_MIN;
+        if (y0 >= t.oy_a && y0 < t.oy_b) {
+          uint8_t* row = out + __umul24((uint32_t)y0, (uint32_t)pitch);
+          row[x] = (uint8_t)va;
+          if (xr != INT_MIN) row[xr] = (uint8_t)va;
+        }
+        if (two && y0 + 1 >= t.oy_a && y0 + 1 < t.oy_b) {
+          uint8_t* row = out + __umul24((uint32_t)(y0 + 1), (uint32_t)pitch);
+          row[x] = (uint8_t)vb;
+          if (xr != INT_MIN) row[xr] = (uint8_t)vb;
+        }
+      }
+    }
+    lds_barrier();  // the next level reads this one's LDS copy; the pyramid stores stay in flight
+    PYR_CLK();
+  }
+#ifdef ORBFE_PYR_CLOCKS
+  if (dbg && threadIdx.x == 0 && blockIdx.x == gridDim.x / 2 && blockIdx.y == 0) {
+    printf("pyr blk %d:", blockIdx.x);
+    for (int i = 1; i < nclk; i++) printf(" %d", (int)(tclk[i] - tclk[i - 1]));
+    printf("\n");
+  }
+#endif
+  (void)dbg;
+}
+
 
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
 // padding columns).
@@ -2198,6 +2398,17 @@ struct orbfe_extractor {
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
+  // k_pyramid tiles per image (x, y) for calls of < 8 images / batches; 0: the per-level resize
+  // chain (orbfe_debug_set_pyramid_tiles). One KITTI image: orbfe_extract p50 0.160 ms at 16 x 12
+  // vs 0.169 through the chain (32 x 24 0.163, 8 x 6 0.163; profiles/r6_c2_pyramid.txt); batches
+  // keep the chain: its launches fill the chip, the tiles' level-by-level latency chains do not
+  // (C3 bench 43-59k vs 86.9k stereo frames/s, profiles/r6_sweep_pyramid.txt)
+  int pyr_tiles_small[2] = {16, 12}, pyr_tiles_batch[2] = {0, 0};
+  struct PyrPlan {
+    int ntiles = 0, half_dw = 0;
+    size_t lds = 0;
+    PyrTileLevel* d_tiles = nullptr;
+  } pyr_small, pyr_batch;
   hipStream_t stream = nullptr;
   hipStream_t side = nullptr;               // k_blur runs here, beside k_fast + k_octree
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_l0 = nullptr, ev_f0 = nullptr;
@@ -2284,6 +2495,81 @@ struct orbfe_extractor {
 
 static OctPlan octree_plan(const std::vector<LevelDesc>& lv, int l0, int l1, int budget_kb, int key_cap_override);
 static size_t octree_lds(const orbfe_extractor* h);
+
+// k_pyramid's tiles: level l's 4-column groups and rows cut into tx x ty owned blocks; from the top
+// level down, each tile's computed region at level l is its owned block joined with what its
+// computed region at level l + 1 reads (rows clamp(sy), clamp(sy + 1); the 8-byte window from
+// rgx0, cut at the level's last column). Entry 0 holds level 0's footprint (read from the pyramid
+// block, not computed). Returns the LDS dwords one level buffer needs (0: no plan -- a level
+// without the 8-byte window, one level, or a tile past the LDS budget).
+static int pyramid_plan(const std::vector<LevelDesc>& lv, const std::vector<int2>& yt, const std::vector<int>& rgx0,
+                        int tx, int ty, std::vector<PyrTileLevel>& out, int& tab_dw) {
+  const int L = (int)lv.size();
+  out.clear();
+  tab_dw = 0;
+  if (L < 2 || L > PYR_MAX_LEVELS || tx <= 0 || ty <= 0) return 0;
+  for (int l = 1; l < L; l++)
+    if (!lv[l].rwin_ok) return 0;
+  int half = 0, tab = 0;
+  for (int i = 0; i < ty; i++)
+    for (int j = 0; j < tx; j++) {
+      std::vector<PyrTileLevel> T(L);
+      int fg_a = 0, fg_b = 0, fy_a = 0, fy_b = 0;  // footprint in the level below (empty)
+      for (int l = L - 1; l >= 0; l--) {
+        PyrTileLevel& t = T[l];
+        std::memset(&t, 0, sizeof(t));
+        int ga = fg_a, gb = fg_b, ya = fy_a, yb = fy_b;
+        if (l >= 1) {
+          const int G = (lv[l].w + 3) / 4, H = lv[l].h;
+          t.og_a = (int16_t)(j * G / tx);
+          t.og_b = (int16_t)((j + 1) * G / tx);
+          t.oy_a = (int16_t)(i * H / ty);
+          t.oy_b = (int16_t)((i + 1) * H / ty);
+          if (t.og_a < t.og_b && t.oy_a < t.oy_b) {
+            if (ga < gb && ya < yb) {
+              ga = std::min(ga, (int)t.og_a);
+              gb = std::max(gb, (int)t.og_b);
+              ya = std::min(ya, (int)t.oy_a);
+              yb = std::max(yb, (int)t.oy_b);
+            } else {
+              ga = t.og_a, gb = t.og_b, ya = t.oy_a, yb = t.oy_b;
+            }
+          }
+        }
+        t.ng_a = (int16_t)ga;
+        t.ng_b = (int16_t)gb;
+        t.ny_a = (int16_t)ya;
+        t.ny_b = (int16_t)yb;
+        const int ng = gb - ga;
+        t.gmagic = ng > 0 ? (uint32_t)((0x100000000ull + 4 * ng - 1) / (4 * ng)) : 0u;  // items / (4 ng) columns
+        if (ga >= gb || ya >= yb) t.ng_a = t.ng_b = t.ny_a = t.ny_b = 0;  // nothing computed
+        if (l >= 1 && l + 1 < L && ga < gb && ya < yb) half = std::max(half, (ng + 3) * (yb - ya));
+        fg_a = fg_b = fy_a = fy_b = 0;
+        if (l >= 1 && ga < gb && ya < yb) {  // what this computed region reads of level l - 1
+          const LevelDesc& d = lv[l];
+          const LevelDesc& s = lv[l - 1];
+          fy_a = std::min(std::max(yt[d.tab_y + ya].x, 0), s.h - 1);
+          fy_b = std::min(std::max(yt[d.tab_y + yb - 1].x + 1, 0), s.h - 1) + 1;
+          fg_a = rgx0[d.rgrp_begin + ga] >> 2;
+          fg_b = (std::min(rgx0[d.rgrp_begin + gb - 1] + 7, s.w - 1) >> 2) + 1;
+        }
+      }
+      int off = 0;  // the staged tables, levels 1..L-1
+      for (int l = 1; l < L; l++) {
+        T[l].tab_off = off;
+        off += 9 * (T[l].ng_b - T[l].ng_a) + 2 * (T[l].ny_b - T[l].ny_a);
+      }
+      tab = std::max(tab, off);
+      out.insert(out.end(), T.begin(), T.end());
+    }
+  half = std::max(half, 1);
+  tab_dw = tab;
+  if ((2 * (size_t)half + tab) * 4 > 64 * 1024) {
+    out.clear();
+    return 0;
+  }
+  return half;
+}
 static void drop_graphs(orbfe_extractor* h);
 static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   if (h->rows == rows && h->cols == cols && h->geom_mode == h->resize_mode) return ORBFE_OK;
@@ -2499,6 +2785,23 @@ static int compute_geometry(orbfe_extractor* h, int rows, int cols) {
   h->scan_cap = h->oct_all.scan_cap;
   h->key_lds_cap = h->oct_all.key_lds_cap;
   (void)ncap;
+  for (int k = 0; k < 2; k++) {
+    orbfe_extractor::PyrPlan& P = k == 0 ? h->pyr_small : h->pyr_batch;
+    const int* tt = k == 0 ? h->pyr_tiles_small : h->pyr_tiles_batch;
+    hipFree(P.d_tiles);
+    P = orbfe_extractor::PyrPlan();
+    std::vector<PyrTileLevel> tiles;
+    int tab_dw = 0;
+    const int half = pyramid_plan(lv, yt, rgx0, tt[0], tt[1], tiles, tab_dw);
+    if (half > 0) {
+      ORBFE_HIP_CHECK(hipMalloc(&P.d_tiles, sizeof(PyrTileLevel) * tiles.size()));
+      ORBFE_HIP_CHECK(
+          hipMemcpy(P.d_tiles, tiles.data(), sizeof(PyrTileLevel) * tiles.size(), hipMemcpyHostToDevice));
+      P.ntiles = tt[0] * tt[1];
+      P.half_dw = half;
+      P.lds = sizeof(uint32_t) * (2 * (size_t)half + (size_t)tab_dw);
+    }
+  }
   h->rows = rows;
   h->cols = cols;
   h->geom_mode = h->resize_mode;
@@ -2744,7 +3047,26 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   };
   side_fast(0);
   if (lat && k_side == 1) launch_octree(side, 0, 1, h->oct_all);
-  for (int l = 1; l < h->nlevels; l++) {
+  const orbfe_extractor::PyrPlan& pp = n < 8 ? h->pyr_small : h->pyr_batch;
+  if (pp.ntiles > 0) {
+    // levels 1..L-1 in one launch (k_pyramid); the side's FAST levels 1..k-1 then in one launch
+    #ifdef ORBFE_PYR_CLOCKS
+    static const int pyr_dbg = getenv("ORBFE_PYR_CLOCKS") ? 1 : 0;  // phase clocks (a timing build)
+#else
+    constexpr int pyr_dbg = 0;
+#endif
+    ORBFE_LAUNCH("k_pyramid", k_pyramid, dim3(pp.ntiles, n), dim3(PYR_NT), pp.lds, st, a, pp.d_tiles, pp.half_dw, pyr_dbg);
+    if (k_side > 1) {
+      const hipEvent_t e = h->ev_lvl[1];
+      ORBFE_HIP_CHECK(hipEventRecord(e, st));
+      ORBFE_HIP_CHECK(hipStreamWaitEvent(side, e, 0));
+      const int st_ = launch_fast(side, h->levels[1].cell_begin,
+                                  k_side < h->nlevels ? h->levels[k_side].cell_begin : a.ncells);
+      if (st_ != ORBFE_OK) return st_;
+      if (lat) launch_octree(side, 0, k_side, h->oct_all);
+    }
+  }
+  for (int l = 1; l < h->nlevels && pp.ntiles == 0; l++) {
     const LevelDesc& d = h->levels[l];
     if (d.rwin_ok) {
       const int G = (d.w + 3) / 4, items = G * ((d.h + 1) / 2);
@@ -2846,7 +3168,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch),
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch), (uintptr_t)h->pyr_small.d_tiles, (uintptr_t)h->pyr_batch.d_tiles,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3041,6 +3363,8 @@ extern "C" int orbfe_extractor_destroy(orbfe_extractor* h) {
   hipFree(h->d_ywin);
   hipFree(h->d_rgrp);
   hipFree(h->d_rgx0);
+  hipFree(h->pyr_small.d_tiles);
+  hipFree(h->pyr_batch.d_tiles);
   hipFree(h->d_in);
   hipFree(h->d_out);
   if (h->h_in) hipHostFree(h->h_in);
@@ -3714,6 +4038,20 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_pyramid_tiles(orbfe_extractor* h, int small_tx, int small_ty, int batch_tx,
+                                             int batch_ty) {
+  auto ok = [](int x, int y) { return (x == 0 && y == 0) || (x > 0 && y > 0 && x * y <= 4096); };
+  if (!h || !ok(small_tx, small_ty) || !ok(batch_tx, batch_ty))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_pyramid_tiles: 0 x 0 or a positive tiling");
+  h->pyr_tiles_small[0] = small_tx;
+  h->pyr_tiles_small[1] = small_ty;
+  h->pyr_tiles_batch[0] = batch_tx;
+  h->pyr_tiles_batch[1] = batch_ty;
+  h->rows = h->cols = -1;  // the tile plans follow on the next call's geometry
+  drop_graphs(h);
   return ORBFE_OK;
 }
 

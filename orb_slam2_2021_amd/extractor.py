@@ -314,6 +314,12 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
                 "set_octree_threads")
 
+    def debug_set_pyramid_tiles(self, small=(0, 0), batch=(0, 0)) -> None:
+        """ComputePyramid's levels 1.. in one k_pyramid launch of tx x ty tiles per image for calls of
+        fewer than 8 images / batches of 8+ ((0, 0): one resize launch per level)."""
+        L.check(self._lib.orbfe_debug_set_pyramid_tiles(self._h, int(small[0]), int(small[1]), int(batch[0]),
+                                                        int(batch[1])), "set_pyramid_tiles")
+
     def debug_set_latency_schedule(self, k: int) -> None:
         """Calls of fewer than 8 images: FAST and DistributeOctTree of levels 0..k-1 on the side stream
         beside the main stream's levels k.. (default 1; k <= 0: the throughput schedule)."""

@@ -1,6 +1,7 @@
 """One 1241x376 image through orbfe_extract, 60 calls per schedule (latency k = 1, then the
 throughput schedule; latency k = 1), for a rocprofv3 kernel / memory-copy trace of the C2 call's timeline.
-usage: rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -- python3 profiles/scripts/r5_c2_trace.py"""
+With arguments tx,ty ...: latency k = 1 with k_pyramid at each tiling instead (0,0: the chain).
+usage: rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -- python3 profiles/scripts/r5_c2_trace.py [tx,ty ...]"""
 import os
 import sys
 import time
@@ -18,9 +19,13 @@ def main():
     rows, cols = 376, 1241
     img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
-    for k in (1, 0):
+    tilings = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+    modes = [(1, t) for t in tilings] if tilings else [(1, None), (0, None)]
+    for k, t in modes:
         e = ORBextractor(2000, 1.2, 8, 20, 7)
         e.debug_set_latency_schedule(k)
+        if t is not None:
+            e.debug_set_pyramid_tiles(t, (0, 0))
         cap = e.max_keypoints(rows, cols)
         kp, d, n = np.zeros(cap, L.KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8), c_int()
         for i in range(60):
@@ -28,7 +33,7 @@ def main():
             L.check(lib.orbfe_extract(e._h, L.ptr(img), rows, cols, c_size_t(cols), L.ptr(kp), cap, L.ptr(d),
                                       byref(n)), "orbfe_extract")
             if i == 59:
-                print(f"k={k} last call {(time.perf_counter() - t0) * 1e3:.3f} ms", flush=True)
+                print(f"k={k} tiles={t} last call {(time.perf_counter() - t0) * 1e3:.3f} ms", flush=True)
         time.sleep(0.05)  # a gap in the trace between the schedules
 
 

@@ -195,6 +195,46 @@ def test_octree_block_sizes(require_gpu, threads, cap):
             assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
+def _extract_device_batch(ext, imgs):
+    import torch
+    imgs = np.stack(imgs)
+    n, H, W = imgs.shape
+    cap = ext.max_keypoints(H, W)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(imgs).to(dev)
+    kps = torch.empty(n * cap * 28, dtype=torch.uint8, device=dev)
+    desc = torch.empty(n * cap * 32, dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    ext.extract_batch_device(n, d_in.data_ptr(), H * W, H, W, W, kps.data_ptr(), desc.data_ptr(), cap,
+                             cnt.data_ptr())
+    torch.cuda.synchronize()
+    C = cnt.cpu().numpy()
+    K = kps.cpu().numpy().view(KEYPOINT_DTYPE).reshape(n, cap)
+    D = desc.cpu().numpy().reshape(n, cap, 32)
+    return [(K[i, :C[i]], D[i, :C[i]] if C[i] else None) for i in range(n)]
+
+
+@pytest.mark.parametrize("tiles", [(2, 2), (4, 4), (8, 6), (16, 8), (3, 5), (32, 24), (1, 1)])
+def test_pyramid_tiles(require_gpu, tiles):
+    """ComputePyramid's levels 1.. in one k_pyramid launch (each workgroup builds its tile of every
+    level with the previous level in LDS and the halo recomputed): the same bytes as the per-level
+    chain on KITTI, TUM and odd shapes, 1 image (the small calls' plan) and an 8-image device batch
+    (the batches' plan), textured and noise; (1, 1) needs more LDS than a tile may hold and falls
+    back to the chain."""
+    rng = np.random.default_rng(23)
+    for params, shape in (((2000, 1.2, 8, 20, 7), (376, 1241)), ((1000, 1.2, 8, 20, 7), (480, 640)),
+                          ((500, 1.2, 8, 20, 7), (301, 517)), ((800, 1.1, 12, 20, 7), (480, 640)),
+                          ((1000, 2.0, 3, 20, 7), (600, 1241)), ((500, 1.2, 2, 20, 7), (377, 643))):
+        ext, ref = ORBextractor(*params), RefExtractor(*params)
+        ext.debug_set_pyramid_tiles(tiles, tiles)
+        img = synth_frame(33, *shape)
+        assert_same_extraction(ext, ref, img)
+        imgs = [synth_frame(34 + i, *shape) for i in range(7)] + [rng.integers(0, 256, shape, dtype=np.uint8)]
+        outs = _extract_device_batch(ext, imgs)
+        for i in reversed(range(len(imgs))):
+            assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_large_scale_factors(require_gpu, params):
     """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
