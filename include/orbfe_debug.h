@@ -41,9 +41,15 @@ int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k);
 int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batches);
 /* ComputePyramid's levels 1..L-1 in one k_pyramid launch of tx x ty tiles per image (each
  * workgroup builds its tile of every level, the previous level in LDS, the halo recomputed) for
- * calls of fewer than 8 images / batches of 8+; 0, 0: one k_resize_win launch per level. Same
- * bytes either way; a tiling whose tile needs more than 64 KiB of LDS falls back to the chain. */
+ * calls of fewer than 8 images (default 16 x 12) / batches of 8+ (default 0 x 0: one k_resize_win
+ * launch per level). Same bytes either way; a tiling whose tile needs more than 64 KiB of LDS falls
+ * back to the chain. */
 int orbfe_debug_set_pyramid_tiles(orbfe_extractor* h, int small_tx, int small_ty, int batch_tx, int batch_ty);
+/* Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image straight from pinned host
+ * memory (input != 0, the default) instead of after a separate H2D copy, and (output != 0, the
+ * default; calls without a device-side consumer of the outputs) the kernels write the results into
+ * the pinned host mirror instead of a device block copied down afterwards. Same results. */
+int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */
 int orbfe_debug_set_octree_lds(orbfe_extractor* h, int hi_kb, int lo_kb);

@@ -2458,7 +2458,15 @@ struct orbfe_extractor {
   std::vector<hipEvent_t> ev_in, ev_ext, ev_out;
   // pinned staging of the host-buffer entry points
   uint8_t* h_in = nullptr;
+  uint8_t* h_in_dev = nullptr;  // h_in as the device addresses it (k_copy0 reads it over PCIe)
   size_t h_in_bytes = 0;
+  // calls of < 8 images: k_copy0 reads the staged images straight from pinned host memory instead
+  // of after a separate H2D copy (orbfe_debug_set_zero_copy)
+  int zc_in = 1;
+  // ... and k_octree / k_describe write the results straight into the pinned mirror h_out instead
+  // of a device block copied down afterwards (plain calls: no hook reads the device outputs)
+  int zc_out = 1;
+  uint8_t* h_out_dev = nullptr;
   uint8_t* h_out = nullptr;
   size_t h_out_bytes = 0;
   // last call (for get_level)
@@ -3538,9 +3546,11 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
     h->out_n_alloc = 0;
     if (h->h_out) hipHostFree(h->h_out);
     h->h_out = nullptr;
+    h->h_out_dev = nullptr;
     h->h_out_bytes = 0;
     ORBFE_HIP_CHECK(hipMalloc(&h->d_out, bytes));
-    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_out, bytes, hipHostMallocDefault));
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_out, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    ORBFE_HIP_CHECK(hipHostGetDevicePointer((void**)&h->h_out_dev, h->h_out, 0));
     h->d_kps = reinterpret_cast<orbfe_keypoint*>(h->d_out);
     h->d_desc = h->d_out + cap * sizeof(orbfe_keypoint);
     h->d_counts = reinterpret_cast<int32_t*>(h->d_desc + cap * 32);
@@ -3551,8 +3561,11 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
   if (need_in > h->h_in_bytes) {
     if (h->h_in) hipHostFree(h->h_in);
     h->h_in = nullptr;
-    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_in, hipHostMallocDefault));
+    h->h_in_dev = nullptr;
+    // coherent (fine-grained): k_copy0's reads of it over PCIe are never served from a GPU cache
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_in, hipHostMallocMapped | hipHostMallocCoherent));
     h->h_in_bytes = need_in;
+    ORBFE_HIP_CHECK(hipHostGetDevicePointer((void**)&h->h_in_dev, h->h_in, 0));
   }
   return ORBFE_OK;
 }
@@ -3663,6 +3676,9 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   // small batches (a single image: orbfe_extract) stay on the handle's stream, in one piece:
   // the cross-stream event hops cost more latency than the overlap saves
   const bool small = n < 8;
+  // (one KITTI image: orbfe_extract p50 0.152 with the input read over PCIe by k_copy0, 0.159 after
+  // an H2D copy; profiles/r6_c2_zero_copy.txt)
+  const bool zc_in = small && !direct_in && h->zc_in && h->h_in_dev;
   const int nchunks = ngroups * cpg, npieces = small ? 1 : 2 * ngroups;
   st = ensure_pipeline(h, std::max(nchunks, npieces));
   if (st != ORBFE_OK) return st;
@@ -3686,6 +3702,14 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   // prefix when the block is not much larger than the call (one copy engine transfer instead of
   // three, the counts' through a blit kernel among them: one image 0.17-0.18 vs 0.18-0.20 ms)
   const bool one_copy = small && !direct_out && h->out_cap_alloc <= 2 * (size_t)n * K + 64;
+  // (zero copy out: the kernels' result stores cross PCIe as they happen; with zero copy in 0.134
+  // vs 0.152 ms p50, profiles/r6_c2_zero_copy.txt)
+  const bool zc_out = one_copy && !after_launch && h->zc_out && h->h_out_dev;
+  orbfe_keypoint* o_kps = zc_out ? reinterpret_cast<orbfe_keypoint*>(h->h_out_dev) : h->d_kps;
+  uint8_t* o_desc = zc_out ? h->h_out_dev + (h->d_desc - h->d_out) : h->d_desc;
+  int32_t* o_counts =
+      zc_out ? reinterpret_cast<int32_t*>(h->h_out_dev + (reinterpret_cast<uint8_t*>(h->d_counts) - h->d_out))
+             : h->d_counts;
   static const bool trace = std::getenv("ORBFE_HOST_TRACE") != nullptr;  // phase times to stderr
   auto now = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = trace ? now() : 0.0;
@@ -3717,6 +3741,7 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       } else {  // a small chunk (a single image): the workers' wake-up costs more than the copy
         for (int task = 0; task < nc * bands; task++) stage(task);
       }
+      if (zc_in) continue;  // k_copy0 reads the staging buffer itself
       ORBFE_HIP_CHECK(hipMemcpyAsync(h->d_in + (size_t)i0 * img_bytes, h->h_in + (size_t)i0 * img_bytes,
                                      (size_t)nc * img_bytes, hipMemcpyHostToDevice, s_in));
     }
@@ -3726,8 +3751,8 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_in[g], h->h2d));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->stream, h->ev_in[g], 0));
     }
-    st = launch_extract_graphed(h, ng, h->d_in + (size_t)g0 * img_bytes, (long long)img_bytes, cols,
-                                h->d_kps + (size_t)g0 * K, h->d_desc + (size_t)g0 * K * 32, K, h->d_counts + g0,
+    st = launch_extract_graphed(h, ng, (zc_in ? h->h_in_dev : h->d_in) + (size_t)g0 * img_bytes, (long long)img_bytes, cols,
+                                o_kps + (size_t)g0 * K, o_desc + (size_t)g0 * K * 32, K, o_counts + g0,
                                 h->stream, g0);
     if (st != ORBFE_OK) return st;
     if (trace) std::fprintf(stderr, "[host] group %d launched %.1f\n", g, now() - t_start);
@@ -3748,6 +3773,10 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
     if (!small) {
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_ext[g], h->stream));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->d2h, h->ev_ext[g], 0));
+    }
+    if (zc_out) {  // the results are in h_out once the stream gets here
+      ORBFE_HIP_CHECK(hipEventRecord(h->ev_out[0], s_out));
+      continue;
     }
     if (one_copy) {  // (small: one group, one piece)
       const size_t span = (reinterpret_cast<uint8_t*>(h->d_counts) - h->d_out) + sizeof(int32_t) * (size_t)n;
@@ -4038,6 +4067,13 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_zero_copy: null handle");
+  h->zc_in = input ? 1 : 0;
+  h->zc_out = output ? 1 : 0;
   return ORBFE_OK;
 }
 

@@ -314,6 +314,13 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
                 "set_octree_threads")
 
+    def debug_set_zero_copy(self, inp: bool, out: Optional[bool] = None) -> None:
+        """Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image from pinned host
+        memory, and the kernels write the results into the pinned host mirror (both default) instead
+        of H2D / D2H copies (out defaults to inp)."""
+        out = inp if out is None else out
+        L.check(self._lib.orbfe_debug_set_zero_copy(self._h, int(bool(inp)), int(bool(out))), "set_zero_copy")
+
     def debug_set_pyramid_tiles(self, small=(0, 0), batch=(0, 0)) -> None:
         """ComputePyramid's levels 1.. in one k_pyramid launch of tx x ty tiles per image for calls of
         fewer than 8 images / batches of 8+ ((0, 0): one resize launch per level)."""

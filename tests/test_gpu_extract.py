@@ -243,6 +243,28 @@ def test_large_scale_factors(require_gpu, params):
     assert_same_extraction(ORBextractor(*params), RefExtractor(*params), img)
 
 
+@pytest.mark.parametrize("zc_in,zc_out", [(True, True), (True, False), (False, True), (False, False)])
+def test_host_calls_alternating_images(require_gpu, zc_in, zc_out):
+    """Single-image host-buffer calls through one handle with the image changing every call (A B C A B
+    C ...): k_copy0 reading the staging buffer over PCIe (zero copy in, the default) or after an H2D
+    copy must see each call's bytes, and the results written straight into the pinned host mirror
+    (zero copy out, the default) or copied down must be each call's own -- every call equals the
+    oracle."""
+    ext, ref = ORBextractor(1000, 1.2, 8, 20, 7), RefExtractor(1000, 1.2, 8, 20, 7)
+    ext.debug_set_zero_copy(zc_in, zc_out)
+    imgs = [synth_frame(50 + i, 240, 333) for i in range(3)]
+    expect = [ref(im) for im in imgs]
+    for r in range(4):
+        for i, im in enumerate(imgs):
+            kg, dg = ext(im)
+            kr, dr = expect[i]
+            assert len(kg) == len(kr), f"round {r} image {i}: {len(kg)} vs {len(kr)} keypoints"
+            for f in ("x", "y", "octave", "response"):
+                assert np.array_equal(kg[f], kr[f]), f"round {r} image {i}: field {f}"
+            assert np.array_equal(dg, dr), f"round {r} image {i}: descriptors"
+    assert_same_extraction(ext, ref, imgs[-1], got=(kg, dg))
+
+
 def test_empty_image(require_gpu):
     k, d = ORBextractor(2000, 1.2, 8, 20, 7)(np.zeros((0, 0), np.uint8))
     assert len(k) == 0 and d is None
