@@ -3264,10 +3264,35 @@ static int ensure_host_pyramid(orbfe_extractor* h, int n) {
 // C ABI
 // The side stream gets the highest priority: the runtime serves each priority from its own
 // hardware queues, so k_blur cannot land behind the caller's stream on a shared queue.
+// ORBFE_DEDICATED_QUEUES=1: a handle's own streams (the launch stream and the side stream of its
+// host-buffer calls, the copy streams of large host batches) each get a hardware queue of their own
+// -- a stream created with a CU mask (here: every CU) is not placed on the runtime's shared pool
+// (GPU_MAX_HW_QUEUES, 4 by default). On the pool, with 4+ idle extractor handles alive, one image
+// through orbfe_extract took 0.275-0.283 vs 0.130-0.135 ms p50 (idle torch streams of either
+// priority did not do it); with dedicated queues 0.130 at any handle count
+// (profiles/r6_c2_queues.txt). Not the default: in the bench process, whose legs create many
+// handles, the extra queues slowed the host-fed C3 leg 48.6k -> 22.9k stereo frames/s, the tracking
+// leg 978 -> 511 frames/s and C5 2,736 -> 429 (hardware queue oversubscription).
+static hipError_t create_masked_stream(hipStream_t* s) {
+  int dev = 0, ncu = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return hipErrorUnknown;
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0xffffffffu);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+static bool cu_mask_streams() {
+  static const bool on = std::getenv("ORBFE_DEDICATED_QUEUES") != nullptr;
+  return on;
+}
 static hipError_t create_side_stream(hipStream_t* s) {
+  if (cu_mask_streams()) return create_masked_stream(s);
   int lo = 0, hi = 0;
   if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+static hipError_t create_main_stream(hipStream_t* s) {
+  if (cu_mask_streams()) return create_masked_stream(s);
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
 extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nlevels,
@@ -3321,7 +3346,7 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
     ++v0;
   }
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      create_main_stream(&h->stream) != hipSuccess ||
       create_side_stream(&h->side) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, kForkJoinEvent) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, kForkJoinEvent) != hipSuccess ||
@@ -3431,8 +3456,10 @@ extern "C" int orbfe_stream_create(int device, int high_priority, void** out) {
   *out = nullptr;
   hipStream_t s = nullptr;
   ORBFE_HIP_CHECK(hipSetDevice(device));
-  if (high_priority) {
-    ORBFE_HIP_CHECK(create_side_stream(&s));
+  if (high_priority) {  // (a pooled stream at the highest priority, as requested)
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    ORBFE_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
   } else {
     ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   }
@@ -3618,8 +3645,8 @@ static int ensure_pipeline(orbfe_extractor* h, int nchunks) {
     const unsigned hc = std::thread::hardware_concurrency();
     h->pool = new HostPool((int)std::min(7u, hc > 1 ? hc - 1 : 0u));
   }
-  if (!h->h2d) ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&h->h2d, hipStreamNonBlocking));
-  if (!h->d2h) ORBFE_HIP_CHECK(hipStreamCreateWithFlags(&h->d2h, hipStreamNonBlocking));
+  if (!h->h2d) ORBFE_HIP_CHECK(create_main_stream(&h->h2d));  // (queues of their own: see create_masked_stream)
+  if (!h->d2h) ORBFE_HIP_CHECK(create_main_stream(&h->d2h));
   while ((int)h->ev_in.size() < nchunks) {
     hipEvent_t a = nullptr, b = nullptr, c = nullptr;
     ORBFE_HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
