@@ -45,6 +45,15 @@ int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batc
  * launch per level). Same bytes either way; a tiling whose tile needs more than 64 KiB of LDS falls
  * back to the chain. */
 int orbfe_debug_set_pyramid_tiles(orbfe_extractor* h, int small_tx, int small_ty, int batch_tx, int batch_ty);
+/* Calls of fewer than 8 images pick, per image count, between the latency schedule on the handle's two
+ * streams and the same launch sequence on its launch stream alone by timing their first host-buffer
+ * calls (4 warm-up, then 6 of each, alternating; one stream only if its mean, the largest sample
+ * of each side dropped, is < 0.9x): the
+ * runtime may have put both streams on one hardware queue, where cross-stream waits are slow.
+ * enable = 0 (or ORBFE_SCHED_AUTOTUNE=0): always two streams. Resets the timings. */
+int orbfe_debug_set_schedule_autotune(orbfe_extractor* h, int enable);
+/* The autotune's choice for calls of n_images (1..7) images: -1 still timing, 0 two streams, 1 one. */
+int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_images);
 /* Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image straight from pinned host
  * memory (input != 0, the default) instead of after a separate H2D copy, and (output != 0, the
  * default; calls without a device-side consumer of the outputs) the kernels write the results into

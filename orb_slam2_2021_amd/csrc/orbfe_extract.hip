@@ -2393,6 +2393,19 @@ struct orbfe_extractor {
   int octree_split = 5;              // orbfe_debug_set_octree_split: levels 0..k-1 and k..L-1 in two launches
                                      // (k = 5 86.7-86.9k vs 4 85.7-85.9k stereo frames/s, round 6)
   int lat_sched = 1;                 // orbfe_debug_set_latency_schedule: levels on the side (< 8 images)
+  // Calls of fewer than 8 images choose per image count between the latency schedule on two streams
+  // and the same sequence on the launch stream alone, by timing their first host-buffer calls:
+  // when the runtime has put the handle's launch and side streams on one hardware queue (its pool
+  // holds GPU_MAX_HW_QUEUES queues, 4 by default, for all the process's streams), the cross-stream
+  // waits cost ~140 us per call -- one KITTI image 0.275-0.283 ms with 4+ idle handles alive vs
+  // 0.183 on one stream and 0.130-0.135 on two distinct queues (profiles/r6_c2_queues.txt).
+  // orbfe_debug_set_schedule_autotune(h, 0) (or ORBFE_SCHED_AUTOTUNE=0): always two streams.
+  struct SchedTune {
+    int calls = 0, decided = -1;  // decided: -1 still timing, 0 two streams, 1 the launch stream
+    std::vector<double> t_two, t_one;
+  } tune[8];
+  int autotune = 1;
+  bool call_inline = false;          // this call's choice (launch_extract)
   int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
   int oct_threads_batch = 256;       // ... and for batches of 8+
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
@@ -2930,7 +2943,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   // the handle's high-priority side stream (k_blur and the early FAST levels beside the main chain),
   // or the launch stream itself when the caller overlaps whole extractions instead
   // (orbfe_debug_set_inline_side)
-  const hipStream_t side = h->inline_side ? st : (h->side_ext ? h->side_ext : h->side);
+  const hipStream_t side = (h->inline_side || (h->call_inline && n < 8)) ? st : (h->side_ext ? h->side_ext : h->side);
   ExtractArgs a;
   std::memset(&a, 0, sizeof(a));
   a.levels = h->d_levels;
@@ -3295,6 +3308,7 @@ static hipError_t create_main_stream(hipStream_t* s) {
   return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
+
 extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nlevels,
                                       int ini_th_fast, int min_th_fast, int device,
                                       orbfe_extractor** out) {
@@ -3307,6 +3321,10 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
   if (device < 0 || device >= ndev) return orbfe_set_error(ORBFE_ERR_ARG, "bad device index");
   orbfe_extractor* h = new orbfe_extractor();
   h->device = device;
+  {
+    const char* e = std::getenv("ORBFE_SCHED_AUTOTUNE");
+    h->autotune = (e && e[0] == '0') ? 0 : 1;
+  }
   h->nfeatures = nfeatures;
   h->nlevels = nlevels;
   h->ini_th = ini_th_fast;
@@ -3544,6 +3562,7 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
   st = wait_host_pyramid(h, s);
   if (st != ORBFE_OK) return st;
   h->device_call = true;
+  h->call_inline = n < 8 && h->autotune && h->tune[n].decided == 1;
   st = launch_extract_graphed(h, n, d_imgs, (long long)image_stride, (int)pitch, d_kps, d_desc, cap,
                               d_counts, s);
   h->device_call = false;
@@ -3717,6 +3736,25 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
     if (st != ORBFE_OK) return st;
   }
   const hipStream_t s_in = small ? h->stream : h->h2d, s_out = small ? h->stream : h->d2h;
+  // the schedule autotune (orbfe_extractor::SchedTune): 4 warm-up calls (both arms), then
+  // alternate two streams / one stream until each has 6 timings; one stream is kept if its mean
+  // (the largest sample of each arm dropped) is below 0.9x. On a shared queue the two-stream
+  // calls swing between ~180, ~290 and ~400 us (profiles/r6_c2_queues.txt), so the mean, not the
+  // median, carries the penalty; on distinct queues both arms are steady (~137 vs ~185 us)
+  orbfe_extractor::SchedTune* tune = nullptr;
+  int tune_arm = -1;
+  const auto t_call = std::chrono::steady_clock::now();
+  h->call_inline = false;
+  if (small && h->autotune && !h->inline_side && !h->side_ext && !h->use_graphs && h->lat_sched > 0) {
+    tune = &h->tune[n];
+    if (tune->decided >= 0) {
+      h->call_inline = tune->decided == 1;
+    } else {
+      const int k = tune->calls++;
+      if (k >= 4) tune_arm = k % 2;  // 0: two streams, 1: the launch stream
+      h->call_inline = (k % 2) == 1;
+    }
+  }
   const int K = h->total_key_slots;
   const size_t img_bytes = (size_t)rows * cols;
   const int band = 64;  // staging rows per task
@@ -3846,6 +3884,20 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   }
   if (need > cap || (need > 0 && (!kps || !desc))) ORBFE_HIP_CHECK(hipStreamSynchronize(s_out));
   if (trace) std::fprintf(stderr, "[host] done %.1f\n", now() - t_start);
+  h->call_inline = false;
+  if (tune_arm >= 0) {
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count();
+    (tune_arm ? tune->t_one : tune->t_two).push_back(us);
+    if (tune->t_one.size() >= 6 && tune->t_two.size() >= 6) {
+      auto trimmed_mean = [](std::vector<double> v) {
+        std::sort(v.begin(), v.end());
+        double sum = 0;
+        for (size_t i = 0; i + 1 < v.size(); i++) sum += v[i];
+        return sum / (double)(v.size() - 1);
+      };
+      tune->decided = trimmed_mean(tune->t_one) < 0.9 * trimmed_mean(tune->t_two) ? 1 : 0;
+    }
+  }
   if (need > cap) return orbfe_set_error(ORBFE_ERR_CAPACITY, "keypoint capacity too small");
   if (need > 0 && (!kps || !desc)) return orbfe_set_error(ORBFE_ERR_ARG, "null output buffer");
   return ORBFE_OK;
@@ -4095,6 +4147,18 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
   return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_schedule_autotune(orbfe_extractor* h, int enable) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_schedule_autotune: null handle");
+  h->autotune = enable ? 1 : 0;
+  for (auto& t : h->tune) t = orbfe_extractor::SchedTune();
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_images) {
+  if (!h || n_images < 1 || n_images > 7) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_schedule_choice: bad argument");
+  return h->tune[n_images].decided;
 }
 
 extern "C" int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output) {

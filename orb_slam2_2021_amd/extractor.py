@@ -314,6 +314,15 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
                 "set_octree_threads")
 
+    def debug_set_schedule_autotune(self, on: bool) -> None:
+        """Calls of fewer than 8 images: time the latency schedule on two streams against one stream
+        over the first host-buffer calls and keep the faster (default on); off: always two."""
+        L.check(self._lib.orbfe_debug_set_schedule_autotune(self._h, int(bool(on))), "set_schedule_autotune")
+
+    def debug_schedule_choice(self, n_images: int = 1) -> int:
+        """-1 still timing, 0 two streams, 1 the launch stream alone (calls of n_images images)."""
+        return int(self._lib.orbfe_debug_schedule_choice(self._h, int(n_images)))
+
     def debug_set_zero_copy(self, inp: bool, out: Optional[bool] = None) -> None:
         """Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image from pinned host
         memory, and the kernels write the results into the pinned host mirror (both default) instead

@@ -36,6 +36,8 @@ def fresh(mode):
         e.debug_set_inline_side(True)
     elif mode == "throughput":
         e.debug_set_latency_schedule(0)
+    elif mode == "two_streams":
+        e.debug_set_schedule_autotune(False)
     return e
 
 
@@ -43,7 +45,7 @@ def main():
     ks = [int(a) for a in sys.argv[1:]] or [4, 12]
     img = np.ascontiguousarray(synth_frame(3, 376, 1241))
     keep = []
-    modes = ("default", "inline_side", "throughput")
+    modes = ("default", "two_streams", "inline_side")
     print(f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')}  run_idle={os.environ.get('RUN_IDLE', '1')}")
     for m in modes:
         print(f"idle handles 0 {m:12s}: p50 {p50(fresh(m), img):.4f} ms", flush=True)
@@ -57,7 +59,14 @@ def main():
             keep.append(torch.cuda.Stream())
             have += 1
         for m in modes:
-            print(f"idle handles {k} {m:12s}: p50 {p50(fresh(m), img):.4f} ms", flush=True)
+            e = fresh(m)
+            t = p50(e, img)
+            extra = ""
+            if m == "default":  # the same handle (same queues) with two streams forced
+                choice = e.debug_schedule_choice(1)
+                e.debug_set_schedule_autotune(False)
+                extra = f"  (autotune choice {choice}; this handle with two streams forced: {p50(e, img):.4f} ms)"
+            print(f"idle handles {k} {m:12s}: p50 {t:.4f} ms{extra}", flush=True)
 
 
 if __name__ == "__main__":

@@ -265,6 +265,30 @@ def test_host_calls_alternating_images(require_gpu, zc_in, zc_out):
     assert_same_extraction(ext, ref, imgs[-1], got=(kg, dg))
 
 
+def test_schedule_autotune_decides_and_stays_exact(require_gpu):
+    """Calls of fewer than 8 images time the two-stream latency schedule against the launch stream
+    alone over their first host-buffer calls (per image count) and keep one: the choice is made by
+    the 16th call, every call of both arms equals the oracle, and switching the autotune off
+    resets it (two streams)."""
+    ext, ref = ORBextractor(1000, 1.2, 8, 20, 7), RefExtractor(1000, 1.2, 8, 20, 7)
+    imgs = [synth_frame(60 + i, 240, 333) for i in range(2)]
+    expect = [ref(im) for im in imgs]
+    assert ext.debug_schedule_choice(1) == -1
+    for i in range(18):
+        kg, dg = ext(imgs[i % 2])
+        kr, dr = expect[i % 2]
+        assert len(kg) == len(kr) and np.array_equal(kg["x"], kr["x"]) and np.array_equal(dg, dr), f"call {i}"
+    assert ext.debug_schedule_choice(1) in (0, 1)
+    assert ext.debug_schedule_choice(2) == -1  # per image count
+    outs = ext.extract_batch(imgs)
+    for i in range(2):
+        assert np.array_equal(outs[i][1], expect[i][1])
+    ext.debug_set_schedule_autotune(False)
+    assert ext.debug_schedule_choice(1) == -1
+    kg, dg = ext(imgs[0])
+    assert np.array_equal(dg, expect[0][1])
+
+
 def test_empty_image(require_gpu):
     k, d = ORBextractor(2000, 1.2, 8, 20, 7)(np.zeros((0, 0), np.uint8))
     assert len(k) == 0 and d is None
