@@ -106,6 +106,8 @@ def parse(argv=None):
                    help="DistributeOctTree launch split (orbfe_debug_set_octree_split): levels 0..K-1 at 80 KiB of "
                         "LDS per block, K.. at 40 KiB; 0: one launch (default: the library's, 5: 86.7-86.9k vs 85.7-85.9k "
                         "at 4 and 84.0-84.1k at 0, rounds 5-6)")
+    p.add_argument("--fast-side-merge", action="store_true",
+                   help="side-stream FAST levels 1..k-1 in one launch (orbfe_debug_set_fast_side_merge)")
     p.add_argument("--pyramid-tiles", default="",
                    help="k_pyramid tiles per image sx,sy,bx,by for calls of < 8 images / batches "
                         "(orbfe_debug_set_pyramid_tiles; 0,0: the per-level resize chain)")
@@ -574,6 +576,9 @@ def main():
         small, batch = (int(x) for x in args.octree_threads.split(","))
         for e in exts:
             e.debug_set_octree_threads(small, batch)
+    if args.fast_side_merge:
+        for e in exts:
+            e.debug_set_fast_side_merge(True)
     if args.pyramid_tiles:
         t = [int(x) for x in args.pyramid_tiles.split(",")]
         for e in exts:

@@ -52,6 +52,9 @@ int orbfe_debug_set_pyramid_tiles(orbfe_extractor* h, int small_tx, int small_ty
  * runtime may have put both streams on one hardware queue, where cross-stream waits are slow.
  * enable = 0 (or ORBFE_SCHED_AUTOTUNE=0): always two streams. Resets the timings. */
 int orbfe_debug_set_schedule_autotune(orbfe_extractor* h, int enable);
+/* Batches: FAST of the side-stream levels 1..k-1 (orbfe_debug_set_fast_side_levels) in one launch
+ * once level k-1 is built, instead of one launch (and event pair) per level as each is built. */
+int orbfe_debug_set_fast_side_merge(orbfe_extractor* h, int merge);
 /* The autotune's choice for calls of n_images (1..7) images: -1 still timing, 0 two streams, 1 one. */
 int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_images);
 /* Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image straight from pinned host

@@ -178,6 +178,7 @@ _SIGNATURES = {
     "orbfe_debug_set_pyramid_tiles": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
     "orbfe_debug_set_zero_copy": (c_int, [c_void_p, c_int, c_int]),
     "orbfe_debug_set_schedule_autotune": (c_int, [c_void_p, c_int]),
+    "orbfe_debug_set_fast_side_merge": (c_int, [c_void_p, c_int]),
     "orbfe_debug_schedule_choice": (c_int, [c_void_p, c_int]),
     "orbfe_debug_set_octree_lds": (c_int, [c_void_p, c_int, c_int]),
     "orbfe_debug_set_fast_wpb": (c_int, [c_void_p, c_int, c_int]),

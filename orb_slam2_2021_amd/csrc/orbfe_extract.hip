@@ -2411,6 +2411,7 @@ struct orbfe_extractor {
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
+  int fast_side_merge = 0;           // orbfe_debug_set_fast_side_merge: side FAST levels 1..k-1 in one launch
   // k_pyramid tiles per image (x, y) for calls of < 8 images / batches; 0: the per-level resize
   // chain (orbfe_debug_set_pyramid_tiles). One KITTI image: orbfe_extract p50 0.160 ms at 16 x 12
   // vs 0.169 through the chain (32 x 24 0.163, 8 x 6 0.163; profiles/r6_c2_pyramid.txt); batches
@@ -3098,7 +3099,17 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
       dim3 grid((d.w + 255) / 256, (d.h + 4 * RESIZE_ROWS - 1) / (4 * RESIZE_ROWS), n), block(64, 4);
       ORBFE_LAUNCH("k_resize", k_resize, grid, block, 0, st, a, l);
     }
-    if (l < k_side) side_fast(l);
+    if (l < k_side) {
+      if (!h->fast_side_merge || lat) {
+        side_fast(l);
+      } else if (l == k_side - 1) {  // levels 1..k-1 in one side launch once level k-1 is built
+        ORBFE_HIP_CHECK(hipEventRecord(h->ev_lvl[l], st));
+        ORBFE_HIP_CHECK(hipStreamWaitEvent(side, h->ev_lvl[l], 0));
+        const int c1 = l + 1 < h->nlevels ? h->levels[l + 1].cell_begin : a.ncells;
+        const int r = launch_fast(side, h->levels[1].cell_begin, c1);
+        if (r != ORBFE_OK) return r;
+      }
+    }
     if (lat && l == k_side - 1) launch_octree(side, 0, k_side, h->oct_all);
   }
   // main: FAST of the other levels, then the side's FAST levels joined. Fork: GaussianBlur needs
@@ -3189,7 +3200,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch), (uintptr_t)h->pyr_small.d_tiles, (uintptr_t)h->pyr_batch.d_tiles,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->fast_side_merge, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch), (uintptr_t)h->pyr_small.d_tiles, (uintptr_t)h->pyr_batch.d_tiles,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -4146,6 +4157,13 @@ extern "C" int orbfe_debug_set_octree_split(orbfe_extractor* h, int k) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_split: null handle");
   h->octree_split = k > 0 ? k : 0;
   h->rows = h->cols = -1;  // the LDS plans follow on the next call's geometry
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_fast_side_merge(orbfe_extractor* h, int merge) {
+  if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_fast_side_merge: null handle");
+  h->fast_side_merge = merge ? 1 : 0;
+  drop_graphs(h);
   return ORBFE_OK;
 }
 

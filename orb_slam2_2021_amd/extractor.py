@@ -314,6 +314,10 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
                 "set_octree_threads")
 
+    def debug_set_fast_side_merge(self, on: bool) -> None:
+        """Batches: the side stream's FAST levels 1..k-1 in one launch after level k-1 is built."""
+        L.check(self._lib.orbfe_debug_set_fast_side_merge(self._h, int(bool(on))), "set_fast_side_merge")
+
     def debug_set_schedule_autotune(self, on: bool) -> None:
         """Calls of fewer than 8 images: time the latency schedule on two streams against one stream
         over the first host-buffer calls and keep the faster (default on); off: always two."""

@@ -235,6 +235,20 @@ def test_pyramid_tiles(require_gpu, tiles):
             assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
+@pytest.mark.parametrize("fast_side", [2, 4])
+def test_fast_side_merge(require_gpu, fast_side):
+    """Batches with the side stream's FAST levels 1..k-1 in one launch (orbfe_debug_set_fast_side_merge)
+    instead of one per level: the same candidates and keypoints, 8-image device batch."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_fast_side_levels(fast_side)
+    ext.debug_set_fast_side_merge(True)
+    rng = np.random.default_rng(29)
+    imgs = [synth_frame(70 + i, 376, 1241) for i in range(7)] + [rng.integers(0, 256, (376, 1241), dtype=np.uint8)]
+    outs = _extract_device_batch(ext, imgs)
+    for i in reversed(range(len(imgs))):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
 @pytest.mark.parametrize("params", [(1000, 2.0, 3, 20, 7), (1000, 2.5, 3, 20, 7)])
 def test_large_scale_factors(require_gpu, params):
     """Scale 2.0 still fits the 8-byte window resize (k_resize_win); 2.5 takes the byte-gather
