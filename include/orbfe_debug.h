@@ -39,6 +39,9 @@ int orbfe_debug_set_latency_schedule(orbfe_extractor* h, int k);
 /* DistributeOctTree's block size (256, 512 or 1024 threads; same results) for calls of fewer than 8
  * images (default 512) and for batches of 8+ (default 256). */
 int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batches);
+/* Calls of fewer than 8 images: the block size of the octree launch that holds level 0 (the latency
+ * schedule's side launch); 0 (default): the small calls' size. */
+int orbfe_debug_set_octree_threads_l0(orbfe_extractor* h, int threads);
 /* ComputePyramid's levels 1..L-1 in one k_pyramid launch of tx x ty tiles per image (each
  * workgroup builds its tile of every level, the previous level in LDS, the halo recomputed) for
  * calls of fewer than 8 images (default 16 x 12) / batches of 8+ (default 0 x 0: one k_resize_win
@@ -60,7 +63,9 @@ int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_images);
 /* Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image straight from pinned host
  * memory (input != 0, the default) instead of after a separate H2D copy, and (output != 0, the
  * default; calls without a device-side consumer of the outputs) the kernels write the results into
- * the pinned host mirror instead of a device block copied down afterwards. Same results. */
+ * the pinned host mirror instead of a device block copied down afterwards. input = 1 stages the
+ * image in the level-0 layout (padded rows, REFLECT_101 columns written by the host; one straight
+ * k_copy_l0), input = 2 stages plain rows that k_copy0 pads. Same results. */
 int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */

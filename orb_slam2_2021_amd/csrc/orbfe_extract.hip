@@ -581,6 +581,31 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(ExtractArgs a, const PyrTile
 }
 
 
+// k_copy_l0: level 0 from a host staging buffer the caller-side code already laid out like the
+// pyramid block (rows `pitch` apart, the REFLECT_101 columns filled on the host): one straight copy
+// of pitch x h bytes, 16-byte loads, four per thread in flight -- the zero-copy path of the small
+// host calls, where the loads cross PCIe and k_copy0's row-by-row dword loads of an unaligned row
+// ran at ~23 GB/s.
+__global__ __launch_bounds__(256) void k_copy_l0(ExtractArgs a) {
+  const LevelDesc ld = a.levels[0];
+  const int img = blockIdx.y;
+  const int n16 = (ld.pitch * ld.h) >> 4;
+  const uint4* src = reinterpret_cast<const uint4*>(a.img0 + (long long)img * a.img_stride);
+  uint4* dst = reinterpret_cast<uint4*>(a.pyr + (long long)img * a.pyr_stride + ld.pyr_off - 4);
+  const int i0 = blockIdx.x * 1024 + threadIdx.x;
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + 256 * k;
+    if (i < n16) v[k] = src[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + 256 * k;
+    if (i < n16) dst[i] = v[k];
+  }
+}
+
 // k_copy0: the input image into level 0 of the pyramid block (64-byte aligned rows, REFLECT_101
 // padding columns).
 __global__ __launch_bounds__(256) void k_copy0(ExtractArgs a) {
@@ -2408,6 +2433,7 @@ struct orbfe_extractor {
   bool call_inline = false;          // this call's choice (launch_extract)
   int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
   int oct_threads_batch = 256;       // ... and for batches of 8+
+  int oct_threads_l0 = 0;            // ... for a small call's launch that holds level 0 (0: oct_threads_small)
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -2477,6 +2503,7 @@ struct orbfe_extractor {
   // calls of < 8 images: k_copy0 reads the staged images straight from pinned host memory instead
   // of after a separate H2D copy (orbfe_debug_set_zero_copy)
   int zc_in = 1;
+  bool input_l0 = false;  // this call's input is already in the level-0 layout (k_copy_l0)
   // ... and k_octree / k_describe write the results straight into the pinned mirror h_out instead
   // of a device block copied down afterwards (plain calls: no hook reads the device outputs)
   int zc_out = 1;
@@ -3012,9 +3039,14 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
   };
   {
     const LevelDesc& d = h->levels[0];
-    dim3 grid((d.h + 3) / 4, n);
-    const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
-    ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, st, a);
+    if (h->input_l0) {
+      dim3 grid(((d.pitch * d.h) / 16 + 1023) / 1024, n);
+      ORBFE_LAUNCH("k_copy_l0", k_copy_l0, grid, dim3(256), 0, st, a);
+    } else {
+      dim3 grid((d.h + 3) / 4, n);
+      const size_t lds = 4 * sizeof(uint32_t) * (size_t)((d.pitch >> 2) + 4);
+      ORBFE_LAUNCH("k_copy0", k_copy0, grid, dim3(256), lds, st, a);
+    }
   }
   // the FAST cells of levels 0..k-1 run on the side stream, each level as soon as the main stream
   // has built it, beside the chain of small dependent resize launches that leaves most CUs idle;
@@ -3059,7 +3091,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     // KITTI image: the octree's two launches 84.6 us summed at 512 vs 95.4 at 256 and 92.9 at 1024
     // threads (16 wavefronts pay more per barrier and spill 2 VGPRs); orbfe_extract p50 0.196 vs
     // 0.198 / 0.202 ms (profiles/r6_c2_octree.txt)
-    const int nt = n < 8 ? h->oct_threads_small : h->oct_threads_batch;
+    const int nt = n >= 8 ? h->oct_threads_batch : (l0 == 0 && h->oct_threads_l0 > 0) ? h->oct_threads_l0 : h->oct_threads_small;
     if (nt == 1024)
       ORBFE_LAUNCH("k_octree", k_octree<1024>, grid, dim3(1024), P.lds, s, ao, l0);
     else if (nt == 512)
@@ -3200,7 +3232,7 @@ static int launch_extract_graphed(orbfe_extractor* h, int n, const uint8_t* d_im
       (uintptr_t)h->rows, (uintptr_t)h->cols, (uintptr_t)h->geom_mode, (uintptr_t)h->d_levels,
       (uintptr_t)h->d_pyr, (uintptr_t)h->d_blur, (uintptr_t)h->d_cand, (uintptr_t)h->d_cellcnt,
       (uintptr_t)h->d_keys_a, (uintptr_t)h->d_keys_b, (uintptr_t)h->d_lvlkeys, (uintptr_t)h->d_lvlcnt,
-      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->fast_side_merge, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch), (uintptr_t)h->pyr_small.d_tiles, (uintptr_t)h->pyr_batch.d_tiles,
+      (uintptr_t)h->key_lds_cap, (uintptr_t)h->octree_split, (uintptr_t)(h->oct_hi_kb * 1024 + h->oct_lo_kb), (uintptr_t)h->device_call, (uintptr_t)(h->fast_wpb_side * 16 + h->fast_wpb_main), (uintptr_t)h->fast_side_levels, (uintptr_t)h->fast_side_merge, (uintptr_t)h->input_l0, (uintptr_t)h->inline_side, (uintptr_t)(h->oct_threads_small * 4096 + h->oct_threads_batch), (uintptr_t)h->pyr_small.d_tiles, (uintptr_t)h->pyr_batch.d_tiles,
       (uintptr_t)h->blur_mode};
   h->graph_clock++;
   hipGraphExec_t exec = nullptr;
@@ -3582,6 +3614,8 @@ extern "C" int orbfe_extract_batch_device(orbfe_extractor* h, int n, const uint8
 
 static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
   const size_t need_in = (size_t)n * rows * cols;
+  // (the zero-copy staging of a small call holds each image in the level-0 layout)
+  const size_t need_h_in = std::max(need_in, (size_t)n * h->levels[0].pitch * h->levels[0].h);
   if (need_in > h->in_bytes) {
     hipFree(h->d_in);
     h->d_in = nullptr;
@@ -3615,13 +3649,13 @@ static int ensure_host_io(orbfe_extractor* h, int n, int rows, int cols) {
     h->out_n_alloc = nn;
     h->out_bytes = h->h_out_bytes = bytes;
   }
-  if (need_in > h->h_in_bytes) {
+  if (need_h_in > h->h_in_bytes) {
     if (h->h_in) hipHostFree(h->h_in);
     h->h_in = nullptr;
     h->h_in_dev = nullptr;
     // coherent (fine-grained): k_copy0's reads of it over PCIe are never served from a GPU cache
-    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_in, hipHostMallocMapped | hipHostMallocCoherent));
-    h->h_in_bytes = need_in;
+    ORBFE_HIP_CHECK(hipHostMalloc((void**)&h->h_in, need_h_in, hipHostMallocMapped | hipHostMallocCoherent));
+    h->h_in_bytes = need_h_in;
     ORBFE_HIP_CHECK(hipHostGetDevicePointer((void**)&h->h_in_dev, h->h_in, 0));
   }
   return ORBFE_OK;
@@ -3736,6 +3770,9 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   // (one KITTI image: orbfe_extract p50 0.152 with the input read over PCIe by k_copy0, 0.159 after
   // an H2D copy; profiles/r6_c2_zero_copy.txt)
   const bool zc_in = small && !direct_in && h->zc_in && h->h_in_dev;
+  // zc_in == 1: the staging holds each image in the level-0 layout (k_copy_l0); 2: plain rows (k_copy0)
+  const bool zc_l0 = zc_in && h->zc_in == 1;
+  const size_t l0_bytes = zc_l0 ? (size_t)h->levels[0].pitch * h->levels[0].h : (size_t)rows * cols;  // staging image stride
   const int nchunks = ngroups * cpg, npieces = small ? 1 : 2 * ngroups;
   st = ensure_pipeline(h, std::max(nchunks, npieces));
   if (st != ORBFE_OK) return st;
@@ -3805,6 +3842,21 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       }
       auto stage = [&](int task) {
         const int i = i0 + task / bands, r0 = (task % bands) * band, r1 = std::min(rows, r0 + band);
+        if (zc_l0) {  // the level-0 layout: 4 bytes before column 0, REFLECT_101 columns -3..-1, w..w+2
+          const int P = h->levels[0].pitch, w = cols;
+          for (int r = r0; r < r1; r++) {
+            const uint8_t* srow = imgs[i] + (size_t)r * step;
+            uint8_t* row = h->h_in + (size_t)i * l0_bytes + (size_t)r * P + 4;
+            std::memcpy(row, srow, cols);
+            row[-1] = srow[1];
+            row[-2] = srow[2];
+            row[-3] = srow[3];
+            row[w] = srow[w - 2];
+            row[w + 1] = srow[w - 3];
+            row[w + 2] = srow[w - 4];
+          }
+          return;
+        }
         uint8_t* dst = h->h_in + (size_t)i * img_bytes;
         if (step == (size_t)cols) {
           std::memcpy(dst + (size_t)r0 * cols, imgs[i] + (size_t)r0 * cols, (size_t)(r1 - r0) * cols);
@@ -3827,9 +3879,12 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       ORBFE_HIP_CHECK(hipEventRecord(h->ev_in[g], h->h2d));
       ORBFE_HIP_CHECK(hipStreamWaitEvent(h->stream, h->ev_in[g], 0));
     }
-    st = launch_extract_graphed(h, ng, (zc_in ? h->h_in_dev : h->d_in) + (size_t)g0 * img_bytes, (long long)img_bytes, cols,
+    h->input_l0 = zc_l0;
+    st = launch_extract_graphed(h, ng, zc_in ? h->h_in_dev + (size_t)g0 * l0_bytes : h->d_in + (size_t)g0 * img_bytes,
+                                zc_in ? (long long)l0_bytes : (long long)img_bytes, zc_l0 ? h->levels[0].pitch : cols,
                                 o_kps + (size_t)g0 * K, o_desc + (size_t)g0 * K * 32, K, o_counts + g0,
                                 h->stream, g0);
+    h->input_l0 = false;
     if (st != ORBFE_OK) return st;
     if (trace) std::fprintf(stderr, "[host] group %d launched %.1f\n", g, now() - t_start);
     if (after_launch) {  // (small: one group on the handle's stream, before the results' copies)
@@ -4181,7 +4236,7 @@ extern "C" int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_image
 
 extern "C" int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output) {
   if (!h) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_zero_copy: null handle");
-  h->zc_in = input ? 1 : 0;
+  h->zc_in = input == 2 ? 2 : input ? 1 : 0;
   h->zc_out = output ? 1 : 0;
   return ORBFE_OK;
 }
@@ -4206,6 +4261,13 @@ extern "C" int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_call
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_threads: 256, 512 or 1024");
   h->oct_threads_small = small_calls;
   h->oct_threads_batch = batches;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_threads_l0(orbfe_extractor* h, int threads) {
+  if (!h || !(threads == 0 || threads == 256 || threads == 512 || threads == 1024))
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_threads_l0: 0, 256, 512 or 1024");
+  h->oct_threads_l0 = threads;
   return ORBFE_OK;
 }
 

@@ -1,6 +1,7 @@
 """C2 latency A/B of the input path of a host-buffer call: one 1241x376 image through orbfe_extract
-with k_copy0 reading the pinned staging buffer over PCIe and the results written straight into the
-pinned host mirror (zero copy in + out, the default), zero copy in only, and H2D / D2H copies
+with k_copy_l0 reading the pinned staging buffer (laid out as pyramid level 0 by the host) over PCIe and
+the results written straight into the pinned host mirror (zero copy in + out, the default), the same
+with plain staged rows read by k_copy0 (zero copy mode 2), zero copy in only, and H2D / D2H copies
 (orbfe_debug_set_zero_copy(h, 0, 0)), all with the default k_pyramid, the copies also with the
 per-level chain; interleaved rounds of 200 calls, outputs compared bit for bit.
 usage: python profiles/scripts/c2_zero_copy.py [rounds]"""
@@ -20,13 +21,19 @@ from orb_slam2_2021_amd import _lib as L  # noqa: E402
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     rows, cols = 376, 1241
-    img = np.ascontiguousarray(synth_frame(3, rows, cols))
+    if os.environ.get("C2_SEQ_IMAGE"):  # the bench's C2 image: frame 0 of its driving sequence
+        from orb_slam2_2021_amd.extractor import synth_sequence_frame
+        im = synth_sequence_frame(0x0C3, 0, rows, cols)
+        img = np.ascontiguousarray(im[0] if isinstance(im, tuple) else im)
+    else:
+        img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
-    modes = {"zc_in_out": (1, 1, True), "zc_in": (1, 0, True), "copies": (0, 0, True), "copies_chain": (0, 0, False)}
+    modes = {"zc_l0_out": (1, 1, True), "zc_rows_out": (2, 1, True), "zc_in": (1, 0, True), "copies": (0, 0, True),
+             "copies_chain": (0, 0, False)}
     exts = {}
     for m, (zi, zo, pyr) in modes.items():
         e = ORBextractor(2000, 1.2, 8, 20, 7)
-        e.debug_set_zero_copy(bool(zi), bool(zo))
+        L.check(L.lib().orbfe_debug_set_zero_copy(e._h, zi, zo), "zero_copy")
         if not pyr:
             e.debug_set_pyramid_tiles((0, 0), (0, 0))
         exts[m] = e

@@ -17,7 +17,12 @@ from orb_slam2_2021_amd import _lib as L  # noqa: E402
 
 def main():
     rows, cols = 376, 1241
-    img = np.ascontiguousarray(synth_frame(3, rows, cols))
+    if os.environ.get("C2_SEQ_IMAGE"):  # the bench's C2 image: frame 0 of its driving sequence
+        from orb_slam2_2021_amd.extractor import synth_sequence_frame
+        im = synth_sequence_frame(0x0C3, 0, rows, cols)
+        img = np.ascontiguousarray(im[0] if isinstance(im, tuple) else im)
+    else:
+        img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
     tilings = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
     modes = [(1, t) for t in tilings] if tilings else [(1, None), (0, None)]
