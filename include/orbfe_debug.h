@@ -63,9 +63,9 @@ int orbfe_debug_schedule_choice(const orbfe_extractor* h, int n_images);
 /* Host-buffer calls of fewer than 8 images: k_copy0 reads the staged image straight from pinned host
  * memory (input != 0, the default) instead of after a separate H2D copy, and (output != 0, the
  * default; calls without a device-side consumer of the outputs) the kernels write the results into
- * the pinned host mirror instead of a device block copied down afterwards. input = 1 stages the
- * image in the level-0 layout (padded rows, REFLECT_101 columns written by the host; one straight
- * k_copy_l0), input = 2 stages plain rows that k_copy0 pads. Same results. */
+ * the pinned host mirror instead of a device block copied down afterwards. input = 2 stages the
+ * image in the level-0 layout instead (padded rows, REFLECT_101 columns written by the host; one
+ * straight k_copy_l0 copy): not faster. Same results. */
 int orbfe_debug_set_zero_copy(orbfe_extractor* h, int input, int output);
 /* The LDS budgets (KiB per block) of the two octree launches: levels below the split (default 80)
  * and from it on (default 40). Keys beyond a plan's capacity take the global-memory path. */

@@ -3770,8 +3770,10 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   // (one KITTI image: orbfe_extract p50 0.152 with the input read over PCIe by k_copy0, 0.159 after
   // an H2D copy; profiles/r6_c2_zero_copy.txt)
   const bool zc_in = small && !direct_in && h->zc_in && h->h_in_dev;
-  // zc_in == 1: the staging holds each image in the level-0 layout (k_copy_l0); 2: plain rows (k_copy0)
-  const bool zc_l0 = zc_in && h->zc_in == 1;
+  // zc_in == 2: the staging holds each image in the level-0 layout (k_copy_l0); 1: plain rows read by
+  // k_copy0 (one KITTI image 0.141-0.144 vs 0.144-0.146 ms in the layout: the host's padding costs
+  // what the straight copy saves; profiles/r6_c2_zero_copy.txt)
+  const bool zc_l0 = zc_in && h->zc_in == 2;
   const size_t l0_bytes = zc_l0 ? (size_t)h->levels[0].pitch * h->levels[0].h : (size_t)rows * cols;  // staging image stride
   const int nchunks = ngroups * cpg, npieces = small ? 1 : 2 * ngroups;
   st = ensure_pipeline(h, std::max(nchunks, npieces));

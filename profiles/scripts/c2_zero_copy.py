@@ -1,7 +1,8 @@
 """C2 latency A/B of the input path of a host-buffer call: one 1241x376 image through orbfe_extract
-with k_copy_l0 reading the pinned staging buffer (laid out as pyramid level 0 by the host) over PCIe and
-the results written straight into the pinned host mirror (zero copy in + out, the default), the same
-with plain staged rows read by k_copy0 (zero copy mode 2), zero copy in only, and H2D / D2H copies
+with k_copy0 reading the pinned staging buffer's rows over PCIe and the results written straight into
+the pinned host mirror (zero copy in + out, the default: zc_rows_out), the same with the staging laid
+out as pyramid level 0 by the host and one straight k_copy_l0 (zero copy mode 2: zc_l0_out), zero
+copy in only, and H2D / D2H copies
 (orbfe_debug_set_zero_copy(h, 0, 0)), all with the default k_pyramid, the copies also with the
 per-level chain; interleaved rounds of 200 calls, outputs compared bit for bit.
 usage: python profiles/scripts/c2_zero_copy.py [rounds]"""
@@ -28,7 +29,7 @@ def main():
     else:
         img = np.ascontiguousarray(synth_frame(3, rows, cols))
     lib = L.lib()
-    modes = {"zc_l0_out": (1, 1, True), "zc_rows_out": (2, 1, True), "zc_in": (1, 0, True), "copies": (0, 0, True),
+    modes = {"zc_l0_out": (2, 1, True), "zc_rows_out": (1, 1, True), "zc_in": (1, 0, True), "copies": (0, 0, True),
              "copies_chain": (0, 0, False)}
     exts = {}
     for m, (zi, zo, pyr) in modes.items():
