@@ -1593,7 +1593,24 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
     if (lane == 0) bcnt[w * nini + bkt] = cnt;
   }
   __syncthreads();
-  if (t == 0) {
+  if (nini * NW <= 64) {  // bucket-major offsets by one wavefront's scan (lane q: bucket q / NW, wave q % NW)
+    if (w == 0) {
+      const int q = lane, bkt = q / NW, ww = q - bkt * NW;
+      const bool in = q < nini * NW;
+      const int v = in ? bcnt[ww * nini + bkt] : 0;
+      int inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      const int first = __shfl(inc - v, min(bkt, 63 / NW) * NW, 64);  // the bucket's first exclusive sum
+      if (in) {
+        boff[ww * nini + bkt] = inc - v;
+        if (ww == NW - 1) sb[bkt] = inc - first;
+      }
+    }
+  } else if (t == 0) {
     int run = 0;
     for (int bkt = 0; bkt < nini; bkt++) {
       sb[bkt] = 0;
@@ -3367,6 +3384,8 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
   {
     const char* e = std::getenv("ORBFE_SCHED_AUTOTUNE");
     h->autotune = (e && e[0] == '0') ? 0 : 1;
+    const char* o = std::getenv("ORBFE_OCT_THREADS_SMALL");  // (A/B runs of whole processes)
+    if (o && (std::atoi(o) == 256 || std::atoi(o) == 512 || std::atoi(o) == 1024)) h->oct_threads_small = std::atoi(o);
   }
   h->nfeatures = nfeatures;
   h->nlevels = nlevels;
