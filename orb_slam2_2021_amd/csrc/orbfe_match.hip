@@ -2225,11 +2225,13 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   }
   sweep = sweep && m->sweep_attr > 0;
   sbp_launch_init(m, p, F, sweep);
+  m->sbp_deferred = false;
   if (sweep) {
     sbp_sweep_launch(m, p, F, dF, md);
   } else {
     const int rounds = md.no_claims && p.cache ? 1 : m->max_rounds;
-    sbp_rounds(m, p, F, dF, md, 0, rounds, defer && m->round_cap > rounds);
+    m->sbp_deferred = defer && m->round_cap > rounds;
+    sbp_rounds(m, p, F, dF, md, 0, rounds, m->sbp_deferred);
   }
   ORBFE_HIP_CHECK(hipGetLastError());
   return ORBFE_OK;
@@ -2239,9 +2241,12 @@ int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatch
               const orbfe_frame_view* dF, const SbpMode* md) {
   uint8_t* A = m->arena;
   int32_t nm = 0, state[2] = {0, 0}, serial = 0;
-  if (p.nq > 0 && F && dF && md && !(md->no_claims && p.cache)) {
+  static const bool always_check = std::getenv("ORBFE_SBP_FETCH_SYNC") != nullptr;  // (A/B: the check every call)
+  if (p.nq > 0 && F && dF && md && !(md->no_claims && p.cache) && (m->sbp_deferred || always_check)) {
     // a fixpoint still unsettled continues in doubling chunks of rounds (a rare case: one sync
-    // per chunk), the serial walk only past round_cap
+    // per chunk), the serial walk only past round_cap. Only launches that deferred (the grid-wide
+    // rounds with a round budget below round_cap) can leave it unsettled: after k_sbp_sweep, or
+    // rounds whose k_sbp_finish walks the rest itself, this host round trip is skipped
     ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
     ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
     int done = m->max_rounds;
