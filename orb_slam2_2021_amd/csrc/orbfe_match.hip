@@ -1992,11 +1992,11 @@ void sbp_plan_scratch(Arena& ar, const orbfe_frame_view* F, SbpPlan& p) {
   p.oblk = ar.add(4 * f1);
   p.ostate = ar.add(4 * (SBP_ROUND_CAP + 4));
   p.obest = ar.add(4 * q1);
+  p.onm = ar.add(4);  // (state, best, count adjacent: sbp_fetch takes them down in one copy)
   p.cache = F->n <= 65535;  // candidate keypoint indices are 16-bit (cand_pack)
   const size_t cq = p.cache ? (size_t)cand_cap * q1 : 0;
   p.ocand = ar.add(4 * cq);
   p.ocand_n = ar.add(p.cache ? 4 * q1 : 0);
-  p.onm = ar.add(4);
   p.oown3 = ar.add(4 * f1);
   // k_sbp_sweep keeps own[n] and the taken bits of the frame's keypoints in LDS
   p.sweep = p.cache && p.nq > 0 && F->n <= SWEEP_MAX_KEYS;
@@ -2226,6 +2226,7 @@ int sbp_launch(orbfe_matcher* m, const SbpPlan& p, const orbfe_frame_view* F, co
   sweep = sweep && m->sweep_attr > 0;
   sbp_launch_init(m, p, F, sweep);
   m->sbp_deferred = false;
+  m->sbp_swept = sweep;
   if (sweep) {
     sbp_sweep_launch(m, p, F, dF, md);
   } else {
@@ -2262,14 +2263,31 @@ int sbp_fetch(orbfe_matcher* m, const SbpPlan& p, int32_t* best_idx, int* nmatch
   }
   // the device part ends after the last round (continuations included, with their host syncs)
   prof_end(m);
+  // the round state, the results and the match count are adjacent in the arena (sbp_plan_scratch):
+  // one copy into the pinned mirror at the same offsets, then host copies out (instead of three
+  // copies, one of them into the caller's pageable array); the serial-walk flag only when a walk
+  // could have run (k_sbp_sweep settles the claim order itself)
+  static const bool split_copies = std::getenv("ORBFE_SBP_FETCH_SPLIT") != nullptr;  // (A/B: three copies)
+  const bool one_copy =
+      !split_copies && p.ostate < p.obest && p.obest < p.onm && m->pinned && p.onm + 4 <= m->pinned_bytes;
   if (p.nq > 0) {
-    if (best_idx)
-      ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, A + p.obest, 4 * (size_t)p.nq, hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, A + p.onm, 4, hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(state, A + p.ostate, 8, hipMemcpyDeviceToHost, m->stream));
-    ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
+    if (one_copy) {
+      ORBFE_HIP_CHECK(hipMemcpyAsync(m->pinned + p.ostate, A + p.ostate, p.onm + 4 - p.ostate, hipMemcpyDeviceToHost,
+                                     m->stream));
+    } else {
+      if (best_idx)
+        ORBFE_HIP_CHECK(hipMemcpyAsync(best_idx, A + p.obest, 4 * (size_t)p.nq, hipMemcpyDeviceToHost, m->stream));
+      ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, A + p.onm, 4, hipMemcpyDeviceToHost, m->stream));
+      ORBFE_HIP_CHECK(hipMemcpyAsync(state, A + p.ostate, 8, hipMemcpyDeviceToHost, m->stream));
+    }
+    if (!m->sbp_swept) ORBFE_HIP_CHECK(hipMemcpyAsync(&serial, m->d_serial, 4, hipMemcpyDeviceToHost, m->stream));
   }
   ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  if (p.nq > 0 && one_copy) {
+    if (best_idx) std::memcpy(best_idx, m->pinned + p.obest, 4 * (size_t)p.nq);
+    std::memcpy(&nm, m->pinned + p.onm, 4);
+    std::memcpy(state, m->pinned + p.ostate, 8);
+  }
   m->last_rounds = state[1];
   m->last_serial = serial;
   if (nmatches) *nmatches = nm;

@@ -53,6 +53,7 @@ struct orbfe_matcher {
   std::vector<std::tuple<size_t, const void*, size_t>> d2d;
   int last_rounds = 0, last_serial = 0;
   bool sbp_deferred = false;  // the last SearchByProjection launch left its rounds to the host (sbp_fetch)
+  bool sbp_swept = false;     // ... and whether k_sbp_sweep settled its claim order
   int max_rounds = SBP_MAX_ROUNDS;
   int round_cap = SBP_ROUND_CAP;  // >= max_rounds; equal: no continuation (serial fallback at once)
   // orbfe_debug_matcher_set_sweep (0: the defaults): queries per k_sbp_sweep chunk, Jacobi rounds a
