@@ -620,14 +620,11 @@ int run_bow(orbfe_matcher* m, int mode, int n_pairs, const orbfe_frame_view* As,
   size_t off = 0;
   for (int p = 0; p < n_pairs; p++) {  // mode 0: per Frame keypoint; mode 1: per KF1 keypoint
     const int n = mode == 0 ? Bs[shared_b ? 0 : p].n : As[p].n;
-    if (n > 0)
-      ORBFE_HIP_CHECK(hipMemcpyAsync(out + off, A + (mode == 0 ? oout[p] : omatch[p]), 4 * (size_t)n,
-                                     hipMemcpyDeviceToHost, m->stream));
+    if (n > 0) orbfe_mi::stage_d2h(m, out + off, A + (mode == 0 ? oout[p] : omatch[p]), 4 * (size_t)n);
     off += (size_t)n;
   }
-  ORBFE_HIP_CHECK(hipMemcpyAsync(counts, A + ocounts, 4 * (size_t)n_pairs, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
-  return ORBFE_OK;
+  orbfe_mi::stage_d2h(m, counts, A + ocounts, 4 * (size_t)n_pairs);
+  return orbfe_mi::fetch_d2h(m);
 }
 
 bool bow_frame_ok(const orbfe_frame_view* f) {
@@ -772,10 +769,10 @@ extern "C" int orbfe_search_for_initialization(orbfe_matcher* m, const orbfe_fra
   ORBFE_LAUNCH("k_init_seq", k_init_seq, dim3(1), dim3(64), lds, m->stream, sa);
   ORBFE_HIP_CHECK(hipGetLastError());
   int32_t nm = 0;
-  ORBFE_HIP_CHECK(hipMemcpyAsync(match12, A + om, 4 * (size_t)n1, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipMemcpyAsync(prev_matched, A + oprev, 8 * (size_t)n1, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, A + onm, 4, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  orbfe_mi::stage_d2h(m, match12, A + om, 4 * (size_t)n1);
+  orbfe_mi::stage_d2h(m, prev_matched, A + oprev, 8 * (size_t)n1);
+  orbfe_mi::stage_d2h(m, &nm, A + onm, 4);
+  if ((st = orbfe_mi::fetch_d2h(m))) return st;
   *nmatches = nm;
   return ORBFE_OK;
 }
@@ -820,7 +817,6 @@ extern "C" int orbfe_compute_distinctive_descriptors(orbfe_matcher* m, int n_poi
   if ((st = orbfe_compute_distinctive_descriptors_device(m, n_points, (const int32_t*)(A + oo), A + od,
                                                          (int32_t*)(A + ob), m->stream)))
     return st;
-  ORBFE_HIP_CHECK(hipMemcpyAsync(best_index, A + ob, 4 * (size_t)n_points, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
-  return ORBFE_OK;
+  orbfe_mi::stage_d2h(m, best_index, A + ob, 4 * (size_t)n_points);
+  return orbfe_mi::fetch_d2h(m);
 }

@@ -1671,6 +1671,7 @@ int ensure_arena(orbfe_matcher* m, size_t bytes) {
   m->stage_lo = SIZE_MAX;
   m->stage_hi = 0;
   m->d2d.clear();
+  m->d2h.clear();
   if (bytes > m->arena_bytes) {
     hipFree(m->arena);
     m->arena = nullptr;
@@ -1735,6 +1736,37 @@ int flush_h2d(orbfe_matcher* m) {
                                    hipMemcpyDeviceToDevice, m->stream));
   m->d2d.clear();
   return ORBFE_OK;
+}
+
+void stage_d2h(orbfe_matcher* m, void* dst, const void* src, size_t n) {
+  if (n == 0 || !dst) return;
+  m->d2h.emplace_back(dst, (size_t)((const uint8_t*)src - m->arena), n);
+}
+
+int fetch_d2h(orbfe_matcher* m) {
+  size_t lo = SIZE_MAX, hi = 0, sum = 0;
+  for (const auto& r : m->d2h) {
+    lo = std::min(lo, std::get<1>(r));
+    hi = std::max(hi, std::get<1>(r) + std::get<2>(r));
+    sum += std::get<2>(r);
+  }
+  const bool span = !m->d2h.empty() && m->pinned && hi <= m->pinned_bytes && hi - lo <= 4 * sum + (64u << 10);
+  int st = ORBFE_OK;
+  if (span) {
+    if (hipMemcpyAsync(m->pinned + lo, m->arena + lo, hi - lo, hipMemcpyDeviceToHost, m->stream) != hipSuccess)
+      st = orbfe_set_error(ORBFE_ERR_HIP, "fetch_d2h: hipMemcpyAsync");
+  } else {
+    for (const auto& r : m->d2h)
+      if (st == ORBFE_OK && hipMemcpyAsync(std::get<0>(r), m->arena + std::get<1>(r), std::get<2>(r),
+                                           hipMemcpyDeviceToHost, m->stream) != hipSuccess)
+        st = orbfe_set_error(ORBFE_ERR_HIP, "fetch_d2h: hipMemcpyAsync");
+  }
+  if (hipStreamSynchronize(m->stream) != hipSuccess && st == ORBFE_OK)
+    st = orbfe_set_error(ORBFE_ERR_HIP, "fetch_d2h: hipStreamSynchronize");
+  if (span && st == ORBFE_OK)
+    for (const auto& r : m->d2h) std::memcpy(std::get<0>(r), m->pinned + std::get<1>(r), std::get<2>(r));
+  m->d2h.clear();
+  return st;
 }
 
 // Layout of one frame view in the arena (FrameOffsets)
@@ -1957,10 +1989,9 @@ extern "C" int orbfe_search_for_triangulation(orbfe_matcher* m, const orbfe_fram
   st = orbfe_search_for_triangulation_batch_device(m, 1, &P, only_stereo, m->stream);
   if (st) return st;
   int32_t nm = 0;
-  if (kf1->n > 0)
-    ORBFE_HIP_CHECK(hipMemcpyAsync(match12, P.match12, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipMemcpyAsync(&nm, P.nmatches, 4, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  if (kf1->n > 0) orbfe_mi::stage_d2h(m, match12, P.match12, 4 * (size_t)kf1->n);
+  orbfe_mi::stage_d2h(m, &nm, P.nmatches, 4);
+  if ((st = orbfe_mi::fetch_d2h(m))) return st;
   *nmatches = nm;
   return ORBFE_OK;
 }
@@ -2588,16 +2619,17 @@ static int fetch_frustum(orbfe_matcher* m, uint8_t* A, const FrustumPlan& p, int
                          int* n_in_view) {
   const size_t n = (size_t)M;
   if (out && M > 0) {
-    if (out->flags) ORBFE_HIP_CHECK(hipMemcpyAsync(out->flags, A + p.o_flags, n, hipMemcpyDeviceToHost, m->stream));
-    if (out->proj_x) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_x, A + p.o_px, 4 * n, hipMemcpyDeviceToHost, m->stream));
-    if (out->proj_y) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_y, A + p.o_py, 4 * n, hipMemcpyDeviceToHost, m->stream));
-    if (out->proj_xr) ORBFE_HIP_CHECK(hipMemcpyAsync(out->proj_xr, A + p.o_pxr, 4 * n, hipMemcpyDeviceToHost, m->stream));
-    if (out->level) ORBFE_HIP_CHECK(hipMemcpyAsync(out->level, A + p.o_lvl, 4 * n, hipMemcpyDeviceToHost, m->stream));
-    if (out->view_cos) ORBFE_HIP_CHECK(hipMemcpyAsync(out->view_cos, A + p.o_vc, 4 * n, hipMemcpyDeviceToHost, m->stream));
+    if (out->flags) orbfe_mi::stage_d2h(m, out->flags, A + p.o_flags, n);
+    if (out->proj_x) orbfe_mi::stage_d2h(m, out->proj_x, A + p.o_px, 4 * n);
+    if (out->proj_y) orbfe_mi::stage_d2h(m, out->proj_y, A + p.o_py, 4 * n);
+    if (out->proj_xr) orbfe_mi::stage_d2h(m, out->proj_xr, A + p.o_pxr, 4 * n);
+    if (out->level) orbfe_mi::stage_d2h(m, out->level, A + p.o_lvl, 4 * n);
+    if (out->view_cos) orbfe_mi::stage_d2h(m, out->view_cos, A + p.o_vc, 4 * n);
   }
   int32_t nv = 0;
-  ORBFE_HIP_CHECK(hipMemcpyAsync(&nv, A + p.counter, 4, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  orbfe_mi::stage_d2h(m, &nv, A + p.counter, 4);
+  const int st = orbfe_mi::fetch_d2h(m);
+  if (st) return st;
   if (n_in_view) *n_in_view = nv;
   return ORBFE_OK;
 }

@@ -51,6 +51,9 @@ struct orbfe_matcher {
   // inputs the caller passed in device memory: arena offset, source, bytes; copied on the device
   // after the staged span's H2D copy (which may cover their arena regions)
   std::vector<std::tuple<size_t, const void*, size_t>> d2d;
+  // results wanted on the host: caller destination, arena offset, bytes (fetch_d2h takes them down
+  // through the pinned mirror, one copy when their span is small)
+  std::vector<std::tuple<void*, size_t, size_t>> d2h;
   int last_rounds = 0, last_serial = 0;
   bool sbp_deferred = false;  // the last SearchByProjection launch left its rounds to the host (sbp_fetch)
   bool sbp_swept = false;     // ... and whether k_sbp_sweep settled its claim order
@@ -181,6 +184,11 @@ struct Arena {
 int ensure_arena(orbfe_matcher* m, size_t bytes);
 void stage_h2d(orbfe_matcher* m, const void* dst, const void* src, size_t n);
 int flush_h2d(orbfe_matcher* m);
+// Queue `n` bytes of arena address `src` for the host address `dst`; fetch_d2h copies every queued
+// region down (one copy of their span into the pinned mirror when it is at most 4x their bytes plus
+// 64 KiB, else one copy each), synchronises the matcher's stream and copies them out.
+void stage_d2h(orbfe_matcher* m, void* dst, const void* src, size_t n);
+int fetch_d2h(orbfe_matcher* m);
 
 struct FrameOffsets {
   size_t keys, ur, desc, mp, scale, sigma2;

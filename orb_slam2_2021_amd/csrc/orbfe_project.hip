@@ -399,9 +399,9 @@ extern "C" int orbfe_search_by_sim3(orbfe_matcher* m, const orbfe_frame_view* kf
                        (int32_t*)(A + om), (int32_t*)(A + on));
   ORBFE_HIP_CHECK(hipGetLastError());
   int32_t nf = 0;
-  if (kf1->n > 0) ORBFE_HIP_CHECK(hipMemcpyAsync(match12, A + om, 4 * (size_t)kf1->n, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipMemcpyAsync(&nf, A + on, 4, hipMemcpyDeviceToHost, m->stream));
-  ORBFE_HIP_CHECK(hipStreamSynchronize(m->stream));
+  if (kf1->n > 0) orbfe_mi::stage_d2h(m, match12, A + om, 4 * (size_t)kf1->n);
+  orbfe_mi::stage_d2h(m, &nf, A + on, 4);
+  if ((st = orbfe_mi::fetch_d2h(m))) return st;
   *nfound = nf;
   return ORBFE_OK;
 }
