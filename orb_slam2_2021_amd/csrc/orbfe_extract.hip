@@ -3750,7 +3750,10 @@ extern "C" int orbfe_extract_batch(orbfe_extractor* h, int n, const uint8_t* con
 
 int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const* imgs, int rows, int cols,
                                  size_t step, orbfe_keypoint* kps, uint8_t* desc, int cap, int32_t* counts,
-                                 const std::function<int()>& after_launch) {
+                                 const std::function<int()>& after_launch, orbfe_keypoint* const* kps_img,
+                                 uint8_t* const* desc_img) {
+  const bool per_image = kps_img && desc_img;
+  if (per_image && n >= 8) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_internal_extract_batch: per-image outputs on a large batch");
   if (!h || n < 0 || !imgs || !counts) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_extract_batch: bad argument");
   if (after_launch && n >= 8) return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_internal_extract_batch: hook on a large batch");
   if (n == 0) return ORBFE_OK;
@@ -3779,7 +3782,8 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
   bool direct_in = step == (size_t)cols;
   for (int i = 0; i < n && direct_in; i++) direct_in = host_registered(imgs[i], (size_t)rows * cols);
   const int K0 = h->total_key_slots;
-  const bool direct_out = cap == K0 && kps && desc && host_registered(kps, (size_t)n * cap * sizeof(orbfe_keypoint)) &&
+  const bool direct_out = !per_image && cap == K0 && kps && desc &&
+                          host_registered(kps, (size_t)n * cap * sizeof(orbfe_keypoint)) &&
                           host_registered(desc, (size_t)n * cap * 32);
   const int ngroups = env_groups > 0 ? std::min(env_groups, std::max(1, n / 8)) : 1;
   const int cpg = std::max(1, std::min(4, n / (8 * ngroups)));  // H2D chunks per group
@@ -3960,16 +3964,17 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
       counts[i] = hc[i];
       need = std::max(need, (int)hc[i]);
     }
-    if (need > cap || (need > 0 && (!kps || !desc))) break;  // reported below
+    if (need > cap || (need > 0 && !per_image && (!kps || !desc))) break;  // reported below
     if (direct_out) continue;  // the slots landed in the caller's buffers
-    h->pool->parallel_for(np, [&](int k) {
+    auto unpack = [&](int k) {
       const int i = i0 + k;
       if (hc[i] == 0) return;
-      std::memcpy(kps + (size_t)i * cap, hk + (size_t)i * K, sizeof(orbfe_keypoint) * hc[i]);
-      std::memcpy(desc + (size_t)i * cap * 32, hd + (size_t)i * K * 32, (size_t)32 * hc[i]);
-    });
+      std::memcpy(per_image ? kps_img[i] : kps + (size_t)i * cap, hk + (size_t)i * K, sizeof(orbfe_keypoint) * hc[i]);
+      std::memcpy(per_image ? desc_img[i] : desc + (size_t)i * cap * 32, hd + (size_t)i * K * 32, (size_t)32 * hc[i]);
+    };
+    h->pool->parallel_for(np, unpack);
   }
-  if (need > cap || (need > 0 && (!kps || !desc))) ORBFE_HIP_CHECK(hipStreamSynchronize(s_out));
+  if (need > cap || (need > 0 && !per_image && (!kps || !desc))) ORBFE_HIP_CHECK(hipStreamSynchronize(s_out));
   if (trace) std::fprintf(stderr, "[host] done %.1f\n", now() - t_start);
   h->call_inline = false;
   if (tune_arm >= 0) {
@@ -3986,7 +3991,7 @@ int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const
     }
   }
   if (need > cap) return orbfe_set_error(ORBFE_ERR_CAPACITY, "keypoint capacity too small");
-  if (need > 0 && (!kps || !desc)) return orbfe_set_error(ORBFE_ERR_ARG, "null output buffer");
+  if (need > 0 && !per_image && (!kps || !desc)) return orbfe_set_error(ORBFE_ERR_ARG, "null output buffer");
   return ORBFE_OK;
 }
 

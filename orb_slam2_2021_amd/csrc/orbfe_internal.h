@@ -32,9 +32,12 @@ int orbfe_internal_pyramid(orbfe_extractor* h, OrbfePyramid* out);
 // orbfe_extract_batch with a hook run right after the extraction's launches, before its results are
 // copied down (calls of fewer than 8 images: the handle's stream, where the hook enqueues its own
 // work and copies; the call's final wait covers them). An empty hook: orbfe_extract_batch.
+// kps_img / desc_img (optional, n pointers each): image i's keypoints / descriptors go to
+// kps_img[i] / desc_img[i] instead of kps + i * cap / desc + i * cap * 32.
 int orbfe_internal_extract_batch(orbfe_extractor* h, int n, const uint8_t* const* imgs, int rows, int cols,
                                  size_t step, orbfe_keypoint* kps, uint8_t* desc, int cap, int32_t* counts,
-                                 const std::function<int()>& after_launch);
+                                 const std::function<int()>& after_launch, orbfe_keypoint* const* kps_img = nullptr,
+                                 uint8_t* const* desc_img = nullptr);
 
 // Stereo scratch owned by the handle (created lazily by orbfe_stereo.hip, freed with the handle).
 struct OrbfeStereoScratch;

@@ -615,8 +615,8 @@ extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const
   // behind the extraction on the handle's stream, its uRight / depth copied down with the keypoints
   // (one wait for the whole Frame; the kernels see the keypoint counts on the device)
   const uint8_t* imgs[2] = {left, right};
-  std::vector<orbfe_keypoint> k2(2 * (size_t)K);
-  std::vector<uint8_t> d2(2 * (size_t)K * 32);
+  orbfe_keypoint* const kp_img[2] = {kps_l, kps_r};  // the results go straight to the caller's arrays
+  uint8_t* const desc_img[2] = {desc_l, desc_r};
   int32_t counts[2] = {0, 0};
   float* ho = nullptr;
   auto stereo = [&]() -> int {
@@ -633,14 +633,11 @@ extern "C" int orbfe_stereo_frame(orbfe_extractor* h, const uint8_t* left, const
     ORBFE_HIP_CHECK(hipMemcpyAsync(ho, S->d_out, sizeof(float) * 2 * (size_t)K, hipMemcpyDeviceToHost, P.stream));
     return ORBFE_OK;
   };
-  const int st = orbfe_internal_extract_batch(h, 2, imgs, rows, cols, step, k2.data(), d2.data(), K, counts, stereo);
+  const int st = orbfe_internal_extract_batch(h, 2, imgs, rows, cols, step, nullptr, nullptr, cap, counts, stereo,
+                                              kp_img, desc_img);
   if (st != ORBFE_OK) return st;
   *n_l = counts[0];
   *n_r = counts[1];
-  std::memcpy(kps_l, k2.data(), sizeof(orbfe_keypoint) * counts[0]);
-  std::memcpy(desc_l, d2.data(), (size_t)counts[0] * 32);
-  std::memcpy(kps_r, k2.data() + K, sizeof(orbfe_keypoint) * counts[1]);
-  std::memcpy(desc_r, d2.data() + (size_t)K * 32, (size_t)counts[1] * 32);
   if (counts[0] == 0) return ORBFE_OK;
   std::memcpy(u_right, ho, sizeof(float) * counts[0]);
   std::memcpy(depth, ho + K, sizeof(float) * counts[0]);
