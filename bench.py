@@ -156,6 +156,9 @@ def parse(argv=None):
                    help="--feed host: copy streams per sub-batch's H2D (2: two halves on two streams)")
     p.add_argument("--input-slots", type=int, default=0,
                    help="--feed host: device input slots (0: two per extractor handle)")
+    p.add_argument("--copies-ahead", type=int, default=-1,
+                   help="--feed host: copies enqueued this many sub-batches ahead of their extraction "
+                        "(-1: (R - 1) / 2 of the R input slots; 0: each just before its extraction)")
     p.add_argument("--host-pin", choices=("torch", "register"), default="torch",
                    help="--feed host: page-lock the host images with torch's pin_memory (hipHostMalloc) or "
                         "register the numpy buffer in place (orbfe_host_register, hipHostRegister)")
@@ -354,9 +357,15 @@ class HostFeed:
     event); the copy into slot k mod R for sub-batch k waits for sub-batch k - R's event. R defaults
     to two per extractor handle, so the copies run up to R sub-batches ahead of the extraction and
     the link, not slot reuse, bounds the rate when 2B images take longer to copy than to process
-    (round 4 tied the slots to the handles' pyramid events, R = 4: 45.8k stereo frames/s)."""
+    (round 4 tied the slots to the handles' pyramid events, R = 4: 45.8k stereo frames/s).
 
-    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0, copy_streams=1, pin="torch"):
+    The copies are enqueued `prefetch` sub-batches ahead of the extraction that reads them (at most
+    R - 1, so the event a copy waits for is always recorded): when the device queues are full a
+    launch blocks the host thread (~55 us each, half of a sub-batch's launches in this mode), and a
+    copy enqueued just before its own extraction then starts ~240 us after the previous copy
+    finished, leaving the link idle a third of the time (profiles/r6_hostfed_prefetch.txt)."""
+
+    def __init__(self, host, n_img, H, W, dev, copy_stream, slots=0, copy_streams=1, pin="torch", prefetch=-1):
         import torch
         self.pin = pin
         if pin == "register":  # the numpy buffer itself, page-aligned, registered with the runtime
@@ -379,20 +388,40 @@ class HostFeed:
         self.slots_req = slots
         self.n_img, self.H, self.W, self.dev = n_img, H, W, dev
         self.cs = copy_stream
-        self.k = 0
+        self.k = 0        # copies enqueued
+        self.taken = 0    # sub-batches handed to the pipeline
+        self.prefetch_req = prefetch
+        self.prefetch = 0
+        self.pending = []
         self.ready = []
         self.consumed = []
         self.bytes_per_subbatch = n_img * H * W
 
-    def upload(self, j, pipe):
+    def take(self, n_of, pipe):
+        """The next sub-batch's (slot pointer, ready event); first enqueues the copies of the
+        sub-batches up to `prefetch` ahead (n_of(i): the host batch of the i-th sub-batch)."""
+        if self.slots is None:
+            self._alloc(pipe)
+        while self.k <= self.taken + self.prefetch:
+            self.pending.append(self.upload(n_of(self.k), pipe))
+        self.taken += 1
+        return self.pending.pop(0)
+
+    def _alloc(self, pipe):
         import torch
         from orb_slam2_2021_amd.pipeline import new_event
         if self.slots is None:
             self.R = self.slots_req if self.slots_req > 0 else 2 * len(pipe.exts)
+            self.prefetch = (self.R - 1) // 2 if self.prefetch_req < 0 else min(self.prefetch_req, self.R - 1)
             self.slots = torch.empty((self.R, self.n_img, self.H, self.W), dtype=torch.uint8, device=self.dev)
             self.ready = [new_event(self.dev.index) for _ in range(self.R)]
             self.consumed = [new_event(self.dev.index) for _ in range(self.R)]
             self.joined = [new_event(self.dev.index) for _ in range(self.R)] if self.cs2 else []
+
+    def upload(self, j, pipe):
+        import torch
+        if self.slots is None:
+            self._alloc(pipe)
         slot = self.k % self.R
         if self.k >= self.R:  # sub-batch k - R's extraction read this slot
             self.consumed[slot].wait(self.cs)
@@ -415,12 +444,14 @@ class HostFeed:
 
     def extracted(self, pipe):
         """After pipe.run() of the last uploaded sub-batch: its slot is free once that extraction is."""
-        self.consumed[(self.k - 1) % self.R].record(pipe.last_stream)
+        self.consumed[(self.taken - 1) % self.R].record(pipe.last_stream)
 
     def describe(self, subbatches_per_s):
         gbs = self.bytes_per_subbatch * subbatches_per_s / 1e9
         return {"mode": "host", "h2d_bytes_per_subbatch": self.bytes_per_subbatch, "h2d_GBps": round(gbs, 2),
-                "device_slots": self.R, "copy_streams": 1 + len(self.cs2), "host_pin": self.pin,
+                "device_slots": self.R, "copies_ahead": self.prefetch,
+                "copy_streams": 1 + len(self.cs2),
+                "host_pin": self.pin,
                 "source_pinned": bool(self.h.is_pinned()),
                 "what": "every sub-batch's images H2D from pinned host memory on a copy stream of its own, "
                         "overlapped with the other sub-batches' kernels; outputs stay in HBM"}
@@ -533,6 +564,7 @@ def main():
     feed = None
     if args.feed == "host":
         feed = HostFeed(host, n_img, H, W, dev, pstreams.copy, slots=args.input_slots, pin=args.host_pin,
+                        prefetch=args.copies_ahead,
                         copy_streams=args.copy_streams)
     ext = ORBextractor(args.nfeatures, 1.2, 8, 20, 7, device=dev.index)
     tree = S.Vocabulary.synthetic_orbvoc(levels=args.vocab_levels)
@@ -614,7 +646,7 @@ def main():
         j = counter[0] % NB
         counter[0] += 1
         if feed is not None:  # the images go up from pinned host memory first (copy stream)
-            ptr, ready = feed.upload(j, pipe)
+            ptr, ready = feed.take(lambda i: i % NB, pipe)
             pipe.run(ptr, after_match=g.pack if g else None, input_ready=ready)
             feed.extracted(pipe)
         else:
