@@ -42,6 +42,10 @@ int orbfe_debug_set_octree_threads(orbfe_extractor* h, int small_calls, int batc
 /* Calls of fewer than 8 images: the block size of the octree launch that holds level 0 (the latency
  * schedule's side launch); 0 (default): the small calls' size. */
 int orbfe_debug_set_octree_threads_l0(orbfe_extractor* h, int threads);
+/* DistributeOctTree's node splits: a node of at most this many keys is split by one thread, a larger
+ * one by a wavefront (1..128; default 48 for both), for calls of fewer than 8 images / batches. Same
+ * results. */
+int orbfe_debug_set_octree_serial(orbfe_extractor* h, int small_calls, int batches);
 /* ComputePyramid's levels 1..L-1 in one k_pyramid launch of tx x ty tiles per image (each
  * workgroup builds its tile of every level, the previous level in LDS, the halo recomputed) for
  * calls of fewer than 8 images (default 16 x 12) / batches of 8+ (default 0 x 0: one k_resize_win

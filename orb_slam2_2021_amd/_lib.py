@@ -176,6 +176,7 @@ _SIGNATURES = {
     "orbfe_debug_set_latency_schedule": (c_int, [c_void_p, c_int]),
     "orbfe_debug_set_octree_threads": (c_int, [c_void_p, c_int, c_int]),
     "orbfe_debug_set_octree_threads_l0": (c_int, [c_void_p, c_int]),
+    "orbfe_debug_set_octree_serial": (c_int, [c_void_p, c_int, c_int]),
     "orbfe_debug_set_pyramid_tiles": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
     "orbfe_debug_set_zero_copy": (c_int, [c_void_p, c_int, c_int]),
     "orbfe_debug_set_schedule_autotune": (c_int, [c_void_p, c_int]),

@@ -117,6 +117,7 @@ struct ExtractArgs {
   int ini_th, min_th;
   int roi_w_max, roi_h_max;
   int node_cap, sort_cap, scan_cap, key_lds_cap;
+  int oct_small;          // k_octree: nodes of <= oct_small keys split by one thread, larger by a wavefront
   const uint4* rgrp;      // k_resize: per 4-column group {sel[4]}, {alpha[4]} (2 x uint4)
   const int* rgx0;        // k_resize: first source column of each group
   int umax[16];
@@ -1281,12 +1282,14 @@ __device__ __forceinline__ void wave_child_partition(const ONode& nd, int4 cnt, 
   }
 }
 
-// Thread-serial forms for small nodes (count <= OCT_SMALL): one lane walks the whole segment.
+// Thread-serial forms for small nodes (count <= ExtractArgs::oct_small, default OCT_SMALL): one lane
+// walks the whole segment.
 #ifndef OCT_SMALL  // (a build option for the threshold's sweep: profiles/r5_octree_passes.txt)
 #define OCT_SMALL 48
 #endif
+#define OCT_SMALL_MAX 128  // (the host clamps oct_small to it)
 // Four keys per step (four independent loads in flight); the four counts / offsets are packed in
-// the bytes of one register (count <= OCT_SMALL < 256), not a dynamically indexed array.
+// the bytes of one register (count <= oct_small <= OCT_SMALL_MAX < 256), not a dynamically indexed array.
 __device__ __forceinline__ int4 serial_child_counts(const ONode& nd, const uint32_t* ka, const uint32_t* kb) {
   const uint32_t* src = ((nd.flags & 1) ? kb : ka) + nd.begin;
   const int mx = nd.x0 + ((nd.x1 - nd.x0 + 1) >> 1), my = nd.y0 + ((nd.y1 - nd.y0 + 1) >> 1);
@@ -1441,17 +1444,17 @@ __device__ __forceinline__ int comp4(int4 c, int k) {
   return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
 }
 
-// The nodes of list positions [0, m) (position p -> node index idx(p)) holding more than OCT_SMALL
+// The nodes of list positions [0, m) (position p -> node index idx(p)) holding more than `small`
 // keys, dealt round-robin over the block's NW wavefronts in position order: each wavefront reads the
 // counts of 64 positions at a time (one LDS read per lane) and walks the ballot of the big ones, so
 // no wavefront steps through the small nodes one dependent read at a time.
 template <int NW, typename Idx, typename F>
-__device__ __forceinline__ void for_big_nodes(const ONode* L, int m, Idx idx, F f) {
+__device__ __forceinline__ void for_big_nodes(const ONode* L, int m, int small, Idx idx, F f) {
   const int w = wave_id(), lane = lane_id();
   int ord = 0;
   for (int c0 = 0; c0 < m; c0 += 64) {
     const int p = c0 + lane;
-    const bool big = p < m && L[idx(p)].count > OCT_SMALL;
+    const bool big = p < m && L[idx(p)].count > small;
     uint64_t bal = wave_ballot(big);
     while (bal) {
       const int b = __builtin_ctzll(bal);
@@ -1491,6 +1494,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
   const int img = blockIdx.y;
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
   const int NC = a.node_cap, SC = a.sort_cap, SA = a.scan_cap;
+  const int SMALL = a.oct_small;
   ONode* nodes0 = reinterpret_cast<ONode*>(smem);
   ONode* nodes1 = nodes0 + NC;
   int4* cc = reinterpret_cast<int4*>(nodes1 + NC);
@@ -1686,11 +1690,11 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       if (n_passes == ORBFE_OCT_PROF_PASS) OCT_MARK(14, wall_clock64());
 #endif
       // ---- full pass (:603-668) ----
-      // each node's split and its scan inputs by whoever splits it (a thread for <= OCT_SMALL
+      // each node's split and its scan inputs by whoever splits it (a thread for <= oct_small
       // keys, a wavefront above): children (sa), kept single-key nodes (sb), multi-key children (sx)
       for (int i = t; i < S; i += NT) {
         const ONode nd = Lc[i];
-        if (nd.count > OCT_SMALL) continue;
+        if (nd.count > SMALL) continue;
         const bool par = nd.count > 1;
         const int4 c4 = par ? serial_child_split(nd, ka, kb) : make_int4(0, 0, 0, 0);
         if (par) cc[i] = c4;
@@ -1702,7 +1706,7 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
 #ifdef ORBFE_OCT_PROF_PASS
       unsigned long long split_cyc = 0, split_n = 0;
 #endif
-      for_big_nodes<NW>(Lc, S, [](int p) { return p; }, [&](int i) {
+      for_big_nodes<NW>(Lc, S, SMALL, [](int p) { return p; }, [&](int i) {
 #ifdef ORBFE_OCT_PROF_PASS
         const unsigned long long c0 = clock64();
         const int4 c4 = wave_child_split(Lc[i], ka, kb);
@@ -1839,9 +1843,9 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       // child counts of every candidate, in processing order
       for (int k = t; k < nR; k += NT) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
-        if (nd.count <= OCT_SMALL) cc[k] = serial_child_counts(nd, ka, kb);
+        if (nd.count <= SMALL) cc[k] = serial_child_counts(nd, ka, kb);
       }
-      for_big_nodes<NW>(Lc, nR, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+      for_big_nodes<NW>(Lc, nR, SMALL, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
         const int4 c4 = wave_child_counts(Lc[(int)(sk[k] & 0xfffffull)], ka, kb);
         if (lane == 0) cc[k] = c4;
       });
@@ -1865,9 +1869,9 @@ __device__ __forceinline__ void octree_run(const ExtractArgs& a, uint8_t* smem, 
       // partition the divided nodes' keys
       for (int k = t; k < nproc; k += NT) {
         const ONode nd = Lc[(int)(sk[k] & 0xfffffull)];
-        if (nd.count <= OCT_SMALL) serial_child_partition(nd, cc[k], ka, kb);
+        if (nd.count <= SMALL) serial_child_partition(nd, cc[k], ka, kb);
       }
-      for_big_nodes<NW>(Lc, nproc, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
+      for_big_nodes<NW>(Lc, nproc, SMALL, [&](int k) { return (int)(sk[k] & 0xfffffull); }, [&](int k) {
         wave_child_partition(Lc[(int)(sk[k] & 0xfffffull)], cc[k], ka, kb);
       });
       for (int k = t; k < nR; k += NT) sx[k] = k < nproc ? nonempty4(cc[k]) : 0;
@@ -2451,6 +2455,8 @@ struct orbfe_extractor {
   int oct_threads_small = 512;       // k_octree block size for calls of < 8 images (orbfe_debug_set_octree_threads)
   int oct_threads_batch = 256;       // ... and for batches of 8+
   int oct_threads_l0 = 0;            // ... for a small call's launch that holds level 0 (0: oct_threads_small)
+  int oct_small_small = OCT_SMALL;   // k_octree's thread-serial node size for calls of < 8 images ...
+  int oct_small_batch = OCT_SMALL;   // ... and batches (orbfe_debug_set_octree_serial)
   int oct_hi_kb = OCT_LDS_KB, oct_lo_kb = OCT_LDS_KB / 2;  // their LDS budgets (orbfe_debug_set_octree_lds)
   bool device_call = false;          // the current call is orbfe_extract_batch_device (may take the split)
   int fast_wpb_side = 4, fast_wpb_main = 1;  // k_fast cells per workgroup (orbfe_debug_set_fast_wpb)
@@ -3101,6 +3107,7 @@ static int launch_extract(orbfe_extractor* h, int n, const uint8_t* d_imgs, long
     ao.sort_cap = P.sort_cap;
     ao.scan_cap = P.scan_cap;
     ao.key_lds_cap = P.key_lds_cap;
+    ao.oct_small = n >= 8 ? h->oct_small_batch : h->oct_small_small;
     dim3 grid(nl, n);
     // calls of fewer than 8 images leave the chip nearly idle: one 512-thread block per level (8
     // wavefronts share each pass's node splits and the refinement's child counts, partitions and
@@ -3386,6 +3393,8 @@ extern "C" int orbfe_extractor_create(int nfeatures, float scale_factor, int nle
     h->autotune = (e && e[0] == '0') ? 0 : 1;
     const char* o = std::getenv("ORBFE_OCT_THREADS_SMALL");  // (A/B runs of whole processes)
     if (o && (std::atoi(o) == 256 || std::atoi(o) == 512 || std::atoi(o) == 1024)) h->oct_threads_small = std::atoi(o);
+    const char* q = std::getenv("ORBFE_OCT_SERIAL_SMALL");  // (A/B runs of whole processes)
+    if (q && std::atoi(q) >= 1 && std::atoi(q) <= OCT_SMALL_MAX) h->oct_small_small = std::atoi(q);
   }
   h->nfeatures = nfeatures;
   h->nlevels = nlevels;
@@ -4294,6 +4303,15 @@ extern "C" int orbfe_debug_set_octree_threads_l0(orbfe_extractor* h, int threads
   if (!h || !(threads == 0 || threads == 256 || threads == 512 || threads == 1024))
     return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_threads_l0: 0, 256, 512 or 1024");
   h->oct_threads_l0 = threads;
+  return ORBFE_OK;
+}
+
+extern "C" int orbfe_debug_set_octree_serial(orbfe_extractor* h, int small_calls, int batches) {
+  if (!h || small_calls < 1 || small_calls > OCT_SMALL_MAX || batches < 1 || batches > OCT_SMALL_MAX)
+    return orbfe_set_error(ORBFE_ERR_ARG, "orbfe_debug_set_octree_serial: 1 .. 128 keys");
+  h->oct_small_small = small_calls;
+  h->oct_small_batch = batches;
+  drop_graphs(h);  // (the captured launches hold the old value)
   return ORBFE_OK;
 }
 

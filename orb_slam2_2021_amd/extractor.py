@@ -314,6 +314,12 @@ class ORBextractor:
         L.check(self._lib.orbfe_debug_set_octree_threads(self._h, int(small_calls), int(batches)),
                 "set_octree_threads")
 
+    def debug_set_octree_serial(self, small_calls: int, batches: int = 48) -> None:
+        """DistributeOctTree: nodes of at most this many keys split by one thread, larger ones by a
+        wavefront (1..128), for calls of fewer than 8 images / batches of 8+."""
+        L.check(self._lib.orbfe_debug_set_octree_serial(self._h, int(small_calls), int(batches)),
+                "set_octree_serial")
+
     def debug_set_fast_side_merge(self, on: bool) -> None:
         """Batches: the side stream's FAST levels 1..k-1 in one launch after level k-1 is built."""
         L.check(self._lib.orbfe_debug_set_fast_side_merge(self._h, int(bool(on))), "set_fast_side_merge")

@@ -1,0 +1,66 @@
+"""C2 A/B on the bench's own C2 image (frame 0 of the seeded driving sequence): DistributeOctTree's
+thread-serial / wavefront split threshold for small calls (orbfe_debug_set_octree_serial);
+interleaved rounds of 200 orbfe_extract calls, outputs compared bit for bit.
+usage: python profiles/scripts/c2_octree_serial.py [rounds]"""
+import os
+import sys
+import time
+from ctypes import byref, c_int, c_size_t
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+from orb_slam2_2021_amd import ORBextractor  # noqa: E402
+from orb_slam2_2021_amd import _lib as L  # noqa: E402
+from orb_slam2_2021_amd.extractor import synth_sequence_frame  # noqa: E402
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    rows, cols = 376, 1241
+    img = synth_sequence_frame(0x0C3, 0, rows, cols)
+    img = np.ascontiguousarray(img[0] if isinstance(img, tuple) else img)
+    lib = L.lib()
+    modes = {"s48": 48, "s64": 64, "s80": 80, "s32": 32}
+    exts = {}
+    for m, v in modes.items():
+        e = ORBextractor(2000, 1.2, 8, 20, 7)
+        e.debug_set_octree_serial(v, 48)
+        exts[m] = e
+    ref = "s48"
+    cap = exts[ref].max_keypoints(rows, cols)
+    out = {m: (np.zeros(cap, L.KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8), c_int()) for m in modes}
+
+    def call(m):
+        k, d, n = out[m]
+        L.check(lib.orbfe_extract(exts[m]._h, L.ptr(img), rows, cols, c_size_t(cols), L.ptr(k), cap, L.ptr(d),
+                                  byref(n)), "orbfe_extract")
+
+    for m in modes:
+        for _ in range(30):
+            call(m)
+    n0 = out[ref][2].value
+    for m in modes:
+        n = out[m][2].value
+        same = n == n0 and out[m][0][:n].tobytes() == out[ref][0][:n0].tobytes() and \
+            np.array_equal(out[m][1][:n], out[ref][1][:n0])
+        print(f"{m:9s} keypoints {n}  identical: {same}  schedule {exts[m].debug_schedule_choice(1)}", flush=True)
+    res = {m: [] for m in modes}
+    for r in range(rounds):
+        for m in modes:
+            t = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                call(m)
+                t.append(time.perf_counter() - t0)
+            res[m] += t
+            print(f"round {r} {m:9s} p50 {np.median(t) * 1e3:.4f} ms", flush=True)
+    for m in modes:
+        t = np.array(res[m])
+        print(f"ALL {m:9s} p50 {np.median(t) * 1e3:.4f} ms  p99 {np.percentile(t, 99) * 1e3:.4f} ms  "
+              f"min {t.min() * 1e3:.4f} ms")
+
+
+if __name__ == "__main__":
+    main()

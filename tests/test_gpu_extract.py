@@ -195,6 +195,28 @@ def test_octree_block_sizes(require_gpu, threads, cap):
             assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
 
 
+@pytest.mark.parametrize("small,batch,cap", [(64, 48, -1), (128, 16, -1), (1, 128, -1), (64, 64, 0)])
+def test_octree_serial_threshold(require_gpu, small, batch, cap):
+    """DistributeOctTree with other thread-serial / wavefront split thresholds
+    (orbfe_debug_set_octree_serial) for small calls and batches: the same survivors, one image,
+    three per call and an 8-image device batch, keys in LDS or (cap 0) on the global path."""
+    ext, ref = ORBextractor(2000, 1.2, 8, 20, 7), RefExtractor(2000, 1.2, 8, 20, 7)
+    ext.debug_set_octree_serial(small, batch)
+    if cap >= 0:
+        ext.debug_set_octree_key_cap(cap)
+    rng = np.random.default_rng(23)
+    for shape in ((376, 1241), (301, 517)):
+        imgs = [synth_frame(41, *shape), rng.integers(0, 256, shape, dtype=np.uint8), synth_frame(42, *shape)]
+        assert_same_extraction(ext, ref, imgs[0])
+        outs = ext.extract_batch(imgs)
+        for i in reversed(range(len(imgs))):
+            assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+    imgs = [synth_frame(80 + i, 376, 1241) for i in range(8)]
+    outs = _extract_device_batch(ext, imgs)
+    for i in (0, 5, 7):
+        assert_same_extraction(ext, ref, imgs[i], image_index=i, got=outs[i])
+
+
 def _extract_device_batch(ext, imgs):
     import torch
     imgs = np.stack(imgs)
