@@ -1,8 +1,9 @@
 """C2 A/B on the bench's own C2 image (frame 0 of the seeded driving sequence: 3,651 level-0 FAST
 candidates against 2,890 in synth_frame(3)): the block size of the octree launch that holds level 0
-(orbfe_debug_set_octree_threads_l0) and of the other small-call octree launch; interleaved rounds of
-200 orbfe_extract calls, outputs compared bit for bit.
-usage: python profiles/scripts/c2_octree_l0.py [rounds]"""
+(orbfe_debug_set_octree_threads_l0) and of the other small-call octree launch, or (`serial`) the
+small calls' thread-serial / wavefront split threshold (orbfe_debug_set_octree_serial); interleaved
+rounds of 200 orbfe_extract calls, outputs compared bit for bit.
+usage: python profiles/scripts/c2_octree_l0.py [rounds] [threads|serial]"""
 import os
 import sys
 import time
@@ -23,14 +24,21 @@ def main():
     img = synth_sequence_frame(0x0C3, 0, rows, cols)
     img = np.ascontiguousarray(img[0] if isinstance(img, tuple) else img)
     lib = L.lib()
-    modes = {"l0_512": (512, 512), "l0_1024": (1024, 512), "l0_256": (256, 512), "all_1024": (1024, 1024)}
     exts = {}
-    for m, (t0, ts) in modes.items():
-        e = ORBextractor(2000, 1.2, 8, 20, 7)
-        e.debug_set_octree_threads(ts, 256)
-        L.check(lib.orbfe_debug_set_octree_threads_l0(e._h, t0), "l0")
-        exts[m] = e
-    ref = "l0_512"
+    if len(sys.argv) > 2 and sys.argv[2] == "serial":
+        modes = {"s48": 48, "s64": 64, "s80": 80, "s32": 32}
+        for m, v in modes.items():
+            exts[m] = ORBextractor(2000, 1.2, 8, 20, 7)
+            exts[m].debug_set_octree_serial(v, 48)
+        ref = "s48"
+    else:
+        modes = {"l0_512": (512, 512), "l0_1024": (1024, 512), "l0_256": (256, 512), "all_1024": (1024, 1024)}
+        for m, (t0, ts) in modes.items():
+            e = ORBextractor(2000, 1.2, 8, 20, 7)
+            e.debug_set_octree_threads(ts, 256)
+            L.check(lib.orbfe_debug_set_octree_threads_l0(e._h, t0), "l0")
+            exts[m] = e
+        ref = "l0_512"
     cap = exts[ref].max_keypoints(rows, cols)
     out = {m: (np.zeros(cap, L.KEYPOINT_DTYPE), np.zeros((cap, 32), np.uint8), c_int()) for m in modes}
 
